@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark: strong solve of the 2^32-position subtraction game.
+
+Workload (BASELINE.json config 5): 8 heaps x 4 bits, root 0xFFFFFFFF,
+all 2^32 positions reachable.  One step = one complete strong solve (value and
+remoteness of every position) by libgmsolve.so's dense tiered kernel; the table
+lives in HBM (a torch-allocated int16 tensor adopted by the library) before the
+timed region starts.  Synthetic by construction: the game is the input.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (driver contract), including
+  roofline      the tier kernel's algorithmic bytes per launch (31 B per position,
+                SURVEY §8d, x positions per launch) / its average launch time, from
+                HIP events recorded around every launch on the launch stream;
+                traffic = rocprofv3 PMC bytes per launch from profiles/ when present;
+  cpu_baseline  the C oracle's dense solver (oracle/gm_oracle.c, 1 thread) on a
+                bounded sample (7 heaps = 2^28 positions) on this host.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+ALGO_BYTES_PER_POSITION = 31.0  # SURVEY §8d edge-traffic model at 8 heaps (2 * (1 + 14.5))
+METRIC = "positions solved/sec (node) at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
+
+
+def cpu_baseline(heaps=7):
+    """The C oracle's sequential dense solver on a bounded sample (positions/s, 1 thread)."""
+    path = os.path.join(REPO, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(path):
+        return None
+    import numpy as np
+    L = ctypes.CDLL(path)
+    L.oracle_subtract_dense.argtypes = [ctypes.c_int, ctypes.c_void_p]
+    out = np.empty(1 << (4 * heaps), dtype=np.uint16)
+    t0 = time.perf_counter()
+    rc = L.oracle_subtract_dense(heaps, out.ctypes.data)
+    dt = time.perf_counter() - t0
+    if rc != 0:
+        return None
+    n = 1 << (4 * heaps)
+    return {"value": n / dt, "unit": "positions/s", "cores": 1, "kind": "port",
+            "sample": "%d-heap subtraction game, all %d positions, sequential key-order retrograde "
+                      "(oracle/gm_oracle.c oracle_subtract_dense), %.1f s" % (heaps, n, dt)}
+
+
+def pmc_traffic(heaps, launches_per_solve):
+    """HBM bytes per launch of the tier kernel from a committed rocprofv3 PMC summary."""
+    path = os.path.join(REPO, "profiles", "traffic_subtract%d.json" % heaps)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    return t.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--heaps", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-heaps", type=int, default=7)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from gamesmanmpi_amd import Context, _lib
+
+    ctx = Context(_lib.GAME_SUBTRACT, (args.heaps,), device=local)
+    if world > 1:
+        uid = [None]
+        if rank == 0:
+            buf = ctypes.create_string_buffer(128)
+            _lib.check(_lib.lib().gm_comm_unique_id(buf, 128))
+            uid[0] = buf.raw
+        dist.broadcast_object_list(uid, src=0)
+        ctx.set_comm(rank, world, uid[0])
+    slots_local = (1 << (4 * args.heaps)) // world if world > 1 else 1 << (4 * args.heaps)
+    table = torch.empty(slots_local, dtype=torch.int16, device="cuda")
+    ctx.adopt_dense_table(table.data_ptr(), table.numel() * 2)
+    # A dedicated (non-null) stream: the tier launches are replayed as a hipGraph,
+    # which cannot be captured on the legacy default stream.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    ctx.set_option(_lib.OPT_TIMING, 1)
+    root = ctx.initial()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        n, rec = ctx.solve(root)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kernel_ms = 0.0
+    launches = 0
+    for _ in range(args.steps):
+        n, rec = ctx.solve(root)
+        st = ctx.stats()
+        kernel_ms += st["kernel_ms"]
+        launches += st["kernel_launches"]
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # closed-form check of the root: LOSS iff xor over heaps of (h mod 3) == 0
+    g = 0
+    for i in range(args.heaps):
+        g ^= ((root >> (4 * i)) & 15) % 3
+    assert (rec >> 14) == (1 if g == 0 else 0), "root record %#x contradicts the closed form" % rec
+
+    positions = n
+    value = positions * args.steps / elapsed
+    st = ctx.stats()
+    launches_per_solve = max(1, launches // max(1, args.steps))
+    algo_per_launch = ALGO_BYTES_PER_POSITION * positions / world / launches_per_solve
+    avg_launch_s = (kernel_ms / 1e3) / max(1, launches)
+    achieved = algo_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "positions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (the game itself: every position of the 2^32-state subtraction game)",
+        "config": {"workload": "subtraction game, %d heaps x 4 bits, root %#x (config 5)" % (args.heaps, root),
+                   "positions": positions, "parallelism": "1 GPU" if world == 1 else "block-sharded x%d" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                     "traffic": pmc_traffic(args.heaps, launches_per_solve),
+                     "kernel": "sub_tier_kernel<3,%d>" % (args.heaps - 3),
+                     "launches_per_solve": launches_per_solve,
+                     "avg_launch_us": avg_launch_s * 1e6,
+                     "kernel_ms_per_solve": kernel_ms / max(1, args.steps),
+                     "algo_bytes_per_position": ALGO_BYTES_PER_POSITION},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_heaps)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

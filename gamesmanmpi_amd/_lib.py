@@ -1,0 +1,108 @@
+"""ctypes binding of libgmsolve.so (include/gmsolve.h).
+
+The library is built in-tree (``python -m gamesmanmpi_amd.build``).  There is no
+fallback: if the library is missing or cannot be loaded, importing the solver
+raises, so a GPU run can never silently use some other code path.
+"""
+import ctypes
+import os
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libgmsolve.so")
+
+GAME_FOUR_TO_ONE, GAME_TTT, GAME_TOOT, GAME_OTHELLO, GAME_SUBTRACT = 1, 2, 3, 4, 5
+ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE = 0, 1, 2
+OPT_ENGINE, OPT_SUB_LOW, OPT_GRAPH, OPT_TIMING = 1, 2, 3, 4
+BUF_DENSE_TABLE = 1
+REC_UNSOLVED = 0xFFFF
+
+ERRORS = {
+    -1: "GM_E_ARG", -2: "GM_E_GAME", -3: "GM_E_HIP", -4: "GM_E_NOMEM", -5: "GM_E_STATE",
+    -6: "GM_E_DRAW", -7: "GM_E_NOMOVES", -8: "GM_E_CAP", -9: "GM_E_COMM", -10: "GM_E_KEY",
+}
+
+# Every symbol include/gmsolve.h declares (tests check the library exports them).
+SYMBOLS = ("gm_version", "gm_last_error", "gm_device_count", "gm_open", "gm_set_stream",
+           "gm_set_option", "gm_pack_initial", "gm_expand_host", "gm_comm_unique_id",
+           "gm_set_comm", "gm_solve", "gm_export", "gm_query", "gm_digest", "gm_stats",
+           "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_close")
+
+
+class GMError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__("%s (%d): %s" % (ERRORS.get(code, "GM_E?"), code, message))
+        self.code = code
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("n_positions", ctypes.c_uint64),
+        ("n_primitive", ctypes.c_uint64),
+        ("n_tiers", ctypes.c_int32),
+        ("world", ctypes.c_int32),
+        ("solve_ms", ctypes.c_double),
+        ("forward_ms", ctypes.c_double),
+        ("backward_ms", ctypes.c_double),
+        ("exchange_ms", ctypes.c_double),
+        ("algo_bytes", ctypes.c_uint64),
+        ("table_bytes", ctypes.c_uint64),
+        ("exchanged_bytes", ctypes.c_uint64),
+        ("kernel_ms", ctypes.c_double),
+        ("kernel_launches", ctypes.c_int32),
+        ("engine", ctypes.c_int32),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """Load libgmsolve.so once; raise loudly when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libgmsolve.so is not built (%s); run `python -m gamesmanmpi_amd.build`"
+                           % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    u64, i32, i64 = ctypes.c_uint64, ctypes.c_int32, ctypes.c_int64
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    sig = {
+        "gm_version": (ctypes.c_int, []),
+        "gm_last_error": (ctypes.c_char_p, []),
+        "gm_device_count": (ctypes.c_int, []),
+        "gm_open": (ctypes.c_int, [ctypes.c_int, P(i32), ctypes.c_int, ctypes.c_int, P(vp)]),
+        "gm_set_stream": (ctypes.c_int, [vp, vp]),
+        "gm_set_option": (ctypes.c_int, [vp, ctypes.c_int, i64]),
+        "gm_pack_initial": (ctypes.c_int, [vp, P(u64)]),
+        "gm_expand_host": (ctypes.c_int, [vp, u64, P(u64), ctypes.c_int, P(ctypes.c_int),
+                                          P(ctypes.c_int), P(i64)]),
+        "gm_comm_unique_id": (ctypes.c_int, [vp, ctypes.c_int]),
+        "gm_set_comm": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int]),
+        "gm_solve": (ctypes.c_int, [vp, u64, P(u64), P(ctypes.c_uint16)]),
+        "gm_export": (ctypes.c_int, [vp, vp, vp, u64, P(u64)]),
+        "gm_query": (ctypes.c_int, [vp, vp, vp, u64]),
+        "gm_digest": (ctypes.c_int, [vp, P(u64), P(u64)]),
+        "gm_stats": (ctypes.c_int, [vp, P(Stats)]),
+        "gm_tier_counts": (ctypes.c_int, [vp, vp, ctypes.c_int, P(ctypes.c_int)]),
+        "gm_adopt_buffer": (ctypes.c_int, [vp, ctypes.c_int, vp, u64]),
+        "gm_dense_table": (ctypes.c_int, [vp, P(vp), P(u64)]),
+        "gm_close": (None, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().gm_last_error()
+        raise GMError(rc, msg.decode() if msg else "")
+    return rc

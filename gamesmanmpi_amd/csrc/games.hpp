@@ -1,0 +1,273 @@
+// games.hpp -- bit-packed game descriptors (host + device).
+//
+// Each descriptor restates one reference plugin over a u64 key:
+//   primitive(k)          -> WIN/LOSS/TIE/DRAW/UNDECIDED     (plugin primitive())
+//   children(k, out)      -> number of children, keys in out  (gen_moves + do_move,
+//                            i.e. GameState.expand, reference src/game_state.py:33-41)
+//   tier(k)               -> a potential that strictly increases along every move;
+//                            children land 1..MAX_SKIP tiers deeper
+//   valid(k)              -> whether k is a position the plugin can represent
+//
+// Board games work on the key's planes directly.  A key stores cell (x, y) of an
+// L x H board at plane bit c' = A-1-(L*y + x) (the reference string is MSB-first,
+// App. B), i.e. the board rotated by 180 degrees: x' = L-1-x, y' = H-1-y and
+// c' = L*y' + x'.  Word/line/flip rules are invariant under that rotation, so
+// the descriptors use ordinary shift arithmetic in (x', y').
+#pragma once
+#include "gm_common.hpp"
+
+namespace gm {
+
+// ---------------------------------------------------------------- Four-To-One
+// reference test_games/four_to_one.py:8-31 (moves are always -1, -2: the
+// `x == 1` test at :15 compares a str with an int and never fires).
+struct DescF2O {
+    static constexpr int MAX_SKIP = 2;
+    static constexpr int MAXC = 2;
+    GM_HD int primitive(uint64_t k) const { return (int64_t)k <= 0 ? LOSS : UNDECIDED; }
+    GM_HD int children(uint64_t k, uint64_t *out) const {
+        out[0] = k - 1;
+        out[1] = k - 2;
+        return 2;
+    }
+    GM_HD int64_t tier(uint64_t k) const { return -(int64_t)k; }
+    GM_HD bool valid(uint64_t k) const {
+        int64_t x = (int64_t)k;
+        return x > -((int64_t)1 << 60) && x < ((int64_t)1 << 60);
+    }
+};
+
+// ---------------------------------------------------------------- Tic-tac-toe
+// reference test_games/mttt.py:11-127 and tic_tac_toe_np.py:7-61.
+// key = sum c_i 3^i, i = x + 3y, c: 0 blank, 1 X (player 1), 2 O (player 2).
+struct DescTTT {
+    static constexpr int MAX_SKIP = 1;
+    static constexpr int MAXC = 9;
+    static constexpr uint32_t SLOTS = 19683;
+    GM_HD static uint32_t pow3(int i) {
+        uint32_t p = 1;
+        for (int j = 0; j < i; j++) p *= 3;
+        return p;
+    }
+    GM_HD static void decode(uint64_t k, int c[9]) {
+        uint32_t v = (uint32_t)k;
+        for (int i = 0; i < 9; i++) { c[i] = (int)(v % 3u); v /= 3u; }
+    }
+    GM_HD int primitive(uint64_t k) const {
+        int c[9];
+        decode(k, c);
+        // rows, columns, diagonals: the lines checked from each piece in
+        // directions (1,0), (0,1), (1,1), (-1,1) by mttt.py:69-83
+        const int L[8][3] = {{0, 1, 2}, {3, 4, 5}, {6, 7, 8}, {0, 3, 6},
+                             {1, 4, 7}, {2, 5, 8}, {0, 4, 8}, {2, 4, 6}};
+        for (int l = 0; l < 8; l++) {
+            int a = c[L[l][0]];
+            if (a && a == c[L[l][1]] && a == c[L[l][2]]) return LOSS;
+        }
+        for (int i = 0; i < 9; i++)
+            if (!c[i]) return UNDECIDED;
+        return TIE;
+    }
+    GM_HD int children(uint64_t k, uint64_t *out) const {
+        int c[9], nx = 0, no = 0, n = 0;
+        decode(k, c);
+        for (int i = 0; i < 9; i++) { nx += c[i] == 1; no += c[i] == 2; }
+        uint64_t mover = no >= nx ? 1 : 2;   // mttt.py:39-43
+        uint64_t p = 1;
+        for (int i = 0; i < 9; i++, p *= 3)
+            if (!c[i]) out[n++] = k + mover * p;
+        return n;
+    }
+    GM_HD int64_t tier(uint64_t k) const {
+        int c[9], n = 0;
+        decode(k, c);
+        for (int i = 0; i < 9; i++) n += c[i] != 0;
+        return n;
+    }
+    GM_HD bool valid(uint64_t k) const { return k < SLOTS; }
+};
+
+// ---------------------------------------------------------------- Toot-and-Otto
+// reference test_games/toot_and_otto_bitstring.py.  Key = first 2A+16 string
+// bits: T plane at key bits [A+16, 2A+16), O plane at [16, A+16), then the hand
+// nibbles P1-T (bits 12..15), P1-O (8..11), P2-T (4..7), P2-O (0..3).  The turn
+// bit of the string equals the piece count mod 2 (player 2 moves first).
+struct DescToot {
+    static constexpr int MAX_SKIP = 1;
+    static constexpr int MAXC = 16;
+    int L, H, A;
+    uint32_t amask;
+    uint32_t start_h, start_v, start_d, start_a;   // segment starts per direction
+    uint32_t colmask;                              // cells of column x' = 0
+
+    static bool make(int L_, int H_, DescToot *d) {
+        if (L_ < 1 || H_ < 1 || L_ > 8 || 2 * L_ * H_ + 16 > 64) return false;
+        d->L = L_; d->H = H_; d->A = L_ * H_;
+        d->amask = d->A == 32 ? 0xFFFFFFFFu : ((1u << d->A) - 1u);
+        d->start_h = d->start_v = d->start_d = d->start_a = 0;
+        d->colmask = 0;
+        for (int y = 0; y < H_; y++) {
+            d->colmask |= 1u << (L_ * y);
+            for (int x = 0; x < L_; x++) {
+                uint32_t b = 1u << (L_ * y + x);
+                if (x + 3 < L_) d->start_h |= b;
+                if (y + 3 < H_) d->start_v |= b;
+                if (x + 3 < L_ && y + 3 < H_) d->start_d |= b;
+                if (x - 3 >= 0 && y + 3 < H_) d->start_a |= b;
+            }
+        }
+        return true;
+    }
+    GM_HD uint32_t tplane(uint64_t k) const { return (uint32_t)(k >> (A + 16)) & amask; }
+    GM_HD uint32_t oplane(uint64_t k) const { return (uint32_t)(k >> 16) & amask; }
+    GM_HD static int words(uint32_t a, uint32_t b, int d, uint32_t start) {
+        // segments a b b a along step d (TOOT with a = T plane, OTTO with a = O plane)
+        return popc64(a & (b >> d) & (b >> (2 * d)) & (a >> (3 * d)) & start);
+    }
+    GM_HD int primitive(uint64_t k) const {
+        uint32_t t = tplane(k), o = oplane(k);
+        int toot = words(t, o, 1, start_h) + words(t, o, L, start_v) +
+                   words(t, o, L + 1, start_d) + words(t, o, L - 1, start_a);
+        int otto = words(o, t, 1, start_h) + words(o, t, L, start_v) +
+                   words(o, t, L + 1, start_d) + words(o, t, L - 1, start_a);
+        int pieces = popc64(t | o);
+        if (toot == otto) return pieces == A ? TIE : UNDECIDED;
+        bool p1 = pieces & 1;                         // is_player1_turn (:218-219)
+        return ((toot > otto) != p1) ? LOSS : WIN;    // :82-85
+    }
+    GM_HD int children(uint64_t k, uint64_t *out) const {
+        uint32_t occ = tplane(k) | oplane(k);
+        bool p1 = popc64(occ) & 1;
+        int tsh = p1 ? 12 : 4, osh = p1 ? 8 : 0;     // get_hand_count (:202-207)
+        uint32_t th = (uint32_t)(k >> tsh) & 15u, oh = (uint32_t)(k >> osh) & 15u;
+        bool have_t = th >= 1 && th <= 7, have_o = oh >= 1 && oh <= 7;  // signed nibble > 0
+        int n = 0;
+        for (int x = 0; x < L; x++) {                 // gen_moves order (:94-99)
+            int xr = L - 1 - x;
+            if (occ & (1u << xr)) continue;           // top cell (x, H-1) taken
+            int filled = popc64(occ & (colmask << xr));
+            int bit = L * (H - 1 - filled) + xr;      // lowest empty y (:112-115)
+            if (have_t) out[n++] = k - (1ull << tsh) + (1ull << (A + 16 + bit));
+            if (have_o) out[n++] = k - (1ull << osh) + (1ull << (16 + bit));
+        }
+        return n;
+    }
+    GM_HD int64_t tier(uint64_t k) const { return popc64(tplane(k) | oplane(k)); }
+    GM_HD bool valid(uint64_t k) const {
+        uint32_t t = tplane(k), o = oplane(k);
+        if (t & o) return false;
+        if (2 * A + 16 < 64 && (k >> (2 * A + 16))) return false;
+        uint32_t occ = t | o;
+        for (int xr = 0; xr < L; xr++) {              // pieces stacked from the bottom
+            int filled = popc64(occ & (colmask << xr));
+            for (int yr = 0; yr < H; yr++) {
+                bool want = yr >= H - filled;
+                if (((occ >> (L * yr + xr)) & 1u) != (uint32_t)want) return false;
+            }
+        }
+        return true;
+    }
+};
+
+// ---------------------------------------------------------------- Othello
+// reference test_games/othello_bit_new.py (square boards).  Key = all 2A+16
+// string bits: WHITE plane at [A+16, 2A+16), BLACK plane at [16, A+16), the
+// signed turn byte (1 BLACK, 2 WHITE) at bits 8..15, the pass byte at 0..7.
+struct DescOthello {
+    static constexpr int MAX_SKIP = 3;
+    static constexpr int MAXC = 24;
+    int L, A;
+    uint32_t amask;
+
+    static bool make(int L_, int H_, DescOthello *d) {
+        if (L_ != H_ || L_ < 2 || (L_ & 1) || 2 * L_ * H_ + 16 > 64) return false;
+        d->L = L_; d->A = L_ * H_;
+        d->amask = (1u << d->A) - 1u;
+        return true;
+    }
+    GM_HD uint32_t wplane(uint64_t k) const { return (uint32_t)(k >> (A + 16)) & amask; }
+    GM_HD uint32_t bplane(uint64_t k) const { return (uint32_t)(k >> 16) & amask; }
+    GM_HD static int sbyte(uint64_t k, int sh) { return (int)(int8_t)(uint8_t)(k >> sh); }
+    GM_HD int primitive(uint64_t k) const {
+        uint32_t w = wplane(k), b = bplane(k);
+        int pass = sbyte(k, 0), turn = sbyte(k, 8);
+        if (popc64(w | b) != A && pass < 2) return UNDECIDED;   // :311-320
+        int nb = popc64(b), nw = popc64(w);
+        if (nb == nw) return TIE;
+        return ((nb > nw) != (turn == 1)) ? LOSS : WIN;         // :305-309
+    }
+    // Pieces of `opp` flipped by `me` playing at (x, y) (rotated coordinates).
+    GM_HD uint32_t flips(uint32_t me, uint32_t opp, int x, int y) const {
+        uint32_t all = 0;
+        for (int dx = -1; dx <= 1; dx++)
+            for (int dy = -1; dy <= 1; dy++) {
+                if (!dx && !dy) continue;
+                uint32_t run = 0;
+                int cx = x + dx, cy = y + dy;
+                while (cx >= 0 && cy >= 0 && cx < L && cy < L) {
+                    uint32_t b = 1u << (L * cy + cx);
+                    if (opp & b) { run |= b; }
+                    else { if (me & b) all |= run; break; }
+                    cx += dx; cy += dy;
+                }
+            }
+        return all;
+    }
+    GM_HD int children(uint64_t k, uint64_t *out) const {
+        uint32_t w = wplane(k), b = bplane(k);
+        int turn = sbyte(k, 8);
+        bool black = turn == 1;
+        uint32_t me = black ? b : w, opp = black ? w : b;
+        uint64_t low = ((uint64_t)(uint8_t)(3 - turn)) << 8;     // incr_turn, pass reset
+        int n = 0;
+        for (int y = 0; y < L; y++)
+            for (int x = 0; x < L; x++) {
+                uint32_t cell = 1u << (L * y + x);
+                if ((w | b) & cell) continue;
+                uint32_t f = flips(me, opp, x, y);
+                if (!f) continue;                                 // legit_move (:370-382)
+                uint32_t nme = me | cell | f, nopp = opp & ~f;
+                uint32_t nw = black ? nopp : nme, nb = black ? nme : nopp;
+                out[n++] = ((uint64_t)nw << (A + 16)) | ((uint64_t)nb << 16) | low;
+            }
+        if (!n) out[n++] = k + 1;                                 // [None]: pass + 1 (:122-124)
+        return n;
+    }
+    GM_HD int64_t tier(uint64_t k) const {
+        return 3 * popc64(wplane(k) | bplane(k)) + sbyte(k, 0);
+    }
+    GM_HD bool valid(uint64_t k) const {
+        if (wplane(k) & bplane(k)) return false;
+        if (2 * A + 16 < 64 && (k >> (2 * A + 16))) return false;
+        int turn = sbyte(k, 8), pass = sbyte(k, 0);
+        return (turn == 1 || turn == 2) && pass >= 0 && pass <= 2;
+    }
+};
+
+// ---------------------------------------------------------------- Subtract
+// The build's synthetic game: `heaps` heaps of 4 bits; a move
+// takes 1 or 2 from one non-empty heap, floor 0 (duplicate children dropped);
+// all heaps empty is a LOSS.  One heap = Four-To-One for piles >= 0.
+struct DescSub {
+    static constexpr int MAX_SKIP = 2;
+    static constexpr int MAXC = 16;
+    int heaps;
+    GM_HD int primitive(uint64_t k) const { return k == 0 ? LOSS : UNDECIDED; }
+    GM_HD int children(uint64_t k, uint64_t *out) const {
+        int n = 0;
+        for (int i = 0; i < heaps; i++) {
+            uint64_t h = (k >> (4 * i)) & 15u;
+            if (h >= 1) out[n++] = k - (1ull << (4 * i));
+            if (h >= 2) out[n++] = k - (2ull << (4 * i));
+        }
+        return n;
+    }
+    GM_HD int64_t tier(uint64_t k) const {
+        int64_t s = 0;
+        for (int i = 0; i < heaps; i++) s += (k >> (4 * i)) & 15u;
+        return -s;
+    }
+    GM_HD bool valid(uint64_t k) const { return heaps >= 16 || (k >> (4 * heaps)) == 0; }
+};
+
+}  // namespace gm

@@ -1,0 +1,336 @@
+// gm_api.hip -- the C ABI (include/gmsolve.h): contexts, dispatch, errors.
+#include "gm_internal.hpp"
+
+#include <chrono>
+#include <string.h>
+
+namespace gm {
+
+static thread_local char g_err[512];
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+int dev_error_to_gm(uint32_t f) {
+    if (f & DEV_ERR_DRAW) { set_error("a DRAW primitive was reached (unsupported)"); return GM_E_DRAW; }
+    if (f & DEV_ERR_NOMOVES) { set_error("a non-primitive position has no moves"); return GM_E_NOMOVES; }
+    if (f & DEV_ERR_TIER) { set_error("descriptor tier does not increase by 1..MAX_SKIP along a move"); return GM_E_GAME; }
+    if (f & DEV_ERR_TABLE_FULL) { set_error("tier table overflow"); return GM_E_NOMEM; }
+    if (f & DEV_ERR_MISSING_CHILD) { set_error("retrograde found a child missing from its tier table"); return GM_E_STATE; }
+    if (f & DEV_ERR_OVERFLOW) { set_error("remoteness exceeds 14 bits"); return GM_E_CAP; }
+    set_error("device error flags 0x%x", f);
+    return GM_E_STATE;
+}
+
+double now_ms() {
+    using namespace std::chrono;
+    return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+static int engine_for(const Ctx *c) {
+    if (c->engine_opt == GM_ENGINE_SPARSE) return GM_ENGINE_SPARSE;
+    if (c->engine_opt == GM_ENGINE_DENSE) {
+        if (c->game == GM_GAME_SUBTRACT || c->game == GM_GAME_TTT) return GM_ENGINE_DENSE;
+        return GM_ENGINE_SPARSE;
+    }
+    return (c->game == GM_GAME_SUBTRACT || c->game == GM_GAME_TTT) ? GM_ENGINE_DENSE : GM_ENGINE_SPARSE;
+}
+
+static bool key_valid(const Ctx *c, uint64_t k) {
+    switch (c->game) {
+    case GM_GAME_FOUR_TO_ONE: return c->f2o.valid(k);
+    case GM_GAME_TTT: return c->ttt.valid(k);
+    case GM_GAME_TOOT: return c->toot.valid(k);
+    case GM_GAME_OTHELLO: return c->oth.valid(k);
+    case GM_GAME_SUBTRACT: return c->sub.valid(k);
+    }
+    return false;
+}
+
+static void free_engines(Ctx *c) {
+    dense_sub_free(c);
+    small_dense_free(c);
+    sparse_free(c);
+}
+
+}  // namespace gm
+
+using namespace gm;
+
+extern "C" {
+
+int gm_version(void) { return GM_ABI_VERSION; }
+
+const char *gm_last_error(void) { return g_err; }
+
+int gm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int gm_open(int game, const int32_t *params, int nparams, int device, gm_ctx **out) {
+    if (!out) { set_error("out is NULL"); return GM_E_ARG; }
+    *out = nullptr;
+    if (nparams < 0 || nparams > 4 || (nparams && !params)) { set_error("bad params"); return GM_E_ARG; }
+    gm_ctx *h = new gm_ctx();
+    Ctx *c = &h->c;
+    c->game = game;
+    for (int i = 0; i < nparams; i++) c->params[i] = params[i];
+    bool ok = true;
+    switch (game) {
+    case GM_GAME_FOUR_TO_ONE: case GM_GAME_TTT: break;
+    case GM_GAME_TOOT:
+        ok = DescToot::make(nparams > 0 ? params[0] : 6, nparams > 1 ? params[1] : 4, &c->toot);
+        break;
+    case GM_GAME_OTHELLO:
+        ok = DescOthello::make(nparams > 0 ? params[0] : 4, nparams > 1 ? params[1] : 4, &c->oth);
+        break;
+    case GM_GAME_SUBTRACT:
+        c->sub.heaps = nparams > 0 ? params[0] : 8;
+        ok = c->sub.heaps >= 1 && c->sub.heaps <= 8;
+        break;
+    default:
+        ok = false;
+    }
+    if (!ok) {
+        set_error("game %d with these parameters is not supported", game);
+        delete h;
+        return GM_E_GAME;
+    }
+    int ndev = gm_device_count();
+    if (ndev <= 0) {
+        // Contexts can still be used for gm_pack_initial / gm_expand_host.
+        c->device = -1;
+        *out = h;
+        return GM_OK;
+    }
+    if (device < 0) {
+        if (hipGetDevice(&c->device) != hipSuccess) c->device = 0;
+    } else {
+        if (device >= ndev) { set_error("device %d out of range (%d visible)", device, ndev); delete h; return GM_E_ARG; }
+        c->device = device;
+    }
+    if (hipSetDevice(c->device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error("cannot initialise HIP device %d", c->device);
+        delete h;
+        return GM_E_HIP;
+    }
+    c->stream = c->own_stream;
+    *out = h;
+    return GM_OK;
+}
+
+int gm_set_stream(gm_ctx *h, void *s) {
+    if (!h) return GM_E_ARG;
+    h->c.stream = s ? (hipStream_t)s : h->c.own_stream;
+    return GM_OK;
+}
+
+int gm_set_option(gm_ctx *h, int opt, int64_t v) {
+    if (!h) return GM_E_ARG;
+    Ctx *c = &h->c;
+    switch (opt) {
+    case GM_OPT_ENGINE:
+        if (v < GM_ENGINE_AUTO || v > GM_ENGINE_SPARSE) { set_error("bad engine"); return GM_E_ARG; }
+        c->engine_opt = (int)v;
+        return GM_OK;
+    case GM_OPT_SUB_LOW:
+        if (v < 1 || v > 3) { set_error("sub_low must be 1..3"); return GM_E_ARG; }
+        c->sub_low = (int)v;
+        return GM_OK;
+    case GM_OPT_GRAPH: c->use_graph = v != 0; return GM_OK;
+    case GM_OPT_TIMING: c->timing = v != 0; return GM_OK;
+    }
+    set_error("unknown option %d", opt);
+    return GM_E_ARG;
+}
+
+int gm_pack_initial(gm_ctx *h, uint64_t *key) {
+    if (!h || !key) return GM_E_ARG;
+    Ctx *c = &h->c;
+    switch (c->game) {
+    case GM_GAME_FOUR_TO_ONE: *key = 4; return GM_OK;   // four_to_one.py:8-10
+    case GM_GAME_TTT: *key = 0; return GM_OK;           // empty board
+    case GM_GAME_TOOT: *key = 0x6666; return GM_OK;     // empty planes, hands 6/6/6/6 (:36-44)
+    case GM_GAME_OTHELLO: {                              // othello_bit_new.py:36-55
+        const DescOthello &o = c->oth;
+        int L = o.L, A = o.A;
+        auto bit = [&](int x, int y) { return 1u << (A - 1 - (L * y + x)); };   // rotated plane bit
+        uint32_t w = bit(L / 2 - 1, L / 2 - 1) | bit(L / 2, L / 2);
+        uint32_t b = bit(L / 2 - 1, L / 2) | bit(L / 2, L / 2 - 1);
+        *key = ((uint64_t)w << (A + 16)) | ((uint64_t)b << 16) | (2ull << 8);
+        return GM_OK;
+    }
+    case GM_GAME_SUBTRACT: *key = (1ull << (4 * c->sub.heaps)) - 1; return GM_OK;
+    }
+    return GM_E_GAME;
+}
+
+int gm_expand_host(gm_ctx *h, uint64_t key, uint64_t *children, int cap, int *n, int *prim, int64_t *tier) {
+    if (!h || !n || !prim || !tier) return GM_E_ARG;
+    Ctx *c = &h->c;
+    uint64_t kids[32];
+    int p = UNDECIDED, k = 0;
+    int64_t t = 0;
+    if (!key_valid(c, key)) { set_error("key is not a valid position"); return GM_E_KEY; }
+    switch (c->game) {
+    case GM_GAME_FOUR_TO_ONE: p = c->f2o.primitive(key); t = c->f2o.tier(key); if (p == UNDECIDED) k = c->f2o.children(key, kids); break;
+    case GM_GAME_TTT: p = c->ttt.primitive(key); t = c->ttt.tier(key); if (p == UNDECIDED) k = c->ttt.children(key, kids); break;
+    case GM_GAME_TOOT: p = c->toot.primitive(key); t = c->toot.tier(key); if (p == UNDECIDED) k = c->toot.children(key, kids); break;
+    case GM_GAME_OTHELLO: p = c->oth.primitive(key); t = c->oth.tier(key); if (p == UNDECIDED) k = c->oth.children(key, kids); break;
+    case GM_GAME_SUBTRACT: p = c->sub.primitive(key); t = c->sub.tier(key); if (p == UNDECIDED) k = c->sub.children(key, kids); break;
+    default: return GM_E_GAME;
+    }
+    *prim = p;
+    *tier = t;
+    *n = k;
+    if (k > cap) { set_error("children buffer holds %d, need %d", cap, k); return GM_E_CAP; }
+    if (children)
+        for (int i = 0; i < k; i++) children[i] = kids[i];
+    return GM_OK;
+}
+
+int gm_comm_unique_id(void *uid, int bytes) {
+    if (!uid || bytes < (int)sizeof(ncclUniqueId)) { set_error("uid buffer must hold %d bytes", (int)sizeof(ncclUniqueId)); return GM_E_ARG; }
+    ncclUniqueId id;
+    GM_NCCL(ncclGetUniqueId(&id));
+    memcpy(uid, &id, sizeof id);
+    return GM_OK;
+}
+
+int gm_set_comm(gm_ctx *h, int rank, int world, const void *uid, int bytes) {
+    if (!h || world < 1 || rank < 0 || rank >= world) { set_error("bad rank/world"); return GM_E_ARG; }
+    Ctx *c = &h->c;
+    if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    c->rank = rank;
+    c->world = world;
+    if (world == 1) return GM_OK;
+    if (!uid || bytes < (int)sizeof(ncclUniqueId)) { set_error("uid must hold %d bytes", (int)sizeof(ncclUniqueId)); return GM_E_ARG; }
+    if (c->device < 0) { set_error("no HIP device"); return GM_E_HIP; }
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof id);
+    GM_HIP(hipSetDevice(c->device));
+    GM_NCCL(ncclCommInitRank(&c->comm, world, id, rank));
+    return GM_OK;
+}
+
+int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_record) {
+    if (!h) return GM_E_ARG;
+    Ctx *c = &h->c;
+    if (c->device < 0) { set_error("no HIP device is visible: the solver needs an MI355X (gfx950)"); return GM_E_HIP; }
+    if (!key_valid(c, root)) { set_error("root key 0x%llx is not a valid position", (unsigned long long)root); return GM_E_KEY; }
+    GM_HIP(hipSetDevice(c->device));
+    c->solved = false;
+    int32_t launches = c->stats.kernel_launches;
+    c->stats = gm_stats_t{};
+    c->stats.kernel_launches = c->timing ? launches : 0;
+    c->stats.world = c->world;
+    c->root = root;
+    int eng = engine_for(c);
+    if (c->world > 1) {
+        set_error("multi-GPU solve is not available for this game/engine yet");
+        return GM_E_STATE;
+    }
+    int rc;
+    if (eng == GM_ENGINE_DENSE)
+        rc = c->game == GM_GAME_SUBTRACT ? dense_sub_solve(c, root) : small_dense_solve(c, root);
+    else
+        rc = sparse_solve(c, root);
+    if (rc != GM_OK) return rc;
+    c->engine = eng;
+    c->stats.engine = eng;
+    c->solved = true;
+    if (n_positions) *n_positions = c->n_positions;
+    if (root_record) *root_record = c->root_record;
+    return GM_OK;
+}
+
+static int need_solved(gm_ctx *h) {
+    if (!h) return GM_E_ARG;
+    if (!h->c.solved) { set_error("call gm_solve first"); return GM_E_STATE; }
+    return GM_OK;
+}
+
+int gm_export(gm_ctx *h, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
+    GM_TRY(need_solved(h));
+    if (!n || (keys && !recs)) return GM_E_ARG;
+    Ctx *c = &h->c;
+    GM_HIP(hipSetDevice(c->device));
+    if (c->engine == GM_ENGINE_DENSE)
+        return c->game == GM_GAME_SUBTRACT ? dense_sub_export(c, keys, recs, cap, n)
+                                           : small_dense_export(c, keys, recs, cap, n);
+    return sparse_export(c, keys, recs, cap, n);
+}
+
+int gm_query(gm_ctx *h, const uint64_t *keys, uint16_t *recs, uint64_t n) {
+    GM_TRY(need_solved(h));
+    if (n && (!keys || !recs)) return GM_E_ARG;
+    Ctx *c = &h->c;
+    GM_HIP(hipSetDevice(c->device));
+    if (c->engine == GM_ENGINE_DENSE)
+        return c->game == GM_GAME_SUBTRACT ? dense_sub_query(c, keys, recs, n) : small_dense_query(c, keys, recs, n);
+    return sparse_query(c, keys, recs, n);
+}
+
+int gm_digest(gm_ctx *h, uint64_t *digest, uint64_t *n) {
+    GM_TRY(need_solved(h));
+    if (!digest || !n) return GM_E_ARG;
+    Ctx *c = &h->c;
+    GM_HIP(hipSetDevice(c->device));
+    if (c->engine == GM_ENGINE_DENSE)
+        return c->game == GM_GAME_SUBTRACT ? dense_sub_digest(c, digest, n) : small_dense_digest(c, digest, n);
+    return sparse_digest(c, digest, n);
+}
+
+int gm_stats(gm_ctx *h, gm_stats_t *out) {
+    if (!h || !out) return GM_E_ARG;
+    *out = h->c.stats;
+    return GM_OK;
+}
+
+int gm_tier_counts(gm_ctx *h, uint64_t *counts, int cap, int *n) {
+    GM_TRY(need_solved(h));
+    if (!n) return GM_E_ARG;
+    Ctx *c = &h->c;
+    *n = (int)c->tier_counts.size();
+    if (!counts) return GM_OK;
+    if (cap < *n) { set_error("tier buffer too small"); return GM_E_CAP; }
+    for (int i = 0; i < *n; i++) counts[i] = c->tier_counts[i];
+    return GM_OK;
+}
+
+int gm_adopt_buffer(gm_ctx *h, int role, void *p, uint64_t bytes) {
+    if (!h || !p) return GM_E_ARG;
+    if (role != GM_BUF_DENSE_TABLE) { set_error("unknown buffer role %d", role); return GM_E_ARG; }
+    h->c.adopted_dense = p;
+    h->c.adopted_dense_bytes = bytes;
+    return GM_OK;
+}
+
+int gm_dense_table(gm_ctx *h, void **p, uint64_t *bytes) {
+    GM_TRY(need_solved(h));
+    if (!p || !bytes) return GM_E_ARG;
+    if (h->c.engine != GM_ENGINE_DENSE || h->c.game != GM_GAME_SUBTRACT) {
+        set_error("only the SUBTRACT dense path has a dense table");
+        return GM_E_STATE;
+    }
+    return dense_sub_table(&h->c, p, bytes);
+}
+
+void gm_close(gm_ctx *h) {
+    if (!h) return;
+    Ctx *c = &h->c;
+    if (c->device >= 0) hipSetDevice(c->device);
+    free_engines(c);
+    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->own_stream) hipStreamDestroy(c->own_stream);
+    delete h;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+// gm_internal.hpp -- context and helpers shared by the libgmsolve translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <string>
+#include <vector>
+
+#include "../../include/gmsolve.h"
+#include "games.hpp"
+
+namespace gm {
+
+void set_error(const char *fmt, ...);
+
+#define GM_HIP(expr)                                                              \
+    do {                                                                          \
+        hipError_t e_ = (expr);                                                   \
+        if (e_ != hipSuccess) {                                                   \
+            ::gm::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                            __FILE__, __LINE__);                                  \
+            return GM_E_HIP;                                                      \
+        }                                                                         \
+    } while (0)
+
+#define GM_TRY(expr)            \
+    do {                        \
+        int r_ = (expr);        \
+        if (r_ != GM_OK) return r_; \
+    } while (0)
+
+#define GM_NCCL(expr)                                                              \
+    do {                                                                           \
+        ncclResult_t r_ = (expr);                                                  \
+        if (r_ != ncclSuccess) {                                                   \
+            ::gm::set_error("%s failed: %s", #expr, ncclGetErrorString(r_));       \
+            return GM_E_COMM;                                                      \
+        }                                                                          \
+    } while (0)
+
+// Device error flags written by kernels (bitwise OR).
+enum : uint32_t {
+    DEV_ERR_DRAW = 1,
+    DEV_ERR_NOMOVES = 2,
+    DEV_ERR_TABLE_FULL = 4,
+    DEV_ERR_MISSING_CHILD = 8,
+    DEV_ERR_OVERFLOW = 16,
+    DEV_ERR_TIER = 32
+};
+
+int dev_error_to_gm(uint32_t flags);
+
+struct DenseSub;
+struct SmallDense;
+struct Sparse;
+
+struct Ctx {
+    int game = 0;
+    int device = 0;
+    int32_t params[4] = {0, 0, 0, 0};
+    DescF2O f2o;
+    DescTTT ttt;
+    DescToot toot;
+    DescOthello oth;
+    DescSub sub;
+
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+
+    int engine_opt = GM_ENGINE_AUTO;
+    int sub_low = 3;
+    bool use_graph = true;
+    bool timing = false;
+
+    // multi-GPU
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+
+    // results
+    bool solved = false;
+    int engine = 0;          // engine used by the last solve
+    uint64_t root = 0;
+    uint64_t n_positions = 0;
+    uint16_t root_record = REC_UNSOLVED;
+    gm_stats_t stats{};
+    std::vector<uint64_t> tier_counts;
+
+    // adopted buffers
+    void *adopted_dense = nullptr;
+    uint64_t adopted_dense_bytes = 0;
+
+    DenseSub *dsub = nullptr;
+    SmallDense *sd = nullptr;
+    Sparse *sp = nullptr;
+};
+
+// engines (each returns GM_OK or a GM_E_* code)
+int dense_sub_solve(Ctx *c, uint64_t root);
+int dense_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int dense_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int dense_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n);
+void dense_sub_free(Ctx *c);
+int dense_sub_table(Ctx *c, void **p, uint64_t *bytes);
+
+int small_dense_solve(Ctx *c, uint64_t root);
+int small_dense_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int small_dense_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int small_dense_digest(Ctx *c, uint64_t *digest, uint64_t *n);
+void small_dense_free(Ctx *c);
+
+int sparse_solve(Ctx *c, uint64_t root);
+int sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int sparse_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n);
+void sparse_free(Ctx *c);
+
+double now_ms();
+
+}  // namespace gm
+
+struct gm_ctx {
+    gm::Ctx c;
+};

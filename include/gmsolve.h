@@ -1,0 +1,182 @@
+/*
+ * gmsolve.h -- C ABI of libgmsolve.so, the MI355X strong solver.
+ *
+ * This is the drop-in boundary for the reference's solve path.  In the reference
+ * a solve is the mpi4py job loop of src/new_process.py (Process.run :37-60,
+ * lookup :102-133, distribute :145-162, resolve :223-265) over the shelve tables
+ * of src/cache_dict.py, started by solver_launcher.py:132-164.  Here a solve is
+ * one call, gm_solve(), over HBM-resident tables; the Python host
+ * (gamesmanmpi_amd/, solver_launcher.py, solve_local.py) binds these symbols with
+ * ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - every function returns GM_OK (0) or a negative GM_E_* code and never aborts;
+ *     gm_last_error() describes the last failure on the calling thread;
+ *   - host arrays are owned by the caller; device tables are owned by the context
+ *     (or adopted from the caller with gm_adopt_buffer) and die with gm_close();
+ *   - a gm_ctx is not thread-safe; use one per host thread;
+ *   - no torch types: plain pointers and sizes only.
+ *
+ * Records (u16): bits 15..14 = value (0 WIN, 1 LOSS, 2 TIE; the codes of
+ * reference src/utils.py:4), bits 13..0 = remoteness.  0xFFFF = not reached.
+ */
+#ifndef GMSOLVE_H
+#define GMSOLVE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GM_ABI_VERSION 1
+
+/* Game descriptors.  Params per game:
+ *   GM_GAME_FOUR_TO_ONE  none                  (reference test_games/four_to_one.py)
+ *   GM_GAME_TTT          none                  (test_games/mttt.py, tic_tac_toe_np.py)
+ *   GM_GAME_TOOT         {length, height}      (test_games/toot_and_otto_bitstring.py), 2*L*H+16 <= 64
+ *   GM_GAME_OTHELLO      {length, height}      (test_games/othello_bit_new.py), square, 2*L*H+16 <= 64
+ *   GM_GAME_SUBTRACT     {heaps}               (the build's synthetic game, 1..8 heaps of 4 bits)
+ */
+enum {
+    GM_GAME_FOUR_TO_ONE = 1,
+    GM_GAME_TTT = 2,
+    GM_GAME_TOOT = 3,
+    GM_GAME_OTHELLO = 4,
+    GM_GAME_SUBTRACT = 5
+};
+
+enum {
+    GM_OK = 0,
+    GM_E_ARG = -1,          /* bad argument */
+    GM_E_GAME = -2,         /* unknown game or unsupported parameters */
+    GM_E_HIP = -3,          /* HIP runtime error (no device, launch failure, ...) */
+    GM_E_NOMEM = -4,        /* device or host allocation failed */
+    GM_E_STATE = -5,        /* call out of order (e.g. export before solve) */
+    GM_E_DRAW = -6,         /* a DRAW primitive was reached (unsupported) */
+    GM_E_NOMOVES = -7,      /* non-primitive position without moves (the reference hangs) */
+    GM_E_CAP = -8,          /* caller buffer too small / remoteness overflow */
+    GM_E_COMM = -9,         /* RCCL failure */
+    GM_E_KEY = -10          /* root key is not a valid position of the game */
+};
+
+/* Internal engine selection (gm_set_option GM_OPT_ENGINE). */
+enum {
+    GM_ENGINE_AUTO = 0,     /* dense for SUBTRACT / TTT, sparse otherwise */
+    GM_ENGINE_DENSE = 1,
+    GM_ENGINE_SPARSE = 2
+};
+
+enum {
+    GM_OPT_ENGINE = 1,      /* GM_ENGINE_* */
+    GM_OPT_SUB_LOW = 2,     /* SUBTRACT dense path: heaps solved per workgroup in LDS (1..4) */
+    GM_OPT_GRAPH = 3,       /* SUBTRACT dense path: replay the tier launches as a hipGraph (0/1) */
+    GM_OPT_TIMING = 4       /* record HIP events around every launch of the dominant kernel (0/1) */
+};
+
+/* Buffer roles for gm_adopt_buffer. */
+enum {
+    GM_BUF_DENSE_TABLE = 1  /* SUBTRACT dense table: 2 bytes per slot, 16^heaps slots */
+};
+
+typedef struct gm_ctx gm_ctx;
+
+typedef struct {
+    uint64_t n_positions;   /* reachable positions with a final record (all ranks) */
+    uint64_t n_primitive;   /* of which primitive (this rank; dense path: all) */
+    int32_t n_tiers;        /* tiers walked */
+    int32_t world;          /* ranks in the solve */
+    double solve_ms;        /* wall time of the last gm_solve (host clock, device-synchronised) */
+    double forward_ms;      /* sparse path: forward expansion part */
+    double backward_ms;     /* retrograde part */
+    double exchange_ms;     /* multi-GPU: time inside RCCL calls (host-observed) */
+    uint64_t algo_bytes;    /* algorithmic HBM bytes of the solve (SURVEY §8d edge model) */
+    uint64_t table_bytes;   /* device bytes held by the tables */
+    uint64_t exchanged_bytes; /* multi-GPU: bytes sent over RCCL by this rank */
+    double kernel_ms;       /* GM_OPT_TIMING: summed event time of the dominant kernel's launches */
+    int32_t kernel_launches;/* GM_OPT_TIMING: number of those launches */
+    int32_t engine;         /* GM_ENGINE_DENSE or GM_ENGINE_SPARSE */
+} gm_stats_t;
+
+/* Library version (GM_ABI_VERSION). */
+int gm_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char *gm_last_error(void);
+
+/* Number of visible HIP devices (0 when none). */
+int gm_device_count(void);
+
+/* Create a context for one game on one HIP device (device < 0: the current one).
+ * Replaces the per-rank Process construction (reference src/new_process.py:62-94). */
+int gm_open(int game_id, const int32_t *params, int nparams, int device, gm_ctx **out);
+
+/* Run subsequent work on the caller's HIP stream (hipStream_t), e.g. torch's
+ * current stream; NULL restores the context's own stream. */
+int gm_set_stream(gm_ctx *ctx, void *hip_stream);
+
+/* Tunables (GM_OPT_*). */
+int gm_set_option(gm_ctx *ctx, int option, int64_t value);
+
+/* Key of the game's initial position (reference GameState.INITIAL_POS,
+ * src/game_state.py:15, i.e. initial_position() of the plugin). */
+int gm_pack_initial(gm_ctx *ctx, uint64_t *key);
+
+/* Host twin of the device descriptor for ONE position: its primitive value
+ * (0..4, src/utils.py:4), its tier, and (if not primitive) its children keys in
+ * the plugin's gen_moves order.  Used to match a plugin module to a descriptor
+ * and by tests; not on the solve path (reference GameState.expand /
+ * GameState.primitive, src/game_state.py:33-41, :59-85). */
+int gm_expand_host(gm_ctx *ctx, uint64_t key, uint64_t *children, int cap,
+                   int *n_children, int *primitive, int64_t *tier);
+
+/* Multi-GPU: join a solve of `world` ranks (one process per GPU).  `uid` is a
+ * 128-byte ncclUniqueId produced by gm_comm_unique_id on rank 0 and shared by
+ * the caller (e.g. over torch.distributed).  Replaces the mpi4py COMM_WORLD the
+ * reference passes to Process (solver_launcher.py:47-52, :132-140). */
+int gm_comm_unique_id(void *uid, int bytes);
+int gm_set_comm(gm_ctx *ctx, int rank, int world, const void *uid, int bytes);
+
+/* Strong-solve every position reachable from root_key (collective when a
+ * communicator is set: every rank calls it with the same root).  Returns the
+ * global number of reachable positions and the root's record (on every rank).
+ * Replaces Process.run/lookup/distribute/check_for_updates/send_back/resolve
+ * (src/new_process.py:37-265) and the root line of :42-53. */
+int gm_solve(gm_ctx *ctx, uint64_t root_key, uint64_t *n_positions, uint16_t *root_record);
+
+/* Copy this rank's solved table to host arrays, sorted by key.  With keys ==
+ * NULL only *n is set (the count).  Replaces reading the resolved/remote shelve
+ * tables (src/cache_dict.py:38-79, src/new_process.py:76-78). */
+int gm_export(gm_ctx *ctx, uint64_t *keys, uint16_t *records, uint64_t cap, uint64_t *n);
+
+/* Records of n keys (0xFFFF for keys this rank does not hold).  Replaces
+ * `pos in self.resolved` / `self.resolved[pos]` lookups (src/new_process.py:111-117). */
+int gm_query(gm_ctx *ctx, const uint64_t *keys, uint16_t *records, uint64_t n);
+
+/* Order-independent digest of this rank's table:
+ * sum over positions of mix64(key * 0x9E3779B97F4A7C15 + record) (mod 2^64),
+ * computed on the device; sums of the ranks' digests compare across world sizes. */
+int gm_digest(gm_ctx *ctx, uint64_t *digest, uint64_t *n);
+
+/* Solve statistics of the last gm_solve. */
+int gm_stats(gm_ctx *ctx, gm_stats_t *out);
+
+/* Positions per tier of the last solve (this rank); *n = number of tiers. */
+int gm_tier_counts(gm_ctx *ctx, uint64_t *counts, int cap, int *n);
+
+/* Back a table with caller-owned device memory (e.g. a torch tensor's storage).
+ * The caller keeps it alive until gm_close. */
+int gm_adopt_buffer(gm_ctx *ctx, int role, void *dev_ptr, uint64_t bytes);
+
+/* Device pointer and size of the dense table (GM_BUF_DENSE_TABLE) after a solve;
+ * its slots hold preference scores ("HBM layout"), not records. */
+int gm_dense_table(gm_ctx *ctx, void **dev_ptr, uint64_t *bytes);
+
+/* Release everything. */
+void gm_close(gm_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GMSOLVE_H */

@@ -1,0 +1,187 @@
+"""GPU parity: libgmsolve.so on the MI355X against the golden tables and the C oracle.
+
+Every comparison is bit-exact on (key, value, remoteness).  Fixtures come from
+the reference's own plugins (tests/golden/make_golden.py); larger cases compare
+with the C oracle (oracle/gm_oracle.c), which is itself pinned to the fixtures
+by tests/test_oracle_golden.py; full-size cases use size-independent properties
+(closed-form values, the reference-independent per-ply counts of SURVEY App. D).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, digest, golden, load_plugin
+
+pytestmark = pytest.mark.gpu
+
+from gamesmanmpi_amd import Context, Solver, _lib, games  # noqa: E402
+
+F2O, TTT, TOOT, OTH, SUB = 1, 2, 3, 4, 5
+
+
+def _solve(game, params=(), root=None, engine=None, **opts):
+    ctx = Context(game, params, device=0)
+    if engine is not None:
+        ctx.set_option(_lib.OPT_ENGINE, engine)
+    for k, v in opts.items():
+        ctx.set_option(getattr(_lib, "OPT_" + k.upper()), v)
+    if root is None:
+        root = ctx.initial()
+    n, rec = ctx.solve(root)
+    return ctx, n, rec
+
+
+def test_device_visible():
+    assert _lib.lib().gm_device_count() >= 1
+
+
+@pytest.mark.parametrize("engine", [_lib.ENGINE_DENSE, _lib.ENGINE_SPARSE])
+def test_ttt_full_table(engine):
+    keys, recs = golden("ttt")
+    ctx, n, rec = _solve(TTT, engine=engine)
+    k, r = ctx.export()
+    assert n == len(keys) == 5478
+    assert np.array_equal(k, keys) and np.array_equal(r, recs)
+    assert rec == (2 << 14) | 9          # TIE in 9
+    assert ctx.digest() == (digest(keys, recs), len(keys))
+
+
+@pytest.mark.parametrize("case", ["four", "six", "one", "zero"])
+def test_four_to_one_roots(case):
+    keys, recs = golden("four_to_one_" + case)
+    root = {"four": 4, "six": 6, "one": 1, "zero": 0}[case]
+    ctx, n, rec = _solve(F2O, root=root)
+    k, r = ctx.export()
+    assert np.array_equal(k, keys) and np.array_equal(r, recs)
+
+
+def test_othello_4x4():
+    keys, recs = golden("othello_4x4")
+    ctx, n, rec = _solve(OTH, (4, 4))
+    k, r = ctx.export()
+    assert n == 54089
+    assert np.array_equal(k, keys) and np.array_equal(r, recs)
+    assert rec == (1 << 14) | 12         # LOSS in 12
+
+
+@pytest.mark.parametrize("dims", [(3, 3), (4, 3)])
+def test_toot_small_boards(dims):
+    keys, recs = golden("toot_%dx%d" % dims)
+    ctx, n, rec = _solve(TOOT, dims)
+    k, r = ctx.export()
+    assert np.array_equal(k, keys) and np.array_equal(r, recs)
+
+
+def test_toot_4x4_vs_oracle(oracle):
+    ok, orec = oracle.solve(TOOT, (4, 4))
+    assert len(ok) == 3468773
+    ctx, n, rec = _solve(TOOT, (4, 4))
+    assert n == len(ok)
+    assert ctx.digest() == (digest(ok, orec), len(ok))
+    k, r = ctx.export()
+    assert np.array_equal(k, ok) and np.array_equal(r, orec)
+
+
+@pytest.mark.parametrize("heaps", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("low", [1, 2, 3])
+def test_subtract_dense_vs_oracle(oracle, heaps, low):
+    ref = oracle.subtract_dense(heaps)
+    ctx, n, rec = _solve(SUB, (heaps,), sub_low=low)
+    k, r = ctx.export()
+    assert n == 16 ** heaps
+    assert np.array_equal(k, np.arange(16 ** heaps, dtype=np.uint64))
+    assert np.array_equal(r, ref)
+
+
+def test_subtract_graph_replay_is_identical(oracle):
+    ref = oracle.subtract_dense(5)
+    for graph in (0, 1, 1):
+        ctx, n, rec = _solve(SUB, (5,), graph=graph)
+        assert np.array_equal(ctx.export()[1], ref)
+
+
+@pytest.mark.parametrize("heaps", [2, 3])
+def test_subtract_sparse_engine_matches_generic_oracle(oracle, heaps):
+    ok, orec = oracle.solve(SUB, (heaps,))
+    ctx, n, rec = _solve(SUB, (heaps,), engine=_lib.ENGINE_SPARSE)
+    k, r = ctx.export()
+    assert np.array_equal(k, ok) and np.array_equal(r, orec)
+
+
+def test_subtract_custom_root_box(oracle):
+    # root 0x0A35: reachable set is the box h_i <= root_i
+    root = 0x0A35
+    ok, orec = oracle.solve(SUB, (4,), root=root)
+    ctx, n, rec = _solve(SUB, (4,), root=root)
+    k, r = ctx.export()
+    assert n == len(ok) == 11 * 4 * 6 * 1
+    assert np.array_equal(k, ok) and np.array_equal(r, orec)
+
+
+def test_subtract_single_heap_is_four_to_one():
+    # one heap == Four-To-One for piles >= 0; golden from the reference plugin
+    keys, recs = golden("four_to_one_six")
+    ctx, n, rec = _solve(SUB, (1,), root=6)
+    sub = dict(zip(*[a.tolist() for a in ctx.export()]))
+    for k, r in zip(keys.tolist(), recs.tolist()):
+        x = k - (1 << 64) if k >> 63 else k
+        if x >= 0:
+            assert sub[x] == r
+
+
+def _closed_form_values(keys, heaps):
+    g = np.zeros(len(keys), dtype=np.int64)
+    for i in range(heaps):
+        g ^= ((keys >> np.uint64(4 * i)) & np.uint64(15)).astype(np.int64) % 3
+    return np.where(g == 0, 1, 0)   # LOSS iff xor of (h mod 3) == 0
+
+
+def test_subtract_full_2_32_properties():
+    """Config 5 at full size: closed-form values on 4M sampled keys + the root."""
+    ctx, n, rec = _solve(SUB, (8,))
+    assert n == 1 << 32
+    rng = np.random.default_rng(7)
+    keys = rng.integers(0, 1 << 32, size=1 << 22, dtype=np.uint64)
+    recs = ctx.query(keys)
+    assert np.array_equal(recs >> 14, _closed_form_values(keys, 8))
+    # remoteness: heaps of one kind only -> single-heap formula R(3k)=2k, R(3k+1)=R(3k+2)=2k+1
+    for h in range(16):
+        r1 = int(ctx.query([h])[0]) & 0x3FFF
+        assert r1 == (2 * (h // 3) + (0 if h % 3 == 0 else 1))
+    assert rec >> 14 == 1               # all heaps 15: xor of (15 mod 3) = 0 -> LOSS
+
+
+def test_subtract_7_heaps_vs_oracle_digest(oracle):
+    ref = oracle.subtract_dense(7)
+    ctx, n, rec = _solve(SUB, (7,))
+    keys = np.arange(1 << 28, dtype=np.uint64)
+    assert ctx.digest() == (digest(keys, ref), 1 << 28)
+
+
+def test_plugins_route_to_device():
+    """Our plugin modules are matched to descriptors and solved on the device."""
+    root_lines = json.load(open(os.path.join(GOLDEN, "roots.json")))
+    for rel, attrs, expect in [
+        ("test_games/mttt.py", {}, root_lines["mttt/blank"]["canonical"]),
+        ("test_games/tic_tac_toe_np.py", {}, "TIE in 9 moves"),
+        ("test_games/four_to_one.py", {}, "WIN in 3 moves"),
+        ("test_games/othello_bit_new.py", {"length": 4, "height": 4}, "LOSS in 12 moves"),
+        ("test_games/toot_and_otto_bitstring.py", {"length": 4, "height": 3}, "TIE in 12 moves"),
+    ]:
+        mod = load_plugin(rel, **attrs)
+        s = Solver(mod, device=0)
+        s.solve()
+        assert s.root_line() == expect, rel
+
+
+@pytest.mark.slow
+def test_toot_6x4_known_per_ply_counts():
+    """Config 3 at full size: per-ply reachable counts = SURVEY Appendix D."""
+    app_d = [1, 12, 114, 748, 4266, 19692, 81140, 285708, 928196, 2665424, 7098172, 17010952,
+             37792450, 64636776, 100084356, 136321692, 169785424, 180777508, 172831136,
+             135153280, 91440950, 45953432, 19196602, 4537828, 606968]
+    ctx, n, rec = _solve(TOOT, (6, 4))
+    assert n == 1187212827
+    assert [int(x) for x in ctx.tier_counts()] == app_d
