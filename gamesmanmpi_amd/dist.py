@@ -1,0 +1,34 @@
+"""Multi-GPU bootstrap: one process per GPU, ranks from torch.distributed.run.
+
+Replaces the reference's ``mpi4py.MPI.COMM_WORLD`` set-up
+(solver_launcher.py:47-52): rank 0 creates an RCCL unique id through the C ABI
+(``gm_comm_unique_id``), every rank receives it over a torch.distributed group
+(gloo by default: the bootstrap touches no GPU), and each context joins the RCCL
+communicator with ``gm_set_comm``.  All data-path exchange then happens inside
+libgmsolve.so (RCCL over xGMI).
+"""
+import ctypes
+
+from . import _lib
+
+
+def unique_id():
+    buf = ctypes.create_string_buffer(128)
+    _lib.check(_lib.lib().gm_comm_unique_id(buf, 128))
+    return buf.raw
+
+
+def share_unique_id(rank, backend="gloo"):
+    import torch.distributed as tdist
+    if not tdist.is_initialized():
+        tdist.init_process_group(backend)
+    uid = [unique_id() if rank == 0 else None]
+    tdist.broadcast_object_list(uid, src=0)
+    return uid[0]
+
+
+def join(ctx, rank, world, backend="gloo"):
+    """Make ``ctx`` (a solver.Context) one rank of a ``world``-GPU solve."""
+    uid = share_unique_id(rank, backend) if world > 1 else None
+    ctx.set_comm(rank, world, uid)
+    return uid

@@ -1,0 +1,139 @@
+"""CPU checks of the C-ABI library: it loads, exports what include/gmsolve.h declares,
+and its host-side descriptor twins agree with the oracle.  No device work here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO, golden, load_plugin
+from gamesmanmpi_amd import _lib, games
+
+F2O, TTT, TOOT, OTH, SUB = 1, 2, 3, 4, 5
+
+
+def header_symbols():
+    text = open(os.path.join(REPO, "include", "gmsolve.h")).read()
+    return set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(gm_\w+)\s*\(", text, re.M))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.lib()
+    declared = header_symbols()
+    assert declared == set(_lib.SYMBOLS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (gm_\w+)", out))
+    assert declared <= exported
+    for name in declared:
+        assert getattr(lib, name) is not None
+    assert lib.gm_version() == 1
+
+
+def test_library_is_gfx950_code():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
+                         capture_output=True, text=True, cwd="/tmp")
+    text = out.stdout + out.stderr
+    assert "gfx950" in text
+
+
+def test_no_gpu_means_loud_failure():
+    if _lib.lib().gm_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    from gamesmanmpi_amd import Context, GMError
+    ctx = Context(TTT, ())
+    with pytest.raises(GMError, match="no HIP device"):
+        ctx.solve(0)
+
+
+def test_open_rejects_bad_games():
+    from gamesmanmpi_amd import Context, GMError
+    for game, params in [(99, ()), (TOOT, (9, 4)), (OTH, (4, 3)), (SUB, (9,)), (OTH, (6, 6))]:
+        with pytest.raises(GMError):
+            Context(game, params)
+
+
+@pytest.mark.parametrize("game,params", [(F2O, ()), (TTT, ()), (TOOT, (6, 4)), (TOOT, (4, 3)),
+                                         (OTH, (4, 4)), (SUB, (8,)), (SUB, (3,))])
+def test_initial_keys_match_oracle(oracle, game, params):
+    from gamesmanmpi_amd import Context
+    assert Context(game, params).initial() == oracle.initial(game, params)
+
+
+@pytest.mark.parametrize("name,codec", [
+    ("ttt", games.TTTStringCodec()), ("othello_4x4", games.OthelloCodec(4, 4)),
+    ("toot_3x3", games.TootCodec(3, 3)), ("toot_4x3", games.TootCodec(4, 3)),
+    ("four_to_one_six", games.FourToOneCodec())])
+def test_descriptor_host_twin_matches_oracle_on_golden_positions(oracle, name, codec):
+    hd = games.HostDescriptor(codec)
+    keys, _ = golden(name)
+    step = max(1, len(keys) // 20000)
+    for k in keys[::step].tolist():
+        p1, c1, t1 = hd.expand(k)
+        assert (p1, sorted(c1), t1) == oracle.expand(codec.game_id, codec.params, k), hex(k)
+
+
+def test_toot_6x4_descriptor_random_playouts(oracle):
+    codec = games.TootCodec(6, 4)
+    hd = games.HostDescriptor(codec)
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        k = hd.initial()
+        while True:
+            p, kids, t = hd.expand(k)
+            assert (p, sorted(kids), t) == oracle.expand(TOOT, (6, 4), k)
+            if not kids:
+                break
+            k = kids[rng.integers(len(kids))]
+
+
+def test_expand_rejects_invalid_keys():
+    hd = games.HostDescriptor(games.OthelloCodec(4, 4))
+    with pytest.raises(_lib.GMError):
+        hd.expand(0)           # turn byte 0 is not a position
+
+
+@pytest.mark.parametrize("rel,attrs,name,params", [
+    ("test_games/four_to_one.py", {}, "four_to_one", ()),
+    ("test_games/mttt.py", {}, "mttt", ()),
+    ("test_games/tic_tac_toe_np.py", {}, "tic_tac_toe_np", ()),
+    ("test_games/toot_and_otto_bitstring.py", {}, "toot_and_otto", (6, 4)),
+    ("test_games/toot_and_otto_bitstring.py", {"length": 4, "height": 3}, "toot_and_otto", (4, 3)),
+    ("test_games/othello_bit_new.py", {"length": 4, "height": 4}, "othello", (4, 4)),
+    ("test_games/subtraction.py", {}, "subtraction", (8,)),
+])
+def test_identify_plugins(rel, attrs, name, params):
+    mod = load_plugin(rel, **attrs)
+    c = games.identify(mod)
+    assert c is not None and c.name == name and tuple(c.params) == params
+    root = mod.initial_position()
+    assert c.key(c.pos(c.key(root))) == c.key(root)
+
+
+def test_identify_rejects_a_modified_game():
+    mod = load_plugin("test_games/mttt.py")
+    orig = mod.primitive
+
+    def misere(pos):      # a different game: full board is a LOSS instead of a TIE
+        v = orig(pos)
+        return 1 if v == 2 else v
+    mod.primitive = misere
+    assert games.identify(mod) is None
+
+
+def test_othello_8x8_has_no_descriptor():
+    mod = load_plugin("test_games/othello_bit_new.py")     # reference default 8x8
+    assert games.identify(mod) is None
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present (GPU box)")
+@pytest.mark.parametrize("rel,name", [("test_games/mttt.py", "mttt"), ("test_games/four_to_one.py", "four_to_one")])
+def test_reference_plugin_files_route_to_descriptors(rel, name):
+    """Unmodified reference plugins import our src.utils and match a descriptor."""
+    mod = load_plugin(os.path.join(REF, rel))
+    c = games.identify(mod)
+    assert c is not None and c.name == name

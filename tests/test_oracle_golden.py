@@ -1,0 +1,154 @@
+"""The oracle is pinned: C and Python restatements reproduce the golden fixtures.
+
+The fixtures (tests/golden/*.npz, roots.json) were generated from the REFERENCE's
+own plugin modules by tests/golden/make_golden.py; live.json records that the
+reference's live engine (src/new_process.py) agrees with them on every value.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import canonical
+from conftest import GOLDEN, golden, load_plugin
+
+F2O, TTT, TOOT, OTH, SUB = 1, 2, 3, 4, 5
+
+CASES = [
+    ("ttt", TTT, (), None),
+    ("othello_4x4", OTH, (4, 4), None),
+    ("toot_3x3", TOOT, (3, 3), None),
+    ("toot_4x3", TOOT, (4, 3), None),
+    ("four_to_one_four", F2O, (), 4),
+    ("four_to_one_six", F2O, (), 6),
+    ("four_to_one_one", F2O, (), 1),
+    ("four_to_one_zero", F2O, (), 0),
+]
+
+
+@pytest.mark.parametrize("name,game,params,root", CASES)
+def test_c_oracle_matches_golden(oracle, name, game, params, root):
+    keys, recs = golden(name)
+    k, r = oracle.solve(game, params, root)
+    assert np.array_equal(k, keys)
+    assert np.array_equal(r, recs)
+
+
+def test_golden_summary_counts():
+    # SURVEY Appendix C probe numbers
+    for name, (w, l, t) in {"ttt": (2836, 1574, 1068), "othello_4x4": (24481, 24069, 5539),
+                            "toot_4x3": (36057, 15393, 148677), "toot_3x3": (0, 0, 11097)}.items():
+        v = golden(name)[1] >> 14
+        assert ((v == 0).sum(), (v == 1).sum(), (v == 2).sum()) == (w, l, t)
+
+
+def test_reference_root_expectations():
+    roots = json.load(open(os.path.join(GOLDEN, "roots.json")))
+    agree = [k for k, v in roots.items() if "reference_test_expects" in v
+             and v["canonical"] == v["reference_test_expects"]]
+    # 8 of the reference's 9 game_tests agree with the canonical semantics; one_row's
+    # expectation (mttt_test.py:61-71, TIE in 3) is wrong under every reference path.
+    assert len(agree) == 8
+    assert roots["mttt/one_row"]["canonical"] == "WIN in 5 moves"
+    assert roots["othello_4x4"]["canonical"] == "LOSS in 12 moves"
+    assert roots["toot_4x3"]["canonical"] == "TIE in 12 moves"
+
+
+def test_live_reference_engine_agrees_on_values():
+    live = json.load(open(os.path.join(GOLDEN, "live.json")))
+    for case, v in live.items():
+        assert v["value_mismatches"] == 0, case
+        assert v["positions_live"] == v["positions_canonical"], case
+        # its remoteness is only ever one short
+        assert set(v["remoteness_deltas"]) <= {"-1"}, case
+
+
+def _key_mttt(pos):
+    return sum({"_": 0, "X": 1, "O": 2}[c] * 3 ** i for i, c in enumerate(pos))
+
+
+def test_python_canonical_on_our_mttt_plugin():
+    mod = load_plugin("test_games/mttt.py")
+    table, positions = canonical.solve(mod)
+    keys, recs = golden("ttt")
+    got = sorted((_key_mttt(positions[k]), (v << 14) | r) for k, (v, r) in table.items())
+    assert [g[0] for g in got] == keys.tolist()
+    assert [g[1] for g in got] == recs.tolist()
+
+
+def test_python_canonical_on_our_ttt_numpy_plugin():
+    mod = load_plugin("test_games/tic_tac_toe_np.py")
+    table, positions = canonical.solve(mod)
+    keys, recs = golden("ttt_np")
+    got = sorted((sum(int(positions[k][x][y]) * 3 ** (x + 3 * y) for x in range(3) for y in range(3)),
+                  (v << 14) | r) for k, (v, r) in table.items())
+    assert [g[0] for g in got] == keys.tolist()
+    assert [g[1] for g in got] == recs.tolist()
+
+
+@pytest.mark.parametrize("root,name", [("4", "four"), ("6", "six"), ("1", "one"), ("0", "zero")])
+def test_python_canonical_on_our_four_to_one_plugin(root, name):
+    mod = load_plugin("test_games/four_to_one.py")
+    table, positions = canonical.solve(mod, root)
+    keys, recs = golden("four_to_one_" + name)
+    got = sorted((int(positions[k]) & (2 ** 64 - 1), (v << 14) | r) for k, (v, r) in table.items())
+    assert [g[0] for g in got] == keys.tolist()
+    assert [g[1] for g in got] == recs.tolist()
+
+
+def _bits_key(nkeep):
+    def k(pos):
+        raw = pos.encode("ISO-8859-1")
+        return int.from_bytes(raw, "big") >> (8 * len(raw) - nkeep)
+    return k
+
+
+@pytest.mark.parametrize("plugin,dims,name,nkeep", [
+    ("test_games/othello_bit_new.py", (4, 4), "othello_4x4", 48),
+    ("test_games/toot_and_otto_bitstring.py", (3, 3), "toot_3x3", 34),
+])
+def test_python_canonical_on_our_bitboard_plugins(plugin, dims, name, nkeep):
+    mod = load_plugin(plugin, length=dims[0], height=dims[1])
+    table, positions = canonical.solve(mod)
+    keys, recs = golden(name)
+    kf = _bits_key(nkeep)
+    got = sorted((kf(positions[k]), (v << 14) | r) for k, (v, r) in table.items())
+    assert [g[0] for g in got] == keys.tolist()
+    assert [g[1] for g in got] == recs.tolist()
+
+
+def test_subtract_oracle_closed_form_and_f2o(oracle):
+    # values: LOSS iff xor_i (h_i mod 3) == 0; one heap == Four-To-One (golden) for piles >= 0
+    rec = oracle.subtract_dense(4)
+    keys = np.arange(1 << 16, dtype=np.uint64)
+    g = np.zeros(len(keys), dtype=np.int64)
+    for i in range(4):
+        g ^= ((keys >> np.uint64(4 * i)) & np.uint64(15)).astype(np.int64) % 3
+    assert np.array_equal(rec >> 14, np.where(g == 0, 1, 0))
+    one = oracle.subtract_dense(1)
+    fk, fr = golden("four_to_one_six")
+    for k, r in zip(fk.tolist(), fr.tolist()):
+        if k < 16:
+            assert one[k] == r
+
+
+def test_subtract_dense_equals_generic_oracle(oracle):
+    dense = oracle.subtract_dense(3)
+    k, r = oracle.solve(SUB, (3,))
+    assert np.array_equal(k, np.arange(4096, dtype=np.uint64)) and np.array_equal(r, dense)
+
+
+def test_subtract_plugin_canonical(oracle):
+    mod = load_plugin("test_games/subtraction.py", HEAPS=2)
+    table, positions = canonical.solve(mod)
+    k, r = oracle.solve(SUB, (2,))
+    got = sorted((positions[key], (v << 14) | rr) for key, (v, rr) in table.items())
+    assert [g[0] for g in got] == k.tolist() and [g[1] for g in got] == r.tolist()
+
+
+def test_toot_4x4_oracle_totals(oracle):
+    # 4x4 = 3,468,773 positions
+    k, r = oracle.solve(TOOT, (4, 4))
+    assert len(k) == 3468773
+    assert (r != 0xFFFF).all()
