@@ -174,6 +174,14 @@ static tier_kernel_t pick_kernel(int low, int high) {
     return nullptr;
 }
 
+bool sub_kernel_exists(int low, int high) { return pick_kernel(low, high) != nullptr; }
+
+void launch_sub_tier(int low, int high, uint32_t nblocks, uint16_t *table, const uint32_t *list,
+                     const uint16_t *zero, hipStream_t s) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(pick_kernel(low, high), dim3(nblocks), dim3(256), 0, s, table, list, nblocks, zero);
+}
+
 // ---------------------------------------------------------------------------
 __global__ void sub_digest_kernel(const uint16_t *__restrict__ table, uint64_t slots, int heaps,
                                   uint64_t root, unsigned long long *acc) {

@@ -55,6 +55,8 @@ static void free_engines(Ctx *c) {
     dense_sub_free(c);
     small_dense_free(c);
     sparse_free(c);
+    dist_sub_free(c);
+    dist_sparse_free(c);
 }
 
 }  // namespace gm
@@ -146,6 +148,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         return GM_OK;
     case GM_OPT_GRAPH: c->use_graph = v != 0; return GM_OK;
     case GM_OPT_TIMING: c->timing = v != 0; return GM_OK;
+    case GM_OPT_VIRTUAL_RANKS:
+        if (v < 1 || v > 64) { set_error("virtual ranks must be 1..64"); return GM_E_ARG; }
+        c->virtual_ranks = (int)v;
+        return GM_OK;
     }
     set_error("unknown option %d", opt);
     return GM_E_ARG;
@@ -233,15 +239,22 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     c->stats.world = c->world;
     c->root = root;
     int eng = engine_for(c);
-    if (c->world > 1) {
-        set_error("multi-GPU solve is not available for this game/engine yet");
-        return GM_E_STATE;
+    bool sharded = c->world > 1 || c->virtual_ranks > 1;
+    if (sharded && c->world > 1 && c->virtual_ranks > 1) {
+        set_error("virtual ranks and a multi-process communicator are exclusive");
+        return GM_E_ARG;
     }
+    if (sharded) eng = (eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT) ? GM_ENGINE_DIST_DENSE
+                                                                              : GM_ENGINE_DIST_SPARSE;
     int rc;
-    if (eng == GM_ENGINE_DENSE)
+    switch (eng) {
+    case GM_ENGINE_DENSE:
         rc = c->game == GM_GAME_SUBTRACT ? dense_sub_solve(c, root) : small_dense_solve(c, root);
-    else
-        rc = sparse_solve(c, root);
+        break;
+    case GM_ENGINE_DIST_DENSE: rc = dist_sub_solve(c, root); break;
+    case GM_ENGINE_DIST_SPARSE: rc = dist_sparse_solve(c, root); break;
+    default: rc = sparse_solve(c, root);
+    }
     if (rc != GM_OK) return rc;
     c->engine = eng;
     c->stats.engine = eng;
@@ -265,6 +278,8 @@ int gm_export(gm_ctx *h, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t 
     if (c->engine == GM_ENGINE_DENSE)
         return c->game == GM_GAME_SUBTRACT ? dense_sub_export(c, keys, recs, cap, n)
                                            : small_dense_export(c, keys, recs, cap, n);
+    if (c->engine == GM_ENGINE_DIST_DENSE) return dist_sub_export(c, keys, recs, cap, n);
+    if (c->engine == GM_ENGINE_DIST_SPARSE) return dist_sparse_export(c, keys, recs, cap, n);
     return sparse_export(c, keys, recs, cap, n);
 }
 
@@ -275,6 +290,8 @@ int gm_query(gm_ctx *h, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     GM_HIP(hipSetDevice(c->device));
     if (c->engine == GM_ENGINE_DENSE)
         return c->game == GM_GAME_SUBTRACT ? dense_sub_query(c, keys, recs, n) : small_dense_query(c, keys, recs, n);
+    if (c->engine == GM_ENGINE_DIST_DENSE) return dist_sub_query(c, keys, recs, n);
+    if (c->engine == GM_ENGINE_DIST_SPARSE) return dist_sparse_query(c, keys, recs, n);
     return sparse_query(c, keys, recs, n);
 }
 
@@ -285,6 +302,8 @@ int gm_digest(gm_ctx *h, uint64_t *digest, uint64_t *n) {
     GM_HIP(hipSetDevice(c->device));
     if (c->engine == GM_ENGINE_DENSE)
         return c->game == GM_GAME_SUBTRACT ? dense_sub_digest(c, digest, n) : small_dense_digest(c, digest, n);
+    if (c->engine == GM_ENGINE_DIST_DENSE) return dist_sub_digest(c, digest, n);
+    if (c->engine == GM_ENGINE_DIST_SPARSE) return dist_sparse_digest(c, digest, n);
     return sparse_digest(c, digest, n);
 }
 
@@ -330,6 +349,7 @@ void gm_close(gm_ctx *h) {
     free_engines(c);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
+    if (c->comm_stream) hipStreamDestroy(c->comm_stream);
     delete h;
 }
 

@@ -55,6 +55,8 @@ int dev_error_to_gm(uint32_t flags);
 struct DenseSub;
 struct SmallDense;
 struct Sparse;
+struct DistSub;
+struct DistSparse;
 
 struct Ctx {
     int game = 0;
@@ -77,6 +79,8 @@ struct Ctx {
     // multi-GPU
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
+    int virtual_ranks = 1;   // >1: run that many ranks inside this context (loopback transport)
+    hipStream_t comm_stream = nullptr;
 
     // results
     bool solved = false;
@@ -94,6 +98,8 @@ struct Ctx {
     DenseSub *dsub = nullptr;
     SmallDense *sd = nullptr;
     Sparse *sp = nullptr;
+    DistSub *dist_sub = nullptr;
+    DistSparse *dist_sp = nullptr;
 };
 
 // engines (each returns GM_OK or a GM_E_* code)
@@ -103,6 +109,24 @@ int dense_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
 int dense_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n);
 void dense_sub_free(Ctx *c);
 int dense_sub_table(Ctx *c, void **p, uint64_t *bytes);
+
+// the dense tier kernel, shared with the partitioned (multi-GPU) driver
+bool sub_kernel_exists(int low, int high);
+void launch_sub_tier(int low, int high, uint32_t nblocks, uint16_t *table, const uint32_t *list,
+                     const uint16_t *zero, hipStream_t s);
+
+// partitioned dense solve: `world` ranks, real (RCCL, one per process) or virtual (loopback)
+int dist_sub_solve(Ctx *c, uint64_t root);
+int dist_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int dist_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int dist_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n);
+void dist_sub_free(Ctx *c);
+
+int dist_sparse_solve(Ctx *c, uint64_t root);
+int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int dist_sparse_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int dist_sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n);
+void dist_sparse_free(Ctx *c);
 
 int small_dense_solve(Ctx *c, uint64_t root);
 int small_dense_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);

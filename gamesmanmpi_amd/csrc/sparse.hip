@@ -14,25 +14,9 @@
 //       u16 max over preference scores, parent score (gm_common.hpp)
 // The reference expands a position once per path that reaches it (tree
 // search); here each distinct position is expanded once.
-#include "gm_internal.hpp"
-
-#include <algorithm>
+#include "sparse_common.hpp"
 
 namespace gm {
-
-struct Table {
-    uint64_t *keys = nullptr;
-    uint16_t *score = nullptr;
-    uint64_t cap = 0;      // power of two (0 = not allocated)
-    uint64_t count = 0;    // distinct keys held (host mirror)
-};
-
-struct TableRef {
-    uint64_t *keys;
-    uint16_t *score;
-    uint64_t mask;
-    unsigned long long *count;
-};
 
 template <int S>
 struct NextTables {
@@ -48,42 +32,6 @@ struct Sparse {
     int64_t t_root = 0;
     int max_skip = 1;
 };
-
-// ----------------------------------------------------------------- device helpers
-__device__ __forceinline__ bool table_insert(const TableRef &t, uint64_t key, uint32_t *err) {
-    uint64_t h = mix64(key) & t.mask;
-    for (uint64_t probe = 0; probe <= t.mask; probe++) {
-        uint64_t cur = t.keys[h];
-        if (cur == key) return false;
-        if (cur == EMPTY_KEY) {
-            unsigned long long prev = atomicCAS((unsigned long long *)&t.keys[h],
-                                                (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-            if (prev == EMPTY_KEY) return true;
-            if (prev == key) return false;
-        }
-        h = (h + 1) & t.mask;
-    }
-    atomicOr(err, DEV_ERR_TABLE_FULL);
-    return false;
-}
-
-__device__ __forceinline__ int64_t table_find(const TableRef &t, uint64_t key) {
-    if (!t.keys) return -1;
-    uint64_t h = mix64(key) & t.mask;
-    for (uint64_t probe = 0; probe <= t.mask; probe++) {
-        uint64_t cur = t.keys[h];
-        if (cur == key) return (int64_t)h;
-        if (cur == EMPTY_KEY) return -1;
-        h = (h + 1) & t.mask;
-    }
-    return -1;
-}
-
-// wave-level sum then one atomic per wave
-__device__ __forceinline__ void wave_add(unsigned long long *dst, uint64_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, (unsigned long long)v);
-}
 
 // ----------------------------------------------------------------- kernels
 template <class D>
@@ -180,55 +128,8 @@ __global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restr
     }
 }
 
-__global__ void rehash_kernel(const uint64_t *__restrict__ okeys, const uint16_t *__restrict__ oscore,
-                              uint64_t ocap, TableRef dst, uint32_t *err) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ocap;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t k = okeys[i];
-        if (k == EMPTY_KEY) continue;
-        uint64_t h = mix64(k) & dst.mask;
-        bool placed = false;
-        for (uint64_t probe = 0; probe <= dst.mask; probe++) {
-            unsigned long long prev = atomicCAS((unsigned long long *)&dst.keys[h],
-                                                (unsigned long long)EMPTY_KEY, (unsigned long long)k);
-            if (prev == EMPTY_KEY) { dst.score[h] = oscore[i]; placed = true; break; }
-            h = (h + 1) & dst.mask;
-        }
-        if (!placed) atomicOr(err, DEV_ERR_TABLE_FULL);
-    }
-}
-
-__global__ void fill_empty_kernel(uint64_t *keys, uint64_t n) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        keys[i] = EMPTY_KEY;
-}
-
 __global__ void insert_one_kernel(TableRef t, uint64_t key, uint32_t *err) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && table_insert(t, key, err)) atomicAdd(t.count, 1ull);
-}
-
-__global__ void digest_kernel(const uint64_t *__restrict__ keys, const uint16_t *__restrict__ score,
-                              uint64_t cap, unsigned long long *acc) {
-    uint64_t sum = 0;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t k = keys[i];
-        if (k != EMPTY_KEY) sum += digest_term(k, record_of_score(score[i]));
-    }
-    wave_add(acc, sum);
-}
-
-__global__ void gather_kernel(const uint64_t *__restrict__ keys, const uint16_t *__restrict__ score,
-                              uint64_t cap, uint64_t *okeys, uint16_t *orec, unsigned long long *cursor) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t k = keys[i];
-        if (k == EMPTY_KEY) continue;
-        unsigned long long at = atomicAdd(cursor, 1ull);
-        okeys[at] = k;
-        orec[at] = record_of_score(score[i]);
-    }
 }
 
 template <class D>
@@ -247,17 +148,6 @@ __global__ void query_kernel(D d, int64_t t_root, const TableRef *tabs, int ntab
 }
 
 // ----------------------------------------------------------------- host side
-static unsigned grid_for(uint64_t n) {
-    uint64_t g = (n + 255) / 256;
-    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(g, 8192));
-}
-
-static uint64_t pow2_at_least(uint64_t n) {
-    uint64_t c = 1024;
-    while (c < n) c <<= 1;
-    return c;
-}
-
 static int ensure_counts(Sparse *sp, size_t n) {
     if (n <= sp->counts_cap) return GM_OK;
     uint64_t cap = std::max<uint64_t>(64, pow2_at_least(n));
@@ -283,33 +173,8 @@ static TableRef ref_of(Sparse *sp, size_t t) {
     return r;
 }
 
-static int alloc_table(Ctx *c, Table &T, uint64_t cap) {
-    T.cap = cap;
-    if (hipMalloc(&T.keys, cap * 8) != hipSuccess || hipMalloc(&T.score, cap * 2) != hipSuccess) {
-        set_error("out of device memory for a %llu-slot tier table", (unsigned long long)cap);
-        return GM_E_NOMEM;
-    }
-    hipLaunchKernelGGL(fill_empty_kernel, dim3(grid_for(cap)), dim3(256), 0, c->stream, T.keys, cap);
-    GM_HIP(hipMemsetAsync(T.score, 0, cap * 2, c->stream));
-    return GM_OK;
-}
-
-// Re-home tier t into a table of `cap` slots (grow, or shrink to load <= 1/2).
-static int resize_table(Ctx *c, Sparse *sp, size_t t, uint64_t cap) {
-    Table &T = sp->tiers[t];
-    Table N;
-    GM_TRY(alloc_table(c, N, cap));
-    if (T.cap) {
-        TableRef dst{N.keys, N.score, cap - 1, sp->d_counts + t};
-        hipLaunchKernelGGL(rehash_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.keys, T.score,
-                           T.cap, dst, sp->d_err);
-        GM_HIP(hipStreamSynchronize(c->stream));
-        hipFree(T.keys);
-        hipFree(T.score);
-    }
-    N.count = T.count;
-    T = N;
-    return GM_OK;
+static int resize_tier(Ctx *c, Sparse *sp, size_t t, uint64_t cap) {
+    return resize_table(c->stream, sp->tiers[t], cap, sp->d_err);
 }
 
 static int read_err(Ctx *c, Sparse *sp) {
@@ -333,7 +198,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     double t0 = now_ms();
 
     sp->tiers.resize(1);
-    GM_TRY(alloc_table(c, sp->tiers[0], 1024));
+    GM_TRY(alloc_table(c->stream, sp->tiers[0], 1024));
     hipLaunchKernelGGL(insert_one_kernel, dim3(1), dim3(64), 0, c->stream, ref_of(sp, 0), root, sp->d_err);
     sp->tiers[0].count = 1;
 
@@ -343,7 +208,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         Table &T = sp->tiers[t];
         // final now: shrink to load <= 1/2 (improves retro probing and memory)
         uint64_t want = pow2_at_least(2 * T.count);
-        if (T.cap > 2 * want) GM_TRY(resize_table(c, sp, t, want));
+        if (T.cap > 2 * want) GM_TRY(resize_tier(c, sp, t, want));
         GM_HIP(hipMemsetAsync(sp->d_scratch, 0, S * sizeof(unsigned long long), c->stream));
         hipLaunchKernelGGL(count_edges_kernel<D>, dim3(grid_for(sp->tiers[t].cap)), dim3(256), 0, c->stream, d,
                            sp->tiers[t].keys, sp->tiers[t].cap, sp->d_scratch, sp->d_err);
@@ -357,7 +222,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         for (int s = 0; s < S; s++) {
             size_t u = t + 1 + s;
             uint64_t need = pow2_at_least((sp->tiers[u].count + edges[s]) * 5 / 4 + 1);
-            if (edges[s] && sp->tiers[u].cap < need) GM_TRY(resize_table(c, sp, u, need));
+            if (edges[s] && sp->tiers[u].cap < need) GM_TRY(resize_tier(c, sp, u, need));
         }
         NextTables<S> nx;
         for (int s = 0; s < S; s++) nx.t[s] = ref_of(sp, t + 1 + s);
@@ -522,10 +387,7 @@ int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
 void sparse_free(Ctx *c) {
     Sparse *sp = c->sp;
     if (!sp) return;
-    for (auto &T : sp->tiers) {
-        if (T.keys) hipFree(T.keys);
-        if (T.score) hipFree(T.score);
-    }
+    for (auto &T : sp->tiers) free_table(T);
     if (sp->d_counts) hipFree(sp->d_counts);
     if (sp->d_scratch) hipFree(sp->d_scratch);
     if (sp->d_err) hipFree(sp->d_err);

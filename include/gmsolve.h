@@ -64,14 +64,19 @@ enum {
 enum {
     GM_ENGINE_AUTO = 0,     /* dense for SUBTRACT / TTT, sparse otherwise */
     GM_ENGINE_DENSE = 1,
-    GM_ENGINE_SPARSE = 2
+    GM_ENGINE_SPARSE = 2,
+    GM_ENGINE_DIST_DENSE = 3,   /* reported in gm_stats_t.engine: sharded dense path */
+    GM_ENGINE_DIST_SPARSE = 4   /* reported in gm_stats_t.engine: sharded sparse path */
 };
 
 enum {
     GM_OPT_ENGINE = 1,      /* GM_ENGINE_* */
     GM_OPT_SUB_LOW = 2,     /* SUBTRACT dense path: heaps solved per workgroup in LDS (1..4) */
     GM_OPT_GRAPH = 3,       /* SUBTRACT dense path: replay the tier launches as a hipGraph (0/1) */
-    GM_OPT_TIMING = 4       /* record HIP events around every launch of the dominant kernel (0/1) */
+    GM_OPT_TIMING = 4,      /* record HIP events around every launch of the dominant kernel (0/1) */
+    GM_OPT_VIRTUAL_RANKS = 5 /* >1: run the sharded algorithm with that many ranks inside this one
+                                context on one GPU (loopback transport instead of RCCL); for testing
+                                the multi-GPU partition on a single device */
 };
 
 /* Buffer roles for gm_adopt_buffer. */
