@@ -4,15 +4,17 @@
 Workload (BASELINE.json config 5): 8 heaps x 4 bits, root 0xFFFFFFFF,
 all 2^32 positions reachable.  One step = one complete strong solve (value and
 remoteness of every position) by libgmsolve.so's dense tiered kernel; the table
-lives in HBM (a torch-allocated int16 tensor adopted by the library) before the
+lives in HBM (a torch-allocated uint8 tensor of 1-byte codes adopted by the
+library) before the
 timed region starts.  Synthetic by construction: the game is the input.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0 (driver contract), including
-  roofline      the tier kernel's algorithmic bytes per launch (31 B per position,
-                SURVEY §8d, x positions per launch) / its average launch time, from
+  roofline      the tier kernel's algorithmic bytes per launch (SURVEY §8d edge
+                model with 1-byte records: 1 + 14.5 = 15.5 B per position, x
+                positions per launch) / its average launch time, from
                 HIP events recorded around every launch on the launch stream;
                 traffic = rocprofv3 PMC bytes per launch from profiles/ when present;
   cpu_baseline  the C oracle's dense solver (oracle/gm_oracle.c, 1 thread) on a
@@ -29,7 +31,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-ALGO_BYTES_PER_POSITION = 31.0  # SURVEY §8d edge-traffic model at 8 heaps (2 * (1 + 14.5))
+ALGO_BYTES_PER_POSITION = 15.5  # SURVEY §8d edge model at 8 heaps, 1-B records: 1 write + 14.5 child reads
 METRIC = "positions solved/sec (node) at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
 
 
@@ -71,6 +73,8 @@ def main():
     ap.add_argument("--heaps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-heaps", type=int, default=7)
+    ap.add_argument("--virtual-ranks", type=int, default=1,
+                    help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -96,15 +100,18 @@ def main():
             uid[0] = buf.raw
         dist.broadcast_object_list(uid, src=0)
         ctx.set_comm(rank, world, uid[0])
-    slots_local = (1 << (4 * args.heaps)) // world if world > 1 else 1 << (4 * args.heaps)
-    table = torch.empty(slots_local, dtype=torch.int16, device="cuda")
-    ctx.adopt_dense_table(table.data_ptr(), table.numel() * 2)
+    # Every rank keeps the table in the global key layout (it writes only its own
+    # blocks and the halo it receives), so each GPU holds 1 B x 16^heaps.
+    table = torch.empty(1 << (4 * args.heaps), dtype=torch.uint8, device="cuda")
+    ctx.adopt_dense_table(table.data_ptr(), table.numel())
     # A dedicated (non-null) stream: the tier launches are replayed as a hipGraph,
     # which cannot be captured on the legacy default stream.
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_option(_lib.OPT_TIMING, 1)
+    if args.virtual_ranks > 1:
+        ctx.set_option(_lib.OPT_VIRTUAL_RANKS, args.virtual_ranks)
     root = ctx.initial()
 
     def barrier():
@@ -141,7 +148,8 @@ def main():
     value = positions * args.steps / elapsed
     st = ctx.stats()
     launches_per_solve = max(1, launches // max(1, args.steps))
-    algo_per_launch = ALGO_BYTES_PER_POSITION * positions / world / launches_per_solve
+    # bytes this rank's tier launches move, per the SURVEY §8d model
+    algo_per_launch = st["algo_bytes"] / launches_per_solve
     avg_launch_s = (kernel_ms / 1e3) / max(1, launches)
     achieved = algo_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
     out = {
@@ -155,18 +163,23 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u16",
+        "dtype": "u8",
         "data": "synthetic (the game itself: every position of the 2^32-state subtraction game)",
         "config": {"workload": "subtraction game, %d heaps x 4 bits, root %#x (config 5)" % (args.heaps, root),
                    "positions": positions, "parallelism": "1 GPU" if world == 1 else "block-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": pmc_traffic(args.heaps, launches_per_solve),
-                     "kernel": "sub_tier_kernel<3,%d>" % (args.heaps - 3),
+                     "kernel": "sub_tier_kernel_x4<%d>" % (args.heaps - 3),
                      "launches_per_solve": launches_per_solve,
                      "avg_launch_us": avg_launch_s * 1e6,
                      "kernel_ms_per_solve": kernel_ms / max(1, args.steps),
-                     "algo_bytes_per_position": ALGO_BYTES_PER_POSITION},
+                     "algo_bytes_per_position": ALGO_BYTES_PER_POSITION,
+                     "timing": ("HIP events bracketing each solve's tier-launch graph replay on the launch "
+                                "stream; avg launch = span / launches (includes in-graph gaps)"
+                                if world == 1 else
+                                "HIP events around rank 0's whole sharded solve (includes halo waits)")},
+        "exchanged_bytes_per_step_rank0": st["exchanged_bytes"],
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -2,28 +2,33 @@
 //
 // Replaces, for config 5, the reference's per-edge job loop (Process.lookup /
 // distribute / resolve, src/new_process.py:102-265) and its shelve tables
-// (src/cache_dict.py): every one of the 16^heaps positions gets a 2-byte slot
-// in one HBM array indexed by the key itself.
+// (src/cache_dict.py): every one of the 16^heaps positions gets a 1-byte slot
+// in one HBM array indexed by the key itself (the order-preserving codes of
+// gm_common.hpp: WIN R -> R+1, LOSS R -> 255-R; exported as u16 records).
 //
 // Decomposition.  A key is `heaps` nibbles.  The low LOW nibbles index a
-// position inside a *block* of 16^LOW slots (8 KiB at LOW = 3) that one
-// workgroup solves in LDS; the high HIGH = heaps - LOW nibbles name the block.
-// A move lowers exactly one nibble, so a position's children are either in its
-// own block (low move) or at the same offset of a block whose high part is
-// 1 or 2 smaller in one nibble (high move).  Blocks are therefore processed in
-// tiers of their high-nibble sum, one launch per tier:
+// position inside a *block* of 16^LOW slots (4 KiB at LOW = 3) that a workgroup
+// solves in LDS; the high HIGH = heaps - LOW nibbles name the block.  A move
+// lowers exactly one nibble, so a position's children are either in its own
+// block (low move) or at the same offset of a block whose high part is 1 or 2
+// smaller in one nibble (high move).  Blocks are processed in tiers of their
+// high-nibble sum, one launch per tier:
 //
 //   pass A  fold the high children: for every valid child block, stream its
-//           16^LOW scores with 16-B loads and keep the running u16 max
-//           (v_pk_max_u16) -- fully coalesced whole-block reads;
-//   pass B  walk the block's own low tiers (low-nibble sum 0..15*LOW) in LDS:
-//           each position folds its <= 2*LOW in-block children and turns the
-//           best score into its own (gm_common.hpp), one barrier per low tier;
+//           codes with 16-B buffer loads and keep the running max -- fully
+//           coalesced whole-block reads, one scalar buffer descriptor per child;
+//   pass B  walk the block's low tiers (low-nibble sum 0..15*LOW) in LDS: each
+//           position folds its <= 2*LOW in-block children and turns the best
+//           code into its own (parent_code), one barrier per low tier;
 //   pass C  write the block back with 16-B stores.
 //
-// HBM traffic per position: 2 B written + 2 B per high child (1.8125 per high
-// nibble on average); the SURVEY's algorithmic figure (31 B/position) counts
-// every child edge as a 2-B read.
+// The default kernel (sub_tier_kernel_x4) solves FOUR blocks per workgroup with
+// their LDS images interleaved (slot 4L+k), so every address, branch and LDS
+// access of pass B serves four positions and the arithmetic is packed u16.
+//
+// HBM bytes per position: 1 written + 1 per high child (1.8125 per high nibble
+// on average).  The SURVEY §8d edge model charges 1 B per record and per child
+// edge: 1 + 14.5 = 15.5 B per position at 8 heaps (31 B with u16 records).
 #include "gm_internal.hpp"
 
 #include <algorithm>
@@ -32,86 +37,133 @@
 namespace gm {
 
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 struct DenseSub {
-    int heaps = 0, low = 0, high = 0;
-    uint16_t *table = nullptr;          // 16^heaps scores
+    int heaps = 0, low = 0, high = 0, nt = 128;   // nt 0 = interleaved x4 kernel
+    int want_threads = 0, want_x4 = 0;
+    uint8_t *table = nullptr;           // 16^heaps codes
     bool owned = false;
     uint64_t slots = 0;
-    uint16_t *zero = nullptr;           // one block of zeros (padding source)
+    uint8_t *zero = nullptr;            // one block of zeros (padding source)
     uint32_t *d_blocks = nullptr;       // high parts sorted by (tier, value)
     std::vector<uint32_t> tier_off;     // block offsets per high tier
     uint64_t *d_acc = nullptr;          // digest / counters
     hipGraphExec_t graph = nullptr;
     hipStream_t graph_stream = nullptr;
-    std::vector<hipEvent_t> ev;         // per-launch timing events
+    std::vector<hipEvent_t> ev;         // timing events
 };
 
-// ---------------------------------------------------------------------------
-template <int LOW, int HIGH>
-__global__ __launch_bounds__(256) void sub_tier_kernel(uint16_t *__restrict__ table,
-                                                       const uint32_t *__restrict__ blocks,
-                                                       uint32_t nblk,
-                                                       const uint16_t *__restrict__ zero) {
-    constexpr int NPOS = 1 << (4 * LOW);
-    constexpr int NCH = NPOS >= 8 ? NPOS / 8 : 1;      // 16-B chunks per block
-    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;   // child blocks, padded
-    __shared__ __attribute__((aligned(16))) uint16_t s[NPOS < 8 ? 8 : NPOS];
-    const int tid = threadIdx.x;
+// one scalar buffer descriptor per block (num_records = block bytes; 0 drops stores)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t block_rsrc(const uint8_t *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, bytes, 0x00020000);
+}
 
-    // XCD-aware order: blocks b and b+8 share an XCD (MI355X_MICROARCH.md
-    // "Workgroup dispatch"), so give each XCD a contiguous run of the tier list;
-    // neighbouring high parts share child blocks in that XCD's L2.
-    const uint32_t b = blockIdx.x, q = nblk >> 3, r = nblk & 7u, x = b & 7u, i = b >> 3;
-    const uint32_t logical = x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
-    const uint32_t hp = blocks[logical];
-    uint16_t *const out = table + ((uint64_t)hp << (4 * LOW));
+__device__ __forceinline__ u32x4v load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
 
-    // ---- pass A: high children -------------------------------------------
-    // Slot k = 2j + s is the child "take s+1 from high nibble j".  A missing
-    // child (nibble too small) re-reads the first existing child block (max is
-    // idempotent and the repeat is an L2 hit) or, with no child at all, the
-    // zero block.  Every index is a compile-time constant after unrolling, so
-    // the pointers stay in (scalar) registers.
-    const uint16_t *src[NMAX];
-    {
-        const uint16_t *first = zero;
+// Byte codes have no packed max on CDNA4, so 16 codes (one u32x4 load) are
+// split into u16 pairs -- even bytes (positions 4j, 4j+2) with one v_and, odd
+// bytes (4j+1, 4j+3) with one v_perm -- and folded with v_pk_max_u16.
+struct Fold16 {
+    uint32_t e[4], o[4];
+};
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t even_bytes(uint32_t x) { return x & 0x00FF00FFu; }
+__device__ __forceinline__ uint32_t odd_bytes(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); }
+template <int N>
+__device__ __forceinline__ Fold16 fold16(const u32x4v (&v)[N]) {
+    Fold16 f;
 #pragma unroll
-        for (int j = HIGH - 1; j >= 0; j--) {
-            const uint32_t h = (hp >> (4 * j)) & 15u;
-            if (h >= 1) first = table + ((uint64_t)(hp - (1u << (4 * j))) << (4 * LOW));
-        }
+    for (int j = 0; j < 4; j++) {
+        f.e[j] = even_bytes(v[0][j]);
+        f.o[j] = odd_bytes(v[0][j]);
 #pragma unroll
-        for (int j = 0; j < HIGH; j++) {
-            const uint32_t h = (hp >> (4 * j)) & 15u;
-            src[2 * j] = h >= 1 ? table + ((uint64_t)(hp - (1u << (4 * j))) << (4 * LOW)) : first;
-            src[2 * j + 1] = h >= 2 ? table + ((uint64_t)(hp - (2u << (4 * j))) << (4 * LOW)) : first;
+        for (int m = 1; m < N; m++) {
+            f.e[j] = pk_max(f.e[j], even_bytes(v[m][j]));
+            f.o[j] = pk_max(f.o[j], odd_bytes(v[m][j]));
         }
-        if constexpr (HIGH == 0) src[0] = zero;
     }
-    if constexpr (NPOS >= 8) {
-        for (int c = tid; c < NCH; c += 256) {
-            u16x8 v[NMAX];
+    return f;
+}
+// four u16 codes (positions 4j..4j+3 as pairs (p0,p1), (p2,p3)) -> one dword of bytes
+__device__ __forceinline__ uint32_t pack_bytes(uint32_t p01, uint32_t p23) {
+    return __builtin_amdgcn_perm(p23, p01, 0x06040200u);
+}
+
+// pointers of the 2*HIGH child blocks of high part hp (slot 2j+s = "take s+1
+// from high nibble j"); a missing child re-reads the first existing one (max
+// is idempotent, the repeat is an L2 hit) or, with none, the zero block
+template <int LOW, int HIGH, int NMAX>
+__device__ __forceinline__ void child_blocks(const uint8_t *table, const uint8_t *zero, uint32_t hp, bool valid,
+                                             const uint8_t *(&src)[NMAX]) {
+    const uint8_t *first = zero;
 #pragma unroll
-            for (int k = 0; k < NMAX; k++) v[k] = *(const u16x8 *)(src[k] + 8 * c);
-            u16x8 acc = v[0];
+    for (int j = HIGH - 1; j >= 0; j--) {
+        const uint32_t h = (hp >> (4 * j)) & 15u;
+        if (valid && h >= 1) first = table + ((uint64_t)(hp - (1u << (4 * j))) << (4 * LOW));
+    }
 #pragma unroll
-            for (int k = 1; k < NMAX; k++) acc = __builtin_elementwise_max(acc, v[k]);
-            *(u16x8 *)(s + 8 * c) = acc;
-        }
-    } else {
-        if (tid < NPOS) {
-            uint16_t acc = 0;
+    for (int j = 0; j < HIGH; j++) {
+        const uint32_t h = (hp >> (4 * j)) & 15u;
+        src[2 * j] = (valid && h >= 1) ? table + ((uint64_t)(hp - (1u << (4 * j))) << (4 * LOW)) : first;
+        src[2 * j + 1] = (valid && h >= 2) ? table + ((uint64_t)(hp - (2u << (4 * j))) << (4 * LOW)) : first;
+    }
+    if constexpr (HIGH == 0) src[0] = zero;
+}
+
+__device__ __forceinline__ uint32_t xcd_order(uint32_t b, uint32_t n) {
+    // blocks b and b+8 share an XCD (MI355X_MICROARCH.md "Workgroup dispatch"):
+    // give each XCD a contiguous run of the tier list, whose neighbouring high
+    // parts share child blocks in that XCD's L2
+    const uint32_t q = n >> 3, r = n & 7u, x = b & 7u, i = b >> 3;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
+// ---------------------------------------------------------------------------
+// One block per workgroup of NT threads (any LOW).
+template <int LOW, int HIGH, int NT>
+__global__ __launch_bounds__(NT) void sub_tier_kernel(uint8_t *__restrict__ table,
+                                                      const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                      const uint8_t *__restrict__ zero) {
+    constexpr int NPOS = 1 << (4 * LOW);
+    constexpr int NCH = NPOS / 16;                      // 16-position chunks
+    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
+    __shared__ __attribute__((aligned(16))) uint16_t s[NPOS];
+    const int tid = threadIdx.x;
+    const uint32_t hp = blocks[xcd_order(blockIdx.x, nblk)];
+
+    const uint8_t *src[NMAX];
+    child_blocks<LOW, HIGH, NMAX>(table, zero, hp, true, src);
+    __amdgpu_buffer_rsrc_t rs[NMAX];
 #pragma unroll
-            for (int k = 0; k < NMAX; k++) acc = acc > src[k][tid] ? acc : src[k][tid];
-            s[tid] = acc;
-        }
+    for (int k = 0; k < NMAX; k++) rs[k] = block_rsrc(src[k], NPOS);
+    for (uint32_t c = tid; c < (uint32_t)NCH; c += NT) {
+        u32x4v v[NMAX];
+#pragma unroll
+        for (int k = 0; k < NMAX; k++) v[k] = load16(rs[k], 16u * c);
+        const Fold16 f = fold16(v);
+        u32x4v lo, hi;   // positions 16c..16c+7, 16c+8..16c+15 as u16 pairs
+        lo[0] = __builtin_amdgcn_perm(f.o[0], f.e[0], 0x05040100u);
+        lo[1] = __builtin_amdgcn_perm(f.o[0], f.e[0], 0x07060302u);
+        lo[2] = __builtin_amdgcn_perm(f.o[1], f.e[1], 0x05040100u);
+        lo[3] = __builtin_amdgcn_perm(f.o[1], f.e[1], 0x07060302u);
+        hi[0] = __builtin_amdgcn_perm(f.o[2], f.e[2], 0x05040100u);
+        hi[1] = __builtin_amdgcn_perm(f.o[2], f.e[2], 0x07060302u);
+        hi[2] = __builtin_amdgcn_perm(f.o[3], f.e[3], 0x05040100u);
+        hi[3] = __builtin_amdgcn_perm(f.o[3], f.e[3], 0x07060302u);
+        *(u32x4v *)(s + 16 * c) = lo;
+        *(u32x4v *)(s + 16 * c + 8) = hi;
     }
     __syncthreads();
 
-    // ---- pass B: low tiers in LDS -----------------------------------------
-    const int a0 = tid & 15, a1 = (tid >> 4) & 15;
-    auto solve_one = [&](int L) {
+    auto best_of = [&](int L) -> uint32_t {
         uint32_t best = s[L];
 #pragma unroll
         for (int j = 0; j < LOW; j++) {
@@ -119,71 +171,235 @@ __global__ __launch_bounds__(256) void sub_tier_kernel(uint16_t *__restrict__ ta
             if (h >= 1) best = max(best, (uint32_t)s[L - (1 << (4 * j))]);
             if (h >= 2) best = max(best, (uint32_t)s[L - (2 << (4 * j))]);
         }
-        s[L] = (hp == 0 && L == 0) ? (uint16_t)0xFFFF : parent_score(best);
+        return (hp == 0 && L == 0) ? 255u : parent_code(best);
     };
     if constexpr (LOW == 3) {
-        // thread = low two nibbles; the third nibble is fixed by the tier
-        const int s0 = a0 + a1;
-        for (int tau = 0; tau <= 45; tau++) {
-            const int c = tau - s0;
-            if (c >= 0 && c <= 15) solve_one(tid + 256 * c);
-            __syncthreads();
-        }
-    } else {
-        const int L = tid;
-        int sum = 0;
+        // (heap0, heap1) pairs spread over the threads; heap2 is fixed by the tier.
+        // A step's positions are independent: all reads before any write.
+        constexpr int PER = 256 / NT;
+        int sum[PER];
 #pragma unroll
-        for (int j = 0; j < LOW; j++) sum += (L >> (4 * j)) & 15;
+        for (int k = 0; k < PER; k++) {
+            const int p = tid + NT * k;
+            sum[k] = (p & 15) + (p >> 4);
+        }
+        for (int tau = 0; tau <= 45; tau++) {
+            uint32_t res[PER];
+#pragma unroll
+            for (int k = 0; k < PER; k++) {
+                const int c = tau - sum[k];
+                res[k] = (c >= 0 && c <= 15) ? best_of(tid + NT * k + 256 * c) : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < PER; k++) {
+                const int c = tau - sum[k];
+                if (c >= 0 && c <= 15) s[tid + NT * k + 256 * c] = (uint16_t)res[k];
+            }
+            __syncthreads();
+        }
+    } else {
         for (int tau = 0; tau <= 15 * LOW; tau++) {
-            if (L < NPOS && sum == tau) solve_one(L);
+            for (int L = tid; L < NPOS; L += NT) {
+                int sum = 0;
+#pragma unroll
+                for (int j = 0; j < LOW; j++) sum += (L >> (4 * j)) & 15;
+                if (sum == tau) s[L] = (uint16_t)best_of(L);
+            }
             __syncthreads();
         }
     }
 
-    // ---- pass C: write back -------------------------------------------------
-    if constexpr (NPOS >= 8) {
-        for (int c = tid; c < NCH; c += 256) *(u16x8 *)(out + 8 * c) = *(const u16x8 *)(s + 8 * c);
-    } else {
-        if (tid < NPOS) out[tid] = s[tid];
+    const __amdgpu_buffer_rsrc_t wr = block_rsrc(table + ((uint64_t)hp << (4 * LOW)), NPOS);
+    for (uint32_t c = tid; c < (uint32_t)NCH; c += NT) {
+        const u32x4v lo = *(const u32x4v *)(s + 16 * c), hi = *(const u32x4v *)(s + 16 * c + 8);
+        u32x4v o;
+        o[0] = pack_bytes(lo[0], lo[1]);
+        o[1] = pack_bytes(lo[2], lo[3]);
+        o[2] = pack_bytes(hi[0], hi[1]);
+        o[3] = pack_bytes(hi[2], hi[3]);
+        __builtin_amdgcn_raw_buffer_store_b128(o, wr, 16u * c, 0, 0);
     }
-}
-
-typedef void (*tier_kernel_t)(uint16_t *, const uint32_t *, uint32_t, const uint16_t *);
-
-template <int LOW>
-static tier_kernel_t pick_high(int high) {
-    switch (high) {
-    case 0: return sub_tier_kernel<LOW, 0>;
-    case 1: return sub_tier_kernel<LOW, 1>;
-    case 2: return sub_tier_kernel<LOW, 2>;
-    case 3: return sub_tier_kernel<LOW, 3>;
-    case 4: return sub_tier_kernel<LOW, 4>;
-    case 5: return sub_tier_kernel<LOW, 5>;
-    case 6: return LOW <= 2 ? sub_tier_kernel<LOW, 6> : nullptr;
-    case 7: return LOW <= 1 ? sub_tier_kernel<LOW, 7> : nullptr;
-    }
-    return nullptr;
-}
-
-static tier_kernel_t pick_kernel(int low, int high) {
-    switch (low) {
-    case 1: return pick_high<1>(high);
-    case 2: return pick_high<2>(high);
-    case 3: return pick_high<3>(high);
-    }
-    return nullptr;
-}
-
-bool sub_kernel_exists(int low, int high) { return pick_kernel(low, high) != nullptr; }
-
-void launch_sub_tier(int low, int high, uint32_t nblocks, uint16_t *table, const uint32_t *list,
-                     const uint16_t *zero, hipStream_t s) {
-    if (!nblocks) return;
-    hipLaunchKernelGGL(pick_kernel(low, high), dim3(nblocks), dim3(256), 0, s, table, list, nblocks, zero);
 }
 
 // ---------------------------------------------------------------------------
-__global__ void sub_digest_kernel(const uint16_t *__restrict__ table, uint64_t slots, int heaps,
+// Four blocks per workgroup (LOW = 3), LDS images interleaved: position L of the
+// group's k-th block is the u16 at 4L + k.  Pass B handles the four copies of a
+// position with one address, one validity test and one ds_read_b64 per child,
+// in packed u16 arithmetic.  Pass A folds each block's children separately and
+// transposes 4 x 8 codes at a time with v_perm_b32; pass C transposes back.
+__device__ __forceinline__ u16x4 parent_code_x4(u16x4 b) {
+    return ((u16x4)(uint16_t)255 - b) + ((b >> (uint16_t)7) << (uint16_t)1);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ table,
+                                                          const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                          const uint8_t *__restrict__ zero) {
+    constexpr int NPOS = 4096, NCH = 256, NT = 256, K = 4;
+    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
+    __shared__ __attribute__((aligned(16))) uint16_t s[NPOS * K];   // 32 KiB
+    const int tid = threadIdx.x;
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
+    uint32_t hp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = grp * K + k;
+        valid[k] = idx < nblk;
+        hp[k] = valid[k] ? blocks[idx] : 0u;
+    }
+
+    // ---- pass A -------------------------------------------------------------
+    // NCH == NT: one 16-position chunk per thread.  The blocks are folded one
+    // after the other (sched_barrier) so that only one block's descriptors and
+    // loads are live at a time: 2*HIGH loads of 16 B in flight per thread.
+    static_assert(NCH == NT, "one chunk per thread");
+    {
+        const uint32_t c = tid;
+        Fold16 f[K];   // f[k].e[j] = positions (4j, 4j+2), .o[j] = (4j+1, 4j+3) of chunk c, block k
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint8_t *src[NMAX];
+            child_blocks<3, HIGH, NMAX>(table, zero, hp[k], valid[k], src);
+            u32x4v v[NMAX];
+#pragma unroll
+            for (int m = 0; m < NMAX; m++) v[m] = load16(block_rsrc(src[m], NPOS), 16u * c);
+            f[k] = fold16(v);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // transpose to the interleaved image: position p -> 4 u16 (blocks 0..3)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            u32x4v o0, o1;
+            o0[0] = __builtin_amdgcn_perm(f[1].e[j], f[0].e[j], 0x05040100u);   // pos 4j,   blocks 0,1
+            o0[1] = __builtin_amdgcn_perm(f[3].e[j], f[2].e[j], 0x05040100u);   // pos 4j,   blocks 2,3
+            o0[2] = __builtin_amdgcn_perm(f[1].o[j], f[0].o[j], 0x05040100u);   // pos 4j+1
+            o0[3] = __builtin_amdgcn_perm(f[3].o[j], f[2].o[j], 0x05040100u);
+            o1[0] = __builtin_amdgcn_perm(f[1].e[j], f[0].e[j], 0x07060302u);   // pos 4j+2
+            o1[1] = __builtin_amdgcn_perm(f[3].e[j], f[2].e[j], 0x07060302u);
+            o1[2] = __builtin_amdgcn_perm(f[1].o[j], f[0].o[j], 0x07060302u);   // pos 4j+3
+            o1[3] = __builtin_amdgcn_perm(f[3].o[j], f[2].o[j], 0x07060302u);
+            *(u32x4v *)((char *)s + 128u * c + 32u * j) = o0;
+            *(u32x4v *)((char *)s + 128u * c + 32u * j + 16u) = o1;
+        }
+    }
+    __syncthreads();
+
+    // ---- pass B -------------------------------------------------------------
+    const int a0 = tid & 15, a1 = tid >> 4, s0 = a0 + a1;
+    auto S = [&](int L) -> u16x4 { return *(const u16x4 *)((const char *)s + 8 * L); };
+    const bool root_here = valid[0] && hp[0] == 0;   // sorted tier list: block 0 comes first
+    for (int tau = 0; tau <= 45; tau++) {
+        const int c = tau - s0;
+        if (c >= 0 && c <= 15) {
+            const int L = tid + 256 * c;
+            u16x4 best = S(L);
+            if (a0 >= 1) best = __builtin_elementwise_max(best, S(L - 1));
+            if (a0 >= 2) best = __builtin_elementwise_max(best, S(L - 2));
+            if (a1 >= 1) best = __builtin_elementwise_max(best, S(L - 16));
+            if (a1 >= 2) best = __builtin_elementwise_max(best, S(L - 32));
+            if (c >= 1) best = __builtin_elementwise_max(best, S(L - 256));
+            if (c >= 2) best = __builtin_elementwise_max(best, S(L - 512));
+            u16x4 res = parent_code_x4(best);
+            if (root_here && L == 0) res[0] = 255;   // all heaps empty: LOSS in 0
+            *(u16x4 *)((char *)s + 8 * L) = res;
+        }
+        __syncthreads();
+    }
+
+    // ---- pass C -------------------------------------------------------------
+    __amdgpu_buffer_rsrc_t wr[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) wr[k] = block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0);
+    {
+        const uint32_t c = tid;
+        u32x4v out[K];   // 16 codes of chunk c per block
+#pragma unroll
+        for (int j = 0; j < 4; j++) {   // positions 4j..4j+3: 8 B each (blocks 0,1 | 2,3)
+            const u32x4v q0 = *(const u32x4v *)((const char *)s + 128u * c + 32u * j);
+            const u32x4v q1 = *(const u32x4v *)((const char *)s + 128u * c + 32u * j + 16u);
+            // [p0.k, p1.k, p0.k+1, p1.k+1] and [p2.k, p3.k, p2.k+1, p3.k+1] for k = 0 (A) and 2 (B)
+            const uint32_t xa = __builtin_amdgcn_perm(q0[2], q0[0], 0x06020400u);
+            const uint32_t ya = __builtin_amdgcn_perm(q1[2], q1[0], 0x06020400u);
+            const uint32_t xb = __builtin_amdgcn_perm(q0[3], q0[1], 0x06020400u);
+            const uint32_t yb = __builtin_amdgcn_perm(q1[3], q1[1], 0x06020400u);
+            out[0][j] = __builtin_amdgcn_perm(ya, xa, 0x05040100u);
+            out[1][j] = __builtin_amdgcn_perm(ya, xa, 0x07060302u);
+            out[2][j] = __builtin_amdgcn_perm(yb, xb, 0x05040100u);
+            out[3][j] = __builtin_amdgcn_perm(yb, xb, 0x07060302u);
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++)   // num_records 0 drops the store of an unused slot
+            __builtin_amdgcn_raw_buffer_store_b128(out[k], wr[k], 16u * c, 0, 0);
+    }
+}
+
+typedef void (*tier_kernel_t)(uint8_t *, const uint32_t *, uint32_t, const uint8_t *);
+
+static tier_kernel_t pick_x4(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel_x4<0>;
+    case 1: return sub_tier_kernel_x4<1>;
+    case 2: return sub_tier_kernel_x4<2>;
+    case 3: return sub_tier_kernel_x4<3>;
+    case 4: return sub_tier_kernel_x4<4>;
+    case 5: return sub_tier_kernel_x4<5>;
+    }
+    return nullptr;
+}
+
+template <int LOW, int NT>
+static tier_kernel_t pick_high(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel<LOW, 0, NT>;
+    case 1: return sub_tier_kernel<LOW, 1, NT>;
+    case 2: return sub_tier_kernel<LOW, 2, NT>;
+    case 3: return sub_tier_kernel<LOW, 3, NT>;
+    case 4: return sub_tier_kernel<LOW, 4, NT>;
+    case 5: return sub_tier_kernel<LOW, 5, NT>;
+    case 6: if constexpr (LOW <= 2) return sub_tier_kernel<LOW, 6, NT>; else return nullptr;
+    case 7: if constexpr (LOW <= 1) return sub_tier_kernel<LOW, 7, NT>; else return nullptr;
+    }
+    return nullptr;
+}
+
+template <int NT>
+static tier_kernel_t pick_low(int low, int high) {
+    switch (low) {
+    case 1: return pick_high<1, NT>(high);
+    case 2: return pick_high<2, NT>(high);
+    case 3: return pick_high<3, NT>(high);
+    }
+    return nullptr;
+}
+
+static tier_kernel_t pick_kernel(int low, int high, int nt) {
+    switch (nt) {
+    case 64: return pick_low<64>(low, high);
+    case 128: return pick_low<128>(low, high);
+    case 256: return pick_low<256>(low, high);
+    }
+    return nullptr;
+}
+
+// nt == 0 selects the 4-block interleaved kernel (LOW = 3, 256 threads).
+bool sub_kernel_exists(int low, int high, int nt) {
+    return nt == 0 ? (low == 3 && pick_x4(high) != nullptr) : pick_kernel(low, high, nt) != nullptr;
+}
+
+void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table, const uint32_t *list,
+                     const uint8_t *zero, hipStream_t s) {
+    if (!nblocks) return;
+    if (nt == 0)
+        hipLaunchKernelGGL(pick_x4(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
+    else
+        hipLaunchKernelGGL(pick_kernel(low, high, nt), dim3(nblocks), dim3(nt), 0, s, table, list, nblocks, zero);
+}
+
+int sub_kernel_threads(const Ctx *c, int low) { return (low == 3 && c->sub_interleave == 4) ? 0 : c->sub_threads; }
+
+// ---------------------------------------------------------------------------
+__global__ void sub_digest_kernel(const uint8_t *__restrict__ table, uint64_t slots, int heaps,
                                   uint64_t root, unsigned long long *acc) {
     uint64_t sum = 0, cnt = 0;
     for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < slots;
@@ -191,7 +407,7 @@ __global__ void sub_digest_kernel(const uint16_t *__restrict__ table, uint64_t s
         bool in = true;
         for (int j = 0; j < heaps; j++) in &= ((k >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
         if (!in) continue;
-        sum += digest_term(k, record_of_score(table[k]));
+        sum += digest_term(k, record_of_code(table[k]));
         cnt++;
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -204,11 +420,10 @@ __global__ void sub_digest_kernel(const uint16_t *__restrict__ table, uint64_t s
     }
 }
 
-__global__ void sub_query_kernel(const uint16_t *__restrict__ table, uint64_t slots,
-                                 const uint64_t *__restrict__ keys, uint16_t *__restrict__ out,
-                                 uint64_t n) {
+__global__ void sub_query_kernel(const uint8_t *__restrict__ table, uint64_t slots,
+                                 const uint64_t *__restrict__ keys, uint16_t *__restrict__ out, uint64_t n) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i < n) out[i] = keys[i] < slots ? record_of_score(table[keys[i]]) : REC_UNSOLVED;
+    if (i < n) out[i] = keys[i] < slots ? record_of_code(table[keys[i]]) : REC_UNSOLVED;
 }
 
 // ---------------------------------------------------------------------------
@@ -218,11 +433,13 @@ static int prepare(Ctx *c, DenseSub *d) {
     if (low < 1) low = 1;
     if (low > 3) low = 3;
     int high = heaps - low;
-    if (!pick_kernel(low, high)) {
+    int nt = sub_kernel_threads(c, low);
+    if (!sub_kernel_exists(low, high, nt)) {
         set_error("no dense kernel for %d heaps at %d low heaps", heaps, low);
         return GM_E_GAME;
     }
-    d->heaps = heaps; d->low = low; d->high = high;
+    d->heaps = heaps; d->low = low; d->high = high; d->nt = nt;
+    d->want_threads = c->sub_threads; d->want_x4 = c->sub_interleave;
     d->slots = 1ull << (4 * heaps);
     uint64_t nhigh = 1ull << (4 * high);
     // counting sort of high parts by nibble sum (tier)
@@ -235,18 +452,18 @@ static int prepare(Ctx *c, DenseSub *d) {
     for (uint64_t v = 0; v < nhigh; v++) order[pos[tsum(v)]++] = (uint32_t)v;
     GM_HIP(hipMalloc(&d->d_blocks, nhigh * sizeof(uint32_t)));
     GM_HIP(hipMemcpy(d->d_blocks, order.data(), nhigh * sizeof(uint32_t), hipMemcpyHostToDevice));
-    size_t zbytes = std::max<size_t>(16, (size_t)2 << (4 * low));
+    size_t zbytes = std::max<size_t>(16, (size_t)1 << (4 * low));
     GM_HIP(hipMalloc(&d->zero, zbytes));
     GM_HIP(hipMemset(d->zero, 0, zbytes));
     GM_HIP(hipMalloc(&d->d_acc, 2 * sizeof(uint64_t)));
-    uint64_t bytes = d->slots * 2;
+    uint64_t bytes = d->slots;
     if (c->adopted_dense) {
         if (c->adopted_dense_bytes < bytes) {
             set_error("adopted dense table holds %llu bytes, need %llu",
                       (unsigned long long)c->adopted_dense_bytes, (unsigned long long)bytes);
             return GM_E_CAP;
         }
-        d->table = (uint16_t *)c->adopted_dense;
+        d->table = (uint8_t *)c->adopted_dense;
         d->owned = false;
     } else {
         if (hipMalloc(&d->table, bytes) != hipSuccess) {
@@ -269,14 +486,12 @@ static int ensure_events(DenseSub *d) {
 }
 
 static int launch_tiers(Ctx *c, DenseSub *d, bool timed) {
-    tier_kernel_t k = pick_kernel(d->low, d->high);
     int ntiers = (int)d->tier_off.size() - 1;
     for (int t = 0; t < ntiers; t++) {
         uint32_t nb = d->tier_off[t + 1] - d->tier_off[t];
         if (!nb) continue;
         if (timed) GM_HIP(hipEventRecord(d->ev[2 * t], c->stream));
-        hipLaunchKernelGGL(k, dim3(nb), dim3(256), 0, c->stream, d->table,
-                           d->d_blocks + d->tier_off[t], nb, d->zero);
+        launch_sub_tier(d->low, d->high, d->nt, nb, d->table, d->d_blocks + d->tier_off[t], d->zero, c->stream);
         if (timed) GM_HIP(hipEventRecord(d->ev[2 * t + 1], c->stream));
     }
     GM_HIP(hipGetLastError());
@@ -285,7 +500,8 @@ static int launch_tiers(Ctx *c, DenseSub *d, bool timed) {
 
 int dense_sub_solve(Ctx *c, uint64_t root) {
     DenseSub *d = c->dsub;
-    if (!d || d->heaps != c->sub.heaps || d->low != std::min(std::max(c->sub_low, 1), std::min(3, c->sub.heaps)) ||
+    if (!d || d->heaps != c->sub.heaps || d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave ||
+        d->low != std::min(std::max(c->sub_low, 1), std::min(3, c->sub.heaps)) ||
         (c->adopted_dense && d->table != c->adopted_dense)) {
         dense_sub_free(c);
         d = c->dsub = new DenseSub();
@@ -295,12 +511,12 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
     bool timed = c->timing;
     if (timed) GM_TRY(ensure_events(d));
     if (c->use_graph) {
-        // Replay the per-tier launches as one hipGraph.  Timing brackets the
-        // whole replay with one event pair (event-record nodes captured into a
-        // graph do not update the host-visible events), so the per-launch time
-        // it yields includes the graph's inter-kernel gaps.
+        // Replay the per-tier launches as one hipGraph; timing brackets the whole
+        // replay with one event pair (event nodes captured into a graph do not
+        // update host-visible events), so the per-launch time includes the
+        // graph's inter-kernel gaps.
         if (!d->graph || d->graph_stream != c->stream) {
-            if (d->graph) { hipGraphExecDestroy(d->graph); d->graph = nullptr; }
+            if (d->graph) { (void)hipGraphExecDestroy(d->graph); d->graph = nullptr; }
             hipGraph_t g;
             GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
             int rc = launch_tiers(c, d, false);
@@ -317,27 +533,26 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
     } else {
         GM_TRY(launch_tiers(c, d, timed));
     }
-    uint16_t rs;
-    GM_HIP(hipMemcpyAsync(&rs, d->table + root, 2, hipMemcpyDeviceToHost, c->stream));
+    uint8_t rs;
+    GM_HIP(hipMemcpyAsync(&rs, d->table + root, 1, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     double t1 = now_ms();
 
-    c->root_record = record_of_score(rs);
+    c->root_record = record_of_code(rs);
     uint64_t n = 1;
     for (int j = 0; j < d->heaps; j++) n *= ((root >> (4 * j)) & 15u) + 1;
     c->n_positions = n;
     int ntiers = (int)d->tier_off.size() - 1;
-    c->tier_counts.assign(15 * d->heaps + 1, 0);
     // positions per global tier (heap sum) of the full table
     {
-        std::vector<uint64_t> one(16, 1), acc(1, 1);
+        std::vector<uint64_t> acc(1, 1);
         for (int j = 0; j < d->heaps; j++) {
             std::vector<uint64_t> nx(acc.size() + 15, 0);
             for (size_t s = 0; s < acc.size(); s++)
                 for (int h = 0; h < 16; h++) nx[s + h] += acc[s];
             acc.swap(nx);
         }
-        for (size_t s = 0; s < acc.size() && s < c->tier_counts.size(); s++) c->tier_counts[s] = acc[s];
+        c->tier_counts = acc;
     }
     c->stats.n_positions = n;
     c->stats.n_primitive = 1;
@@ -345,10 +560,9 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
     c->stats.solve_ms = t1 - t0;
     c->stats.backward_ms = t1 - t0;
     c->stats.forward_ms = 0;
-    // 2 B written + 2 B per child edge = 2 * (1 + 1.8125 * heaps) per slot
-    double dbar = 1.8125 * d->heaps;
-    c->stats.algo_bytes = (uint64_t)((double)d->slots * 2.0 * (1.0 + dbar));
-    c->stats.table_bytes = d->slots * 2;
+    // SURVEY §8d edge model with 1-byte records: 1 B written + 1 B per child edge
+    c->stats.algo_bytes = (uint64_t)((double)d->slots * (1.0 + 1.8125 * d->heaps));
+    c->stats.table_bytes = d->slots;
     if (timed) {
         float total = 0;
         int launches = 0;
@@ -371,18 +585,19 @@ int dense_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint6
     DenseSub *d = c->dsub;
     *n = c->n_positions;
     if (!keys) return GM_OK;
-    if (cap < c->n_positions) { set_error("export buffer holds %llu, need %llu",
-                                          (unsigned long long)cap, (unsigned long long)c->n_positions);
-                                return GM_E_CAP; }
-    std::vector<uint16_t> h(d->slots);
-    GM_HIP(hipMemcpy(h.data(), d->table, d->slots * 2, hipMemcpyDeviceToHost));
+    if (cap < c->n_positions) {
+        set_error("export buffer holds %llu, need %llu", (unsigned long long)cap, (unsigned long long)c->n_positions);
+        return GM_E_CAP;
+    }
+    std::vector<uint8_t> h(d->slots);
+    GM_HIP(hipMemcpy(h.data(), d->table, d->slots, hipMemcpyDeviceToHost));
     uint64_t j = 0;
     for (uint64_t k = 0; k < d->slots; k++) {
         bool in = true;
         for (int i = 0; i < d->heaps && in; i++) in = ((k >> (4 * i)) & 15u) <= ((c->root >> (4 * i)) & 15u);
         if (!in) continue;
         keys[j] = k;
-        recs[j] = record_of_score(h[k]);
+        recs[j] = record_of_code(h[k]);
         j++;
     }
     return GM_OK;
@@ -396,20 +611,20 @@ int dense_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     GM_HIP(hipMalloc(&dk, n * 8));
     GM_HIP(hipMalloc(&dr, n * 2));
     GM_HIP(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(sub_query_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
-                       d->table, d->slots, dk, dr, n);
+    hipLaunchKernelGGL(sub_query_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d->table,
+                       d->slots, dk, dr, n);
     GM_HIP(hipMemcpyAsync(recs, dr, n * 2, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
-    hipFree(dk);
-    hipFree(dr);
+    (void)hipFree(dk);
+    (void)hipFree(dr);
     return GM_OK;
 }
 
 int dense_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     DenseSub *d = c->dsub;
     GM_HIP(hipMemsetAsync(d->d_acc, 0, 16, c->stream));
-    hipLaunchKernelGGL(sub_digest_kernel, dim3(2048), dim3(256), 0, c->stream, d->table, d->slots,
-                       d->heaps, c->root, (unsigned long long *)d->d_acc);
+    hipLaunchKernelGGL(sub_digest_kernel, dim3(2048), dim3(256), 0, c->stream, d->table, d->slots, d->heaps, c->root,
+                       (unsigned long long *)d->d_acc);
     uint64_t h[2];
     GM_HIP(hipMemcpyAsync(h, d->d_acc, 16, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
@@ -421,19 +636,19 @@ int dense_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
 int dense_sub_table(Ctx *c, void **p, uint64_t *bytes) {
     DenseSub *d = c->dsub;
     *p = d->table;
-    *bytes = d->slots * 2;
+    *bytes = d->slots;
     return GM_OK;
 }
 
 void dense_sub_free(Ctx *c) {
     DenseSub *d = c->dsub;
     if (!d) return;
-    if (d->graph) hipGraphExecDestroy(d->graph);
-    for (auto e : d->ev) hipEventDestroy(e);
-    if (d->owned && d->table) hipFree(d->table);
-    if (d->zero) hipFree(d->zero);
-    if (d->d_blocks) hipFree(d->d_blocks);
-    if (d->d_acc) hipFree(d->d_acc);
+    if (d->graph) (void)hipGraphExecDestroy(d->graph);
+    for (auto e : d->ev) (void)hipEventDestroy(e);
+    if (d->owned && d->table) (void)hipFree(d->table);
+    if (d->zero) (void)hipFree(d->zero);
+    if (d->d_blocks) (void)hipFree(d->d_blocks);
+    if (d->d_acc) (void)hipFree(d->d_acc);
     delete d;
     c->dsub = nullptr;
 }

@@ -9,50 +9,56 @@
 // upper rank needs the two layers h = 6, 7 of its lower neighbour: a halo of
 // <= 25 % of a rank per split heap, exchanged once per tier.
 //
-// Per tier t, on every rank:
-//   exchange  lower neighbours' tier-(t-1) boundary blocks arrive (ncclRecv) while
-//             this rank's tier-(t-1) boundary blocks leave (ncclSend), on a comm
-//             stream, one ncclGroup per tier (point-to-point over xGMI);
-//   compute A the blocks of tier t that need nothing from tier t-1 across a split
-//             (overlaps the exchange);
-//   unpack    the received halo into the table (global key layout on every rank);
-//   compute B the blocks whose split heap is 8 (they read the fresh halo);
-//   pack      this rank's tier-t boundary blocks for the next exchange.
-// Ranks never synchronise globally inside a solve: each waits only for its
-// neighbours' halo, so a rank whose blocks sit in later tiers trails its lower
-// neighbours by a tier instead of idling at a barrier.
+// Per tier t, on every rank (S = compute stream, C = exchange stream):
+//   C  exchange  tier t-1 boundary blocks: ncclRecv from lower neighbours,
+//                ncclSend to upper neighbours, one ncclGroup per tier;
+//   S  compute A the blocks of tier t that need nothing from tier t-1 across a
+//                split (runs while the exchange is in flight);
+//   S  unpack    (after the exchange event) the halo into the table;
+//   S  compute B the blocks whose split heap is 8 (they read the fresh halo);
+//   S  pack      this rank's tier-t boundary blocks into a K-deep ring of send
+//                slots (a lower rank can run up to K-1 tiers ahead of its upper
+//                neighbours; it waits only when a slot is still being sent).
+// There is no global barrier inside a solve: a rank waits only for the halos it
+// reads.  Launches are eager (see run_solve).
 //
 // Transports: RCCL (one process per GPU, gm_set_comm) or loopback (G virtual
-// ranks inside one context on one GPU, halos moved by device copies) -- the same
-// partition, lists, kernels and order of operations, so the loopback mode makes
-// the sharded path parity-testable on a single GPU.
+// ranks inside one context on one GPU, each with its own S and C streams; the
+// receiver's C stream copies from the sender's send slot after the sender's
+// pack event).  Same partition, lists, kernels, streams and events; only the
+// byte movement differs -- so the loopback mode tests the sharded path on one GPU.
 #include "gm_internal.hpp"
 
 #include <algorithm>
 
 namespace gm {
 
+constexpr int KSLOTS = 4;
+
 struct SubRank {
     int rank = 0;
-    uint16_t *table = nullptr;
+    uint8_t *table = nullptr;           // 1-byte codes (gm_common.hpp)
     bool owned = false;
     std::vector<uint32_t> offA, offB;          // per-tier offsets into listA / listB
     uint32_t *dA = nullptr, *dB = nullptr;
     std::vector<uint32_t> send_off[3], recv_off[3];
     uint32_t *dsend[3] = {nullptr, nullptr, nullptr}, *drecv[3] = {nullptr, nullptr, nullptr};
-    uint16_t *sendbuf[3][2] = {}, *recvbuf[3][2] = {};
+    uint8_t *sendbuf[3][KSLOTS] = {}, *recvbuf[3][KSLOTS] = {};
     uint64_t own_blocks = 0;
+    hipStream_t S = nullptr, C = nullptr;      // loopback: own streams; RCCL: the context's
+    bool own_streams = false;
+    hipEvent_t ev_packed[KSLOTS] = {}, ev_xch[KSLOTS] = {};
 };
 
 struct DistSub {
-    int heaps = 0, low = 0, high = 0, g = 0, G = 1, ntiers = 0;
+    int heaps = 0, low = 0, high = 0, g = 0, G = 1, ntiers = 0, nt = 256;
+    int want_threads = 0, want_x4 = 0;
     bool loopback = false;
     std::vector<SubRank> ranks;
-    uint16_t *zero = nullptr;
-    uint64_t *d_acc = nullptr;
+    uint8_t *zero = nullptr;
+    unsigned long long *d_acc = nullptr;
     uint32_t *d_root = nullptr;
-    hipEvent_t ev_packed[2] = {}, ev_recv[2] = {};
-    std::vector<hipEvent_t> ev;                // timing
+    hipEvent_t ev_fork = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
 };
 
 static inline int nib(uint64_t v, int k) { return (int)((v >> (4 * k)) & 15u); }
@@ -65,17 +71,51 @@ static inline int owner_of(const DistSub *d, uint64_t H) {
     return r;
 }
 
-__global__ void block_copy_kernel(const uint16_t *__restrict__ src, const uint32_t *__restrict__ list,
-                                  uint16_t *__restrict__ dst, int low, int pack) {
-    typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+__global__ void block_copy_kernel(const uint8_t *__restrict__ src, const uint32_t *__restrict__ list,
+                                  uint8_t *__restrict__ dst, int low, int pack) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint64_t bsz = 1ull << (4 * low);
     const uint64_t blk = (uint64_t)list[blockIdx.x] << (4 * low);
     const uint64_t stg = (uint64_t)blockIdx.x * bsz;
-    for (uint64_t c = threadIdx.x; c < bsz / 8; c += blockDim.x) {
-        if (pack)
-            *(u16x8 *)(dst + stg + 8 * c) = *(const u16x8 *)(src + blk + 8 * c);
-        else
-            *(u16x8 *)(dst + blk + 8 * c) = *(const u16x8 *)(src + stg + 8 * c);
+    if (bsz >= 16) {
+        for (uint64_t c = threadIdx.x; c < bsz / 16; c += blockDim.x) {
+            if (pack)
+                *(u32x4 *)(dst + stg + 16 * c) = *(const u32x4 *)(src + blk + 16 * c);
+            else
+                *(u32x4 *)(dst + blk + 16 * c) = *(const u32x4 *)(src + stg + 16 * c);
+        }
+    } else {
+        for (uint64_t c = threadIdx.x; c < bsz; c += blockDim.x) {
+            if (pack) dst[stg + c] = src[blk + c];
+            else dst[blk + c] = src[stg + c];
+        }
+    }
+}
+
+// digest over a list of whole blocks, restricted to the root's box
+__global__ void block_digest_kernel(const uint8_t *__restrict__ table, const uint32_t *__restrict__ list,
+                                    uint64_t nblocks, int low, int heaps, uint64_t root,
+                                    unsigned long long *acc) {
+    const uint64_t bsz = 1ull << (4 * low);
+    uint64_t s = 0, k = 0;
+    for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const uint64_t base = (uint64_t)list[b] << (4 * low);
+        for (uint64_t i = threadIdx.x; i < bsz; i += blockDim.x) {
+            uint64_t key = base + i;
+            bool in = true;
+            for (int j = 0; j < heaps; j++) in &= ((key >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
+            if (!in) continue;
+            s += digest_term(key, record_of_code(table[key]));
+            k++;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o);
+        k += __shfl_xor(k, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(acc, (unsigned long long)s);
+        atomicAdd(acc + 1, (unsigned long long)k);
     }
 }
 
@@ -90,8 +130,8 @@ static int build_rank(Ctx *c, DistSub *d, SubRank &R) {
     const int T = d->ntiers;
     const uint64_t nhigh = 1ull << (4 * d->high);
     auto tsum = [&](uint64_t H) { int s = 0; for (int k = 0; k < d->high; k++) s += nib(H, k); return s; };
-    std::vector<std::vector<uint32_t>> A(T), B(T), S[3], Rv[3];
-    for (int a = 0; a < 3; a++) { S[a].resize(T); Rv[a].resize(T); }
+    std::vector<std::vector<uint32_t>> A(T), B(T), Sd[3], Rv[3];
+    for (int a = 0; a < 3; a++) { Sd[a].resize(T); Rv[a].resize(T); }
     for (uint64_t H = 0; H < nhigh; H++) {
         int own = owner_of(d, H), t = tsum(H);
         if (own == R.rank) {
@@ -102,7 +142,7 @@ static int build_rank(Ctx *c, DistSub *d, SubRank &R) {
             R.own_blocks++;
             for (int a = 0; a < d->g; a++) {
                 int h = nib(H, d->high - 1 - a);
-                if (!((R.rank >> a) & 1) && (h == 6 || h == 7)) S[a][t].push_back((uint32_t)H);
+                if (!((R.rank >> a) & 1) && (h == 6 || h == 7)) Sd[a][t].push_back((uint32_t)H);
             }
         } else {
             for (int a = 0; a < d->g; a++) {
@@ -128,20 +168,24 @@ static int build_rank(Ctx *c, DistSub *d, SubRank &R) {
     };
     GM_TRY(flatten(A, R.offA, &R.dA, nullptr));
     GM_TRY(flatten(B, R.offB, &R.dB, nullptr));
-    const uint64_t bbytes = 2ull << (4 * d->low);
+    const uint64_t bbytes = 1ull << (4 * d->low);
     for (int a = 0; a < d->g; a++) {
         size_t ms = 0, mr = 0;
-        GM_TRY(flatten(S[a], R.send_off[a], &R.dsend[a], &ms));
+        GM_TRY(flatten(Sd[a], R.send_off[a], &R.dsend[a], &ms));
         GM_TRY(flatten(Rv[a], R.recv_off[a], &R.drecv[a], &mr));
-        for (int p = 0; p < 2; p++) {
+        for (int p = 0; p < KSLOTS; p++) {
             if (ms) GM_HIP(hipMalloc(&R.sendbuf[a][p], ms * bbytes));
             if (mr) GM_HIP(hipMalloc(&R.recvbuf[a][p], mr * bbytes));
         }
     }
-    const uint64_t bytes = 2ull << (4 * d->heaps);
+    for (int p = 0; p < KSLOTS; p++) {
+        GM_HIP(hipEventCreateWithFlags(&R.ev_packed[p], hipEventDisableTiming));
+        GM_HIP(hipEventCreateWithFlags(&R.ev_xch[p], hipEventDisableTiming));
+    }
+    const uint64_t bytes = 1ull << (4 * d->heaps);
     if (!d->loopback && c->adopted_dense) {
         if (c->adopted_dense_bytes < bytes) { set_error("adopted dense table too small"); return GM_E_CAP; }
-        R.table = (uint16_t *)c->adopted_dense;
+        R.table = (uint8_t *)c->adopted_dense;
     } else {
         if (hipMalloc(&R.table, bytes) != hipSuccess) {
             set_error("hipMalloc of a %llu-byte rank table failed", (unsigned long long)bytes);
@@ -164,210 +208,261 @@ static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
         set_error("%d heaps leave %d block heaps; cannot split %d ways", d->heaps, d->high, G);
         return GM_E_ARG;
     }
-    if (!sub_kernel_exists(d->low, d->high)) { set_error("no dense kernel"); return GM_E_GAME; }
+    d->nt = sub_kernel_threads(c, d->low);
+    d->want_threads = c->sub_threads;
+    d->want_x4 = c->sub_interleave;
+    if (!sub_kernel_exists(d->low, d->high, d->nt)) { set_error("no dense kernel"); return GM_E_GAME; }
     d->ntiers = 15 * d->high + 1;
-    size_t zb = 2ull << (4 * d->low);
+    size_t zb = std::max<size_t>(16, 1ull << (4 * d->low));
     GM_HIP(hipMalloc(&d->zero, zb));
     GM_HIP(hipMemset(d->zero, 0, zb));
     GM_HIP(hipMalloc(&d->d_acc, 16));
     GM_HIP(hipMalloc(&d->d_root, 4));
-    if (loopback) {
-        d->ranks.resize(G);
-        for (int r = 0; r < G; r++) { d->ranks[r].rank = r; GM_TRY(build_rank(c, d, d->ranks[r])); }
-    } else {
-        d->ranks.resize(1);
-        d->ranks[0].rank = c->rank;
-        GM_TRY(build_rank(c, d, d->ranks[0]));
-        for (int p = 0; p < 2; p++) {
-            GM_HIP(hipEventCreateWithFlags(&d->ev_packed[p], hipEventDisableTiming));
-            GM_HIP(hipEventCreateWithFlags(&d->ev_recv[p], hipEventDisableTiming));
+    GM_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+    GM_HIP(hipEventCreate(&d->ev_t0));
+    GM_HIP(hipEventCreate(&d->ev_t1));
+    if (!loopback && !c->comm_stream) GM_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    d->ranks.resize(loopback ? G : 1);
+    for (size_t i = 0; i < d->ranks.size(); i++) {
+        SubRank &R = d->ranks[i];
+        R.rank = loopback ? (int)i : c->rank;
+        GM_TRY(build_rank(c, d, R));
+        if (loopback) {
+            GM_HIP(hipStreamCreateWithFlags(&R.S, hipStreamNonBlocking));
+            GM_HIP(hipStreamCreateWithFlags(&R.C, hipStreamNonBlocking));
+            R.own_streams = true;
         }
-        if (!c->comm_stream) GM_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     }
     return GM_OK;
 }
 
-static void copy_blocks(DistSub *d, const uint16_t *src, const uint32_t *list, uint32_t n, uint16_t *dst,
+static void copy_blocks(DistSub *d, const uint8_t *src, const uint32_t *list, uint32_t n, uint8_t *dst,
                         bool pack, hipStream_t s) {
     if (!n) return;
     hipLaunchKernelGGL(block_copy_kernel, dim3(n), dim3(256), 0, s, src, list, dst, d->low, pack ? 1 : 0);
 }
 
-static uint32_t cnt(const std::vector<uint32_t> &off, int t) { return off[t + 1] - off[t]; }
+static uint32_t cnt(const std::vector<uint32_t> &off, int t) {
+    return (t < 0 || t + 1 >= (int)off.size()) ? 0 : off[t + 1] - off[t];
+}
+static bool is_upper(const SubRank &R, int a) { return (R.rank >> a) & 1; }
+
+// Enqueue one whole solve on the ranks' streams (eager or under capture).
+// S/C of every rank must already be joined to the capture when capturing.
+static int enqueue_solve(Ctx *c, DistSub *d, uint64_t *sent) {
+    const int T = d->ntiers, K = KSLOTS;
+    const uint64_t bbytes = 1ull << (4 * d->low);
+    *sent = 0;
+    for (int t = 0; t < T; t++) {
+        const int u = t - 1;   // tier whose boundary is exchanged at this step
+        // ---- C: exchange tier u
+        for (auto &R : d->ranks) {
+            bool any = false;
+            for (int a = 0; a < d->g; a++) any |= cnt(is_upper(R, a) ? R.recv_off[a] : R.send_off[a], u) > 0;
+            if (!any) continue;
+            GM_HIP(hipStreamWaitEvent(R.C, R.ev_packed[u % K], 0));   // my step u done (send data, recv slot)
+            if (d->loopback) {
+                for (int a = 0; a < d->g; a++) {
+                    if (!is_upper(R, a)) continue;
+                    uint32_t n = cnt(R.recv_off[a], u);
+                    if (!n) continue;
+                    SubRank &L = d->ranks[R.rank ^ (1 << a)];
+                    if (n != cnt(L.send_off[a], u)) { set_error("halo lists disagree"); return GM_E_STATE; }
+                    GM_HIP(hipStreamWaitEvent(R.C, L.ev_packed[u % K], 0));
+                    GM_HIP(hipMemcpyAsync(R.recvbuf[a][u % K], L.sendbuf[a][u % K], n * bbytes,
+                                          hipMemcpyDeviceToDevice, R.C));
+                    *sent += n * bbytes;
+                }
+            } else {
+                GM_NCCL(ncclGroupStart());
+                for (int a = 0; a < d->g; a++) {
+                    int peer = R.rank ^ (1 << a);
+                    if (is_upper(R, a)) {
+                        uint32_t n = cnt(R.recv_off[a], u);
+                        if (n) GM_NCCL(ncclRecv(R.recvbuf[a][u % K], n * bbytes, ncclUint8, peer, c->comm, R.C));
+                    } else {
+                        uint32_t n = cnt(R.send_off[a], u);
+                        if (n) GM_NCCL(ncclSend(R.sendbuf[a][u % K], n * bbytes, ncclUint8, peer, c->comm, R.C));
+                        *sent += n * bbytes;
+                    }
+                }
+                GM_NCCL(ncclGroupEnd());
+            }
+            GM_HIP(hipEventRecord(R.ev_xch[u % K], R.C));
+        }
+        // ---- S: compute, unpack, compute, pack
+        for (auto &R : d->ranks) {
+            launch_sub_tier(d->low, d->high, d->nt, cnt(R.offA, t), R.table, R.dA + R.offA[t], d->zero, R.S);
+            bool recv = false;
+            for (int a = 0; a < d->g; a++) recv |= is_upper(R, a) && cnt(R.recv_off[a], u) > 0;
+            if (recv) {
+                GM_HIP(hipStreamWaitEvent(R.S, R.ev_xch[u % K], 0));
+                for (int a = 0; a < d->g; a++)
+                    if (is_upper(R, a))
+                        copy_blocks(d, R.recvbuf[a][u % K], R.drecv[a] + R.recv_off[a][u], cnt(R.recv_off[a], u),
+                                    R.table, false, R.S);
+            }
+            launch_sub_tier(d->low, d->high, d->nt, cnt(R.offB, t), R.table, R.dB + R.offB[t], d->zero, R.S);
+            // slot t % K last carried tier t-K, exchanged at step t-K+1: wait until it has left
+            for (int a = 0; a < d->g; a++) {
+                if (is_upper(R, a) || !cnt(R.send_off[a], t)) continue;
+                if (cnt(R.send_off[a], t - K) > 0) {
+                    if (d->loopback)
+                        GM_HIP(hipStreamWaitEvent(R.S, d->ranks[R.rank ^ (1 << a)].ev_xch[(t - K) % K], 0));
+                    else
+                        GM_HIP(hipStreamWaitEvent(R.S, R.ev_xch[(t - K) % K], 0));
+                }
+                copy_blocks(d, R.table, R.dsend[a] + R.send_off[a][t], cnt(R.send_off[a], t), R.sendbuf[a][t % K],
+                            true, R.S);
+            }
+            GM_HIP(hipEventRecord(R.ev_packed[t % K], R.S));
+        }
+    }
+    // join every exchange stream back into its compute stream
+    for (auto &R : d->ranks) {
+        GM_HIP(hipEventRecord(R.ev_xch[0], R.C));
+        GM_HIP(hipStreamWaitEvent(R.S, R.ev_xch[0], 0));
+    }
+    return GM_OK;
+}
+
+// Run one solve: fork every rank's streams off the caller's stream, enqueue, join.
+// Launches are eager: HIP 7.2's stream capture crashes on this multi-stream event
+// pattern (tools/diag_dist.py), and in RCCL mode a capture refused half-way would
+// leave the ranks' point-to-point sequence numbers out of step.
+static int run_solve(Ctx *c, DistSub *d, uint64_t *sent) {
+    hipStream_t H = c->stream;
+    if (!d->loopback) { d->ranks[0].S = c->stream; d->ranks[0].C = c->comm_stream; }
+    // eager
+    GM_HIP(hipEventRecord(d->ev_fork, H));
+    for (auto &R : d->ranks) {
+        if (R.S != H) GM_HIP(hipStreamWaitEvent(R.S, d->ev_fork, 0));
+        GM_HIP(hipStreamWaitEvent(R.C, d->ev_fork, 0));
+    }
+    GM_TRY(enqueue_solve(c, d, sent));
+    for (auto &R : d->ranks)
+        if (R.S != H) {
+            GM_HIP(hipEventRecord(R.ev_packed[0], R.S));
+            GM_HIP(hipStreamWaitEvent(H, R.ev_packed[0], 0));
+        }
+    GM_HIP(hipGetLastError());
+    return GM_OK;
+}
 
 int dist_sub_solve(Ctx *c, uint64_t root) {
     const bool loopback = c->virtual_ranks > 1;
     const int G = loopback ? c->virtual_ranks : c->world;
     DistSub *d = c->dist_sub;
-    if (!d || d->heaps != c->sub.heaps || d->G != G || d->loopback != loopback) {
+    if (!d || d->heaps != c->sub.heaps || d->G != G || d->loopback != loopback || d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave ||
+        (!loopback && c->adopted_dense && d->ranks[0].table != c->adopted_dense)) {
         dist_sub_free(c);
         d = c->dist_sub = new DistSub();
         GM_TRY(prepare(c, d, G, loopback));
     }
-    const int T = d->ntiers;
-    const uint64_t bbytes = 2ull << (4 * d->low);
-    hipStream_t S = c->stream;
+    hipStream_t H = c->stream;
     double t0 = now_ms();
     uint64_t sent = 0;
-    if (loopback) {
-        for (int t = 0; t < T; t++) {
-            if (t > 0)   // exchange tier t-1 boundaries: lower neighbour's sendbuf -> my recvbuf
-                for (auto &R : d->ranks)
-                    for (int a = 0; a < d->g; a++) {
-                        if (!((R.rank >> a) & 1)) continue;
-                        SubRank &L = d->ranks[R.rank ^ (1 << a)];
-                        uint32_t n = cnt(R.recv_off[a], t - 1);
-                        if (n != cnt(L.send_off[a], t - 1)) { set_error("halo lists disagree"); return GM_E_STATE; }
-                        if (n) GM_HIP(hipMemcpyAsync(R.recvbuf[a][(t - 1) & 1], L.sendbuf[a][(t - 1) & 1],
-                                                     n * bbytes, hipMemcpyDeviceToDevice, S));
-                        sent += n * bbytes;
-                    }
-            for (auto &R : d->ranks) {
-                launch_sub_tier(d->low, d->high, cnt(R.offA, t), R.table, R.dA + R.offA[t], d->zero, S);
-                if (t > 0)
-                    for (int a = 0; a < d->g; a++)
-                        if ((R.rank >> a) & 1)
-                            copy_blocks(d, R.recvbuf[a][(t - 1) & 1], R.drecv[a] + R.recv_off[a][t - 1],
-                                        cnt(R.recv_off[a], t - 1), R.table, false, S);
-                launch_sub_tier(d->low, d->high, cnt(R.offB, t), R.table, R.dB + R.offB[t], d->zero, S);
-                for (int a = 0; a < d->g; a++)
-                    if (!((R.rank >> a) & 1))
-                        copy_blocks(d, R.table, R.dsend[a] + R.send_off[a][t], cnt(R.send_off[a], t),
-                                    R.sendbuf[a][t & 1], true, S);
-            }
-        }
-        GM_HIP(hipGetLastError());
-        // root record from its owner
-        SubRank &O = d->ranks[owner_of(d, root >> (4 * d->low))];
-        uint16_t rs;
-        GM_HIP(hipMemcpyAsync(&rs, O.table + root, 2, hipMemcpyDeviceToHost, S));
-        GM_HIP(hipStreamSynchronize(S));
-        c->root_record = record_of_score(rs);
-    } else {
-        SubRank &R = d->ranks[0];
-        hipStream_t C = c->comm_stream;
-        for (int t = 0; t < T; t++) {
-            int u = t - 1;   // tier whose boundary is exchanged at this step
-            bool any = false;
-            if (t > 0) {
-                for (int a = 0; a < d->g; a++)
-                    any |= ((R.rank >> a) & 1) ? cnt(R.recv_off[a], u) > 0 : cnt(R.send_off[a], u) > 0;
-            }
-            if (any) {
-                GM_HIP(hipStreamWaitEvent(C, d->ev_packed[u & 1], 0));
-                GM_NCCL(ncclGroupStart());
-                for (int a = 0; a < d->g; a++) {
-                    int peer = R.rank ^ (1 << a);
-                    if ((R.rank >> a) & 1) {
-                        uint32_t n = cnt(R.recv_off[a], u);
-                        if (n) GM_NCCL(ncclRecv(R.recvbuf[a][u & 1], n * bbytes, ncclUint8, peer, c->comm, C));
-                    } else {
-                        uint32_t n = cnt(R.send_off[a], u);
-                        if (n) GM_NCCL(ncclSend(R.sendbuf[a][u & 1], n * bbytes, ncclUint8, peer, c->comm, C));
-                        sent += n * bbytes;
-                    }
-                }
-                GM_NCCL(ncclGroupEnd());
-                GM_HIP(hipEventRecord(d->ev_recv[u & 1], C));
-            }
-            launch_sub_tier(d->low, d->high, cnt(R.offA, t), R.table, R.dA + R.offA[t], d->zero, S);
-            if (any) {
-                GM_HIP(hipStreamWaitEvent(S, d->ev_recv[u & 1], 0));
-                for (int a = 0; a < d->g; a++)
-                    if ((R.rank >> a) & 1)
-                        copy_blocks(d, R.recvbuf[a][u & 1], R.drecv[a] + R.recv_off[a][u], cnt(R.recv_off[a], u),
-                                    R.table, false, S);
-            }
-            launch_sub_tier(d->low, d->high, cnt(R.offB, t), R.table, R.dB + R.offB[t], d->zero, S);
-            for (int a = 0; a < d->g; a++)
-                if (!((R.rank >> a) & 1))
-                    copy_blocks(d, R.table, R.dsend[a] + R.send_off[a][t], cnt(R.send_off[a], t),
-                                R.sendbuf[a][t & 1], true, S);
-            GM_HIP(hipEventRecord(d->ev_packed[t & 1], S));
-        }
-        GM_HIP(hipGetLastError());
-        // root record: max-allreduce of the owner's score (others contribute 0)
-        int own = owner_of(d, root >> (4 * d->low)) == R.rank;
-        GM_HIP(hipMemsetAsync(d->d_root, 0, 4, S));
-        if (own) GM_HIP(hipMemcpyAsync(d->d_root, R.table + root, 2, hipMemcpyDeviceToDevice, S));
-        GM_NCCL(ncclAllReduce(d->d_root, d->d_root, 1, ncclUint32, ncclMax, c->comm, S));
-        uint32_t rs;
-        GM_HIP(hipMemcpyAsync(&rs, d->d_root, 4, hipMemcpyDeviceToHost, S));
-        GM_HIP(hipStreamSynchronize(S));
-        c->root_record = record_of_score((uint16_t)rs);
-    }
+    GM_HIP(hipEventRecord(d->ev_t0, H));
+    GM_TRY(run_solve(c, d, &sent));
+    GM_HIP(hipEventRecord(d->ev_t1, H));
+    // root record: max over ranks of the owner's code (the others contribute 0)
+    GM_HIP(hipMemsetAsync(d->d_root, 0, 4, H));
+    for (auto &R : d->ranks)
+        if (owner_of(d, root >> (4 * d->low)) == R.rank)
+            GM_HIP(hipMemcpyAsync(d->d_root, R.table + root, 1, hipMemcpyDeviceToDevice, H));
+    if (!loopback) GM_NCCL(ncclAllReduce(d->d_root, d->d_root, 1, ncclUint32, ncclMax, c->comm, H));
+    uint32_t rs = 0;
+    GM_HIP(hipMemcpyAsync(&rs, d->d_root, 4, hipMemcpyDeviceToHost, H));
+    GM_HIP(hipStreamSynchronize(H));
     double t1 = now_ms();
+    c->root_record = record_of_code((uint8_t)rs);
     uint64_t n = 1;
     for (int j = 0; j < d->heaps; j++) n *= ((root >> (4 * j)) & 15u) + 1;
     c->n_positions = n;
     c->stats.n_positions = n;
     c->stats.n_primitive = 1;
-    c->stats.n_tiers = T;
+    c->stats.n_tiers = d->ntiers;
     c->stats.world = G;
     c->stats.solve_ms = t1 - t0;
     c->stats.backward_ms = t1 - t0;
     c->stats.exchanged_bytes = sent;
+    if (c->timing) {
+        float ms = 0;
+        GM_HIP(hipEventElapsedTime(&ms, d->ev_t0, d->ev_t1));
+        c->stats.kernel_ms = ms;
+        uint32_t launches = 0;
+        for (auto &R : d->ranks)
+            for (int t = 0; t < d->ntiers; t++) launches += (cnt(R.offA, t) > 0) + (cnt(R.offB, t) > 0);
+        c->stats.kernel_launches = (int32_t)launches;
+    }
     uint64_t ownb = 0;
     for (auto &R : d->ranks) ownb += R.own_blocks;
-    c->stats.algo_bytes = (uint64_t)((double)(ownb << (4 * d->low)) * 2.0 * (1.0 + 1.8125 * d->heaps));
-    c->stats.table_bytes = (2ull << (4 * d->heaps)) * d->ranks.size();
+    c->stats.algo_bytes = (uint64_t)((double)(ownb << (4 * d->low)) * (1.0 + 1.8125 * d->heaps));
+    c->stats.table_bytes = (1ull << (4 * d->heaps)) * d->ranks.size();
     c->tier_counts.clear();
     return GM_OK;
 }
 
-// host copy of the blocks this context owns (one rank, or every virtual rank)
-template <class F>
-static int for_owned_blocks(Ctx *c, F f) {
-    DistSub *d = c->dist_sub;
-    const uint64_t bsz = 1ull << (4 * d->low);
-    std::vector<uint16_t> buf(bsz);
-    const uint64_t nhigh = 1ull << (4 * d->high);
-    for (uint64_t H = 0; H < nhigh; H++) {
-        int own = owner_of(d, H);
-        SubRank *R = nullptr;
-        for (auto &x : d->ranks)
-            if (x.rank == own) R = &x;
-        if (!R) continue;
-        GM_HIP(hipMemcpy(buf.data(), R->table + (H << (4 * d->low)), bsz * 2, hipMemcpyDeviceToHost));
-        f(H << (4 * d->low), buf.data(), bsz);
-    }
-    return GM_OK;
-}
-
+// ---------------------------------------------------------------- results
 static bool in_box(uint64_t k, uint64_t root, int heaps) {
     for (int i = 0; i < heaps; i++)
         if (((k >> (4 * i)) & 15u) > ((root >> (4 * i)) & 15u)) return false;
     return true;
 }
 
-int dist_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
+int dist_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     DistSub *d = c->dist_sub;
-    uint64_t cntv = 0;
-    std::vector<std::pair<uint64_t, uint16_t>> out;
-    GM_TRY(for_owned_blocks(c, [&](uint64_t base, const uint16_t *s, uint64_t len) {
-        for (uint64_t i = 0; i < len; i++)
-            if (in_box(base + i, c->root, d->heaps)) {
-                if (keys) out.emplace_back(base + i, record_of_score(s[i]));
-                cntv++;
-            }
-    }));
-    *n = cntv;
-    if (!keys) return GM_OK;
-    if (cap < cntv) { set_error("export buffer too small"); return GM_E_CAP; }
-    std::sort(out.begin(), out.end());
-    for (uint64_t i = 0; i < cntv; i++) { keys[i] = out[i].first; recs[i] = out[i].second; }
+    hipStream_t H = c->stream;
+    GM_HIP(hipMemsetAsync(d->d_acc, 0, 16, H));
+    for (auto &R : d->ranks) {
+        uint32_t na = R.offA.back(), nb = R.offB.back();
+        if (na) hipLaunchKernelGGL(block_digest_kernel, dim3(std::min<uint32_t>(na, 8192)), dim3(256), 0, H, R.table,
+                                   R.dA, (uint64_t)na, d->low, d->heaps, c->root, d->d_acc);
+        if (nb) hipLaunchKernelGGL(block_digest_kernel, dim3(std::min<uint32_t>(nb, 8192)), dim3(256), 0, H, R.table,
+                                   R.dB, (uint64_t)nb, d->low, d->heaps, c->root, d->d_acc);
+    }
+    unsigned long long h[2];
+    GM_HIP(hipMemcpyAsync(h, d->d_acc, 16, hipMemcpyDeviceToHost, H));
+    GM_HIP(hipStreamSynchronize(H));
+    *digest = h[0];
+    *n = h[1];
     return GM_OK;
 }
 
-int dist_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
+int dist_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
     DistSub *d = c->dist_sub;
-    uint64_t s = 0, k = 0;
-    GM_TRY(for_owned_blocks(c, [&](uint64_t base, const uint16_t *v, uint64_t len) {
-        for (uint64_t i = 0; i < len; i++)
-            if (in_box(base + i, c->root, d->heaps)) { s += digest_term(base + i, record_of_score(v[i])); k++; }
-    }));
-    *digest = s;
-    *n = k;
+    hipStream_t H = c->stream;
+    const uint64_t bsz = 1ull << (4 * d->low);
+    std::vector<std::pair<uint64_t, uint16_t>> out;
+    uint64_t total = 0;
+    for (auto &R : d->ranks) {
+        for (int which = 0; which < 2; which++) {
+            uint32_t nb = which ? R.offB.back() : R.offA.back();
+            const uint32_t *lst = which ? R.dB : R.dA;
+            if (!nb) continue;
+            uint8_t *stg;
+            GM_HIP(hipMalloc(&stg, (uint64_t)nb * bsz));
+            copy_blocks(d, R.table, lst, nb, stg, true, H);
+            std::vector<uint8_t> hs((uint64_t)nb * bsz);
+            std::vector<uint32_t> hl(nb);
+            GM_HIP(hipMemcpyAsync(hs.data(), stg, hs.size(), hipMemcpyDeviceToHost, H));
+            GM_HIP(hipMemcpyAsync(hl.data(), lst, nb * 4, hipMemcpyDeviceToHost, H));
+            GM_HIP(hipStreamSynchronize(H));
+            (void)hipFree(stg);
+            for (uint32_t b = 0; b < nb; b++)
+                for (uint64_t i = 0; i < bsz; i++) {
+                    uint64_t key = ((uint64_t)hl[b] << (4 * d->low)) + i;
+                    if (!in_box(key, c->root, d->heaps)) continue;
+                    total++;
+                    if (keys) out.emplace_back(key, record_of_code(hs[(uint64_t)b * bsz + i]));
+                }
+        }
+    }
+    *n = total;
+    if (!keys) return GM_OK;
+    if (cap < total) { set_error("export buffer too small"); return GM_E_CAP; }
+    std::sort(out.begin(), out.end());
+    for (uint64_t i = 0; i < total; i++) { keys[i] = out[i].first; recs[i] = out[i].second; }
     return GM_OK;
 }
 
@@ -379,9 +474,9 @@ int dist_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
         int own = owner_of(d, keys[i] >> (4 * d->low));
         for (auto &R : d->ranks)
             if (R.rank == own) {
-                uint16_t s;
-                GM_HIP(hipMemcpy(&s, R.table + keys[i], 2, hipMemcpyDeviceToHost));
-                recs[i] = record_of_score(s);
+                uint8_t s;
+                GM_HIP(hipMemcpy(&s, R.table + keys[i], 1, hipMemcpyDeviceToHost));
+                recs[i] = record_of_code(s);
             }
     }
     return GM_OK;
@@ -391,25 +486,31 @@ void dist_sub_free(Ctx *c) {
     DistSub *d = c->dist_sub;
     if (!d) return;
     for (auto &R : d->ranks) {
-        if (R.owned && R.table) hipFree(R.table);
-        if (R.dA) hipFree(R.dA);
-        if (R.dB) hipFree(R.dB);
+        if (R.owned && R.table) (void)hipFree(R.table);
+        if (R.dA) (void)hipFree(R.dA);
+        if (R.dB) (void)hipFree(R.dB);
         for (int a = 0; a < 3; a++) {
-            if (R.dsend[a]) hipFree(R.dsend[a]);
-            if (R.drecv[a]) hipFree(R.drecv[a]);
-            for (int p = 0; p < 2; p++) {
-                if (R.sendbuf[a][p]) hipFree(R.sendbuf[a][p]);
-                if (R.recvbuf[a][p]) hipFree(R.recvbuf[a][p]);
+            if (R.dsend[a]) (void)hipFree(R.dsend[a]);
+            if (R.drecv[a]) (void)hipFree(R.drecv[a]);
+            for (int p = 0; p < KSLOTS; p++) {
+                if (R.sendbuf[a][p]) (void)hipFree(R.sendbuf[a][p]);
+                if (R.recvbuf[a][p]) (void)hipFree(R.recvbuf[a][p]);
             }
         }
+        for (int p = 0; p < KSLOTS; p++) {
+            if (R.ev_packed[p]) (void)hipEventDestroy(R.ev_packed[p]);
+            if (R.ev_xch[p]) (void)hipEventDestroy(R.ev_xch[p]);
+        }
+        if (R.own_streams) {
+            (void)hipStreamDestroy(R.S);
+            (void)hipStreamDestroy(R.C);
+        }
     }
-    for (int p = 0; p < 2; p++) {
-        if (d->ev_packed[p]) hipEventDestroy(d->ev_packed[p]);
-        if (d->ev_recv[p]) hipEventDestroy(d->ev_recv[p]);
-    }
-    if (d->zero) hipFree(d->zero);
-    if (d->d_acc) hipFree(d->d_acc);
-    if (d->d_root) hipFree(d->d_root);
+    for (hipEvent_t e : {d->ev_fork, d->ev_t0, d->ev_t1})
+        if (e) (void)hipEventDestroy(e);
+    if (d->zero) (void)hipFree(d->zero);
+    if (d->d_acc) (void)hipFree(d->d_acc);
+    if (d->d_root) (void)hipFree(d->d_root);
     delete d;
     c->dist_sub = nullptr;
 }

@@ -148,6 +148,14 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         return GM_OK;
     case GM_OPT_GRAPH: c->use_graph = v != 0; return GM_OK;
     case GM_OPT_TIMING: c->timing = v != 0; return GM_OK;
+    case GM_OPT_SUB_THREADS:
+        if (v != 64 && v != 128 && v != 256) { set_error("sub_threads must be 64, 128 or 256"); return GM_E_ARG; }
+        c->sub_threads = (int)v;
+        return GM_OK;
+    case GM_OPT_SUB_INTERLEAVE:
+        if (v != 1 && v != 4) { set_error("sub_interleave must be 1 or 4"); return GM_E_ARG; }
+        c->sub_interleave = (int)v;
+        return GM_OK;
     case GM_OPT_VIRTUAL_RANKS:
         if (v < 1 || v > 64) { set_error("virtual ranks must be 1..64"); return GM_E_ARG; }
         c->virtual_ranks = (int)v;

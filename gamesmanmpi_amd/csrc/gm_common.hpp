@@ -77,6 +77,21 @@ GM_HD bool score_overflows(uint32_t b) {
     return (cls == 3 && low == 0) || (cls == 2 && low == 0) || (cls == 1 && low >= 0x3FFE);
 }
 
+// 1-byte codes of the dense subtraction path.  That game has a single primitive
+// (all heaps empty: LOSS in 0), so only WIN and LOSS classes exist, and its
+// remoteness is at most the heap total (<= 120 for 8 heaps of 4 bits):
+//     WIN R -> R + 1 (1..127)      LOSS R -> 255 - R (129..255)      none -> 0
+// The order matches the u16 scores above, so the best child is still a max, and
+//     parent_code(b) = (255 - b) + 2 * (b >> 7)
+// (best child LOSS R -> WIN R+1; best child WIN R -> LOSS R+1).
+GM_HD uint32_t parent_code(uint32_t b) { return (255u - b) + ((b >> 7) << 1); }
+
+GM_HD uint16_t record_of_code(uint8_t b) {
+    if (b == 0) return REC_UNSOLVED;
+    if (b >= 128) return (uint16_t)((1u << 14) | (255u - b));   // LOSS
+    return (uint16_t)(b - 1u);                                   // WIN
+}
+
 GM_HD uint64_t mix64(uint64_t x) {
     x ^= x >> 33;
     x *= 0xff51afd7ed558ccdull;

@@ -73,6 +73,8 @@ struct Ctx {
 
     int engine_opt = GM_ENGINE_AUTO;
     int sub_low = 3;
+    int sub_threads = 128;
+    int sub_interleave = 4;
     bool use_graph = true;
     bool timing = false;
 
@@ -111,9 +113,10 @@ void dense_sub_free(Ctx *c);
 int dense_sub_table(Ctx *c, void **p, uint64_t *bytes);
 
 // the dense tier kernel, shared with the partitioned (multi-GPU) driver
-bool sub_kernel_exists(int low, int high);
-void launch_sub_tier(int low, int high, uint32_t nblocks, uint16_t *table, const uint32_t *list,
-                     const uint16_t *zero, hipStream_t s);
+bool sub_kernel_exists(int low, int high, int nt);
+void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table, const uint32_t *list,
+                     const uint8_t *zero, hipStream_t s);
+int sub_kernel_threads(const Ctx *c, int low);   // 0 = the 4-block interleaved kernel
 
 // partitioned dense solve: `world` ranks, real (RCCL, one per process) or virtual (loopback)
 int dist_sub_solve(Ctx *c, uint64_t root);

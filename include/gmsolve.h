@@ -74,14 +74,16 @@ enum {
     GM_OPT_SUB_LOW = 2,     /* SUBTRACT dense path: heaps solved per workgroup in LDS (1..4) */
     GM_OPT_GRAPH = 3,       /* SUBTRACT dense path: replay the tier launches as a hipGraph (0/1) */
     GM_OPT_TIMING = 4,      /* record HIP events around every launch of the dominant kernel (0/1) */
-    GM_OPT_VIRTUAL_RANKS = 5 /* >1: run the sharded algorithm with that many ranks inside this one
+    GM_OPT_VIRTUAL_RANKS = 5, /* >1: run the sharded algorithm with that many ranks inside this one
                                 context on one GPU (loopback transport instead of RCCL); for testing
                                 the multi-GPU partition on a single device */
+    GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
+    GM_OPT_SUB_INTERLEAVE = 7 /* SUBTRACT dense path: blocks per workgroup, 4 (interleaved, default) or 1 */
 };
 
 /* Buffer roles for gm_adopt_buffer. */
 enum {
-    GM_BUF_DENSE_TABLE = 1  /* SUBTRACT dense table: 2 bytes per slot, 16^heaps slots */
+    GM_BUF_DENSE_TABLE = 1  /* SUBTRACT dense table: 1 byte per slot, 16^heaps slots */
 };
 
 typedef struct gm_ctx gm_ctx;
@@ -174,7 +176,7 @@ int gm_tier_counts(gm_ctx *ctx, uint64_t *counts, int cap, int *n);
 int gm_adopt_buffer(gm_ctx *ctx, int role, void *dev_ptr, uint64_t bytes);
 
 /* Device pointer and size of the dense table (GM_BUF_DENSE_TABLE) after a solve;
- * its slots hold preference scores ("HBM layout"), not records. */
+ * its slots hold 1-byte order-preserving codes ("HBM layout"), not records. */
 int gm_dense_table(gm_ctx *ctx, void **dev_ptr, uint64_t *bytes);
 
 /* Release everything. */
