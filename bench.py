@@ -32,6 +32,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 ALGO_BYTES_PER_POSITION = 15.5  # SURVEY §8d edge model at 8 heaps, 1-B records: 1 write + 14.5 child reads
+COMPULSORY_BYTES_PER_POSITION = 3.0  # SURVEY §8d compulsory bound with 1-B records: 1 write + 2 producer-tier reads
 METRIC = "positions solved/sec (node) at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
 
 
@@ -55,14 +56,31 @@ def cpu_baseline(heaps=7):
                       "(oracle/gm_oracle.c oracle_subtract_dense), %.1f s" % (heaps, n, dt)}
 
 
-def pmc_traffic(heaps, launches_per_solve):
-    """HBM bytes per launch of the tier kernel from a committed rocprofv3 PMC summary."""
+def pmc_traffic(heaps):
+    """HBM bytes per launch / per solve of the tier kernel from a committed rocprofv3 PMC summary."""
     path = os.path.join(REPO, "profiles", "traffic_subtract%d.json" % heaps)
     if not os.path.exists(path):
-        return None
+        return None, None
     with open(path) as f:
         t = json.load(f)
-    return t.get("hbm_bytes_per_launch")
+    return t.get("hbm_bytes_per_launch"), t.get("hbm_bytes_per_solve")
+
+
+def copy_bandwidth(torch, nbytes=1 << 31, reps=10):
+    """Measured device-to-device copy bandwidth (read + write bytes / s), SURVEY §8d."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbs
 
 
 def main():
@@ -148,6 +166,11 @@ def main():
     value = positions * args.steps / elapsed
     st = ctx.stats()
     launches_per_solve = max(1, launches // max(1, args.steps))
+    traffic_launch, traffic_solve = pmc_traffic(args.heaps)
+    copy_gbs = copy_bandwidth(torch) if world == 1 else None
+    kernel_s_per_solve = kernel_ms / 1e3 / max(1, args.steps)
+    compulsory_gbs = (COMPULSORY_BYTES_PER_POSITION * positions / kernel_s_per_solve / 1e9
+                      if kernel_s_per_solve > 0 else None)
     # bytes this rank's tier launches move, per the SURVEY §8d model
     algo_per_launch = st["algo_bytes"] / launches_per_solve
     avg_launch_s = (kernel_ms / 1e3) / max(1, launches)
@@ -169,12 +192,19 @@ def main():
                    "positions": positions, "parallelism": "1 GPU" if world == 1 else "block-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                     "traffic": pmc_traffic(args.heaps, launches_per_solve),
+                     "traffic": traffic_launch,
                      "kernel": "sub_tier_kernel_x4<%d>" % (args.heaps - 3),
                      "launches_per_solve": launches_per_solve,
                      "avg_launch_us": avg_launch_s * 1e6,
                      "kernel_ms_per_solve": kernel_ms / max(1, args.steps),
                      "algo_bytes_per_position": ALGO_BYTES_PER_POSITION,
+                     "survey_u16_model_bytes_per_position": 31.0,
+                     "traffic_bytes_per_position": (traffic_solve / positions) if traffic_solve else None,
+                     "traffic_gbs": (traffic_solve / kernel_s_per_solve / 1e9) if traffic_solve else None,
+                     "compulsory_bytes_per_position": COMPULSORY_BYTES_PER_POSITION,
+                     "compulsory_gbs": compulsory_gbs,
+                     "compulsory_frac": (compulsory_gbs / HBM_PEAK_GBS) if compulsory_gbs else None,
+                     "measured_copy_gbs": copy_gbs,
                      "timing": ("HIP events bracketing each solve's tier-launch graph replay on the launch "
                                 "stream; avg launch = span / launches (includes in-graph gaps)"
                                 if world == 1 else

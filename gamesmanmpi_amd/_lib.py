@@ -8,7 +8,8 @@ import ctypes
 import os
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libgmsolve.so")
+# GM_LIB_PATH: development aid to load an experimental build of the same library
+LIB_PATH = os.environ.get("GM_LIB_PATH") or os.path.join(PKG, "libgmsolve.so")
 
 GAME_FOUR_TO_ONE, GAME_TTT, GAME_TOOT, GAME_OTHELLO, GAME_SUBTRACT = 1, 2, 3, 4, 5
 ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE, ENGINE_DIST_DENSE, ENGINE_DIST_SPARSE = 0, 1, 2, 3, 4

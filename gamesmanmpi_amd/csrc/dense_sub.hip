@@ -104,6 +104,9 @@ template <int LOW, int HIGH, int NMAX>
 __device__ __forceinline__ void child_blocks(const uint8_t *table, const uint8_t *zero, uint32_t hp, bool valid,
                                              const uint8_t *(&src)[NMAX]) {
     const uint8_t *first = zero;
+#if defined(GM_EXP) && (GM_EXP & 2)
+    valid = false;   // experiment: no child-block traffic
+#endif
 #pragma unroll
     for (int j = HIGH - 1; j >= 0; j--) {
         const uint32_t h = (hp >> (4 * j)) & 15u;
@@ -289,7 +292,12 @@ __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ 
     const int a0 = tid & 15, a1 = tid >> 4, s0 = a0 + a1;
     auto S = [&](int L) -> u16x4 { return *(const u16x4 *)((const char *)s + 8 * L); };
     const bool root_here = valid[0] && hp[0] == 0;   // sorted tier list: block 0 comes first
-    for (int tau = 0; tau <= 45; tau++) {
+#if defined(GM_EXP) && (GM_EXP & 1)
+    constexpr int TAU_END = -1;   // experiment: no pass B
+#else
+    constexpr int TAU_END = 45;
+#endif
+    for (int tau = 0; tau <= TAU_END; tau++) {
         const int c = tau - s0;
         if (c >= 0 && c <= 15) {
             const int L = tid + 256 * c;
