@@ -40,6 +40,7 @@ typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 
 struct DenseSub {
     int heaps = 0, low = 0, high = 0, nt = 128;   // nt 0 = interleaved x4 kernel
@@ -91,6 +92,10 @@ __device__ __forceinline__ Fold16 fold16(const u32x4v (&v)[N]) {
         }
     }
     return f;
+}
+// parent_code on a pair of u16 codes (each <= 255, so no borrow crosses the halves)
+__device__ __forceinline__ uint32_t code_x2(uint32_t b) {
+    return (0x00FF00FFu - b) + ((b >> 6) & 0x00020002u);
 }
 // four u16 codes (positions 4j..4j+3 as pairs (p0,p1), (p2,p3)) -> one dword of bytes
 __device__ __forceinline__ uint32_t pack_bytes(uint32_t p01, uint32_t p23) {
@@ -230,9 +235,6 @@ __global__ __launch_bounds__(NT) void sub_tier_kernel(uint8_t *__restrict__ tabl
 // position with one address, one validity test and one ds_read_b64 per child,
 // in packed u16 arithmetic.  Pass A folds each block's children separately and
 // transposes 4 x 8 codes at a time with v_perm_b32; pass C transposes back.
-__device__ __forceinline__ u16x4 parent_code_x4(u16x4 b) {
-    return ((u16x4)(uint16_t)255 - b) + ((b >> (uint16_t)7) << (uint16_t)1);
-}
 
 template <int HIGH>
 __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ table,
@@ -289,28 +291,42 @@ __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ 
     __syncthreads();
 
     // ---- pass B -------------------------------------------------------------
+    // Thread (a0, a1) owns the column c = 0..15 and solves (a0, a1, c) at low tier
+    // tau = a0 + a1 + c.  An invalid in-block child reads the position itself (max is
+    // idempotent), so the seven ds_read_b64 of a step issue back to back with one
+    // wait and no branches; position 0 (tau = 0) is peeled so the root override
+    // stays out of the loop.
     const int a0 = tid & 15, a1 = tid >> 4, s0 = a0 + a1;
-    auto S = [&](int L) -> u16x4 { return *(const u16x4 *)((const char *)s + 8 * L); };
-    const bool root_here = valid[0] && hp[0] == 0;   // sorted tier list: block 0 comes first
+    const uint32_t d01 = a0 >= 1 ? 8u : 0u, d02 = a0 >= 2 ? 16u : 0u;
+    const uint32_t d11 = a1 >= 1 ? 128u : 0u, d12 = a1 >= 2 ? 256u : 0u;
+    char *const sb = (char *)s;
+    auto ld = [&](uint32_t off) -> u32x2v { return *(const u32x2v *)(sb + off); };
 #if defined(GM_EXP) && (GM_EXP & 1)
-    constexpr int TAU_END = -1;   // experiment: no pass B
+    constexpr int TAU_END = 0;   // experiment: no pass B
 #else
     constexpr int TAU_END = 45;
 #endif
-    for (int tau = 0; tau <= TAU_END; tau++) {
+    if (tid == 0) {
+        u32x2v r = ld(0);
+        r[0] = code_x2(r[0]);
+        r[1] = code_x2(r[1]);
+        if (valid[0] && hp[0] == 0) r[0] = (r[0] & 0xFFFF0000u) | 255u;   // all heaps empty: LOSS in 0
+        *(u32x2v *)sb = r;
+    }
+    __syncthreads();
+    for (int tau = 1; tau <= TAU_END; tau++) {
         const int c = tau - s0;
         if (c >= 0 && c <= 15) {
-            const int L = tid + 256 * c;
-            u16x4 best = S(L);
-            if (a0 >= 1) best = __builtin_elementwise_max(best, S(L - 1));
-            if (a0 >= 2) best = __builtin_elementwise_max(best, S(L - 2));
-            if (a1 >= 1) best = __builtin_elementwise_max(best, S(L - 16));
-            if (a1 >= 2) best = __builtin_elementwise_max(best, S(L - 32));
-            if (c >= 1) best = __builtin_elementwise_max(best, S(L - 256));
-            if (c >= 2) best = __builtin_elementwise_max(best, S(L - 512));
-            u16x4 res = parent_code_x4(best);
-            if (root_here && L == 0) res[0] = 255;   // all heaps empty: LOSS in 0
-            *(u16x4 *)((char *)s + 8 * L) = res;
+            const uint32_t o = 8u * (uint32_t)(tid + 256 * c);
+            const uint32_t dc1 = c >= 1 ? 2048u : 0u, dc2 = c >= 2 ? 4096u : 0u;
+            const u32x2v v0 = ld(o), v1 = ld(o - d01), v2 = ld(o - d02), v3 = ld(o - d11), v4 = ld(o - d12),
+                         v5 = ld(o - dc1), v6 = ld(o - dc2);
+            u32x2v r;
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+                r[h] = code_x2(pk_max(pk_max(pk_max(v0[h], v1[h]), pk_max(v2[h], v3[h])),
+                                      pk_max(pk_max(v4[h], v5[h]), v6[h])));
+            *(u32x2v *)(sb + o) = r;
         }
         __syncthreads();
     }
