@@ -15,6 +15,7 @@ GAME_FOUR_TO_ONE, GAME_TTT, GAME_TOOT, GAME_OTHELLO, GAME_SUBTRACT = 1, 2, 3, 4,
 ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE, ENGINE_DIST_DENSE, ENGINE_DIST_SPARSE = 0, 1, 2, 3, 4
 OPT_ENGINE, OPT_SUB_LOW, OPT_GRAPH, OPT_TIMING, OPT_VIRTUAL_RANKS, OPT_SUB_THREADS = 1, 2, 3, 4, 5, 6
 OPT_SUB_INTERLEAVE = 7
+OPT_SUB_ORDER = 8
 BUF_DENSE_TABLE = 1
 REC_UNSOLVED = 0xFFFF
 

@@ -44,7 +44,7 @@ typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 
 struct DenseSub {
     int heaps = 0, low = 0, high = 0, nt = 128;   // nt 0 = interleaved x4 kernel
-    int want_threads = 0, want_x4 = 0;
+    int want_threads = 0, want_x4 = 0, want_order = 0;
     uint8_t *table = nullptr;           // 16^heaps codes
     bool owned = false;
     uint64_t slots = 0;
@@ -451,6 +451,23 @@ __global__ void sub_query_kernel(const uint8_t *__restrict__ table, uint64_t slo
 }
 
 // ---------------------------------------------------------------------------
+// Morton (bit-interleaved) code of a high part's nibbles.  Sorting each tier by it
+// keeps the five same-tier parents of a child block (one high nibble +1 each) close
+// in the launch order, hence on the same XCD at about the same time: their shared
+// child blocks are read from HBM once and then hit that XCD's L2.
+static uint32_t morton_of(uint32_t v, int high) {
+    uint32_t m = 0;
+    for (int b = 0; b < 4; b++)
+        for (int j = 0; j < high; j++) m |= ((v >> (4 * j + b)) & 1u) << (b * high + j);
+    return m;
+}
+
+void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &off, int high) {
+    for (size_t t = 0; t + 1 < off.size(); t++)
+        std::sort(order.begin() + off[t], order.begin() + off[t + 1],
+                  [high](uint32_t a, uint32_t b) { return morton_of(a, high) < morton_of(b, high); });
+}
+
 static int prepare(Ctx *c, DenseSub *d) {
     int heaps = c->sub.heaps;
     int low = std::min(c->sub_low, heaps);
@@ -463,7 +480,7 @@ static int prepare(Ctx *c, DenseSub *d) {
         return GM_E_GAME;
     }
     d->heaps = heaps; d->low = low; d->high = high; d->nt = nt;
-    d->want_threads = c->sub_threads; d->want_x4 = c->sub_interleave;
+    d->want_threads = c->sub_threads; d->want_x4 = c->sub_interleave; d->want_order = c->sub_order;
     d->slots = 1ull << (4 * heaps);
     uint64_t nhigh = 1ull << (4 * high);
     // counting sort of high parts by nibble sum (tier)
@@ -474,6 +491,7 @@ static int prepare(Ctx *c, DenseSub *d) {
     d->tier_off.assign(cnt.begin(), cnt.end());
     std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
     for (uint64_t v = 0; v < nhigh; v++) order[pos[tsum(v)]++] = (uint32_t)v;
+    if (c->sub_order == 1) sort_tiers_morton(order, d->tier_off, high);
     GM_HIP(hipMalloc(&d->d_blocks, nhigh * sizeof(uint32_t)));
     GM_HIP(hipMemcpy(d->d_blocks, order.data(), nhigh * sizeof(uint32_t), hipMemcpyHostToDevice));
     size_t zbytes = std::max<size_t>(16, (size_t)1 << (4 * low));
@@ -525,7 +543,7 @@ static int launch_tiers(Ctx *c, DenseSub *d, bool timed) {
 int dense_sub_solve(Ctx *c, uint64_t root) {
     DenseSub *d = c->dsub;
     if (!d || d->heaps != c->sub.heaps || d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave ||
-        d->low != std::min(std::max(c->sub_low, 1), std::min(3, c->sub.heaps)) ||
+        d->want_order != c->sub_order || d->low != std::min(std::max(c->sub_low, 1), std::min(3, c->sub.heaps)) ||
         (c->adopted_dense && d->table != c->adopted_dense)) {
         dense_sub_free(c);
         d = c->dsub = new DenseSub();

@@ -156,6 +156,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         if (v != 1 && v != 4) { set_error("sub_interleave must be 1 or 4"); return GM_E_ARG; }
         c->sub_interleave = (int)v;
         return GM_OK;
+    case GM_OPT_SUB_ORDER:
+        if (v != 0 && v != 1) { set_error("sub_order must be 0 or 1"); return GM_E_ARG; }
+        c->sub_order = (int)v;
+        return GM_OK;
     case GM_OPT_VIRTUAL_RANKS:
         if (v < 1 || v > 64) { set_error("virtual ranks must be 1..64"); return GM_E_ARG; }
         c->virtual_ranks = (int)v;

@@ -75,6 +75,7 @@ struct Ctx {
     int sub_low = 3;
     int sub_threads = 128;
     int sub_interleave = 4;
+    int sub_order = 1;
     bool use_graph = true;
     bool timing = false;
 
@@ -117,6 +118,7 @@ bool sub_kernel_exists(int low, int high, int nt);
 void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table, const uint32_t *list,
                      const uint8_t *zero, hipStream_t s);
 int sub_kernel_threads(const Ctx *c, int low);   // 0 = the 4-block interleaved kernel
+void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &tier_off, int high);
 
 // partitioned dense solve: `world` ranks, real (RCCL, one per process) or virtual (loopback)
 int dist_sub_solve(Ctx *c, uint64_t root);

@@ -78,7 +78,8 @@ enum {
                                 context on one GPU (loopback transport instead of RCCL); for testing
                                 the multi-GPU partition on a single device */
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
-    GM_OPT_SUB_INTERLEAVE = 7 /* SUBTRACT dense path: blocks per workgroup, 4 (interleaved, default) or 1 */
+    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path: blocks per workgroup, 4 (interleaved, default) or 1 */
+    GM_OPT_SUB_ORDER = 8    /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton (default) */
 };
 
 /* Buffer roles for gm_adopt_buffer. */

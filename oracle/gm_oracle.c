@@ -28,6 +28,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stdio.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define WIN 0
 #define LOSS 1
@@ -596,4 +599,69 @@ int oracle_subtract_dense(int heaps, uint16_t *rec) {
         rec[k] = from_pref(best);
     }
     return 0;
+}
+
+/* The same dense solve on `threads` OpenMP threads (<= 0: all), in the GPU's
+ * decomposition: blocks of 16^low keys sharing their high nibbles, blocks grouped
+ * by the sum of the high nibbles (a child block has a smaller sum), the blocks of
+ * one group in parallel, each block swept in ascending key order.  The bench's
+ * multi-core cpu_baseline. */
+int oracle_subtract_dense_mt(int heaps, uint16_t *rec, int threads) {
+    if (heaps < 1 || heaps > 8) { snprintf(g_err, sizeof g_err, "heaps must be 1..8"); return -1; }
+    const int low = heaps < 3 ? heaps : 3, high = heaps - low;
+    const uint64_t bsz = 1ull << (4 * low), nhigh = 1ull << (4 * high);
+    uint32_t *order = (uint32_t *)malloc(nhigh * sizeof(uint32_t));
+    uint64_t *off = (uint64_t *)calloc(15 * high + 2, sizeof(uint64_t));
+    if (!order || !off) { free(order); free(off); snprintf(g_err, sizeof g_err, "out of memory"); return -1; }
+    for (uint64_t v = 0; v < nhigh; v++) {
+        int s = 0;
+        for (int j = 0; j < high; j++) s += (int)((v >> (4 * j)) & 15);
+        off[s + 1]++;
+    }
+    for (int t = 1; t < 15 * high + 2; t++) off[t] += off[t - 1];
+    {
+        uint64_t *pos = (uint64_t *)malloc((15 * high + 1) * sizeof(uint64_t));
+        if (!pos) { free(order); free(off); snprintf(g_err, sizeof g_err, "out of memory"); return -1; }
+        memcpy(pos, off, (15 * high + 1) * sizeof(uint64_t));
+        for (uint64_t v = 0; v < nhigh; v++) {
+            int s = 0;
+            for (int j = 0; j < high; j++) s += (int)((v >> (4 * j)) & 15);
+            order[pos[s]++] = (uint32_t)v;
+        }
+        free(pos);
+    }
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+    for (int t = 0; t <= 15 * high; t++) {
+        const long long b0 = (long long)off[t], b1 = (long long)off[t + 1];
+#pragma omp parallel for schedule(dynamic, 4)
+        for (long long b = b0; b < b1; b++) {
+            const uint64_t base = (uint64_t)order[b] << (4 * low);
+            for (uint64_t i = 0; i < bsz; i++) {
+                const uint64_t k = base + i;
+                if (k == 0) { rec[0] = (uint16_t)(LOSS << 14); continue; }
+                uint32_t best = 0;
+                for (int j = 0; j < heaps; j++) {
+                    uint64_t h = (k >> (4 * j)) & 15;
+                    if (h >= 1) { uint32_t s = pref(rec[k - (1ull << (4 * j))]); if (s > best) best = s; }
+                    if (h >= 2) { uint32_t s = pref(rec[k - (2ull << (4 * j))]); if (s > best) best = s; }
+                }
+                rec[k] = from_pref(best);
+            }
+        }
+    }
+    free(order);
+    free(off);
+    return 0;
+}
+
+int oracle_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
 }

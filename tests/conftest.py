@@ -54,6 +54,7 @@ class Oracle:
         L.oracle_expand.argtypes = [ctypes.c_int, P(ctypes.c_int32), ctypes.c_int, ctypes.c_uint64,
                                     P(ctypes.c_uint64), P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int64)]
         L.oracle_subtract_dense.argtypes = [ctypes.c_int, ctypes.c_void_p]
+        L.oracle_subtract_dense_mt.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_free.argtypes = [ctypes.c_void_p]
         self.L = L
@@ -93,6 +94,11 @@ class Oracle:
     def subtract_dense(self, heaps):
         out = np.empty(1 << (4 * heaps), dtype=np.uint16)
         assert self.L.oracle_subtract_dense(heaps, out.ctypes.data) == 0
+        return out
+
+    def subtract_dense_mt(self, heaps, threads=0):
+        out = np.empty(1 << (4 * heaps), dtype=np.uint16)
+        assert self.L.oracle_subtract_dense_mt(heaps, out.ctypes.data, threads) == 0
         return out
 
 

@@ -139,6 +139,12 @@ def test_subtract_dense_equals_generic_oracle(oracle):
     assert np.array_equal(k, np.arange(4096, dtype=np.uint64)) and np.array_equal(r, dense)
 
 
+@pytest.mark.parametrize("heaps", [1, 2, 3, 4, 5, 6])
+def test_subtract_dense_multithreaded_equals_sequential(oracle, heaps):
+    # the bench's multi-core cpu_baseline must compute the same table
+    assert np.array_equal(oracle.subtract_dense_mt(heaps, 4), oracle.subtract_dense(heaps))
+
+
 def test_subtract_plugin_canonical(oracle):
     mod = load_plugin("test_games/subtraction.py", HEAPS=2)
     table, positions = canonical.solve(mod)
