@@ -124,6 +124,8 @@ def main():
     ap.add_argument("--heaps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-heaps", type=int, default=8)
+    ap.add_argument("--dist-batch", type=int, default=4, help="N>1: tiers per halo exchange")
+    ap.add_argument("--dist-slots", type=int, default=4, help="N>1: halo buffers per split heap")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     args = ap.parse_args()
@@ -161,6 +163,8 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_option(_lib.OPT_TIMING, 1)
+    ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch)
+    ctx.set_option(_lib.OPT_DIST_SLOTS, args.dist_slots)
     if args.virtual_ranks > 1:
         ctx.set_option(_lib.OPT_VIRTUAL_RANKS, args.virtual_ranks)
     root = ctx.initial()
@@ -175,12 +179,14 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kernel_ms = 0.0
+    enqueue_ms = 0.0
     launches = 0
     for _ in range(args.steps):
         n, rec = ctx.solve(root)
         st = ctx.stats()
         kernel_ms += st["kernel_ms"]
         launches += st["kernel_launches"]
+        enqueue_ms += st["forward_ms"] if (world > 1 or args.virtual_ranks > 1) else 0.0
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -243,6 +249,9 @@ def main():
                                 if world == 1 else
                                 "HIP events around rank 0's whole sharded solve (includes halo waits)")},
         "exchanged_bytes_per_step_rank0": st["exchanged_bytes"],
+        "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
+            "halo_batch_tiers": args.dist_batch, "halo_slots": args.dist_slots,
+            "host_enqueue_ms_per_step_rank0": enqueue_ms / max(1, args.steps)},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -16,6 +16,8 @@ ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE, ENGINE_DIST_DENSE, ENGINE_DIST_SPARSE 
 OPT_ENGINE, OPT_SUB_LOW, OPT_GRAPH, OPT_TIMING, OPT_VIRTUAL_RANKS, OPT_SUB_THREADS = 1, 2, 3, 4, 5, 6
 OPT_SUB_INTERLEAVE = 7
 OPT_SUB_ORDER = 8
+OPT_DIST_BATCH = 9
+OPT_DIST_SLOTS = 10
 BUF_DENSE_TABLE = 1
 REC_UNSOLVED = 0xFFFF
 
@@ -53,6 +55,7 @@ class Stats(ctypes.Structure):
         ("kernel_ms", ctypes.c_double),
         ("kernel_launches", ctypes.c_int32),
         ("engine", ctypes.c_int32),
+        ("n_edges", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -6,59 +6,83 @@
 // owner (GameState.get_hash, src/game_state.py:23-31) and sends one message per
 // edge (src/new_process.py:159,186); here a move changes one heap by 1 or 2, so a
 // block's children live on its own rank except across a split heap, where the
-// upper rank needs the two layers h = 6, 7 of its lower neighbour: a halo of
-// <= 25 % of a rank per split heap, exchanged once per tier.
+// upper rank reads the two layers h = 6, 7 of its lower neighbour (tier t reads
+// the neighbour's tiers t-1 and t-2): a halo of <= 25 % of a rank per split heap.
 //
-// Per tier t, on every rank (S = compute stream, C = exchange stream):
-//   C  exchange  tier t-1 boundary blocks: ncclRecv from lower neighbours,
-//                ncclSend to upper neighbours, one ncclGroup per tier;
-//   S  compute A the blocks of tier t that need nothing from tier t-1 across a
-//                split (runs while the exchange is in flight);
-//   S  unpack    (after the exchange event) the halo into the table;
-//   S  compute B the blocks whose split heap is 8 (they read the fresh halo);
-//   S  pack      this rank's tier-t boundary blocks into a K-deep ring of send
-//                slots (a lower rank can run up to K-1 tiers ahead of its upper
-//                neighbours; it waits only when a slot is still being sent).
-// There is no global barrier inside a solve: a rank waits only for the halos it
-// reads.  Launches are eager (see run_solve).
+// Schedule.  Tiers (high-nibble sums) are grouped in batches of B (GM_OPT_DIST_BATCH);
+// batch j is tiers [jB, jB+B).  Before batch j an upper rank needs its lower
+// neighbour's halo of tiers [jB-1, jB+B-2] -- message X_j, which the lower rank
+// packs and sends right after computing tier jB+B-2.  So a rank makes one launch
+// per tier and one exchange per batch and split heap; an upper rank trails its
+// lower neighbour by about one batch, which the partition's own stagger absorbs
+// (rank r's blocks start at tier 8*popcount(r)).
 //
-// Transports: RCCL (one process per GPU, gm_set_comm) or loopback (G virtual
-// ranks inside one context on one GPU, each with its own S and C streams; the
-// receiver's C stream copies from the sender's send slot after the sender's
-// pack event).  Same partition, lists, kernels, streams and events; only the
-// byte movement differs -- so the loopback mode tests the sharded path on one GPU.
+// Streams and communicators (RCCL mode, one process per GPU): the compute stream
+// S, plus one exchange stream X[a] and one communicator per split heap a
+// (ncclCommSplit of the world communicator).  On axis a a rank is either the
+// lower side (it only sends) or the upper side (it only receives), so an exchange
+// stream never holds both a send and a receive, and a lower rank waits for an
+// upper one only when its ring of K send buffers (GM_OPT_DIST_SLOTS) is full.
+//
+// Every rank's work is a precomputed list of ops (tier launch, pack, unpack,
+// send, receive, event record / wait).  RCCL mode runs its list in order.  The
+// loopback mode (GM_OPT_VIRTUAL_RANKS: G ranks inside one context on one GPU,
+// for testing the partition without a second GPU) runs the same lists on per-rank
+// streams, a receive being a device copy from the sender's ring slot after the
+// sender's pack event; a host-side scheduler interleaves the lists so that every
+// cross-rank wait is enqueued after the record it waits for.
 #include "gm_internal.hpp"
 
 #include <algorithm>
 
 namespace gm {
 
-constexpr int KSLOTS = 4;
+constexpr int MAX_AXES = 3;
+
+enum EvKind { EV_PACKED = 0, EV_XCH = 1, EV_UNPACKED = 2, EV_KINDS = 3 };
+enum OpKind { OP_TIER, OP_PACK, OP_UNPACK, OP_SEND, OP_RECV, OP_RECORD, OP_WAIT };
+
+struct Op {
+    uint8_t kind, axis, ev, on_x;   // on_x: runs on X[axis], else on S
+    int32_t arg;                    // tier (OP_TIER) or batch
+    int32_t peer;                   // rank owning the event (OP_WAIT) / the other side (OP_SEND, OP_RECV)
+};
 
 struct SubRank {
     int rank = 0;
     uint8_t *table = nullptr;           // 1-byte codes (gm_common.hpp)
     bool owned = false;
-    std::vector<uint32_t> offA, offB;          // per-tier offsets into listA / listB
-    uint32_t *dA = nullptr, *dB = nullptr;
-    std::vector<uint32_t> send_off[3], recv_off[3];
-    uint32_t *dsend[3] = {nullptr, nullptr, nullptr}, *drecv[3] = {nullptr, nullptr, nullptr};
-    uint8_t *sendbuf[3][KSLOTS] = {}, *recvbuf[3][KSLOTS] = {};
+    std::vector<uint32_t> off;          // per-tier offsets into dlist (owned blocks)
+    uint32_t *dlist = nullptr;
+    std::vector<uint32_t> send_off[MAX_AXES], recv_off[MAX_AXES];   // per-batch offsets
+    uint32_t *dsend[MAX_AXES] = {}, *drecv[MAX_AXES] = {};
+    uint8_t *sendbuf[MAX_AXES] = {}, *recvbuf[MAX_AXES] = {};       // rings of nslots slots
+    uint64_t send_slot[MAX_AXES] = {}, recv_slot[MAX_AXES] = {};    // bytes per slot
+    std::vector<hipEvent_t> ev[EV_KINDS][MAX_AXES];                 // nslots each
+    hipEvent_t ev_join[MAX_AXES] = {};
     uint64_t own_blocks = 0;
-    hipStream_t S = nullptr, C = nullptr;      // loopback: own streams; RCCL: the context's
-    bool own_streams = false;
-    hipEvent_t ev_packed[KSLOTS] = {}, ev_xch[KSLOTS] = {};
+    hipStream_t S = nullptr;
+    hipStream_t X[MAX_AXES] = {};
+    bool own_S = false;
+    std::vector<Op> ops;
+    size_t pc = 0;
+    int recorded[EV_KINDS][MAX_AXES] = {};   // batches whose event is enqueued (host order)
 };
 
 struct DistSub {
     int heaps = 0, low = 0, high = 0, g = 0, G = 1, ntiers = 0, nt = 256;
-    int want_threads = 0, want_x4 = 0;
+    int batch = 4, nbatch = 0, nslots = 0;
+    int want_threads = 0, want_x4 = 0, want_order = 0, want_batch = 0, want_slots = 0;
     bool loopback = false;
     std::vector<SubRank> ranks;
+    std::vector<int> lo, hi;            // per batch: tier range of X_j (empty if lo > hi)
     uint8_t *zero = nullptr;
     unsigned long long *d_acc = nullptr;
     uint32_t *d_root = nullptr;
     hipEvent_t ev_fork = nullptr, ev_t0 = nullptr, ev_t1 = nullptr;
+    ncclComm_t comm[MAX_AXES] = {};     // comm[0] = the context's; the others split from it
+    bool own_comm[MAX_AXES] = {};
+    uint64_t sent = 0;
 };
 
 static inline int nib(uint64_t v, int k) { return (int)((v >> (4 * k)) & 15u); }
@@ -70,6 +94,8 @@ static inline int owner_of(const DistSub *d, uint64_t H) {
         if (nib(H, d->high - 1 - a) >= 8) r |= 1 << a;
     return r;
 }
+
+static inline bool is_upper(int rank, int a) { return (rank >> a) & 1; }
 
 __global__ void block_copy_kernel(const uint8_t *__restrict__ src, const uint32_t *__restrict__ list,
                                   uint8_t *__restrict__ dst, int low, int pack) {
@@ -125,75 +151,123 @@ static int upload(const std::vector<uint32_t> &v, uint32_t **d) {
     return GM_OK;
 }
 
-// Build rank r's block lists (identical enumeration on every rank).
-static int build_rank(Ctx *c, DistSub *d, SubRank &R) {
-    const int T = d->ntiers;
+static uint32_t cnt(const std::vector<uint32_t> &off, int i) {
+    return (i < 0 || i + 1 >= (int)off.size()) ? 0 : off[i + 1] - off[i];
+}
+
+// Build rank R's block lists (identical enumeration on every rank, so a sender's
+// halo list and its receiver's list agree block for block).
+static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
+    const int T = d->ntiers, NB = d->nbatch;
     const uint64_t nhigh = 1ull << (4 * d->high);
     auto tsum = [&](uint64_t H) { int s = 0; for (int k = 0; k < d->high; k++) s += nib(H, k); return s; };
-    std::vector<std::vector<uint32_t>> A(T), B(T), Sd[3], Rv[3];
-    for (int a = 0; a < 3; a++) { Sd[a].resize(T); Rv[a].resize(T); }
+    std::vector<int> xb(T, -1);   // halo message carrying tier t
+    for (int j = 0; j < NB; j++)
+        for (int t = d->lo[j]; t <= d->hi[j]; t++) xb[t] = j;
+    std::vector<std::vector<uint32_t>> own(T), Sd[MAX_AXES], Rv[MAX_AXES];
+    for (int a = 0; a < MAX_AXES; a++) { Sd[a].resize(NB); Rv[a].resize(NB); }
     for (uint64_t H = 0; H < nhigh; H++) {
-        int own = owner_of(d, H), t = tsum(H);
-        if (own == R.rank) {
-            bool needs = false;
-            for (int a = 0; a < d->g; a++)
-                if (((R.rank >> a) & 1) && nib(H, d->high - 1 - a) == 8) needs = true;
-            (needs ? B : A)[t].push_back((uint32_t)H);
+        const int o = owner_of(d, H), t = tsum(H);
+        for (int a = 0; a < d->g; a++) {
+            const int h = nib(H, d->high - 1 - a);
+            if ((h != 6 && h != 7) || xb[t] < 0) continue;
+            if (o == R.rank && !is_upper(R.rank, a)) Sd[a][xb[t]].push_back((uint32_t)H);
+            if (is_upper(R.rank, a) && o == (R.rank ^ (1 << a))) Rv[a][xb[t]].push_back((uint32_t)H);
+        }
+        if (o == R.rank) {
+            own[t].push_back((uint32_t)H);
             R.own_blocks++;
-            for (int a = 0; a < d->g; a++) {
-                int h = nib(H, d->high - 1 - a);
-                if (!((R.rank >> a) & 1) && (h == 6 || h == 7)) Sd[a][t].push_back((uint32_t)H);
-            }
-        } else {
-            for (int a = 0; a < d->g; a++) {
-                int h = nib(H, d->high - 1 - a);
-                if (((R.rank >> a) & 1) && own == (R.rank ^ (1 << a)) && (h == 6 || h == 7))
-                    Rv[a][t].push_back((uint32_t)H);
-            }
         }
     }
-    auto flatten = [&](std::vector<std::vector<uint32_t>> &L, std::vector<uint32_t> &off, uint32_t **dptr,
-                       size_t *maxn) -> int {
-        std::vector<uint32_t> flat;
-        off.assign(T + 1, 0);
-        size_t mx = 0;
-        for (int t = 0; t < T; t++) {
-            off[t] = (uint32_t)flat.size();
-            flat.insert(flat.end(), L[t].begin(), L[t].end());
-            mx = std::max(mx, L[t].size());
+    auto flatten = [&](std::vector<std::vector<uint32_t>> &L, std::vector<uint32_t> &off,
+                       std::vector<uint32_t> &flat) {
+        off.assign(L.size() + 1, 0);
+        for (size_t i = 0; i < L.size(); i++) {
+            off[i] = (uint32_t)flat.size();
+            flat.insert(flat.end(), L[i].begin(), L[i].end());
         }
-        off[T] = (uint32_t)flat.size();
-        if (maxn) *maxn = mx;
-        return upload(flat, dptr);
+        off[L.size()] = (uint32_t)flat.size();
     };
-    GM_TRY(flatten(A, R.offA, &R.dA, nullptr));
-    GM_TRY(flatten(B, R.offB, &R.dB, nullptr));
-    const uint64_t bbytes = 1ull << (4 * d->low);
+    {
+        std::vector<uint32_t> flat;
+        flatten(own, R.off, flat);
+        if (c->sub_order == 1) sort_tiers_morton(flat, R.off, d->high);
+        GM_TRY(upload(flat, &R.dlist));
+    }
+    const uint64_t bb = 1ull << (4 * d->low);
     for (int a = 0; a < d->g; a++) {
-        size_t ms = 0, mr = 0;
-        GM_TRY(flatten(Sd[a], R.send_off[a], &R.dsend[a], &ms));
-        GM_TRY(flatten(Rv[a], R.recv_off[a], &R.drecv[a], &mr));
-        for (int p = 0; p < KSLOTS; p++) {
-            if (ms) GM_HIP(hipMalloc(&R.sendbuf[a][p], ms * bbytes));
-            if (mr) GM_HIP(hipMalloc(&R.recvbuf[a][p], mr * bbytes));
+        std::vector<uint32_t> fs, fr;
+        flatten(Sd[a], R.send_off[a], fs);
+        flatten(Rv[a], R.recv_off[a], fr);
+        GM_TRY(upload(fs, &R.dsend[a]));
+        GM_TRY(upload(fr, &R.drecv[a]));
+        uint64_t ms = 0, mr = 0;
+        for (int j = 0; j < NB; j++) {
+            ms = std::max<uint64_t>(ms, cnt(R.send_off[a], j));
+            mr = std::max<uint64_t>(mr, cnt(R.recv_off[a], j));
         }
-    }
-    for (int p = 0; p < KSLOTS; p++) {
-        GM_HIP(hipEventCreateWithFlags(&R.ev_packed[p], hipEventDisableTiming));
-        GM_HIP(hipEventCreateWithFlags(&R.ev_xch[p], hipEventDisableTiming));
-    }
-    const uint64_t bytes = 1ull << (4 * d->heaps);
-    if (!d->loopback && c->adopted_dense) {
-        if (c->adopted_dense_bytes < bytes) { set_error("adopted dense table too small"); return GM_E_CAP; }
-        R.table = (uint8_t *)c->adopted_dense;
-    } else {
-        if (hipMalloc(&R.table, bytes) != hipSuccess) {
-            set_error("hipMalloc of a %llu-byte rank table failed", (unsigned long long)bytes);
-            return GM_E_NOMEM;
+        R.send_slot[a] = ms * bb;
+        R.recv_slot[a] = mr * bb;
+        if (ms) GM_HIP(hipMalloc(&R.sendbuf[a], ms * bb * d->nslots));
+        if (mr) GM_HIP(hipMalloc(&R.recvbuf[a], mr * bb * d->nslots));
+        for (int k = 0; k < EV_KINDS; k++) {
+            R.ev[k][a].resize(d->nslots);
+            for (auto &e : R.ev[k][a]) GM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
-        R.owned = true;
+        GM_HIP(hipEventCreateWithFlags(&R.ev_join[a], hipEventDisableTiming));
     }
     return GM_OK;
+}
+
+static uint8_t *send_ptr(const DistSub *d, const SubRank &R, int a, int j) {
+    return R.sendbuf[a] + (uint64_t)(j % d->nslots) * R.send_slot[a];
+}
+static uint8_t *recv_ptr(const DistSub *d, const SubRank &R, int a, int j) {
+    return R.recvbuf[a] + (uint64_t)(j % d->nslots) * R.recv_slot[a];
+}
+
+// The op list of rank R for one solve (see the file comment).
+static void build_ops(DistSub *d, SubRank &R) {
+    const int T = d->ntiers, NB = d->nbatch, B = d->batch, NS = d->nslots;
+    auto op = [&](int kind, int axis, int ev, bool on_x, int arg, int peer) {
+        R.ops.push_back(Op{(uint8_t)kind, (uint8_t)axis, (uint8_t)ev, (uint8_t)on_x, arg, peer});
+    };
+    std::vector<std::vector<int>> send_after(T);   // halo messages a lower rank sends after tier t
+    for (int j = 0; j < NB; j++)
+        if (d->lo[j] <= d->hi[j]) send_after[d->hi[j]].push_back(j);
+    R.ops.clear();
+    for (int j = 0; j < NB; j++) {
+        // receive X_j on every axis where this rank is the upper side
+        for (int a = 0; a < d->g; a++) {
+            if (!is_upper(R.rank, a) || !cnt(R.recv_off[a], j)) continue;
+            const int lower = R.rank ^ (1 << a);
+            if (j >= NS && cnt(R.recv_off[a], j - NS)) op(OP_WAIT, a, EV_UNPACKED, true, j - NS, R.rank);
+            if (d->loopback) op(OP_WAIT, a, EV_PACKED, true, j, lower);
+            op(OP_RECV, a, 0, true, j, lower);
+            op(OP_RECORD, a, EV_XCH, true, j, R.rank);
+            op(OP_WAIT, a, EV_XCH, false, j, R.rank);
+            op(OP_UNPACK, a, 0, false, j, R.rank);
+            op(OP_RECORD, a, EV_UNPACKED, false, j, R.rank);
+        }
+        for (int t = j * B; t < std::min(T, j * B + B); t++) {
+            op(OP_TIER, 0, 0, false, t, R.rank);
+            for (int jj : send_after[t])
+                for (int a = 0; a < d->g; a++) {
+                    if (is_upper(R.rank, a) || !cnt(R.send_off[a], jj)) continue;
+                    const int upper = R.rank ^ (1 << a);
+                    // ring slot jj % NS last carried batch jj-NS: wait until it has left
+                    if (jj >= NS && cnt(R.send_off[a], jj - NS))
+                        op(OP_WAIT, a, EV_XCH, false, jj - NS, d->loopback ? upper : R.rank);
+                    op(OP_PACK, a, 0, false, jj, upper);
+                    op(OP_RECORD, a, EV_PACKED, false, jj, R.rank);
+                    if (!d->loopback) {
+                        op(OP_WAIT, a, EV_PACKED, true, jj, R.rank);
+                        op(OP_SEND, a, 0, true, jj, upper);
+                        op(OP_RECORD, a, EV_XCH, true, jj, R.rank);
+                    }
+                }
+        }
+    }
 }
 
 static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
@@ -211,8 +285,20 @@ static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
     d->nt = sub_kernel_threads(c, d->low);
     d->want_threads = c->sub_threads;
     d->want_x4 = c->sub_interleave;
+    d->want_order = c->sub_order;
+    d->want_batch = c->dist_batch;
+    d->want_slots = c->dist_slots;
     if (!sub_kernel_exists(d->low, d->high, d->nt)) { set_error("no dense kernel"); return GM_E_GAME; }
     d->ntiers = 15 * d->high + 1;
+    d->batch = std::max(1, std::min(c->dist_batch, d->ntiers));
+    d->nbatch = (d->ntiers + d->batch - 1) / d->batch;
+    d->nslots = std::max(1, std::min(c->dist_slots, d->nbatch));
+    d->lo.resize(d->nbatch);
+    d->hi.resize(d->nbatch);
+    for (int j = 0; j < d->nbatch; j++) {
+        d->lo[j] = std::max(0, j * d->batch - 1);
+        d->hi[j] = std::min(d->ntiers - 2, j * d->batch + d->batch - 2);
+    }
     size_t zb = std::max<size_t>(16, 1ull << (4 * d->low));
     GM_HIP(hipMalloc(&d->zero, zb));
     GM_HIP(hipMemset(d->zero, 0, zb));
@@ -221,17 +307,36 @@ static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
     GM_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
     GM_HIP(hipEventCreate(&d->ev_t0));
     GM_HIP(hipEventCreate(&d->ev_t1));
-    if (!loopback && !c->comm_stream) GM_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    if (!loopback) {
+        // one communicator per split heap; every rank makes the same calls in the same order
+        d->comm[0] = c->comm;
+        for (int a = 1; a < d->g; a++) {
+            GM_NCCL(ncclCommSplit(c->comm, 0, c->rank, &d->comm[a], nullptr));
+            d->own_comm[a] = true;
+        }
+    }
     d->ranks.resize(loopback ? G : 1);
     for (size_t i = 0; i < d->ranks.size(); i++) {
         SubRank &R = d->ranks[i];
         R.rank = loopback ? (int)i : c->rank;
-        GM_TRY(build_rank(c, d, R));
+        GM_TRY(build_lists(c, d, R));
+        const uint64_t bytes = 1ull << (4 * d->heaps);
+        if (!loopback && c->adopted_dense) {
+            if (c->adopted_dense_bytes < bytes) { set_error("adopted dense table too small"); return GM_E_CAP; }
+            R.table = (uint8_t *)c->adopted_dense;
+        } else {
+            if (hipMalloc(&R.table, bytes) != hipSuccess) {
+                set_error("hipMalloc of a %llu-byte rank table failed", (unsigned long long)bytes);
+                return GM_E_NOMEM;
+            }
+            R.owned = true;
+        }
         if (loopback) {
             GM_HIP(hipStreamCreateWithFlags(&R.S, hipStreamNonBlocking));
-            GM_HIP(hipStreamCreateWithFlags(&R.C, hipStreamNonBlocking));
-            R.own_streams = true;
+            R.own_S = true;
         }
+        for (int a = 0; a < d->g; a++) GM_HIP(hipStreamCreateWithFlags(&R.X[a], hipStreamNonBlocking));
+        build_ops(d, R);
     }
     return GM_OK;
 }
@@ -242,109 +347,103 @@ static void copy_blocks(DistSub *d, const uint8_t *src, const uint32_t *list, ui
     hipLaunchKernelGGL(block_copy_kernel, dim3(n), dim3(256), 0, s, src, list, dst, d->low, pack ? 1 : 0);
 }
 
-static uint32_t cnt(const std::vector<uint32_t> &off, int t) {
-    return (t < 0 || t + 1 >= (int)off.size()) ? 0 : off[t + 1] - off[t];
-}
-static bool is_upper(const SubRank &R, int a) { return (R.rank >> a) & 1; }
-
-// Enqueue one whole solve on the ranks' streams (eager or under capture).
-// S/C of every rank must already be joined to the capture when capturing.
-static int enqueue_solve(Ctx *c, DistSub *d, uint64_t *sent) {
-    const int T = d->ntiers, K = KSLOTS;
-    const uint64_t bbytes = 1ull << (4 * d->low);
-    *sent = 0;
-    for (int t = 0; t < T; t++) {
-        const int u = t - 1;   // tier whose boundary is exchanged at this step
-        // ---- C: exchange tier u
-        for (auto &R : d->ranks) {
-            bool any = false;
-            for (int a = 0; a < d->g; a++) any |= cnt(is_upper(R, a) ? R.recv_off[a] : R.send_off[a], u) > 0;
-            if (!any) continue;
-            GM_HIP(hipStreamWaitEvent(R.C, R.ev_packed[u % K], 0));   // my step u done (send data, recv slot)
-            if (d->loopback) {
-                for (int a = 0; a < d->g; a++) {
-                    if (!is_upper(R, a)) continue;
-                    uint32_t n = cnt(R.recv_off[a], u);
-                    if (!n) continue;
-                    SubRank &L = d->ranks[R.rank ^ (1 << a)];
-                    if (n != cnt(L.send_off[a], u)) { set_error("halo lists disagree"); return GM_E_STATE; }
-                    GM_HIP(hipStreamWaitEvent(R.C, L.ev_packed[u % K], 0));
-                    GM_HIP(hipMemcpyAsync(R.recvbuf[a][u % K], L.sendbuf[a][u % K], n * bbytes,
-                                          hipMemcpyDeviceToDevice, R.C));
-                    *sent += n * bbytes;
-                }
-            } else {
-                GM_NCCL(ncclGroupStart());
-                for (int a = 0; a < d->g; a++) {
-                    int peer = R.rank ^ (1 << a);
-                    if (is_upper(R, a)) {
-                        uint32_t n = cnt(R.recv_off[a], u);
-                        if (n) GM_NCCL(ncclRecv(R.recvbuf[a][u % K], n * bbytes, ncclUint8, peer, c->comm, R.C));
-                    } else {
-                        uint32_t n = cnt(R.send_off[a], u);
-                        if (n) GM_NCCL(ncclSend(R.sendbuf[a][u % K], n * bbytes, ncclUint8, peer, c->comm, R.C));
-                        *sent += n * bbytes;
-                    }
-                }
-                GM_NCCL(ncclGroupEnd());
-            }
-            GM_HIP(hipEventRecord(R.ev_xch[u % K], R.C));
+static int exec_op(DistSub *d, SubRank &R, const Op &o) {
+    const int a = o.axis, j = o.arg;
+    const uint64_t bb = 1ull << (4 * d->low);
+    hipStream_t st = o.on_x ? R.X[a] : R.S;
+    switch (o.kind) {
+    case OP_TIER:
+        launch_sub_tier(d->low, d->high, d->nt, cnt(R.off, j), R.table, R.dlist + R.off[j], d->zero, st);
+        break;
+    case OP_PACK:
+        copy_blocks(d, R.table, R.dsend[a] + R.send_off[a][j], cnt(R.send_off[a], j), send_ptr(d, R, a, j), true,
+                    st);
+        d->sent += cnt(R.send_off[a], j) * bb;
+        break;
+    case OP_UNPACK:
+        copy_blocks(d, recv_ptr(d, R, a, j), R.drecv[a] + R.recv_off[a][j], cnt(R.recv_off[a], j), R.table, false,
+                    st);
+        break;
+    case OP_SEND:
+        GM_NCCL(ncclSend(send_ptr(d, R, a, j), cnt(R.send_off[a], j) * bb, ncclUint8, o.peer, d->comm[a], st));
+        break;
+    case OP_RECV: {
+        const uint64_t n = cnt(R.recv_off[a], j) * bb;
+        if (d->loopback) {
+            const SubRank &L = d->ranks[o.peer];
+            if (cnt(L.send_off[a], j) * bb != n) { set_error("halo lists disagree"); return GM_E_STATE; }
+            GM_HIP(hipMemcpyAsync(recv_ptr(d, R, a, j), send_ptr(d, L, a, j), n, hipMemcpyDeviceToDevice, st));
+        } else {
+            GM_NCCL(ncclRecv(recv_ptr(d, R, a, j), n, ncclUint8, o.peer, d->comm[a], st));
         }
-        // ---- S: compute, unpack, compute, pack
-        for (auto &R : d->ranks) {
-            launch_sub_tier(d->low, d->high, d->nt, cnt(R.offA, t), R.table, R.dA + R.offA[t], d->zero, R.S);
-            bool recv = false;
-            for (int a = 0; a < d->g; a++) recv |= is_upper(R, a) && cnt(R.recv_off[a], u) > 0;
-            if (recv) {
-                GM_HIP(hipStreamWaitEvent(R.S, R.ev_xch[u % K], 0));
-                for (int a = 0; a < d->g; a++)
-                    if (is_upper(R, a))
-                        copy_blocks(d, R.recvbuf[a][u % K], R.drecv[a] + R.recv_off[a][u], cnt(R.recv_off[a], u),
-                                    R.table, false, R.S);
-            }
-            launch_sub_tier(d->low, d->high, d->nt, cnt(R.offB, t), R.table, R.dB + R.offB[t], d->zero, R.S);
-            // slot t % K last carried tier t-K, exchanged at step t-K+1: wait until it has left
-            for (int a = 0; a < d->g; a++) {
-                if (is_upper(R, a) || !cnt(R.send_off[a], t)) continue;
-                if (cnt(R.send_off[a], t - K) > 0) {
-                    if (d->loopback)
-                        GM_HIP(hipStreamWaitEvent(R.S, d->ranks[R.rank ^ (1 << a)].ev_xch[(t - K) % K], 0));
-                    else
-                        GM_HIP(hipStreamWaitEvent(R.S, R.ev_xch[(t - K) % K], 0));
-                }
-                copy_blocks(d, R.table, R.dsend[a] + R.send_off[a][t], cnt(R.send_off[a], t), R.sendbuf[a][t % K],
-                            true, R.S);
-            }
-            GM_HIP(hipEventRecord(R.ev_packed[t % K], R.S));
-        }
+        break;
     }
-    // join every exchange stream back into its compute stream
-    for (auto &R : d->ranks) {
-        GM_HIP(hipEventRecord(R.ev_xch[0], R.C));
-        GM_HIP(hipStreamWaitEvent(R.S, R.ev_xch[0], 0));
+    case OP_RECORD:
+        GM_HIP(hipEventRecord(R.ev[o.ev][a][j % d->nslots], st));
+        R.recorded[o.ev][a] = j + 1;
+        break;
+    case OP_WAIT: {
+        const SubRank &P = d->loopback ? d->ranks[o.peer] : R;
+        GM_HIP(hipStreamWaitEvent(st, P.ev[o.ev][a][j % d->nslots], 0));
+        break;
+    }
     }
     return GM_OK;
 }
 
+// Enqueue one whole solve.  RCCL mode: the single rank's list in order.
+// Loopback: round-robin over the ranks, each running until its next op waits on
+// an event another rank has not enqueued yet.
+static int enqueue_solve(DistSub *d) {
+    for (auto &R : d->ranks) {
+        R.pc = 0;
+        for (auto &k : R.recorded)
+            for (int &x : k) x = 0;
+    }
+    d->sent = 0;
+    for (;;) {
+        bool done = true, progress = false;
+        for (auto &R : d->ranks) {
+            while (R.pc < R.ops.size()) {
+                const Op &o = R.ops[R.pc];
+                if (d->loopback && o.kind == OP_WAIT && o.peer != R.rank &&
+                    d->ranks[o.peer].recorded[o.ev][o.axis] <= o.arg)
+                    break;
+                GM_TRY(exec_op(d, R, o));
+                R.pc++;
+                progress = true;
+            }
+            done &= R.pc == R.ops.size();
+        }
+        if (done) break;
+        if (!progress) { set_error("sharded schedule cannot make progress"); return GM_E_STATE; }
+    }
+    GM_HIP(hipGetLastError());
+    return GM_OK;
+}
+
 // Run one solve: fork every rank's streams off the caller's stream, enqueue, join.
-// Launches are eager: HIP 7.2's stream capture crashes on this multi-stream event
-// pattern (tools/diag_dist.py), and in RCCL mode a capture refused half-way would
+// Launches are eager: in RCCL mode a stream capture refused half-way would
 // leave the ranks' point-to-point sequence numbers out of step.
-static int run_solve(Ctx *c, DistSub *d, uint64_t *sent) {
+static int run_solve(Ctx *c, DistSub *d) {
     hipStream_t H = c->stream;
-    if (!d->loopback) { d->ranks[0].S = c->stream; d->ranks[0].C = c->comm_stream; }
-    // eager
+    if (!d->loopback) d->ranks[0].S = c->stream;
     GM_HIP(hipEventRecord(d->ev_fork, H));
     for (auto &R : d->ranks) {
         if (R.S != H) GM_HIP(hipStreamWaitEvent(R.S, d->ev_fork, 0));
-        GM_HIP(hipStreamWaitEvent(R.C, d->ev_fork, 0));
+        for (int a = 0; a < d->g; a++) GM_HIP(hipStreamWaitEvent(R.X[a], d->ev_fork, 0));
     }
-    GM_TRY(enqueue_solve(c, d, sent));
-    for (auto &R : d->ranks)
-        if (R.S != H) {
-            GM_HIP(hipEventRecord(R.ev_packed[0], R.S));
-            GM_HIP(hipStreamWaitEvent(H, R.ev_packed[0], 0));
+    GM_TRY(enqueue_solve(d));
+    for (auto &R : d->ranks) {
+        for (int a = 0; a < d->g; a++) {
+            GM_HIP(hipEventRecord(R.ev_join[a], R.X[a]));
+            GM_HIP(hipStreamWaitEvent(R.S, R.ev_join[a], 0));
         }
+        if (R.S != H) {
+            GM_HIP(hipEventRecord(R.ev_join[0], R.S));
+            GM_HIP(hipStreamWaitEvent(H, R.ev_join[0], 0));
+        }
+    }
     GM_HIP(hipGetLastError());
     return GM_OK;
 }
@@ -353,7 +452,9 @@ int dist_sub_solve(Ctx *c, uint64_t root) {
     const bool loopback = c->virtual_ranks > 1;
     const int G = loopback ? c->virtual_ranks : c->world;
     DistSub *d = c->dist_sub;
-    if (!d || d->heaps != c->sub.heaps || d->G != G || d->loopback != loopback || d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave ||
+    if (!d || d->heaps != c->sub.heaps || d->G != G || d->loopback != loopback ||
+        d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave || d->want_order != c->sub_order ||
+        d->want_batch != c->dist_batch || d->want_slots != c->dist_slots ||
         (!loopback && c->adopted_dense && d->ranks[0].table != c->adopted_dense)) {
         dist_sub_free(c);
         d = c->dist_sub = new DistSub();
@@ -361,10 +462,10 @@ int dist_sub_solve(Ctx *c, uint64_t root) {
     }
     hipStream_t H = c->stream;
     double t0 = now_ms();
-    uint64_t sent = 0;
     GM_HIP(hipEventRecord(d->ev_t0, H));
-    GM_TRY(run_solve(c, d, &sent));
+    GM_TRY(run_solve(c, d));
     GM_HIP(hipEventRecord(d->ev_t1, H));
+    double t_enq = now_ms();
     // root record: max over ranks of the owner's code (the others contribute 0)
     GM_HIP(hipMemsetAsync(d->d_root, 0, 4, H));
     for (auto &R : d->ranks)
@@ -385,14 +486,15 @@ int dist_sub_solve(Ctx *c, uint64_t root) {
     c->stats.world = G;
     c->stats.solve_ms = t1 - t0;
     c->stats.backward_ms = t1 - t0;
-    c->stats.exchanged_bytes = sent;
+    c->stats.forward_ms = t_enq - t0;   // host time spent enqueueing the solve
+    c->stats.exchanged_bytes = d->sent;
     if (c->timing) {
         float ms = 0;
         GM_HIP(hipEventElapsedTime(&ms, d->ev_t0, d->ev_t1));
         c->stats.kernel_ms = ms;
         uint32_t launches = 0;
         for (auto &R : d->ranks)
-            for (int t = 0; t < d->ntiers; t++) launches += (cnt(R.offA, t) > 0) + (cnt(R.offB, t) > 0);
+            for (int t = 0; t < d->ntiers; t++) launches += cnt(R.off, t) > 0;
         c->stats.kernel_launches = (int32_t)launches;
     }
     uint64_t ownb = 0;
@@ -415,11 +517,9 @@ int dist_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     hipStream_t H = c->stream;
     GM_HIP(hipMemsetAsync(d->d_acc, 0, 16, H));
     for (auto &R : d->ranks) {
-        uint32_t na = R.offA.back(), nb = R.offB.back();
-        if (na) hipLaunchKernelGGL(block_digest_kernel, dim3(std::min<uint32_t>(na, 8192)), dim3(256), 0, H, R.table,
-                                   R.dA, (uint64_t)na, d->low, d->heaps, c->root, d->d_acc);
+        uint32_t nb = R.off.back();
         if (nb) hipLaunchKernelGGL(block_digest_kernel, dim3(std::min<uint32_t>(nb, 8192)), dim3(256), 0, H, R.table,
-                                   R.dB, (uint64_t)nb, d->low, d->heaps, c->root, d->d_acc);
+                                   R.dlist, (uint64_t)nb, d->low, d->heaps, c->root, d->d_acc);
     }
     unsigned long long h[2];
     GM_HIP(hipMemcpyAsync(h, d->d_acc, 16, hipMemcpyDeviceToHost, H));
@@ -436,27 +536,24 @@ int dist_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64
     std::vector<std::pair<uint64_t, uint16_t>> out;
     uint64_t total = 0;
     for (auto &R : d->ranks) {
-        for (int which = 0; which < 2; which++) {
-            uint32_t nb = which ? R.offB.back() : R.offA.back();
-            const uint32_t *lst = which ? R.dB : R.dA;
-            if (!nb) continue;
-            uint8_t *stg;
-            GM_HIP(hipMalloc(&stg, (uint64_t)nb * bsz));
-            copy_blocks(d, R.table, lst, nb, stg, true, H);
-            std::vector<uint8_t> hs((uint64_t)nb * bsz);
-            std::vector<uint32_t> hl(nb);
-            GM_HIP(hipMemcpyAsync(hs.data(), stg, hs.size(), hipMemcpyDeviceToHost, H));
-            GM_HIP(hipMemcpyAsync(hl.data(), lst, nb * 4, hipMemcpyDeviceToHost, H));
-            GM_HIP(hipStreamSynchronize(H));
-            (void)hipFree(stg);
-            for (uint32_t b = 0; b < nb; b++)
-                for (uint64_t i = 0; i < bsz; i++) {
-                    uint64_t key = ((uint64_t)hl[b] << (4 * d->low)) + i;
-                    if (!in_box(key, c->root, d->heaps)) continue;
-                    total++;
-                    if (keys) out.emplace_back(key, record_of_code(hs[(uint64_t)b * bsz + i]));
-                }
-        }
+        uint32_t nb = R.off.back();
+        if (!nb) continue;
+        uint8_t *stg;
+        GM_HIP(hipMalloc(&stg, (uint64_t)nb * bsz));
+        copy_blocks(d, R.table, R.dlist, nb, stg, true, H);
+        std::vector<uint8_t> hs((uint64_t)nb * bsz);
+        std::vector<uint32_t> hl(nb);
+        GM_HIP(hipMemcpyAsync(hs.data(), stg, hs.size(), hipMemcpyDeviceToHost, H));
+        GM_HIP(hipMemcpyAsync(hl.data(), R.dlist, nb * 4, hipMemcpyDeviceToHost, H));
+        GM_HIP(hipStreamSynchronize(H));
+        (void)hipFree(stg);
+        for (uint32_t b = 0; b < nb; b++)
+            for (uint64_t i = 0; i < bsz; i++) {
+                uint64_t key = ((uint64_t)hl[b] << (4 * d->low)) + i;
+                if (!in_box(key, c->root, d->heaps)) continue;
+                total++;
+                if (keys) out.emplace_back(key, record_of_code(hs[(uint64_t)b * bsz + i]));
+            }
     }
     *n = total;
     if (!keys) return GM_OK;
@@ -485,29 +582,26 @@ int dist_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
 void dist_sub_free(Ctx *c) {
     DistSub *d = c->dist_sub;
     if (!d) return;
+    (void)hipDeviceSynchronize();
     for (auto &R : d->ranks) {
         if (R.owned && R.table) (void)hipFree(R.table);
-        if (R.dA) (void)hipFree(R.dA);
-        if (R.dB) (void)hipFree(R.dB);
-        for (int a = 0; a < 3; a++) {
+        if (R.dlist) (void)hipFree(R.dlist);
+        for (int a = 0; a < MAX_AXES; a++) {
             if (R.dsend[a]) (void)hipFree(R.dsend[a]);
             if (R.drecv[a]) (void)hipFree(R.drecv[a]);
-            for (int p = 0; p < KSLOTS; p++) {
-                if (R.sendbuf[a][p]) (void)hipFree(R.sendbuf[a][p]);
-                if (R.recvbuf[a][p]) (void)hipFree(R.recvbuf[a][p]);
-            }
+            if (R.sendbuf[a]) (void)hipFree(R.sendbuf[a]);
+            if (R.recvbuf[a]) (void)hipFree(R.recvbuf[a]);
+            for (int k = 0; k < EV_KINDS; k++)
+                for (auto e : R.ev[k][a]) (void)hipEventDestroy(e);
+            if (R.ev_join[a]) (void)hipEventDestroy(R.ev_join[a]);
+            if (R.X[a]) (void)hipStreamDestroy(R.X[a]);
         }
-        for (int p = 0; p < KSLOTS; p++) {
-            if (R.ev_packed[p]) (void)hipEventDestroy(R.ev_packed[p]);
-            if (R.ev_xch[p]) (void)hipEventDestroy(R.ev_xch[p]);
-        }
-        if (R.own_streams) {
-            (void)hipStreamDestroy(R.S);
-            (void)hipStreamDestroy(R.C);
-        }
+        if (R.own_S) (void)hipStreamDestroy(R.S);
     }
     for (hipEvent_t e : {d->ev_fork, d->ev_t0, d->ev_t1})
         if (e) (void)hipEventDestroy(e);
+    for (int a = 0; a < MAX_AXES; a++)
+        if (d->own_comm[a] && d->comm[a]) (void)ncclCommDestroy(d->comm[a]);
     if (d->zero) (void)hipFree(d->zero);
     if (d->d_acc) (void)hipFree(d->d_acc);
     if (d->d_root) (void)hipFree(d->d_root);

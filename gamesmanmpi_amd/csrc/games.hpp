@@ -2,8 +2,10 @@
 //
 // Each descriptor restates one reference plugin over a u64 key:
 //   primitive(k)          -> WIN/LOSS/TIE/DRAW/UNDECIDED     (plugin primitive())
-//   children(k, out)      -> number of children, keys in out  (gen_moves + do_move,
-//                            i.e. GameState.expand, reference src/game_state.py:33-41)
+//   visit(k, f)           -> calls f(child) for each child in gen_moves order until f
+//                            returns false (gen_moves + do_move, i.e. GameState.expand,
+//                            reference src/game_state.py:33-41); children(k, out)
+//                            collects them into an array
 //   tier(k)               -> a potential that strictly increases along every move;
 //                            children land 1..MAX_SKIP tiers deeper
 //   valid(k)              -> whether k is a position the plugin can represent
@@ -18,6 +20,19 @@
 
 namespace gm {
 
+// children(k, out) of every descriptor: its visit() order (the plugin's gen_moves
+// order) into an array.  Device kernels call visit() directly, so no child array
+// has to live in (scratch) memory.
+template <class D>
+GM_HD int collect(const D &d, uint64_t k, uint64_t *out) {
+    int n = 0;
+    d.visit(k, [&](uint64_t c) {
+        out[n++] = c;
+        return true;
+    });
+    return n;
+}
+
 // ---------------------------------------------------------------- Four-To-One
 // reference test_games/four_to_one.py:8-31 (moves are always -1, -2: the
 // `x == 1` test at :15 compares a str with an int and never fires).
@@ -25,11 +40,11 @@ struct DescF2O {
     static constexpr int MAX_SKIP = 2;
     static constexpr int MAXC = 2;
     GM_HD int primitive(uint64_t k) const { return (int64_t)k <= 0 ? LOSS : UNDECIDED; }
-    GM_HD int children(uint64_t k, uint64_t *out) const {
-        out[0] = k - 1;
-        out[1] = k - 2;
-        return 2;
+    template <class F>
+    GM_HD void visit(uint64_t k, F &&f) const {
+        if (f(k - 1)) f(k - 2);
     }
+    GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
     GM_HD int64_t tier(uint64_t k) const { return -(int64_t)k; }
     GM_HD bool valid(uint64_t k) const {
         int64_t x = (int64_t)k;
@@ -68,16 +83,17 @@ struct DescTTT {
             if (!c[i]) return UNDECIDED;
         return TIE;
     }
-    GM_HD int children(uint64_t k, uint64_t *out) const {
-        int c[9], nx = 0, no = 0, n = 0;
+    template <class F>
+    GM_HD void visit(uint64_t k, F &&f) const {
+        int c[9], nx = 0, no = 0;
         decode(k, c);
         for (int i = 0; i < 9; i++) { nx += c[i] == 1; no += c[i] == 2; }
         uint64_t mover = no >= nx ? 1 : 2;   // mttt.py:39-43
         uint64_t p = 1;
         for (int i = 0; i < 9; i++, p *= 3)
-            if (!c[i]) out[n++] = k + mover * p;
-        return n;
+            if (!c[i] && !f(k + mover * p)) return;
     }
+    GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
     GM_HD int64_t tier(uint64_t k) const {
         int c[9], n = 0;
         decode(k, c);
@@ -135,23 +151,23 @@ struct DescToot {
         bool p1 = pieces & 1;                         // is_player1_turn (:218-219)
         return ((toot > otto) != p1) ? LOSS : WIN;    // :82-85
     }
-    GM_HD int children(uint64_t k, uint64_t *out) const {
+    template <class F>
+    GM_HD void visit(uint64_t k, F &&f) const {
         uint32_t occ = tplane(k) | oplane(k);
         bool p1 = popc64(occ) & 1;
         int tsh = p1 ? 12 : 4, osh = p1 ? 8 : 0;     // get_hand_count (:202-207)
         uint32_t th = (uint32_t)(k >> tsh) & 15u, oh = (uint32_t)(k >> osh) & 15u;
         bool have_t = th >= 1 && th <= 7, have_o = oh >= 1 && oh <= 7;  // signed nibble > 0
-        int n = 0;
         for (int x = 0; x < L; x++) {                 // gen_moves order (:94-99)
             int xr = L - 1 - x;
             if (occ & (1u << xr)) continue;           // top cell (x, H-1) taken
             int filled = popc64(occ & (colmask << xr));
             int bit = L * (H - 1 - filled) + xr;      // lowest empty y (:112-115)
-            if (have_t) out[n++] = k - (1ull << tsh) + (1ull << (A + 16 + bit));
-            if (have_o) out[n++] = k - (1ull << osh) + (1ull << (16 + bit));
+            if (have_t && !f(k - (1ull << tsh) + (1ull << (A + 16 + bit)))) return;
+            if (have_o && !f(k - (1ull << osh) + (1ull << (16 + bit)))) return;
         }
-        return n;
     }
+    GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
     GM_HD int64_t tier(uint64_t k) const { return popc64(tplane(k) | oplane(k)); }
     GM_HD bool valid(uint64_t k) const {
         uint32_t t = tplane(k), o = oplane(k);
@@ -213,7 +229,8 @@ struct DescOthello {
             }
         return all;
     }
-    GM_HD int children(uint64_t k, uint64_t *out) const {
+    template <class F>
+    GM_HD void visit(uint64_t k, F &&fn) const {
         uint32_t w = wplane(k), b = bplane(k);
         int turn = sbyte(k, 8);
         bool black = turn == 1;
@@ -228,11 +245,12 @@ struct DescOthello {
                 if (!f) continue;                                 // legit_move (:370-382)
                 uint32_t nme = me | cell | f, nopp = opp & ~f;
                 uint32_t nw = black ? nopp : nme, nb = black ? nme : nopp;
-                out[n++] = ((uint64_t)nw << (A + 16)) | ((uint64_t)nb << 16) | low;
+                n++;
+                if (!fn(((uint64_t)nw << (A + 16)) | ((uint64_t)nb << 16) | low)) return;
             }
-        if (!n) out[n++] = k + 1;                                 // [None]: pass + 1 (:122-124)
-        return n;
+        if (!n) fn(k + 1);                                        // [None]: pass + 1 (:122-124)
     }
+    GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
     GM_HD int64_t tier(uint64_t k) const {
         return 3 * popc64(wplane(k) | bplane(k)) + sbyte(k, 0);
     }
@@ -253,15 +271,15 @@ struct DescSub {
     static constexpr int MAXC = 16;
     int heaps;
     GM_HD int primitive(uint64_t k) const { return k == 0 ? LOSS : UNDECIDED; }
-    GM_HD int children(uint64_t k, uint64_t *out) const {
-        int n = 0;
+    template <class F>
+    GM_HD void visit(uint64_t k, F &&f) const {
         for (int i = 0; i < heaps; i++) {
             uint64_t h = (k >> (4 * i)) & 15u;
-            if (h >= 1) out[n++] = k - (1ull << (4 * i));
-            if (h >= 2) out[n++] = k - (2ull << (4 * i));
+            if (h >= 1 && !f(k - (1ull << (4 * i)))) return;
+            if (h >= 2 && !f(k - (2ull << (4 * i)))) return;
         }
-        return n;
     }
+    GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
     GM_HD int64_t tier(uint64_t k) const {
         int64_t s = 0;
         for (int i = 0; i < heaps; i++) s += (k >> (4 * i)) & 15u;

@@ -84,6 +84,8 @@ struct Ctx {
     ncclComm_t comm = nullptr;
     int virtual_ranks = 1;   // >1: run that many ranks inside this context (loopback transport)
     hipStream_t comm_stream = nullptr;
+    int dist_batch = 4;      // sharded dense path: tiers per halo exchange
+    int dist_slots = 4;      // sharded dense path: ring of exchange buffers, in batches
 
     // results
     bool solved = false;
@@ -93,6 +95,9 @@ struct Ctx {
     uint16_t root_record = REC_UNSOLVED;
     gm_stats_t stats{};
     std::vector<uint64_t> tier_counts;
+
+    // device buffer cache (dev_alloc / dev_free)
+    std::vector<std::pair<void *, uint64_t>> buf_live, buf_cache;
 
     // adopted buffers
     void *adopted_dense = nullptr;
@@ -146,6 +151,14 @@ int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n);
 void sparse_free(Ctx *c);
 
 double now_ms();
+
+// Device buffers of the per-solve tables, cached per context and reused by the
+// next solve (dev_free keeps the buffer; gm_close releases them).  Buffers are
+// only used on the context's stream, so reuse is stream-ordered.  GM_TRACE=1
+// logs every hipMalloc with its host time.
+int dev_alloc(Ctx *c, void **p, uint64_t bytes);
+void dev_free(Ctx *c, void *p);
+bool trace_on();
 
 }  // namespace gm
 

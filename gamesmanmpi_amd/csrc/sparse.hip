@@ -1,65 +1,248 @@
-// sparse.hip -- level-synchronous frontier expansion + tiered retrograde over
-// per-tier open-addressing tables in HBM (Four-To-One, Toot-and-Otto, Othello;
-// any descriptor).
+// sparse.hip -- level-synchronous frontier expansion + tiered retrograde for
+// games without a dense index (Four-To-One, Toot-and-Otto, Othello; any
+// descriptor).
 //
 // Replaces the reference's asynchronous job loop and its tables:
-//   LOOK_UP / DISTRIBUTE (src/new_process.py:102-162)  -> expand kernel: one lane
-//       per position of tier t evaluates primitive() and, if undecided,
-//       generates its children and inserts them (atomicCAS on u64 keys) into the
-//       tables of tiers t+1..t+MAX_SKIP; the table IS the deduplicated frontier
-//   CacheDict resolved/remote (src/cache_dict.py)      -> per-tier tables:
-//       u64 key[cap] (2^63 = empty) + u16 score[cap], linear probing on mix64(key)
-//   RESOLVE / _res_red (src/new_process.py:223-265)    -> retro kernel, tiers
-//       deepest first: regenerate children, look each up in its tier's table,
-//       u16 max over preference scores, parent score (gm_common.hpp)
-// The reference expands a position once per path that reaches it (tree
-// search); here each distinct position is expanded once.
+//   LOOK_UP / DISTRIBUTE (src/new_process.py:102-162)  -> per tier: the frontier
+//       table (u64 keys, open addressing; children of the tiers above are
+//       atomicCAS-inserted into it, which deduplicates them) is compacted into a
+//       dense key list; classify_kernel evaluates primitive() once per position,
+//       files the position in the tier's resolved table and appends the
+//       undecided ones to the tier's interior list; expand_kernel generates the
+//       interior positions' children into the frontier tables of tiers
+//       t+1..t+MAX_SKIP
+//   CacheDict resolved/remote (src/cache_dict.py)      -> per-tier resolved
+//       tables: 16-byte slots {key, score} at load <= 1/2, so a lookup reads one
+//       cache line, key and score together
+//   RESOLVE / _res_red (src/new_process.py:223-265)    -> retro_kernel, tiers
+//       deepest first, over the interior list: regenerate children; a primitive
+//       child is scored from primitive() with no memory access (a LOSS-in-0
+//       child ends the search: nothing beats it); the others are looked up in
+//       their tier's resolved table; u16 max over preference scores, parent
+//       score (gm_common.hpp), written into the parent's slot
+// Every kernel walks a dense list, so no lane idles on an empty hash slot.  The
+// reference expands a position once per path that reaches it (tree search,
+// SURVEY §0.2); here each distinct position is expanded once.
 #include "sparse_common.hpp"
 
 namespace gm {
 
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+struct alignas(16) RSlot {
+    uint64_t key;
+    uint64_t score;   // u16 preference score in the low bits
+};
+
+struct FrontRef {
+    uint64_t *keys;
+    uint64_t mask;
+    unsigned long long *count;
+};
+struct ResRef {
+    RSlot *s;
+    uint64_t mask;
+};
 template <int S>
-struct NextTables {
-    TableRef t[S];
+struct Fronts {
+    FrontRef t[S];
+};
+template <int S>
+struct Ress {
+    ResRef t[S];
+};
+
+struct SpTier {
+    uint64_t *fkeys = nullptr;   // frontier table (transient: freed once the tier is classified)
+    uint64_t fcap = 0, fcount = 0;
+    RSlot *res = nullptr;        // resolved table
+    uint64_t rcap = 0, count = 0;
+    uint64_t *ikeys = nullptr;   // interior (undecided) positions and their resolved slots
+    uint32_t *islot = nullptr;
+    uint64_t ni = 0;
 };
 
 struct Sparse {
-    std::vector<Table> tiers;
-    unsigned long long *d_counts = nullptr;   // per-tier distinct counts (device)
+    std::vector<SpTier> tiers;
+    unsigned long long *d_counts = nullptr;   // per-tier frontier counts (device)
     uint64_t counts_cap = 0;
-    unsigned long long *d_scratch = nullptr;  // edge counts / digest / export cursor
+    unsigned long long *d_scratch = nullptr;  // [0,S) edges, [8] cursor, [9] interior count, [10] export cursor
     uint32_t *d_err = nullptr;
+    uint64_t *d_dense = nullptr;              // compacted frontier keys (reused)
+    uint64_t dense_cap = 0;
     int64_t t_root = 0;
-    int max_skip = 1;
+    uint64_t edges = 0;
 };
 
+// ----------------------------------------------------------------- device tables
+namespace {
+
+__device__ __forceinline__ bool front_insert(const FrontRef &t, uint64_t key, uint32_t *err) {
+    uint64_t h = mix64(key) & t.mask;
+    for (uint64_t probe = 0; probe <= t.mask; probe++) {
+        uint64_t cur = t.keys[h];
+        if (cur == key) return false;
+        if (cur == EMPTY_KEY) {
+            unsigned long long prev = atomicCAS((unsigned long long *)&t.keys[h], (unsigned long long)EMPTY_KEY,
+                                                (unsigned long long)key);
+            if (prev == EMPTY_KEY) return true;
+            if (prev == key) return false;
+        }
+        h = (h + 1) & t.mask;
+    }
+    atomicOr(err, DEV_ERR_TABLE_FULL);
+    return false;
+}
+
+// file a key that is known to be new (keys arrive deduplicated)
+__device__ __forceinline__ uint32_t res_insert(const ResRef &t, uint64_t key, uint16_t score, uint32_t *err) {
+    uint64_t h = mix64(key) & t.mask;
+    for (uint64_t probe = 0; probe <= t.mask; probe++) {
+        unsigned long long prev = atomicCAS((unsigned long long *)&t.s[h].key, (unsigned long long)EMPTY_KEY,
+                                            (unsigned long long)key);
+        if (prev == EMPTY_KEY) {
+            t.s[h].score = score;
+            return (uint32_t)h;
+        }
+        h = (h + 1) & t.mask;
+    }
+    atomicOr(err, DEV_ERR_TABLE_FULL);
+    return 0;
+}
+
+// score of key, or -1 when absent; each probe is one 16-byte load
+__device__ __forceinline__ int res_find(const ResRef &t, uint64_t key) {
+    if (!t.s) return -1;
+    uint64_t h = mix64(key) & t.mask;
+    for (uint64_t probe = 0; probe <= t.mask; probe++) {
+        const u64x2 v = *(const u64x2 *)&t.s[h];
+        if (v[0] == key) return (int)(v[1] & 0xFFFFu);
+        if (v[0] == EMPTY_KEY) return -1;
+        h = (h + 1) & t.mask;
+    }
+    return -1;
+}
+
+}  // namespace
+
 // ----------------------------------------------------------------- kernels
+__global__ void res_fill_kernel(RSlot *s, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        *(u64x2 *)&s[i] = u64x2{EMPTY_KEY, 0};
+}
+
+__global__ void front_rehash_kernel(const uint64_t *__restrict__ okeys, uint64_t ocap, FrontRef dst, uint32_t *err) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ocap;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t k = okeys[i];
+        if (k != EMPTY_KEY) front_insert(dst, k, err);
+    }
+}
+
+__global__ void front_insert_one_kernel(FrontRef t, uint64_t key, uint32_t *err) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && front_insert(t, key, err)) atomicAdd(t.count, 1ull);
+}
+
+// Stream compaction of a frontier table into a dense key list.  A workgroup
+// takes CROWS rows of 256 slots, ranks its valid keys through LDS and reserves
+// its output range with ONE atomic (a per-wave atomic on one counter serialises
+// at ~90 per microsecond and dominated this pass).
+constexpr int CROWS = 16;
+__global__ __launch_bounds__(256) void compact_kernel(const uint64_t *__restrict__ keys, uint64_t cap,
+                                                      uint64_t *__restrict__ out, unsigned long long *cursor) {
+    __shared__ uint32_t woff[CROWS * 4];
+    __shared__ unsigned long long sbase;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint64_t chunk = blockIdx.x * (256ull * CROWS); chunk < cap; chunk += (uint64_t)gridDim.x * 256ull * CROWS) {
+        uint64_t k[CROWS], m[CROWS];
+#pragma unroll
+        for (int r = 0; r < CROWS; r++) {
+            const uint64_t i = chunk + 256ull * r + threadIdx.x;
+            k[r] = i < cap ? keys[i] : EMPTY_KEY;
+        }
+#pragma unroll
+        for (int r = 0; r < CROWS; r++) {
+            m[r] = __ballot(k[r] != EMPTY_KEY);
+            if (lane == 0) woff[r * 4 + w] = (uint32_t)__popcll(m[r]);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (int j = 0; j < CROWS * 4; j++) {
+                const uint32_t c = woff[j];
+                woff[j] = acc;
+                acc += c;
+            }
+            sbase = acc ? atomicAdd(cursor, (unsigned long long)acc) : 0ull;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < CROWS; r++)
+            if (k[r] != EMPTY_KEY) out[sbase + woff[r * 4 + w] + __popcll(m[r] & below)] = k[r];
+        __syncthreads();
+    }
+}
+
+// one atomic per workgroup step: rank of this lane's item among the block's items
+__device__ __forceinline__ uint64_t block_reserve(bool v, unsigned long long *cursor, uint32_t *woff,
+                                                  unsigned long long *sbase) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t m = __ballot(v);
+    if (lane == 0) woff[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t a = woff[0], b = woff[1], c = woff[2], d = woff[3], tot = a + b + c + d;
+        woff[0] = 0; woff[1] = a; woff[2] = a + b; woff[3] = a + b + c;
+        *sbase = tot ? atomicAdd(cursor, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    const uint64_t at = *sbase + woff[w] + __popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();
+    return at;
+}
+
+// primitive() once per position; file it; list the undecided; count their edges per tier step
 template <class D>
-__global__ __launch_bounds__(256) void count_edges_kernel(D d, const uint64_t *__restrict__ keys,
-                                                          uint64_t cap, unsigned long long *edges,
-                                                          uint32_t *err) {
+__global__ __launch_bounds__(256) void classify_kernel(D d, const uint64_t *__restrict__ dense, uint64_t n,
+                                                       ResRef rt, uint64_t *__restrict__ ikeys,
+                                                       uint32_t *__restrict__ islot, unsigned long long *icount,
+                                                       unsigned long long *edges, uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
+    __shared__ uint32_t woff[4];
+    __shared__ unsigned long long sbase;
     uint64_t cnt[S];
 #pragma unroll
     for (int s = 0; s < S; s++) cnt[s] = 0;
-    uint64_t kids[D::MAXC];
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t k = keys[i];
-        if (k == EMPTY_KEY) continue;
-        int p = d.primitive(k);
-        if (p != UNDECIDED) {
+    for (uint64_t base = blockIdx.x * 256ull; base < n; base += (uint64_t)gridDim.x * 256ull) {
+        const uint64_t i = base + threadIdx.x;
+        bool interior = false;
+        uint32_t slot = 0;
+        uint64_t k = 0;
+        if (i < n) {
+            k = dense[i];
+            const int p = d.primitive(k);
             if (p == DRAW) atomicOr(err, DEV_ERR_DRAW);
-            continue;
-        }
-        int n = d.children(k, kids);
-        if (!n) atomicOr(err, DEV_ERR_NOMOVES);
-        int64_t tk = d.tier(k);
-        for (int c = 0; c < n; c++) {
-            int64_t dt = d.tier(kids[c]) - tk;
-            if (dt < 1 || dt > S) { atomicOr(err, DEV_ERR_TIER); continue; }
+            interior = p == UNDECIDED;
+            slot = res_insert(rt, k, interior ? 0 : score_of_primitive(p), err);
+            if (interior) {
+                const int64_t tk = d.tier(k);
+                int nk = 0;
+                d.visit(k, [&](uint64_t c) {
+                    const int64_t dt = d.tier(c) - tk;
+                    nk++;
+                    if (dt < 1 || dt > S) atomicOr(err, DEV_ERR_TIER);
 #pragma unroll
-            for (int s = 0; s < S; s++) cnt[s] += dt == s + 1;
+                    for (int s = 0; s < S; s++) cnt[s] += dt == s + 1;
+                    return true;
+                });
+                if (!nk) atomicOr(err, DEV_ERR_NOMOVES);
+            }
+        }
+        const uint64_t at = block_reserve(interior, icount, woff, &sbase);
+        if (interior) {
+            ikeys[at] = k;
+            islot[at] = slot;
         }
     }
 #pragma unroll
@@ -67,84 +250,95 @@ __global__ __launch_bounds__(256) void count_edges_kernel(D d, const uint64_t *_
 }
 
 template <class D>
-__global__ __launch_bounds__(256) void expand_kernel(D d, const uint64_t *__restrict__ keys,
-                                                     uint16_t *__restrict__ score, uint64_t cap,
-                                                     NextTables<D::MAX_SKIP> next, uint32_t *err) {
+__global__ __launch_bounds__(256) void expand_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n,
+                                                     Fronts<D::MAX_SKIP> next, uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
     uint64_t fresh[S];
 #pragma unroll
     for (int s = 0; s < S; s++) fresh[s] = 0;
-    uint64_t kids[D::MAXC];
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t k = keys[i];
-        if (k == EMPTY_KEY) continue;
-        int p = d.primitive(k);
-        if (p != UNDECIDED) {
-            score[i] = score_of_primitive(p);
-            continue;
-        }
-        score[i] = 0;
-        int n = d.children(k, kids);
-        int64_t tk = d.tier(k);
-        for (int c = 0; c < n; c++) {
-            int64_t dt = d.tier(kids[c]) - tk;
+        const uint64_t k = ikeys[i];
+        const int64_t tk = d.tier(k);
+        d.visit(k, [&](uint64_t c) {
+            const int64_t dt = d.tier(c) - tk;
 #pragma unroll
             for (int s = 0; s < S; s++)
-                if (dt == s + 1 && table_insert(next.t[s], kids[c], err)) fresh[s]++;
-        }
+                if (dt == s + 1 && front_insert(next.t[s], c, err)) fresh[s]++;
+            return true;
+        });
     }
 #pragma unroll
     for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
 }
 
 template <class D>
-__global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restrict__ keys,
-                                                    uint16_t *__restrict__ score, uint64_t cap,
-                                                    NextTables<D::MAX_SKIP> next, uint32_t *err) {
+__global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restrict__ ikeys,
+                                                    const uint32_t *__restrict__ islot, uint64_t n, ResRef self,
+                                                    Ress<D::MAX_SKIP> next, uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
-    uint64_t kids[D::MAXC];
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t k = keys[i];
-        if (k == EMPTY_KEY || score[i]) continue;   // empty slot or primitive
-        int n = d.children(k, kids);
-        int64_t tk = d.tier(k);
+        const uint64_t k = ikeys[i];
+        const int64_t tk = d.tier(k);
         uint32_t best = 0;
-        for (int c = 0; c < n; c++) {
-            int64_t dt = d.tier(kids[c]) - tk;
-            uint32_t sc = 0;
+        d.visit(k, [&](uint64_t c) {
+            const int p = d.primitive(c);
+            uint32_t sc;
+            if (p != UNDECIDED) {
+                sc = score_of_primitive(p);
+            } else {
+                const int64_t dt = d.tier(c) - tk;
+                int f = -1;
 #pragma unroll
-            for (int s = 0; s < S; s++)
-                if (dt == s + 1) {
-                    int64_t slot = table_find(next.t[s], kids[c]);
-                    if (slot < 0) atomicOr(err, DEV_ERR_MISSING_CHILD);
-                    else sc = next.t[s].score[slot];
-                }
+                for (int s = 0; s < S; s++)
+                    if (dt == s + 1) f = res_find(next.t[s], c);
+                if (f < 0) { atomicOr(err, DEV_ERR_MISSING_CHILD); f = 0; }
+                sc = (uint32_t)f;
+            }
             best = max(best, sc);
-        }
+            return best != 0xFFFFu;   // a LOSS-in-0 child: nothing can beat it
+        });
         if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
-        score[i] = parent_score(best);
+        self.s[islot[i]].score = parent_score(best);
     }
 }
 
-__global__ void insert_one_kernel(TableRef t, uint64_t key, uint32_t *err) {
-    if (threadIdx.x == 0 && blockIdx.x == 0 && table_insert(t, key, err)) atomicAdd(t.count, 1ull);
-}
-
 template <class D>
-__global__ void query_kernel(D d, int64_t t_root, const TableRef *tabs, int ntabs,
-                             const uint64_t *__restrict__ keys, uint16_t *__restrict__ out, uint64_t n) {
+__global__ void query_kernel(D d, int64_t t_root, const ResRef *tabs, int ntabs, const uint64_t *__restrict__ keys,
+                             uint16_t *__restrict__ out, uint64_t n) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t k = keys[i];
     int64_t t = d.valid(k) ? d.tier(k) - t_root : -1;
     uint16_t r = REC_UNSOLVED;
-    if (t >= 0 && t < ntabs && tabs[t].mask) {
-        int64_t s = table_find(tabs[t], k);
-        if (s >= 0) r = record_of_score(tabs[t].score[s]);
+    if (t >= 0 && t < ntabs) {
+        int s = res_find(tabs[t], k);
+        if (s >= 0) r = record_of_score((uint16_t)s);
     }
     out[i] = r;
+}
+
+__global__ void res_digest_kernel(const RSlot *__restrict__ s, uint64_t cap, unsigned long long *acc) {
+    uint64_t sum = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const u64x2 v = *(const u64x2 *)&s[i];
+        if (v[0] != EMPTY_KEY) sum += digest_term(v[0], record_of_score((uint16_t)v[1]));
+    }
+    wave_add(acc, sum);
+}
+
+__global__ void res_gather_kernel(const RSlot *__restrict__ s, uint64_t cap, uint64_t *okeys, uint16_t *orec,
+                                  unsigned long long *cursor) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const u64x2 v = *(const u64x2 *)&s[i];
+        if (v[0] == EMPTY_KEY) continue;
+        unsigned long long at = atomicAdd(cursor, 1ull);
+        okeys[at] = v[0];
+        orec[at] = record_of_score((uint16_t)v[1]);
+    }
 }
 
 // ----------------------------------------------------------------- host side
@@ -163,18 +357,37 @@ static int ensure_counts(Sparse *sp, size_t n) {
     return GM_OK;
 }
 
-static TableRef ref_of(Sparse *sp, size_t t) {
-    Table &T = sp->tiers[t];
-    TableRef r;
-    r.keys = T.keys;
-    r.score = T.score;
-    r.mask = T.cap ? T.cap - 1 : 0;
-    r.count = sp->d_counts + t;
-    return r;
+static FrontRef front_ref(Sparse *sp, size_t t) {
+    SpTier &T = sp->tiers[t];
+    return FrontRef{T.fkeys, T.fcap ? T.fcap - 1 : 0, sp->d_counts + t};
 }
 
-static int resize_tier(Ctx *c, Sparse *sp, size_t t, uint64_t cap) {
-    return resize_table(c->stream, sp->tiers[t], cap, sp->d_err);
+static ResRef res_ref(Sparse *sp, size_t t) {
+    SpTier &T = sp->tiers[t];
+    return ResRef{T.res, T.rcap ? T.rcap - 1 : 0};
+}
+
+static int front_alloc(Ctx *c, uint64_t **keys, uint64_t cap) {
+    GM_TRY(dev_alloc(c, (void **)keys, cap * 8));
+    hipLaunchKernelGGL(fill_empty_kernel, dim3(grid_for(cap)), dim3(256), 0, c->stream, *keys, cap);
+    return GM_OK;
+}
+
+// grow tier t's frontier table to `cap` slots (re-inserting what it holds)
+static int front_grow(Ctx *c, Sparse *sp, size_t t, uint64_t cap) {
+    SpTier &T = sp->tiers[t];
+    uint64_t *nk;
+    GM_TRY(front_alloc(c, &nk, cap));
+    if (T.fcap) {
+        FrontRef dst{nk, cap - 1, nullptr};
+        // the count is unchanged by a re-insert; front_insert only touches it via the caller
+        hipLaunchKernelGGL(front_rehash_kernel, dim3(grid_for(T.fcap)), dim3(256), 0, c->stream, T.fkeys, T.fcap, dst,
+                           sp->d_err);
+        dev_free(c, T.fkeys);
+    }
+    T.fkeys = nk;
+    T.fcap = cap;
+    return GM_OK;
 }
 
 static int read_err(Ctx *c, Sparse *sp) {
@@ -189,7 +402,6 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     constexpr int S = D::MAX_SKIP;
     sparse_free(c);
     Sparse *sp = c->sp = new Sparse();
-    sp->max_skip = S;
     sp->t_root = d.tier(root);
     GM_HIP(hipMalloc(&sp->d_scratch, 64 * sizeof(unsigned long long)));
     GM_HIP(hipMalloc(&sp->d_err, 4));
@@ -198,75 +410,114 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     double t0 = now_ms();
 
     sp->tiers.resize(1);
-    GM_TRY(alloc_table(c->stream, sp->tiers[0], 1024));
-    hipLaunchKernelGGL(insert_one_kernel, dim3(1), dim3(64), 0, c->stream, ref_of(sp, 0), root, sp->d_err);
-    sp->tiers[0].count = 1;
+    GM_TRY(front_alloc(c, &sp->tiers[0].fkeys, 1024));
+    sp->tiers[0].fcap = 1024;
+    hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, front_ref(sp, 0), root, sp->d_err);
+    sp->tiers[0].fcount = 1;
 
     // ---------------- forward: tier by tier
     for (size_t t = 0; t < sp->tiers.size(); t++) {
-        if (!sp->tiers[t].count) continue;
-        Table &T = sp->tiers[t];
-        // final now: shrink to load <= 1/2 (improves retro probing and memory)
-        uint64_t want = pow2_at_least(2 * T.count);
-        if (T.cap > 2 * want) GM_TRY(resize_tier(c, sp, t, want));
-        GM_HIP(hipMemsetAsync(sp->d_scratch, 0, S * sizeof(unsigned long long), c->stream));
-        hipLaunchKernelGGL(count_edges_kernel<D>, dim3(grid_for(sp->tiers[t].cap)), dim3(256), 0, c->stream, d,
-                           sp->tiers[t].keys, sp->tiers[t].cap, sp->d_scratch, sp->d_err);
-        unsigned long long edges[S];
-        GM_HIP(hipMemcpyAsync(edges, sp->d_scratch, S * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                              c->stream));
+        if (!sp->tiers[t].fcount) {
+            dev_free(c, sp->tiers[t].fkeys);
+            sp->tiers[t].fkeys = nullptr;
+            continue;
+        }
+        const uint64_t n = sp->tiers[t].fcount;
+        // 1. frontier table -> dense key list
+        if (sp->dense_cap < n) {
+            dev_free(c, sp->d_dense);
+            sp->dense_cap = std::max<uint64_t>(n + n / 4, 1 << 16);
+            GM_TRY(dev_alloc(c, (void **)&sp->d_dense, sp->dense_cap * 8));
+        }
+        GM_HIP(hipMemsetAsync(sp->d_scratch, 0, 16 * sizeof(unsigned long long), c->stream));
+        hipLaunchKernelGGL(compact_kernel, dim3(grid_for(sp->tiers[t].fcap)), dim3(256), 0, c->stream,
+                           sp->tiers[t].fkeys, sp->tiers[t].fcap, sp->d_dense, sp->d_scratch + 8);
+        // 2. resolved table (load <= 1/2) + interior list, filled by classify
+        {
+            SpTier &T = sp->tiers[t];
+            T.rcap = pow2_at_least(2 * n);
+            GM_TRY(dev_alloc(c, (void **)&T.res, T.rcap * sizeof(RSlot)));
+            GM_TRY(dev_alloc(c, (void **)&T.ikeys, n * 8));
+            GM_TRY(dev_alloc(c, (void **)&T.islot, n * 4));
+            hipLaunchKernelGGL(res_fill_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap);
+            hipLaunchKernelGGL(classify_kernel<D>, dim3(grid_for(n)), dim3(256), 0, c->stream, d, sp->d_dense, n,
+                               res_ref(sp, t), T.ikeys, T.islot, sp->d_scratch + 9, sp->d_scratch, sp->d_err);
+            GM_HIP(hipGetLastError());
+        }
+        unsigned long long sc[10];
+        GM_HIP(hipMemcpyAsync(sc, sp->d_scratch, sizeof sc, hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
         GM_TRY(read_err(c, sp));
+        if (sc[8] != n) {
+            set_error("tier %zu: compacted %llu keys, expected %llu", t, sc[8], (unsigned long long)n);
+            return GM_E_STATE;
+        }
+        sp->tiers[t].count = n;
+        sp->tiers[t].ni = sc[9];
+        dev_free(c, sp->tiers[t].fkeys);
+        sp->tiers[t].fkeys = nullptr;
+        sp->tiers[t].fcap = 0;
+        if (!sp->tiers[t].ni) continue;
+        // 3. size the frontier tables of the tiers the children land in
         if (sp->tiers.size() < t + S + 1) sp->tiers.resize(t + S + 1);
         GM_TRY(ensure_counts(sp, sp->tiers.size()));
         for (int s = 0; s < S; s++) {
-            size_t u = t + 1 + s;
-            uint64_t need = pow2_at_least((sp->tiers[u].count + edges[s]) * 5 / 4 + 1);
-            if (edges[s] && sp->tiers[u].cap < need) GM_TRY(resize_tier(c, sp, u, need));
+            const size_t u = t + 1 + s;
+            sp->edges += sc[s];
+            const uint64_t need = pow2_at_least((sp->tiers[u].fcount + sc[s]) * 5 / 4 + 1);
+            if (sc[s] && sp->tiers[u].fcap < need) GM_TRY(front_grow(c, sp, u, need));
         }
-        NextTables<S> nx;
-        for (int s = 0; s < S; s++) nx.t[s] = ref_of(sp, t + 1 + s);
-        hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(sp->tiers[t].cap)), dim3(256), 0, c->stream, d,
-                           sp->tiers[t].keys, sp->tiers[t].score, sp->tiers[t].cap, nx, sp->d_err);
+        // 4. expand the interior positions
+        Fronts<S> nx;
+        for (int s = 0; s < S; s++) nx.t[s] = front_ref(sp, t + 1 + s);
+        hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(sp->tiers[t].ni)), dim3(256), 0, c->stream, d,
+                           sp->tiers[t].ikeys, sp->tiers[t].ni, nx, sp->d_err);
         GM_HIP(hipGetLastError());
         std::vector<unsigned long long> cnt(sp->tiers.size());
         GM_HIP(hipMemcpyAsync(cnt.data(), sp->d_counts, cnt.size() * sizeof(unsigned long long),
                               hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
         GM_TRY(read_err(c, sp));
-        for (size_t u = 0; u < cnt.size(); u++) sp->tiers[u].count = cnt[u];
+        for (size_t u = t + 1; u < cnt.size(); u++) sp->tiers[u].fcount = cnt[u];
+        if (trace_on())
+            fprintf(stderr, "[gm] tier %zu: %llu positions, %llu interior, %llu edges, at %.1f ms\n", t,
+                    (unsigned long long)n, (unsigned long long)sp->tiers[t].ni, (unsigned long long)sc[0],
+                    now_ms() - t0);
     }
     while (!sp->tiers.empty() && !sp->tiers.back().count) sp->tiers.pop_back();
+    dev_free(c, sp->d_dense);
+    sp->d_dense = nullptr;
+    sp->dense_cap = 0;
     double t1 = now_ms();
 
     // ---------------- backward: deepest tier first
     for (size_t tt = sp->tiers.size(); tt-- > 0;) {
-        Table &T = sp->tiers[tt];
-        if (!T.count) continue;
-        NextTables<S> nx;
+        SpTier &T = sp->tiers[tt];
+        if (!T.ni) continue;
+        Ress<S> nx;
         for (int s = 0; s < S; s++) {
-            size_t u = tt + 1 + s;
-            nx.t[s] = u < sp->tiers.size() ? ref_of(sp, u) : TableRef{nullptr, nullptr, 0, nullptr};
+            const size_t u = tt + 1 + s;
+            nx.t[s] = u < sp->tiers.size() ? res_ref(sp, u) : ResRef{nullptr, 0};
         }
-        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, d, T.keys, T.score,
-                           T.cap, nx, sp->d_err);
+        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, d, T.ikeys, T.islot, T.ni,
+                           res_ref(sp, tt), nx, sp->d_err);
     }
     GM_HIP(hipGetLastError());
     GM_TRY(read_err(c, sp));
     double t2 = now_ms();
 
-    // root record
     {
         uint64_t rk[1] = {root};
         uint16_t rr[1];
         GM_TRY(sparse_query(c, rk, rr, 1));
         c->root_record = rr[0];
     }
-    uint64_t n = 0;
+    uint64_t n = 0, tb = 0;
     c->tier_counts.clear();
     for (auto &T : sp->tiers) {
         n += T.count;
         c->tier_counts.push_back(T.count);
+        tb += T.rcap * sizeof(RSlot) + T.ni * 12;
     }
     c->n_positions = n;
     c->stats.n_positions = n;
@@ -274,8 +525,9 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     c->stats.forward_ms = t1 - t0;
     c->stats.backward_ms = t2 - t1;
     c->stats.solve_ms = t2 - t0;
-    uint64_t tb = 0;
-    for (auto &T : sp->tiers) tb += T.cap * 10;
+    c->stats.n_edges = sp->edges;
+    // SURVEY §8d sparse model: 8 (parent key) + 8 d (child keys) + 8 d (dedup) + 2 (1 + d) per position
+    c->stats.algo_bytes = 10 * n + 18 * sp->edges;
     c->stats.table_bytes = tb;
     return GM_OK;
 }
@@ -292,30 +544,25 @@ int sparse_solve(Ctx *c, uint64_t root) {
     return GM_E_GAME;
 }
 
-static int sparse_query_refs(Ctx *c, Sparse *sp, TableRef **d_tabs) {
-    std::vector<TableRef> h(sp->tiers.size());
-    for (size_t t = 0; t < h.size(); t++) h[t] = ref_of(sp, t);
-    GM_HIP(hipMalloc(d_tabs, std::max<size_t>(1, h.size()) * sizeof(TableRef)));
-    GM_HIP(hipMemcpy(*d_tabs, h.data(), h.size() * sizeof(TableRef), hipMemcpyHostToDevice));
-    return GM_OK;
-}
-
 template <class D>
-static void launch_query(Ctx *c, const D &d, Sparse *sp, TableRef *tabs, const uint64_t *dk, uint16_t *dr,
+static void launch_query(Ctx *c, const D &d, Sparse *sp, ResRef *tabs, const uint64_t *dk, uint16_t *dr,
                          uint64_t n) {
-    hipLaunchKernelGGL(query_kernel<D>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d,
-                       sp->t_root, tabs, (int)sp->tiers.size(), dk, dr, n);
+    hipLaunchKernelGGL(query_kernel<D>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d, sp->t_root,
+                       tabs, (int)sp->tiers.size(), dk, dr, n);
 }
 
 int sparse_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     Sparse *sp = c->sp;
     if (!n) return GM_OK;
-    TableRef *tabs;
-    GM_TRY(sparse_query_refs(c, sp, &tabs));
+    std::vector<ResRef> h(sp->tiers.size());
+    for (size_t t = 0; t < h.size(); t++) h[t] = res_ref(sp, t);
+    ResRef *tabs;
     uint64_t *dk;
     uint16_t *dr;
+    GM_HIP(hipMalloc(&tabs, std::max<size_t>(1, h.size()) * sizeof(ResRef)));
     GM_HIP(hipMalloc(&dk, n * 8));
     GM_HIP(hipMalloc(&dr, n * 2));
+    if (!h.empty()) GM_HIP(hipMemcpyAsync(tabs, h.data(), h.size() * sizeof(ResRef), hipMemcpyHostToDevice, c->stream));
     GM_HIP(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
     switch (c->game) {
     case GM_GAME_FOUR_TO_ONE: launch_query(c, c->f2o, sp, tabs, dk, dr, n); break;
@@ -326,9 +573,9 @@ int sparse_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     }
     GM_HIP(hipMemcpyAsync(recs, dr, n * 2, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
-    hipFree(dk);
-    hipFree(dr);
-    hipFree(tabs);
+    (void)hipFree(dk);
+    (void)hipFree(dr);
+    (void)hipFree(tabs);
     return GM_OK;
 }
 
@@ -338,24 +585,26 @@ int sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t
     for (auto &T : sp->tiers) total += T.count;
     *n = total;
     if (!keys) return GM_OK;
-    if (cap < total) { set_error("export buffer holds %llu, need %llu", (unsigned long long)cap,
-                                 (unsigned long long)total); return GM_E_CAP; }
+    if (cap < total) {
+        set_error("export buffer holds %llu, need %llu", (unsigned long long)cap, (unsigned long long)total);
+        return GM_E_CAP;
+    }
     uint64_t *dk;
     uint16_t *dr;
     GM_HIP(hipMalloc(&dk, std::max<uint64_t>(1, total) * 8));
     GM_HIP(hipMalloc(&dr, std::max<uint64_t>(1, total) * 2));
-    GM_HIP(hipMemsetAsync(sp->d_scratch, 0, 8, c->stream));
+    GM_HIP(hipMemsetAsync(sp->d_scratch + 10, 0, 8, c->stream));
     for (auto &T : sp->tiers)
         if (T.count)
-            hipLaunchKernelGGL(gather_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.keys, T.score,
-                               T.cap, dk, dr, sp->d_scratch);
+            hipLaunchKernelGGL(res_gather_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap, dk,
+                               dr, sp->d_scratch + 10);
     std::vector<uint64_t> hk(total);
     std::vector<uint16_t> hr(total);
     GM_HIP(hipMemcpyAsync(hk.data(), dk, total * 8, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipMemcpyAsync(hr.data(), dr, total * 2, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
-    hipFree(dk);
-    hipFree(dr);
+    (void)hipFree(dk);
+    (void)hipFree(dr);
     std::vector<uint64_t> idx(total);
     for (uint64_t i = 0; i < total; i++) idx[i] = i;
     std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return hk[a] < hk[b]; });
@@ -368,16 +617,16 @@ int sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t
 
 int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     Sparse *sp = c->sp;
-    GM_HIP(hipMemsetAsync(sp->d_scratch, 0, 8, c->stream));
+    GM_HIP(hipMemsetAsync(sp->d_scratch + 10, 0, 8, c->stream));
     uint64_t total = 0;
     for (auto &T : sp->tiers) {
         total += T.count;
         if (T.count)
-            hipLaunchKernelGGL(digest_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.keys, T.score,
-                               T.cap, sp->d_scratch);
+            hipLaunchKernelGGL(res_digest_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap,
+                               sp->d_scratch + 10);
     }
     unsigned long long h;
-    GM_HIP(hipMemcpyAsync(&h, sp->d_scratch, 8, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipMemcpyAsync(&h, sp->d_scratch + 10, 8, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     *digest = h;
     *n = total;
@@ -387,10 +636,13 @@ int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
 void sparse_free(Ctx *c) {
     Sparse *sp = c->sp;
     if (!sp) return;
-    for (auto &T : sp->tiers) free_table(T);
-    if (sp->d_counts) hipFree(sp->d_counts);
-    if (sp->d_scratch) hipFree(sp->d_scratch);
-    if (sp->d_err) hipFree(sp->d_err);
+    for (auto &T : sp->tiers)
+        for (void *p : {(void *)T.fkeys, (void *)T.res, (void *)T.ikeys, (void *)T.islot}) dev_free(c, p);
+    dev_free(c, sp->d_dense);
+    sp->d_dense = nullptr;
+    (void)hipStreamSynchronize(c->stream);
+    for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err})
+        if (p) (void)hipFree(p);
     delete sp;
     c->sp = nullptr;
 }

@@ -79,7 +79,9 @@ enum {
                                 the multi-GPU partition on a single device */
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
     GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path: blocks per workgroup, 4 (interleaved, default) or 1 */
-    GM_OPT_SUB_ORDER = 8    /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton (default) */
+    GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton (default) */
+    GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
+    GM_OPT_DIST_SLOTS = 10  /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
 };
 
 /* Buffer roles for gm_adopt_buffer. */
@@ -104,6 +106,7 @@ typedef struct {
     double kernel_ms;       /* GM_OPT_TIMING: summed event time of the dominant kernel's launches */
     int32_t kernel_launches;/* GM_OPT_TIMING: number of those launches */
     int32_t engine;         /* GM_ENGINE_DENSE or GM_ENGINE_SPARSE */
+    uint64_t n_edges;       /* sparse path: parent->child edges expanded (this rank) */
 } gm_stats_t;
 
 /* Library version (GM_ABI_VERSION). */

@@ -17,10 +17,12 @@ pytestmark = pytest.mark.gpu
 F2O, TTT, TOOT, OTH, SUB = 1, 2, 3, 4, 5
 
 
-def _solve(game, params, ranks, root=None, engine=None):
+def _solve(game, params, ranks, root=None, engine=None, **opts):
     ctx = Context(game, params, device=0)
     if engine is not None:
         ctx.set_option(_lib.OPT_ENGINE, engine)
+    for k, v in opts.items():
+        ctx.set_option(getattr(_lib, "OPT_" + k.upper()), v)
     if ranks > 1:
         ctx.set_option(_lib.OPT_VIRTUAL_RANKS, ranks)
     if root is None:
@@ -37,6 +39,16 @@ def test_dense_sharded_vs_oracle(oracle, heaps, ranks):
     k, r = ctx.export()
     assert n == 16 ** heaps
     assert np.array_equal(k, np.arange(16 ** heaps, dtype=np.uint64))
+    assert np.array_equal(r, ref)
+
+
+@pytest.mark.parametrize("batch,slots", [(1, 1), (1, 4), (2, 1), (3, 2), (4, 4), (8, 2), (16, 1), (100, 4)])
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_dense_sharded_batches_and_rings(oracle, batch, slots, ranks):
+    """Every halo batch size and send-ring depth gives the oracle's table (6 heaps: 46 tiers)."""
+    ref = oracle.subtract_dense(6)
+    ctx, n, rec = _solve(SUB, (6,), ranks, dist_batch=batch, dist_slots=slots)
+    k, r = ctx.export()
     assert np.array_equal(r, ref)
 
 
