@@ -232,7 +232,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic_launch,
-                     "kernel": "sub_tier_kernel_x4<%d>" % (args.heaps - 3),
+                     "kernel": "sub_tier_kernel_b4<%d>" % (args.heaps - 3),
                      "launches_per_solve": launches_per_solve,
                      "avg_launch_us": avg_launch_s * 1e6,
                      "kernel_ms_per_solve": kernel_ms / max(1, args.steps),

@@ -230,13 +230,29 @@ __global__ __launch_bounds__(NT) void sub_tier_kernel(uint8_t *__restrict__ tabl
 }
 
 // ---------------------------------------------------------------------------
+// Anti-diagonal order of the 256 (a0, a1) pairs of a 16 x 16 plane: sorted by
+// s = a0 + a1, then by a1.  diag_base(s) = pairs with a smaller sum.
+__device__ __forceinline__ int diag_base(int s) {
+    return s <= 16 ? (s * (s + 1)) >> 1 : 136 + (((47 - s) * (s - 16)) >> 1);
+}
+__device__ __forceinline__ int diag_index(int a0, int a1) {
+    const int s = a0 + a1;
+    return diag_base(s) + (s <= 15 ? a1 : a1 - (s - 15));
+}
+
+// ---------------------------------------------------------------------------
 // Four blocks per workgroup (LOW = 3), LDS images interleaved: position L of the
 // group's k-th block is the u16 at 4L + k.  Pass B handles the four copies of a
 // position with one address, one validity test and one ds_read_b64 per child,
 // in packed u16 arithmetic.  Pass A folds each block's children separately and
 // transposes 4 x 8 codes at a time with v_perm_b32; pass C transposes back.
 
-template <int HIGH>
+// DIAG: pass B gives thread t the t-th (a0, a1) pair in anti-diagonal order
+// instead of a0 = t & 15, a1 = t >> 4.  A thread's position at low tier tau is
+// (a0, a1, tau - a0 - a1), valid for a0 + a1 in [tau - 15, tau]; with diagonals
+// packed into waves, a wave whose diagonals are all out of range skips the step
+// (~94 wave-steps per workgroup instead of 4 x 46, most lanes masked).
+template <int HIGH, bool DIAG>
 __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ table,
                                                           const uint32_t *__restrict__ blocks, uint32_t nblk,
                                                           const uint8_t *__restrict__ zero) {
@@ -296,7 +312,15 @@ __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ 
     // idempotent), so the seven ds_read_b64 of a step issue back to back with one
     // wait and no branches; position 0 (tau = 0) is peeled so the root override
     // stays out of the loop.
-    const int a0 = tid & 15, a1 = tid >> 4, s0 = a0 + a1;
+    int a0 = tid & 15, a1 = tid >> 4;
+    if constexpr (DIAG) {
+        int sd = 0;
+        while (diag_base(sd + 1) <= tid) sd++;
+        a1 = sd <= 15 ? tid - diag_base(sd) : tid - diag_base(sd) + sd - 15;
+        a0 = sd - a1;
+    }
+    const int s0 = a0 + a1;
+    const uint32_t me = 8u * (uint32_t)(a0 + 16 * a1);
     const uint32_t d01 = a0 >= 1 ? 8u : 0u, d02 = a0 >= 2 ? 16u : 0u;
     const uint32_t d11 = a1 >= 1 ? 128u : 0u, d12 = a1 >= 2 ? 256u : 0u;
     char *const sb = (char *)s;
@@ -317,7 +341,7 @@ __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ 
     for (int tau = 1; tau <= TAU_END; tau++) {
         const int c = tau - s0;
         if (c >= 0 && c <= 15) {
-            const uint32_t o = 8u * (uint32_t)(tid + 256 * c);
+            const uint32_t o = me + 2048u * (uint32_t)c;
             const uint32_t dc1 = c >= 1 ? 2048u : 0u, dc2 = c >= 2 ? 4096u : 0u;
             const u32x2v v0 = ld(o), v1 = ld(o - d01), v2 = ld(o - d02), v3 = ld(o - d11), v4 = ld(o - d12),
                          v5 = ld(o - dc1), v6 = ld(o - dc2);
@@ -358,16 +382,146 @@ __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Byte-image variant (GM_OPT_SUB_INTERLEAVE 6): the four blocks' codes of a
+// position share one dword of LDS (byte k = block k), so a workgroup's image is
+// 16 KiB instead of 32 and twice as many workgroups can be resident per CU to
+// hide pass B's barrier chain and pass A's load latency.  Pass B reads seven
+// dwords per position and takes the bytewise max as two u16-pair maxima
+// (even / odd bytes).
+__device__ __forceinline__ uint32_t code_x4(uint32_t b) {   // parent_code on four bytes
+    return ~b + ((b >> 6) & 0x02020202u);
+}
+
+#ifndef GM_B4_WAVES
+#define GM_B4_WAVES 1
+#endif
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *__restrict__ table,
+                                                          const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                          const uint8_t *__restrict__ zero) {
+    constexpr int NPOS = 4096, NCH = 256, NT = 256, K = 4;
+    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
+    __shared__ __attribute__((aligned(16))) uint32_t s[NPOS];   // 16 KiB
+    const int tid = threadIdx.x;
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
+    uint32_t hp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = grp * K + k;
+        valid[k] = idx < nblk;
+        hp[k] = valid[k] ? blocks[idx] : 0u;
+    }
+    static_assert(NCH == NT, "one chunk per thread");
+
+    // ---- pass A: chunk tid = positions 16 tid .. 16 tid + 15
+    {
+        const uint32_t c = tid;
+        Fold16 f[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint8_t *src[NMAX];
+            child_blocks<3, HIGH, NMAX>(table, zero, hp[k], valid[k], src);
+            u32x4v v[NMAX];
+#pragma unroll
+            for (int m = 0; m < NMAX; m++) v[m] = load16(block_rsrc(src[m], NPOS), 16u * c);
+            f[k] = fold16(v);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {   // positions 4j .. 4j+3 -> one dword each (bytes = blocks 0..3)
+            const uint32_t xe = __builtin_amdgcn_perm(f[1].e[j], f[0].e[j], 0x06020400u);
+            const uint32_t ye = __builtin_amdgcn_perm(f[3].e[j], f[2].e[j], 0x06020400u);
+            const uint32_t xo = __builtin_amdgcn_perm(f[1].o[j], f[0].o[j], 0x06020400u);
+            const uint32_t yo = __builtin_amdgcn_perm(f[3].o[j], f[2].o[j], 0x06020400u);
+            u32x4v q;
+            q[0] = __builtin_amdgcn_perm(ye, xe, 0x05040100u);   // 4j
+            q[1] = __builtin_amdgcn_perm(yo, xo, 0x05040100u);   // 4j+1
+            q[2] = __builtin_amdgcn_perm(ye, xe, 0x07060302u);   // 4j+2
+            q[3] = __builtin_amdgcn_perm(yo, xo, 0x07060302u);   // 4j+3
+            *(u32x4v *)(s + 16 * c + 4 * j) = q;
+        }
+    }
+    __syncthreads();
+
+    // ---- pass B (see sub_tier_kernel_x4): thread (a0, a1), position c = tau - a0 - a1
+    const int a0 = tid & 15, a1 = tid >> 4, s0 = a0 + a1;
+    const uint32_t d01 = a0 >= 1 ? 1u : 0u, d02 = a0 >= 2 ? 2u : 0u;
+    const uint32_t d11 = a1 >= 1 ? 16u : 0u, d12 = a1 >= 2 ? 32u : 0u;
+#if defined(GM_EXP) && (GM_EXP & 1)
+    constexpr int TAU_END = 0;   // experiment: no pass B
+#else
+    constexpr int TAU_END = 45;
+#endif
+    if (tid == 0) {
+        uint32_t r = code_x4(s[0]);
+        if (valid[0] && hp[0] == 0) r = (r & 0xFFFFFF00u) | 255u;   // all heaps empty: LOSS in 0
+        s[0] = r;
+    }
+    __syncthreads();
+    for (int tau = 1; tau <= TAU_END; tau++) {
+        const int c = tau - s0;
+        if (c >= 0 && c <= 15) {
+            const uint32_t o = (uint32_t)(tid + 256 * c);
+            const uint32_t dc1 = c >= 1 ? 256u : 0u, dc2 = c >= 2 ? 512u : 0u;
+            const uint32_t v0 = s[o], v1 = s[o - d01], v2 = s[o - d02], v3 = s[o - d11], v4 = s[o - d12],
+                           v5 = s[o - dc1], v6 = s[o - dc2];
+            const uint32_t e = pk_max(pk_max(pk_max(even_bytes(v0), even_bytes(v1)), pk_max(even_bytes(v2), even_bytes(v3))),
+                                      pk_max(pk_max(even_bytes(v4), even_bytes(v5)), even_bytes(v6)));
+            const uint32_t od = pk_max(pk_max(pk_max(odd_bytes(v0), odd_bytes(v1)), pk_max(odd_bytes(v2), odd_bytes(v3))),
+                                       pk_max(pk_max(odd_bytes(v4), odd_bytes(v5)), odd_bytes(v6)));
+            s[o] = code_x4(__builtin_amdgcn_perm(od, e, 0x06020400u));
+        }
+        __syncthreads();
+    }
+
+    // ---- pass C: back to four 16-byte rows per chunk
+    __amdgpu_buffer_rsrc_t wr[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) wr[k] = block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0);
+    {
+        const uint32_t c = tid;
+        u32x4v out[K];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const u32x4v q = *(const u32x4v *)(s + 16 * c + 4 * j);
+            const uint32_t t01 = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u);
+            const uint32_t t23 = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u);
+            const uint32_t u01 = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);
+            const uint32_t u23 = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
+            out[0][j] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+            out[1][j] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+            out[2][j] = __builtin_amdgcn_perm(u23, u01, 0x05040100u);
+            out[3][j] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) __builtin_amdgcn_raw_buffer_store_b128(out[k], wr[k], 16u * c, 0, 0);
+    }
+}
+
 typedef void (*tier_kernel_t)(uint8_t *, const uint32_t *, uint32_t, const uint8_t *);
 
-static tier_kernel_t pick_x4(int high) {
+static tier_kernel_t pick_b4(int high) {
     switch (high) {
-    case 0: return sub_tier_kernel_x4<0>;
-    case 1: return sub_tier_kernel_x4<1>;
-    case 2: return sub_tier_kernel_x4<2>;
-    case 3: return sub_tier_kernel_x4<3>;
-    case 4: return sub_tier_kernel_x4<4>;
-    case 5: return sub_tier_kernel_x4<5>;
+    case 0: return sub_tier_kernel_b4<0>;
+    case 1: return sub_tier_kernel_b4<1>;
+    case 2: return sub_tier_kernel_b4<2>;
+    case 3: return sub_tier_kernel_b4<3>;
+    case 4: return sub_tier_kernel_b4<4>;
+    case 5: return sub_tier_kernel_b4<5>;
+    }
+    return nullptr;
+}
+
+static tier_kernel_t pick_x4(int high, bool diag) {
+    switch (high) {
+    case 0: return diag ? sub_tier_kernel_x4<0, true> : sub_tier_kernel_x4<0, false>;
+    case 1: return diag ? sub_tier_kernel_x4<1, true> : sub_tier_kernel_x4<1, false>;
+    case 2: return diag ? sub_tier_kernel_x4<2, true> : sub_tier_kernel_x4<2, false>;
+    case 3: return diag ? sub_tier_kernel_x4<3, true> : sub_tier_kernel_x4<3, false>;
+    case 4: return diag ? sub_tier_kernel_x4<4, true> : sub_tier_kernel_x4<4, false>;
+    case 5: return diag ? sub_tier_kernel_x4<5, true> : sub_tier_kernel_x4<5, false>;
     }
     return nullptr;
 }
@@ -406,21 +560,32 @@ static tier_kernel_t pick_kernel(int low, int high, int nt) {
     return nullptr;
 }
 
-// nt == 0 selects the 4-block interleaved kernel (LOW = 3, 256 threads).
+// nt == 0 / -1 / -2 select the 4-block interleaved kernels (LOW = 3, 256 threads):
+// u16 image with row-major / anti-diagonal pass B, byte image.
+static tier_kernel_t pick_interleaved(int high, int nt) {
+    return nt == -2 ? pick_b4(high) : pick_x4(high, nt == -1);
+}
+
 bool sub_kernel_exists(int low, int high, int nt) {
-    return nt == 0 ? (low == 3 && pick_x4(high) != nullptr) : pick_kernel(low, high, nt) != nullptr;
+    return nt <= 0 ? (low == 3 && pick_interleaved(high, nt) != nullptr) : pick_kernel(low, high, nt) != nullptr;
 }
 
 void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table, const uint32_t *list,
                      const uint8_t *zero, hipStream_t s) {
     if (!nblocks) return;
-    if (nt == 0)
-        hipLaunchKernelGGL(pick_x4(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
+    if (nt <= 0)
+        hipLaunchKernelGGL(pick_interleaved(high, nt), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks,
+                           zero);
     else
         hipLaunchKernelGGL(pick_kernel(low, high, nt), dim3(nblocks), dim3(nt), 0, s, table, list, nblocks, zero);
 }
 
-int sub_kernel_threads(const Ctx *c, int low) { return (low == 3 && c->sub_interleave == 4) ? 0 : c->sub_threads; }
+int sub_kernel_threads(const Ctx *c, int low) {
+    if (low == 3 && c->sub_interleave == 4) return 0;
+    if (low == 3 && c->sub_interleave == 5) return -1;
+    if (low == 3 && c->sub_interleave == 6) return -2;
+    return c->sub_threads;
+}
 
 // ---------------------------------------------------------------------------
 __global__ void sub_digest_kernel(const uint8_t *__restrict__ table, uint64_t slots, int heaps,

@@ -74,7 +74,7 @@ struct Ctx {
     int engine_opt = GM_ENGINE_AUTO;
     int sub_low = 3;
     int sub_threads = 128;
-    int sub_interleave = 4;
+    int sub_interleave = 6;      // 4 u16 image, 5 u16 + diagonal pass B, 6 byte image (default), 1 one block
     int sub_order = 1;
     bool use_graph = true;
     bool timing = false;

@@ -78,7 +78,8 @@ enum {
                                 context on one GPU (loopback transport instead of RCCL); for testing
                                 the multi-GPU partition on a single device */
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
-    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path: blocks per workgroup, 4 (interleaved, default) or 1 */
+    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path, 4 blocks per workgroup: 6 = byte LDS image (default),
+                                  4 = u16 image, 5 = u16 image + anti-diagonal pass B; 1 = one block */
     GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton (default) */
     GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
     GM_OPT_DIST_SLOTS = 10  /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
