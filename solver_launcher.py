@@ -16,8 +16,12 @@ Differences, on purpose:
 * the solve runs in libgmsolve.so on the GPU (one process per GPU; ranks come
   from torch.distributed.run's environment instead of mpiexec), values and
   remoteness are the canonical ones (SURVEY Appendix A);
-* ``-sd DIR`` writes the solved table to ``DIR/stats/<rank>/table.npz``
-  (sorted u64 keys + u16 records) instead of shelve databases;
+* ``-sd DIR`` writes the solved table in the reference's layout -- shelve
+  databases ``DIR/stats/<rank>/resolved`` and ``remote`` keyed by ``str(pos)``,
+  each position on rank ``md5(str(pos)) % world`` (src/cache_dict.py:19-42,
+  gamesmanmpi_amd/persist.py) -- and as ``DIR/stats/<rank>/table.npz`` (sorted
+  u64 keys + u16 records); ``--sd-format`` picks one (shelves are written for
+  tables of up to 2 million positions unless asked for explicitly);
 * extras: ``--dims LxH`` patches board plugins' ``length``/``height``, ``--heaps``
   patches the subtraction plugin, ``--engine``, ``--device``, ``--stats``.
 """
@@ -36,6 +40,9 @@ if REPO not in sys.path:
 import src.utils  # noqa: E402
 
 
+SHELVE_AUTO_LIMIT = 2_000_000
+
+
 def build_parser():
     p = argparse.ArgumentParser()
     p.add_argument("game_file", help="Game to solve for.")
@@ -50,6 +57,9 @@ def build_parser():
     p.add_argument("--engine", choices=("auto", "dense", "sparse"), default="auto")
     p.add_argument("--device", type=int, default=None)
     p.add_argument("--stats", action="store_true", help="print solve statistics (JSON) to stderr")
+    p.add_argument("--sd-format", choices=("auto", "npz", "reference", "both"), default="auto",
+                   help="-sd output: npz table, the reference's shelve layout, or both (auto: both up to "
+                        "%d positions, else npz)" % SHELVE_AUTO_LIMIT)
     return p
 
 
@@ -141,12 +151,37 @@ def run(args, out=sys.stdout):
         st["rank"] = rank
         print(json.dumps(st), file=sys.stderr)
     if args.statsdir:
-        from gamesmanmpi_amd.solver import dump_table
-        keys, recs = solver.table()
-        dump_table(os.path.join(args.statsdir, "stats", str(rank), "table.npz"), keys, recs,
-                   {"game": args.game_file, "codec": solver.codec.name, "params": solver.codec.params})
+        write_statsdir(args, solver, rank, world)
     solver.close()
     return 0
+
+
+def write_statsdir(args, solver, rank, world):
+    """-sd DIR: this rank's npz table and/or the reference's shelve layout (rank 0
+    writes every rank's shelves, gathering the ranks' tables first)."""
+    from gamesmanmpi_amd.persist import write_reference_tables
+    from gamesmanmpi_amd.solver import dump_table
+    keys, recs = solver.table()
+    fmt = args.sd_format
+    if fmt == "auto":
+        total = solver.n_positions or len(keys)
+        fmt = "both" if total <= SHELVE_AUTO_LIMIT else "npz"
+        if fmt == "npz" and rank == 0:
+            print("-sd: %d positions; writing table.npz only (--sd-format reference forces the shelves)" % total,
+                  file=sys.stderr)
+    if fmt in ("npz", "both"):
+        dump_table(os.path.join(args.statsdir, "stats", str(rank), "table.npz"), keys, recs,
+                   {"game": args.game_file, "codec": solver.codec.name, "params": solver.codec.params})
+    if fmt in ("reference", "both"):
+        if world > 1:
+            import numpy as np
+            import torch.distributed as tdist
+            parts = [None] * world
+            tdist.all_gather_object(parts, (keys, recs))
+            keys = np.concatenate([p[0] for p in parts])
+            recs = np.concatenate([p[1] for p in parts])
+        if rank == 0:
+            write_reference_tables(args.statsdir, solver.codec, keys, recs, world)
 
 
 def main(argv=None):

@@ -91,6 +91,14 @@ def test_launcher_statsdir_dump(tmp_path):
     d = np.load(tmp_path / "stats" / "0" / "table.npz")
     g = np.load(os.path.join(GOLDEN, "ttt.npz"))
     assert (d["keys"] == g["keys"]).all() and (d["records"] == g["records"]).all()
+    # the reference's shelve layout (src/cache_dict.py:19-42), keyed by the mttt boards
+    from gamesmanmpi_amd import games
+    from gamesmanmpi_amd.persist import read_reference_tables
+    back = read_reference_tables(str(tmp_path))
+    codec = games.TTTStringCodec()
+    assert len(back) == 5478
+    for k, r in zip(g["keys"].tolist(), g["records"].tolist()):
+        assert back[codec.pos(k)] == (r >> 14, r & 0x3FFF)
 
 
 @pytest.mark.gpu
