@@ -11,8 +11,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # GM_LIB_PATH: development aid to load an experimental build of the same library
 LIB_PATH = os.environ.get("GM_LIB_PATH") or os.path.join(PKG, "libgmsolve.so")
 
-GAME_FOUR_TO_ONE, GAME_TTT, GAME_TOOT, GAME_OTHELLO, GAME_SUBTRACT = 1, 2, 3, 4, 5
-ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE, ENGINE_DIST_DENSE, ENGINE_DIST_SPARSE = 0, 1, 2, 3, 4
+GAME_FOUR_TO_ONE, GAME_TTT, GAME_TOOT, GAME_OTHELLO, GAME_SUBTRACT, GAME_GRAPH = 1, 2, 3, 4, 5, 6
+ENGINE_AUTO, ENGINE_DENSE, ENGINE_SPARSE, ENGINE_DIST_DENSE, ENGINE_DIST_SPARSE, ENGINE_GRAPH = 0, 1, 2, 3, 4, 5
 OPT_ENGINE, OPT_SUB_LOW, OPT_GRAPH, OPT_TIMING, OPT_VIRTUAL_RANKS, OPT_SUB_THREADS = 1, 2, 3, 4, 5, 6
 OPT_SUB_INTERLEAVE = 7
 OPT_SUB_ORDER = 8
@@ -29,7 +29,7 @@ ERRORS = {
 # Every symbol include/gmsolve.h declares (tests check the library exports them).
 SYMBOLS = ("gm_version", "gm_last_error", "gm_device_count", "gm_open", "gm_set_stream",
            "gm_set_option", "gm_pack_initial", "gm_expand_host", "gm_comm_unique_id",
-           "gm_set_comm", "gm_solve", "gm_export", "gm_query", "gm_digest", "gm_stats",
+           "gm_set_comm", "gm_solve", "gm_solve_graph", "gm_export", "gm_query", "gm_digest", "gm_stats",
            "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_close")
 
 
@@ -90,6 +90,7 @@ def lib():
         "gm_comm_unique_id": (ctypes.c_int, [vp, ctypes.c_int]),
         "gm_set_comm": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int]),
         "gm_solve": (ctypes.c_int, [vp, u64, P(u64), P(ctypes.c_uint16)]),
+        "gm_solve_graph": (ctypes.c_int, [vp, u64, vp, vp, vp, P(ctypes.c_uint16)]),
         "gm_export": (ctypes.c_int, [vp, vp, vp, u64, P(u64)]),
         "gm_query": (ctypes.c_int, [vp, vp, vp, u64]),
         "gm_digest": (ctypes.c_int, [vp, P(u64), P(u64)]),

@@ -20,7 +20,8 @@ LIB = os.path.join(PKG, "libgmsolve.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("GM_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["gm_api.hip", "dense_sub.hip", "small_dense.hip", "sparse.hip", "dist_sub.hip", "dist_sparse.hip"]
+SOURCES = ["gm_api.hip", "dense_sub.hip", "small_dense.hip", "sparse.hip", "dist_sub.hip", "dist_sparse.hip",
+           "graph.hip"]
 HEADERS = ["gm_common.hpp", "games.hpp", "gm_internal.hpp"]
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result",

@@ -109,6 +109,7 @@ static bool key_valid(const Ctx *c, uint64_t k) {
 }
 
 static void free_engines(Ctx *c) {
+    graph_free(c);
     dense_sub_free(c);
     small_dense_free(c);
     sparse_free(c);
@@ -142,7 +143,7 @@ int gm_open(int game, const int32_t *params, int nparams, int device, gm_ctx **o
     for (int i = 0; i < nparams; i++) c->params[i] = params[i];
     bool ok = true;
     switch (game) {
-    case GM_GAME_FOUR_TO_ONE: case GM_GAME_TTT: break;
+    case GM_GAME_FOUR_TO_ONE: case GM_GAME_TTT: case GM_GAME_GRAPH: break;
     case GM_GAME_TOOT:
         ok = DescToot::make(nparams > 0 ? params[0] : 6, nparams > 1 ? params[1] : 4, &c->toot);
         break;
@@ -306,6 +307,7 @@ int gm_set_comm(gm_ctx *h, int rank, int world, const void *uid, int bytes) {
 int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_record) {
     if (!h) return GM_E_ARG;
     Ctx *c = &h->c;
+    if (c->game == GM_GAME_GRAPH) { set_error("a GM_GAME_GRAPH context is solved with gm_solve_graph"); return GM_E_GAME; }
     if (c->device < 0) { set_error("no HIP device is visible: the solver needs an MI355X (gfx950)"); return GM_E_HIP; }
     if (!key_valid(c, root)) { set_error("root key 0x%llx is not a valid position", (unsigned long long)root); return GM_E_KEY; }
     GM_HIP(hipSetDevice(c->device));
@@ -341,6 +343,27 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     return GM_OK;
 }
 
+int gm_solve_graph(gm_ctx *h, uint64_t n, const uint8_t *prim, const uint64_t *off, const uint32_t *kid,
+                   uint16_t *root_record) {
+    if (!h || !prim || !off || (off[n] && !kid)) return GM_E_ARG;
+    Ctx *c = &h->c;
+    if (c->game != GM_GAME_GRAPH) { set_error("gm_solve_graph needs a GM_GAME_GRAPH context"); return GM_E_GAME; }
+    if (c->device < 0) { set_error("no HIP device is visible: the solver needs an MI355X (gfx950)"); return GM_E_HIP; }
+    if (n >= (1ull << 32)) { set_error("graphs are limited to 2^32 - 1 positions"); return GM_E_ARG; }
+    for (uint64_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i]) { set_error("child_off is not monotone at %llu", (unsigned long long)i); return GM_E_ARG; }
+    GM_HIP(hipSetDevice(c->device));
+    c->solved = false;
+    c->stats = gm_stats_t{};
+    c->stats.world = 1;
+    GM_TRY(graph_solve(c, n, prim, off, kid));
+    c->engine = GM_ENGINE_GRAPH;
+    c->stats.engine = GM_ENGINE_GRAPH;
+    c->solved = true;
+    if (root_record) *root_record = c->root_record;
+    return GM_OK;
+}
+
 static int need_solved(gm_ctx *h) {
     if (!h) return GM_E_ARG;
     if (!h->c.solved) { set_error("call gm_solve first"); return GM_E_STATE; }
@@ -352,6 +375,7 @@ int gm_export(gm_ctx *h, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t 
     if (!n || (keys && !recs)) return GM_E_ARG;
     Ctx *c = &h->c;
     GM_HIP(hipSetDevice(c->device));
+    if (c->engine == GM_ENGINE_GRAPH) return graph_export(c, keys, recs, cap, n);
     if (c->engine == GM_ENGINE_DENSE)
         return c->game == GM_GAME_SUBTRACT ? dense_sub_export(c, keys, recs, cap, n)
                                            : small_dense_export(c, keys, recs, cap, n);
@@ -365,6 +389,7 @@ int gm_query(gm_ctx *h, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     if (n && (!keys || !recs)) return GM_E_ARG;
     Ctx *c = &h->c;
     GM_HIP(hipSetDevice(c->device));
+    if (c->engine == GM_ENGINE_GRAPH) return graph_query(c, keys, recs, n);
     if (c->engine == GM_ENGINE_DENSE)
         return c->game == GM_GAME_SUBTRACT ? dense_sub_query(c, keys, recs, n) : small_dense_query(c, keys, recs, n);
     if (c->engine == GM_ENGINE_DIST_DENSE) return dist_sub_query(c, keys, recs, n);
@@ -377,6 +402,7 @@ int gm_digest(gm_ctx *h, uint64_t *digest, uint64_t *n) {
     if (!digest || !n) return GM_E_ARG;
     Ctx *c = &h->c;
     GM_HIP(hipSetDevice(c->device));
+    if (c->engine == GM_ENGINE_GRAPH) return graph_digest(c, digest, n);
     if (c->engine == GM_ENGINE_DENSE)
         return c->game == GM_GAME_SUBTRACT ? dense_sub_digest(c, digest, n) : small_dense_digest(c, digest, n);
     if (c->engine == GM_ENGINE_DIST_DENSE) return dist_sub_digest(c, digest, n);

@@ -57,6 +57,7 @@ struct SmallDense;
 struct Sparse;
 struct DistSub;
 struct DistSparse;
+struct Graph;
 
 struct Ctx {
     int game = 0;
@@ -108,6 +109,7 @@ struct Ctx {
     Sparse *sp = nullptr;
     DistSub *dist_sub = nullptr;
     DistSparse *dist_sp = nullptr;
+    Graph *graph = nullptr;
 };
 
 // engines (each returns GM_OK or a GM_E_* code)
@@ -143,6 +145,12 @@ int small_dense_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uin
 int small_dense_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
 int small_dense_digest(Ctx *c, uint64_t *digest, uint64_t *n);
 void small_dense_free(Ctx *c);
+
+int graph_solve(Ctx *c, uint64_t n, const uint8_t *prim, const uint64_t *off, const uint32_t *kid);
+int graph_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int graph_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int graph_digest(Ctx *c, uint64_t *digest, uint64_t *n);
+void graph_free(Ctx *c);
 
 int sparse_solve(Ctx *c, uint64_t root);
 int sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);

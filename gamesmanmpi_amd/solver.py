@@ -62,6 +62,17 @@ class Context:
         _lib.check(self.L.gm_solve(self.h, root, ctypes.byref(n), ctypes.byref(r)))
         return n.value, r.value
 
+    def solve_graph(self, prim, off, kids):
+        """gm_solve_graph over an explicit graph (gamesmanmpi_amd/graph.py)."""
+        import numpy as np
+        prim = np.ascontiguousarray(prim, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        kids = np.ascontiguousarray(kids, dtype=np.uint32)
+        r = ctypes.c_uint16()
+        _lib.check(self.L.gm_solve_graph(self.h, len(prim), prim.ctypes.data, off.ctypes.data,
+                                         kids.ctypes.data if len(kids) else None, ctypes.byref(r)))
+        return len(prim), r.value
+
     def export(self):
         n = ctypes.c_uint64()
         _lib.check(self.L.gm_export(self.h, None, None, 0, ctypes.byref(n)))
@@ -118,17 +129,26 @@ class Solver:
 
     ``module`` is a GamesmanMPI plugin; ``root`` defaults to
     ``module.initial_position()`` (GameState.INITIAL_POS, src/game_state.py:15).
+    A plugin that no device descriptor reproduces is solved as an explicit graph
+    (gamesmanmpi_amd/graph.py): the host enumerates it with the plugin's own
+    functions and the device resolves it; ``graph=True`` forces that path,
+    ``graph=False`` raises NoDescriptor instead.
     """
 
-    def __init__(self, module, root=None, device=-1, engine=None, codec=None):
+    def __init__(self, module, root=None, device=-1, engine=None, codec=None, graph=None):
         self.module = module
         self.root = module.initial_position() if root is None else root
-        self.codec = codec or games.identify(module, self.root)
-        if self.codec is None:
-            raise NoDescriptor(
-                "no device descriptor reproduces plugin %r; supported: Four-To-One, "
-                "tic-tac-toe (mttt / numpy), Toot-and-Otto and Othello bitboards, "
-                "the subtraction game" % getattr(module, "__file__", module))
+        if codec is None and not graph:
+            codec = games.identify(module, self.root)
+        if codec is None:
+            if graph is False:
+                raise NoDescriptor(
+                    "no device descriptor reproduces plugin %r; supported: Four-To-One, "
+                    "tic-tac-toe (mttt / numpy), Toot-and-Otto and Othello bitboards, "
+                    "the subtraction game" % getattr(module, "__file__", module))
+            from .graph import GraphCodec
+            codec = GraphCodec(module, self.root)
+        self.codec = codec
         self.ctx = Context(self.codec.game_id, self.codec.params, device)
         if engine is not None:
             self.ctx.set_option(_lib.OPT_ENGINE, engine)
@@ -137,7 +157,11 @@ class Solver:
         self.root_record = None
 
     def solve(self):
-        self.n_positions, self.root_record = self.ctx.solve(self.root_key)
+        if self.codec.game_id == _lib.GAME_GRAPH:
+            c = self.codec
+            self.n_positions, self.root_record = self.ctx.solve_graph(c.prim, c.off, c.kids)
+        else:
+            self.n_positions, self.root_record = self.ctx.solve(self.root_key)
         return self.n_positions, self.root_record
 
     @property

@@ -37,13 +37,15 @@ extern "C" {
  *   GM_GAME_TOOT         {length, height}      (test_games/toot_and_otto_bitstring.py), 2*L*H+16 <= 64
  *   GM_GAME_OTHELLO      {length, height}      (test_games/othello_bit_new.py), square, 2*L*H+16 <= 64
  *   GM_GAME_SUBTRACT     {heaps}               (the build's synthetic game, 1..8 heaps of 4 bits)
+ *   GM_GAME_GRAPH        none                  (any plugin: an explicit graph from gm_solve_graph)
  */
 enum {
     GM_GAME_FOUR_TO_ONE = 1,
     GM_GAME_TTT = 2,
     GM_GAME_TOOT = 3,
     GM_GAME_OTHELLO = 4,
-    GM_GAME_SUBTRACT = 5
+    GM_GAME_SUBTRACT = 5,
+    GM_GAME_GRAPH = 6
 };
 
 enum {
@@ -66,7 +68,8 @@ enum {
     GM_ENGINE_DENSE = 1,
     GM_ENGINE_SPARSE = 2,
     GM_ENGINE_DIST_DENSE = 3,   /* reported in gm_stats_t.engine: sharded dense path */
-    GM_ENGINE_DIST_SPARSE = 4   /* reported in gm_stats_t.engine: sharded sparse path */
+    GM_ENGINE_DIST_SPARSE = 4,  /* reported in gm_stats_t.engine: sharded sparse path */
+    GM_ENGINE_GRAPH = 5         /* reported in gm_stats_t.engine: explicit graph (gm_solve_graph) */
 };
 
 enum {
@@ -155,6 +158,19 @@ int gm_set_comm(gm_ctx *ctx, int rank, int world, const void *uid, int bytes);
  * Replaces Process.run/lookup/distribute/check_for_updates/send_back/resolve
  * (src/new_process.py:37-265) and the root line of :42-53. */
 int gm_solve(gm_ctx *ctx, uint64_t root_key, uint64_t *n_positions, uint16_t *root_record);
+
+/* Strong-solve an explicit position graph (context opened with GM_GAME_GRAPH):
+ * for plugins no device descriptor reproduces, the host enumerates positions
+ * 0..n-1 with the plugin's own functions (position 0 = the root) and passes
+ * primitive[i] (the plugin's primitive() code, src/utils.py:4) and the children of
+ * i as child_idx[child_off[i] .. child_off[i+1]) (CSR, child_off has n+1 entries).
+ * The device resolves every position (Appendix A); keys of gm_export / gm_query /
+ * gm_digest are then the position indices.  A cycle, a DRAW primitive or an
+ * undecided position without children is an error (the reference would hang).
+ * Replaces the reference's per-position job loop for arbitrary plugins
+ * (src/new_process.py:37-265, GameState.expand src/game_state.py:33-41). */
+int gm_solve_graph(gm_ctx *ctx, uint64_t n, const uint8_t *primitive, const uint64_t *child_off,
+                   const uint32_t *child_idx, uint16_t *root_record);
 
 /* Copy this rank's solved table to host arrays, sorted by key.  With keys ==
  * NULL only *n is set (the count).  Replaces reading the resolved/remote shelve
