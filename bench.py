@@ -89,6 +89,27 @@ def cpu_baseline(heaps=8):
                       "nproc %d" % (heaps, n, dt, threads, cpu, os.cpu_count())}
 
 
+def toot_6x4(repeats=2):
+    """Config 3 beside the headline: Toot-and-Otto 6x4 strong solve on this GPU
+    (sparse engine); reported, not the metric.  Per-ply counts are checked
+    against SURVEY Appendix D's total."""
+    from gamesmanmpi_amd import Context, _lib
+    ctx = Context(_lib.GAME_TOOT, (6, 4), device=0)
+    root = ctx.initial()
+    best = None
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        n, rec = ctx.solve(root)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    st = ctx.stats()
+    ctx.close()
+    assert n == 1187212827, n
+    return {"workload": "Toot-and-Otto 6x4 (config 3), sparse engine", "positions": n, "root_record": rec,
+            "solve_ms": best * 1e3, "positions_per_s": n / best, "edges": st["n_edges"],
+            "algo_bytes_per_position": st["algo_bytes"] / n}
+
+
 def pmc_traffic(heaps):
     """HBM bytes per launch / per solve of the tier kernel from a committed rocprofv3 PMC summary."""
     path = os.path.join(REPO, "profiles", "traffic_subtract%d.json" % heaps)
@@ -123,6 +144,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--heaps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-toot", action="store_true", help="skip the config-3 side measurement")
     ap.add_argument("--cpu-heaps", type=int, default=8)
     ap.add_argument("--dist-batch", type=int, default=4, help="N>1: tiers per halo exchange")
     ap.add_argument("--dist-slots", type=int, default=4, help="N>1: halo buffers per split heap")
@@ -256,9 +278,13 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_heaps)
+    ctx.close()
+    if rank == 0 and world == 1 and args.virtual_ranks == 1 and not args.no_toot:
+        del table
+        torch.cuda.empty_cache()
+        out["other_configs"] = {"toot_6x4": toot_6x4()}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -311,7 +311,9 @@ static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
         // one communicator per split heap; every rank makes the same calls in the same order
         d->comm[0] = c->comm;
         for (int a = 1; a < d->g; a++) {
-            GM_NCCL(ncclCommSplit(c->comm, 0, c->rank, &d->comm[a], nullptr));
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 1;
+            GM_NCCL(ncclCommSplit(c->comm, 0, c->rank, &d->comm[a], &cfg));
             d->own_comm[a] = true;
         }
     }
