@@ -72,6 +72,10 @@ def build(jobs=None, verbose=False):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode:
             raise RuntimeError("link failed:\n%s%s" % (r.stdout, r.stderr))
+    # the device link leaves per-arch temporaries next to the library
+    import glob
+    for tmp in glob.glob(LIB + ".*-*"):
+        os.remove(tmp)
     return LIB
 
 
