@@ -22,7 +22,7 @@ ARCH = os.environ.get("GM_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["gm_api.hip", "dense_sub.hip", "small_dense.hip", "sparse.hip", "dist_sub.hip", "dist_sparse.hip",
            "graph.hip"]
-HEADERS = ["gm_common.hpp", "games.hpp", "gm_internal.hpp"]
+HEADERS = ["gm_common.hpp", "games.hpp", "gm_internal.hpp", "sparse_common.hpp", "sparse_tables.hpp"]
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result",
             "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
