@@ -203,3 +203,19 @@ def test_toot_6x4_known_per_ply_counts():
     ctx, n, rec = _solve(TOOT, (6, 4))
     assert n == 1187212827
     assert [int(x) for x in ctx.tier_counts()] == app_d
+
+
+@pytest.mark.parametrize("board", ["toot_4x4", "toot_5x4"])
+@pytest.mark.parametrize("ranks", [1, 8])
+def test_toot_large_boards_vs_oracle_digest(board, ranks):
+    """Toot 4x4 / 5x4 (3.5 M / 70 M positions): per-ply counts, root record and the
+    full-table digest equal the C oracle's (tests/golden/make_oracle_digests.py)."""
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))[board]
+    L, H = (int(v) for v in board.split("_")[1].split("x"))
+    ctx = Context(TOOT, (L, H), device=0)
+    if ranks > 1:
+        ctx.set_option(_lib.OPT_VIRTUAL_RANKS, ranks)
+    n, rec = ctx.solve(ctx.initial())
+    assert n == ref["positions"] and rec == ref["root_record"]
+    assert [int(x) for x in ctx.tier_counts()] == ref["per_ply"]
+    assert ctx.digest() == (ref["digest"], ref["positions"])
