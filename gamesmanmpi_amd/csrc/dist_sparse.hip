@@ -7,12 +7,11 @@
 // both are batched per tier into bulk-synchronous exchanges over the same
 // per-tier tables as the single-GPU engine (sparse_tables.hpp):
 //
-// forward, tier t:   each rank compacts its tier-t frontier table, classifies
-//                    (one primitive() per position; resolved table; interior
-//                    list), and generates its interior positions' children,
+// forward, tier t:   each rank classifies its tier-t table (one primitive()
+//                    per position, scored in place; interior list), and generates its interior positions' children,
 //                    bucketed by (owner, tier step) through an LDS histogram;
 //                    counts are all-gathered; keys move with one ncclGroup of
-//                    send/recv per peer; owners insert them into their frontier
+//                    send/recv per peer; owners insert them into their tier
 //                    tables (deduplicating on insert).
 // backward, tier t:  each rank regenerates its interior positions' children;
 //                    a primitive child is scored locally from primitive() (a
@@ -35,9 +34,9 @@ struct SpRank {
     unsigned long long *d_hist = nullptr;    // G*S bins
     unsigned long long *d_cursor = nullptr;  // G*S bins
     unsigned long long *d_seg = nullptr;     // G*S bins
-    unsigned long long *d_scr = nullptr;     // [0,8) edges by step, [8] compact cursor, [9] interior count
-    uint64_t *dense = nullptr, *sendk = nullptr, *recvk = nullptr;
-    uint64_t dense_cap = 0, send_cap = 0, recv_cap = 0, best_cap = 0;
+    unsigned long long *d_scr = nullptr;     // [0,8) edges by step, [9] interior count, [10] seen, [12] cursor
+    uint64_t *sendk = nullptr, *recvk = nullptr;
+    uint64_t send_cap = 0, recv_cap = 0, best_cap = 0;
     uint32_t *sendp = nullptr, *best = nullptr;
     uint16_t *reply_out = nullptr, *reply_in = nullptr;
 };
@@ -178,7 +177,7 @@ static int grow_to(Ctx *c, T **p, uint64_t n) {   // paired with a grow64'd buff
 
 static FrontRef fref(SpRank &R, size_t t) {
     SpTier &T = R.tiers[t];
-    return FrontRef{T.fkeys, T.fcap ? T.fcap - 1 : 0, R.d_cnt + t};
+    return FrontRef{T.slots, T.cap ? T.cap - 1 : 0, R.d_cnt + t};
 }
 
 // Cross-rank exchange of G-segmented arrays (RCCL mode; loopback copies are done by the caller).
@@ -305,33 +304,23 @@ static int ensure_cnt(Ctx *c, DistSparse *d, size_t ntiers) {
     return GM_OK;
 }
 
-// compact + classify tier t of every rank (frontier table -> resolved table + interior list)
+// classify tier t of every rank (scores in place + interior list)
 template <class D>
 static int classify_tier(Ctx *c, DistSparse *d, const D &desc, size_t t) {
     for (auto &R : d->ranks) {
         SpTier &T = R.tiers[t];
         const uint64_t n = T.fcount;
         if (!n) continue;
-        if (R.dense_cap < n) GM_TRY(grow64(c, &R.dense, &R.dense_cap, n));
-        GM_HIP(hipMemsetAsync(R.d_scr, 0, 16 * 8, c->stream));
-        hipLaunchKernelGGL(compact_kernel, dim3(grid_for(T.fcap)), dim3(256), 0, c->stream, T.fkeys, T.fcap, R.dense,
-                           R.d_scr + 8);
-        T.rcap = pow2_at_least(2 * n);
-        GM_TRY(dev_alloc(c, (void **)&T.res, T.rcap * sizeof(RSlot)));
-        GM_TRY(dev_alloc(c, (void **)&T.ikeys, n * 8));
-        GM_TRY(dev_alloc(c, (void **)&T.islot, n * 4));
-        hipLaunchKernelGGL(res_fill_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap);
-        hipLaunchKernelGGL(classify_kernel<D>, dim3(grid_for(n)), dim3(256), 0, c->stream, desc, R.dense, n,
-                           res_ref_of(T), T.ikeys, T.islot, R.d_scr + 9, R.d_scr, R.d_err);
-        unsigned long long sc[10];
+        GM_TRY(classify_tier_table(c, desc, T, R.d_scr, R.d_err));
+        unsigned long long sc[11];
         GM_HIP(hipMemcpyAsync(sc, R.d_scr, sizeof sc, hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
-        if (sc[8] != n) { set_error("rank %d tier %zu: compacted %llu of %llu keys", R.rank, t, sc[8], (unsigned long long)n); return GM_E_STATE; }
+        if (sc[10] != n) {
+            set_error("rank %d tier %zu: found %llu of %llu keys", R.rank, t, sc[10], (unsigned long long)n);
+            return GM_E_STATE;
+        }
         T.count = n;
         T.ni = sc[9];
-        dev_free(c, T.fkeys);
-        T.fkeys = nullptr;
-        T.fcap = 0;
     }
     return GM_OK;
 }
@@ -364,8 +353,8 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     // the root lives on its owner
     for (auto &R : d->ranks)
         if ((int)owner_rank(root, G) == R.rank) {
-            GM_TRY(front_alloc(c, &R.tiers[0].fkeys, 1024));
-            R.tiers[0].fcap = 1024;
+            GM_TRY(tier_alloc(c, &R.tiers[0].slots, 1024));
+            R.tiers[0].cap = 1024;
             hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, fref(R, 0), root, R.d_err);
             R.tiers[0].fcount = 1;
         }
@@ -412,7 +401,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
                 const size_t u = t + 1 + s;
                 SpTier &U = R.tiers[u];
                 const uint64_t needc = pow2_at_least((U.fcount + in) * 5 / 4 + 1);
-                if (U.fcap < needc) GM_TRY(front_grow(c, U, needc, R.d_err));
+                if (U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
                 for (int q = 0; q < G; q++) {
                     const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
                     if (n)
@@ -441,11 +430,6 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
         for (size_t u = t + 1; u < need; u++) d->gcount[u] = local[u];
     }
     while (!d->gcount.empty() && !d->gcount.back()) d->gcount.pop_back();
-    for (auto &R : d->ranks) {
-        dev_free(c, R.dense);
-        R.dense = nullptr;
-        R.dense_cap = 0;
-    }
     const double t1 = now_ms();
 
     // ---------------- backward
@@ -518,7 +502,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     uint64_t n = 0, tb = 0;
     for (auto v : d->gcount) n += v;
     for (auto &R : d->ranks)
-        for (auto &T : R.tiers) tb += T.rcap * sizeof(RSlot) + T.ni * 12;
+        for (auto &T : R.tiers) tb += T.cap * sizeof(RSlot) + T.ni * 12;
     c->n_positions = n;
     c->tier_counts = d->gcount;
     c->stats.n_positions = n;
@@ -563,7 +547,7 @@ int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uin
     for (auto &R : d->ranks)
         for (auto &T : R.tiers)
             if (T.count)
-                hipLaunchKernelGGL(res_gather_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap,
+                hipLaunchKernelGGL(res_gather_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap,
                                    dk, dr, cur);
     std::vector<uint64_t> hk(total);
     std::vector<uint16_t> hr(total);
@@ -590,7 +574,7 @@ int dist_sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
         for (auto &T : R.tiers) {
             total += T.count;
             if (T.count)
-                hipLaunchKernelGGL(res_digest_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap,
+                hipLaunchKernelGGL(res_digest_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap,
                                    acc);
         }
     unsigned long long h;
@@ -650,7 +634,7 @@ void dist_sparse_free(Ctx *c) {
     for (auto &R : d->ranks) {
         for (auto &T : R.tiers) free_tier(c, T);
         for (void *p : {(void *)R.d_cnt, (void *)R.d_err, (void *)R.d_hist, (void *)R.d_cursor, (void *)R.d_seg,
-                        (void *)R.d_scr, (void *)R.dense, (void *)R.sendk, (void *)R.recvk, (void *)R.sendp,
+                        (void *)R.d_scr, (void *)R.sendk, (void *)R.recvk, (void *)R.sendp,
                         (void *)R.best, (void *)R.reply_out, (void *)R.reply_in})
             dev_free(c, p);
     }

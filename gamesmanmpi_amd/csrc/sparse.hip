@@ -3,17 +3,15 @@
 // descriptor).
 //
 // Replaces the reference's asynchronous job loop and its tables:
-//   LOOK_UP / DISTRIBUTE (src/new_process.py:102-162)  -> per tier: the frontier
-//       table (u64 keys, open addressing; children of the tiers above are
-//       atomicCAS-inserted into it, which deduplicates them) is compacted into a
-//       dense key list; classify_kernel evaluates primitive() once per position,
-//       files the position in the tier's resolved table and appends the
-//       undecided ones to the tier's interior list; expand_kernel generates the
-//       interior positions' children into the frontier tables of tiers
-//       t+1..t+MAX_SKIP
-//   CacheDict resolved/remote (src/cache_dict.py)      -> per-tier resolved
-//       tables: 16-byte slots {key, score} at load <= 1/2, so a lookup reads one
-//       cache line, key and score together
+//   LOOK_UP / DISTRIBUTE (src/new_process.py:102-162)  -> per tier: the tier
+//       table (16-byte slots {key, score}, open addressing; children of the
+//       tiers above are atomicCAS-inserted into it, which deduplicates them)
+//       is streamed once by classify_kernel, which evaluates primitive() once
+//       per position, writes the score in place and appends the undecided ones
+//       to the tier's interior list; expand_kernel generates the interior
+//       positions' children into the tables of tiers t+1..t+MAX_SKIP
+//   CacheDict resolved/remote (src/cache_dict.py)      -> the same tier
+//       tables: a lookup reads key and score with one 16-byte load
 //   RESOLVE / _res_red (src/new_process.py:223-265)    -> retro_kernel, tiers
 //       deepest first, over the interior list: regenerate children; a primitive
 //       child is scored from primitive() with no memory access (a LOSS-in-0
@@ -31,10 +29,8 @@ struct Sparse {
     std::vector<SpTier> tiers;
     unsigned long long *d_counts = nullptr;   // per-tier frontier counts (device)
     uint64_t counts_cap = 0;
-    unsigned long long *d_scratch = nullptr;  // [0,S) edges, [8] cursor, [9] interior count, [10] export cursor
+    unsigned long long *d_scratch = nullptr;  // [0,S) edges, [9] interior count, [10] seen, [12] export cursor
     uint32_t *d_err = nullptr;
-    uint64_t *d_dense = nullptr;              // compacted frontier keys (reused)
-    uint64_t dense_cap = 0;
     int64_t t_root = 0;
     uint64_t edges = 0;
 };
@@ -113,12 +109,12 @@ static int ensure_counts(Sparse *sp, size_t n) {
 
 static FrontRef front_ref(Sparse *sp, size_t t) {
     SpTier &T = sp->tiers[t];
-    return FrontRef{T.fkeys, T.fcap ? T.fcap - 1 : 0, sp->d_counts + t};
+    return FrontRef{T.slots, T.cap ? T.cap - 1 : 0, sp->d_counts + t};
 }
 
 static ResRef res_ref(Sparse *sp, size_t t) { return res_ref_of(sp->tiers[t]); }
 
-static int front_grow(Ctx *c, Sparse *sp, size_t t, uint64_t cap) { return front_grow(c, sp->tiers[t], cap, sp->d_err); }
+static int tier_grow(Ctx *c, Sparse *sp, size_t t, uint64_t cap) { return tier_grow(c, sp->tiers[t], cap, sp->d_err); }
 
 static int read_err(Ctx *c, Sparse *sp) {
     uint32_t e;
@@ -140,64 +136,38 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     double t0 = now_ms();
 
     sp->tiers.resize(1);
-    GM_TRY(front_alloc(c, &sp->tiers[0].fkeys, 1024));
-    sp->tiers[0].fcap = 1024;
+    GM_TRY(tier_alloc(c, &sp->tiers[0].slots, 1024));
+    sp->tiers[0].cap = 1024;
     hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, front_ref(sp, 0), root, sp->d_err);
     sp->tiers[0].fcount = 1;
 
     // ---------------- forward: tier by tier
     for (size_t t = 0; t < sp->tiers.size(); t++) {
-        if (!sp->tiers[t].fcount) {
-            dev_free(c, sp->tiers[t].fkeys);
-            sp->tiers[t].fkeys = nullptr;
-            continue;
-        }
         const uint64_t n = sp->tiers[t].fcount;
-        // 1. frontier table -> dense key list
-        if (sp->dense_cap < n) {
-            dev_free(c, sp->d_dense);
-            sp->dense_cap = std::max<uint64_t>(n + n / 4, 1 << 16);
-            GM_TRY(dev_alloc(c, (void **)&sp->d_dense, sp->dense_cap * 8));
-        }
-        GM_HIP(hipMemsetAsync(sp->d_scratch, 0, 16 * sizeof(unsigned long long), c->stream));
-        hipLaunchKernelGGL(compact_kernel, dim3(grid_for(sp->tiers[t].fcap)), dim3(256), 0, c->stream,
-                           sp->tiers[t].fkeys, sp->tiers[t].fcap, sp->d_dense, sp->d_scratch + 8);
-        // 2. resolved table (load <= 1/2) + interior list, filled by classify
-        {
-            SpTier &T = sp->tiers[t];
-            T.rcap = pow2_at_least(2 * n);
-            GM_TRY(dev_alloc(c, (void **)&T.res, T.rcap * sizeof(RSlot)));
-            GM_TRY(dev_alloc(c, (void **)&T.ikeys, n * 8));
-            GM_TRY(dev_alloc(c, (void **)&T.islot, n * 4));
-            hipLaunchKernelGGL(res_fill_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap);
-            hipLaunchKernelGGL(classify_kernel<D>, dim3(grid_for(n)), dim3(256), 0, c->stream, d, sp->d_dense, n,
-                               res_ref(sp, t), T.ikeys, T.islot, sp->d_scratch + 9, sp->d_scratch, sp->d_err);
-            GM_HIP(hipGetLastError());
-        }
-        unsigned long long sc[10];
+        if (!n) continue;
+        // 1. the tier is complete: score it in place, list its undecided positions
+        GM_TRY(classify_tier_table(c, d, sp->tiers[t], sp->d_scratch, sp->d_err));
+        unsigned long long sc[11];
         GM_HIP(hipMemcpyAsync(sc, sp->d_scratch, sizeof sc, hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
         GM_TRY(read_err(c, sp));
-        if (sc[8] != n) {
-            set_error("tier %zu: compacted %llu keys, expected %llu", t, sc[8], (unsigned long long)n);
+        if (sc[10] != n) {
+            set_error("tier %zu: found %llu positions, inserted %llu", t, sc[10], (unsigned long long)n);
             return GM_E_STATE;
         }
         sp->tiers[t].count = n;
         sp->tiers[t].ni = sc[9];
-        dev_free(c, sp->tiers[t].fkeys);
-        sp->tiers[t].fkeys = nullptr;
-        sp->tiers[t].fcap = 0;
         if (!sp->tiers[t].ni) continue;
-        // 3. size the frontier tables of the tiers the children land in
+        // 2. size the tables of the tiers the children land in (exact edge counts, load <= 0.8)
         if (sp->tiers.size() < t + S + 1) sp->tiers.resize(t + S + 1);
         GM_TRY(ensure_counts(sp, sp->tiers.size()));
         for (int s = 0; s < S; s++) {
             const size_t u = t + 1 + s;
             sp->edges += sc[s];
             const uint64_t need = pow2_at_least((sp->tiers[u].fcount + sc[s]) * 5 / 4 + 1);
-            if (sc[s] && sp->tiers[u].fcap < need) GM_TRY(front_grow(c, sp, u, need));
+            if (sc[s] && sp->tiers[u].cap < need) GM_TRY(tier_grow(c, sp, u, need));
         }
-        // 4. expand the interior positions
+        // 3. expand the interior positions
         Fronts<S> nx;
         for (int s = 0; s < S; s++) nx.t[s] = front_ref(sp, t + 1 + s);
         hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(sp->tiers[t].ni)), dim3(256), 0, c->stream, d,
@@ -215,9 +185,6 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
                     now_ms() - t0);
     }
     while (!sp->tiers.empty() && !sp->tiers.back().count) sp->tiers.pop_back();
-    dev_free(c, sp->d_dense);
-    sp->d_dense = nullptr;
-    sp->dense_cap = 0;
     double t1 = now_ms();
 
     // ---------------- backward: deepest tier first
@@ -247,7 +214,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     for (auto &T : sp->tiers) {
         n += T.count;
         c->tier_counts.push_back(T.count);
-        tb += T.rcap * sizeof(RSlot) + T.ni * 12;
+        tb += T.cap * sizeof(RSlot) + T.ni * 12;
     }
     c->n_positions = n;
     c->stats.n_positions = n;
@@ -323,11 +290,11 @@ int sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t
     uint16_t *dr;
     GM_HIP(hipMalloc(&dk, std::max<uint64_t>(1, total) * 8));
     GM_HIP(hipMalloc(&dr, std::max<uint64_t>(1, total) * 2));
-    GM_HIP(hipMemsetAsync(sp->d_scratch + 10, 0, 8, c->stream));
+    GM_HIP(hipMemsetAsync(sp->d_scratch + 12, 0, 8, c->stream));
     for (auto &T : sp->tiers)
         if (T.count)
-            hipLaunchKernelGGL(res_gather_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap, dk,
-                               dr, sp->d_scratch + 10);
+            hipLaunchKernelGGL(res_gather_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap, dk,
+                               dr, sp->d_scratch + 12);
     std::vector<uint64_t> hk(total);
     std::vector<uint16_t> hr(total);
     GM_HIP(hipMemcpyAsync(hk.data(), dk, total * 8, hipMemcpyDeviceToHost, c->stream));
@@ -347,16 +314,16 @@ int sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t
 
 int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     Sparse *sp = c->sp;
-    GM_HIP(hipMemsetAsync(sp->d_scratch + 10, 0, 8, c->stream));
+    GM_HIP(hipMemsetAsync(sp->d_scratch + 12, 0, 8, c->stream));
     uint64_t total = 0;
     for (auto &T : sp->tiers) {
         total += T.count;
         if (T.count)
-            hipLaunchKernelGGL(res_digest_kernel, dim3(grid_for(T.rcap)), dim3(256), 0, c->stream, T.res, T.rcap,
-                               sp->d_scratch + 10);
+            hipLaunchKernelGGL(res_digest_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap,
+                               sp->d_scratch + 12);
     }
     unsigned long long h;
-    GM_HIP(hipMemcpyAsync(&h, sp->d_scratch + 10, 8, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipMemcpyAsync(&h, sp->d_scratch + 12, 8, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     *digest = h;
     *n = total;
@@ -366,10 +333,7 @@ int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
 void sparse_free(Ctx *c) {
     Sparse *sp = c->sp;
     if (!sp) return;
-    for (auto &T : sp->tiers)
-        for (void *p : {(void *)T.fkeys, (void *)T.res, (void *)T.ikeys, (void *)T.islot}) dev_free(c, p);
-    dev_free(c, sp->d_dense);
-    sp->d_dense = nullptr;
+    for (auto &T : sp->tiers) free_tier(c, T);
     (void)hipStreamSynchronize(c->stream);
     for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err})
         if (p) (void)hipFree(p);
