@@ -51,6 +51,7 @@ struct DistSparse {
     unsigned long long *d_mat = nullptr;     // all-gathered G*G*S counts (RCCL mode)
     uint32_t *d_root = nullptr;
     uint64_t sent_bytes = 0, edges = 0;
+    DedupEstimate est;
 };
 
 // ------------------------------------------------------------------ kernels
@@ -120,8 +121,10 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__rest
 __global__ void insert_recv_kernel(const uint64_t *__restrict__ in, uint64_t n, FrontRef t, uint32_t *err) {
     uint64_t fresh = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x)
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL) break;   // re-run into a larger table
         if (front_insert(t, in[i], err)) fresh++;
+    }
     wave_add(t.count, fresh);
 }
 
@@ -177,7 +180,7 @@ static int grow_to(Ctx *c, T **p, uint64_t n) {   // paired with a grow64'd buff
 
 static FrontRef fref(SpRank &R, size_t t) {
     SpTier &T = R.tiers[t];
-    return FrontRef{T.slots, T.cap ? T.cap - 1 : 0, R.d_cnt + t};
+    return FrontRef{T.slots, T.cap, R.d_cnt + t};
 }
 
 // Cross-rank exchange of G-segmented arrays (RCCL mode; loopback copies are done by the caller).
@@ -391,23 +394,40 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
             run_bucket<D, true, false>(c, d, desc, R, t, nullptr);
         }
         GM_TRY(exchange(c, d, lay, false));
-        // owners insert into their frontier tables, grown first to hold all they may receive
+        // owners insert into their tier tables, sized for load <= 0.7 of the predicted
+        // distinct keys; a misprediction re-runs the (idempotent) inserts once
+        uint64_t offered = 0, before = 0;
         for (size_t i = 0; i < d->ranks.size(); i++) {
             SpRank &R = d->ranks[i];
+            std::vector<uint64_t> in(S, 0);
             for (int s = 0; s < S; s++) {
-                uint64_t in = 0;
-                for (int q = 0; q < G; q++) in += mat[(size_t)q * nb + R.rank * S + s];
-                if (!in) continue;
-                const size_t u = t + 1 + s;
-                SpTier &U = R.tiers[u];
-                const uint64_t needc = pow2_at_least((U.fcount + in) * 5 / 4 + 1);
-                if (U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
-                for (int q = 0; q < G; q++) {
-                    const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
-                    if (n)
-                        hipLaunchKernelGGL(insert_recv_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream,
-                                           R.recvk + lay[i].recv_seg[q * S + s], n, fref(R, u), R.d_err);
+                for (int q = 0; q < G; q++) in[s] += mat[(size_t)q * nb + R.rank * S + s];
+                offered += in[s];
+                before += R.tiers[t + 1 + s].fcount;
+            }
+            for (int attempt = 0; attempt < 2; attempt++) {
+                for (int s = 0; s < S; s++) {
+                    if (!in[s]) continue;
+                    const size_t u = t + 1 + s;
+                    SpTier &U = R.tiers[u];
+                    const uint64_t needc = table_cap_for(U.fcount + (attempt ? in[s] : d->est.distinct(in[s])));
+                    if (U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
+                    for (int q = 0; q < G; q++) {
+                        const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
+                        if (n)
+                            hipLaunchKernelGGL(insert_recv_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream,
+                                               R.recvk + lay[i].recv_seg[q * S + s], n, fref(R, u), R.d_err);
+                    }
                 }
+                uint32_t e;
+                GM_HIP(hipMemcpyAsync(&e, R.d_err, 4, hipMemcpyDeviceToHost, c->stream));
+                GM_HIP(hipStreamSynchronize(c->stream));
+                if (e != DEV_ERR_TABLE_FULL || attempt) break;
+                if (trace_on())
+                    fprintf(stderr, "[gm] rank %d tier %zu: tables full at ratio %.3f, re-running\n", R.rank, t,
+                            d->est.ratio);
+                GM_HIP(hipMemsetAsync(R.d_err, 0, 4, c->stream));
+                d->est.missed();
             }
         }
         GM_TRY(check_err(c, d));
@@ -428,6 +448,10 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
             GM_HIP(hipStreamSynchronize(c->stream));
         }
         for (size_t u = t + 1; u < need; u++) d->gcount[u] = local[u];
+        uint64_t after = 0;
+        for (auto &R : d->ranks)
+            for (int s = 0; s < S; s++) after += R.tiers[t + 1 + s].fcount;
+        d->est.observe(after - before, offered);
     }
     while (!d->gcount.empty() && !d->gcount.back()) d->gcount.pop_back();
     const double t1 = now_ms();

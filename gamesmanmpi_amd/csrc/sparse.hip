@@ -45,6 +45,7 @@ __global__ __launch_bounds__(256) void expand_kernel(D d, const uint64_t *__rest
     for (int s = 0; s < S; s++) fresh[s] = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
+        if (*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL) break;   // the pass is re-run into larger tables
         const uint64_t k = ikeys[i];
         const int64_t tk = d.tier(k);
         d.visit(k, [&](uint64_t c) {
@@ -109,7 +110,7 @@ static int ensure_counts(Sparse *sp, size_t n) {
 
 static FrontRef front_ref(Sparse *sp, size_t t) {
     SpTier &T = sp->tiers[t];
-    return FrontRef{T.slots, T.cap ? T.cap - 1 : 0, sp->d_counts + t};
+    return FrontRef{T.slots, T.cap, sp->d_counts + t};
 }
 
 static ResRef res_ref(Sparse *sp, size_t t) { return res_ref_of(sp->tiers[t]); }
@@ -140,6 +141,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     sp->tiers[0].cap = 1024;
     hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, front_ref(sp, 0), root, sp->d_err);
     sp->tiers[0].fcount = 1;
+    DedupEstimate est;
 
     // ---------------- forward: tier by tier
     for (size_t t = 0; t < sp->tiers.size(); t++) {
@@ -158,27 +160,49 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         sp->tiers[t].count = n;
         sp->tiers[t].ni = sc[9];
         if (!sp->tiers[t].ni) continue;
-        // 2. size the tables of the tiers the children land in (exact edge counts, load <= 0.8)
+        // 2. size the tables of the tiers the children land in: load <= 0.7 for the
+        //    predicted distinct children; a misprediction costs one re-run
         if (sp->tiers.size() < t + S + 1) sp->tiers.resize(t + S + 1);
         GM_TRY(ensure_counts(sp, sp->tiers.size()));
+        uint64_t offered = 0, before = 0;
         for (int s = 0; s < S; s++) {
             const size_t u = t + 1 + s;
             sp->edges += sc[s];
-            const uint64_t need = pow2_at_least((sp->tiers[u].fcount + sc[s]) * 5 / 4 + 1);
+            offered += sc[s];
+            before += sp->tiers[u].fcount;
+            const uint64_t need = table_cap_for(sp->tiers[u].fcount + est.distinct(sc[s]));
             if (sc[s] && sp->tiers[u].cap < need) GM_TRY(tier_grow(c, sp, u, need));
         }
         // 3. expand the interior positions
-        Fronts<S> nx;
-        for (int s = 0; s < S; s++) nx.t[s] = front_ref(sp, t + 1 + s);
-        hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(sp->tiers[t].ni)), dim3(256), 0, c->stream, d,
-                           sp->tiers[t].ikeys, sp->tiers[t].ni, nx, sp->d_err);
-        GM_HIP(hipGetLastError());
+        for (int attempt = 0;; attempt++) {
+            Fronts<S> nx;
+            for (int s = 0; s < S; s++) nx.t[s] = front_ref(sp, t + 1 + s);
+            hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(sp->tiers[t].ni)), dim3(256), 0, c->stream, d,
+                               sp->tiers[t].ikeys, sp->tiers[t].ni, nx, sp->d_err);
+            GM_HIP(hipGetLastError());
+            uint32_t e;
+            GM_HIP(hipMemcpyAsync(&e, sp->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+            GM_HIP(hipStreamSynchronize(c->stream));
+            if (e != DEV_ERR_TABLE_FULL || attempt) break;
+            // mispredicted: grow to the exact upper bound (every edge distinct) and re-run
+            if (trace_on()) fprintf(stderr, "[gm] tier %zu: tables full at ratio %.3f, re-running\n", t, est.ratio);
+            GM_HIP(hipMemsetAsync(sp->d_err, 0, 4, c->stream));
+            for (int s = 0; s < S; s++) {
+                const size_t u = t + 1 + s;
+                const uint64_t need = table_cap_for(sp->tiers[u].fcount + sc[s]);
+                if (sc[s] && sp->tiers[u].cap < need) GM_TRY(tier_grow(c, sp, u, need));
+            }
+            est.missed();
+        }
         std::vector<unsigned long long> cnt(sp->tiers.size());
         GM_HIP(hipMemcpyAsync(cnt.data(), sp->d_counts, cnt.size() * sizeof(unsigned long long),
                               hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
         GM_TRY(read_err(c, sp));
+        uint64_t after = 0;
         for (size_t u = t + 1; u < cnt.size(); u++) sp->tiers[u].fcount = cnt[u];
+        for (int s = 0; s < S; s++) after += sp->tiers[t + 1 + s].fcount;
+        est.observe(after - before, offered);
         if (trace_on())
             fprintf(stderr, "[gm] tier %zu: %llu positions, %llu interior, %llu edges, at %.1f ms\n", t,
                     (unsigned long long)n, (unsigned long long)sp->tiers[t].ni, (unsigned long long)sc[0],

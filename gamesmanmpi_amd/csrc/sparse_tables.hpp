@@ -1,12 +1,16 @@
 // sparse_tables.hpp -- per-tier tables and the kernels shared by the single-GPU
 // sparse engine (sparse.hip) and its hash-sharded twin (dist_sparse.hip).
 //
-//   tier table     16-byte slots {u64 key, u64 score}, open addressing on mix64,
-//                  sized from the exact number of edges into the tier (load
-//                  <= 0.8, typically ~0.25).  The tiers above atomicCAS-insert
-//                  their children's keys (deduplication); classify_kernel then
-//                  streams it once, scoring every position in place; retrograde
-//                  lookups read key and score with one 16-byte load.
+//   tier table     16-byte slots {u64 key, u64 score}, linear probing from
+//                  home = mixed key * cap >> 64 (any capacity, no power-of-two
+//                  rounding).  Sized for load <= 0.7 from the edges into the
+//                  tier times a predicted distinct fraction (sparse.hip); an
+//                  insert that probes past MAX_PROBE slots flags the table full
+//                  and the insert pass is re-run into a larger table (inserts are
+//                  idempotent).  The tiers above atomicCAS-insert their
+//                  children's keys (deduplication); classify_kernel then streams
+//                  it once, scoring every position in place; retrograde lookups
+//                  read key and score with one 16-byte load.
 //   interior list  dense (key, slot) of the tier's undecided positions.
 // These replace the reference's CacheDict tables (src/cache_dict.py:7-82) and
 // the per-edge LOOK_UP / primitive test of Process.lookup (src/new_process.py:102-133).
@@ -24,13 +28,16 @@ struct alignas(16) RSlot {
 
 struct FrontRef {           // inserting into a tier table
     RSlot *s;
-    uint64_t mask;
+    uint64_t cap;
     unsigned long long *count;
 };
 struct ResRef {             // looking up in a tier table
     RSlot *s;
-    uint64_t mask;
+    uint64_t cap;
 };
+
+constexpr uint64_t MAX_PROBE = 2048;   // an insert probing further marks the table full
+constexpr double TABLE_LOAD = 0.7;     // planned load of a tier table
 template <int S>
 struct Fronts {
     FrontRef t[S];
@@ -52,9 +59,17 @@ struct SpTier {
 
 namespace {
 
+// home slot: the low half of mix64 scaled to cap (the high half picks the owner
+// rank in the sharded engine, so the two stay independent)
+__device__ __forceinline__ uint64_t home_slot(uint64_t key, uint64_t cap) {
+    const uint64_t m = mix64(key);
+    return __umul64hi((m << 32) | (m >> 32), cap);
+}
+
 __device__ __forceinline__ bool front_insert(const FrontRef &t, uint64_t key, uint32_t *err) {
-    uint64_t h = mix64(key) & t.mask;
-    for (uint64_t probe = 0; probe <= t.mask; probe++) {
+    uint64_t h = home_slot(key, t.cap);
+    const uint64_t lim = t.cap < MAX_PROBE ? t.cap : MAX_PROBE;
+    for (uint64_t probe = 0; probe < lim; probe++) {
         const uint64_t cur = t.s[h].key;
         if (cur == key) return false;
         if (cur == EMPTY_KEY) {
@@ -63,7 +78,7 @@ __device__ __forceinline__ bool front_insert(const FrontRef &t, uint64_t key, ui
             if (prev == EMPTY_KEY) return true;
             if (prev == key) return false;
         }
-        h = (h + 1) & t.mask;
+        h = h + 1 == t.cap ? 0 : h + 1;
     }
     atomicOr(err, DEV_ERR_TABLE_FULL);
     return false;
@@ -72,12 +87,12 @@ __device__ __forceinline__ bool front_insert(const FrontRef &t, uint64_t key, ui
 // score of key, or -1 when absent; each probe is one 16-byte load
 __device__ __forceinline__ int res_find(const ResRef &t, uint64_t key) {
     if (!t.s) return -1;
-    uint64_t h = mix64(key) & t.mask;
-    for (uint64_t probe = 0; probe <= t.mask; probe++) {
+    uint64_t h = home_slot(key, t.cap);
+    for (uint64_t probe = 0; probe < t.cap; probe++) {
         const u64x2 v = *(const u64x2 *)&t.s[h];
         if (v[0] == key) return (int)(v[1] & 0xFFFFu);
         if (v[0] == EMPTY_KEY) return -1;
-        h = (h + 1) & t.mask;
+        h = h + 1 == t.cap ? 0 : h + 1;
     }
     return -1;
 }
@@ -230,7 +245,7 @@ inline int tier_grow(Ctx *c, SpTier &T, uint64_t cap, uint32_t *d_err) {
     RSlot *ns;
     GM_TRY(tier_alloc(c, &ns, cap));
     if (T.cap) {
-        FrontRef dst{ns, cap - 1, nullptr};
+        FrontRef dst{ns, cap, nullptr};
         hipLaunchKernelGGL(front_rehash_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap, dst,
                            d_err);
         dev_free(c, T.slots);
@@ -240,7 +255,36 @@ inline int tier_grow(Ctx *c, SpTier &T, uint64_t cap, uint32_t *d_err) {
     return GM_OK;
 }
 
-inline ResRef res_ref_of(const SpTier &T) { return ResRef{T.slots, T.cap ? T.cap - 1 : 0}; }
+inline ResRef res_ref_of(const SpTier &T) { return ResRef{T.slots, T.cap}; }
+
+// capacity for `n` keys at the planned load (multiple of 1024)
+inline uint64_t table_cap_for(uint64_t n) {
+    const uint64_t c = (uint64_t)((double)n / TABLE_LOAD) + 1;
+    return std::max<uint64_t>(1024, (c + 1023) & ~1023ull);
+}
+
+// Distinct fraction of a tier's incoming edges, predicted from the last insert
+// pass (fresh keys / keys offered) with a margin; 1 (the exact upper bound)
+// until a pass of some size has been seen.  GM_TEST_DEDUP_RATIO pins the
+// ratio (tests use a tiny one to drive the full-table re-run path).
+struct DedupEstimate {
+    double ratio = 1.0;
+    bool pinned = false;
+    DedupEstimate() {
+        if (const char *e = getenv("GM_TEST_DEDUP_RATIO")) {
+            ratio = atof(e);
+            pinned = true;
+        }
+    }
+    void observe(uint64_t fresh, uint64_t offered) {
+        if (pinned || offered < (1u << 20)) return;
+        ratio = std::min(1.0, 1.25 * (double)fresh / (double)offered + 0.05);
+    }
+    void missed() {
+        if (!pinned) ratio = 1.0;
+    }
+    uint64_t distinct(uint64_t offered) const { return (uint64_t)(ratio * (double)offered) + 1; }
+};
 
 // classify a finished tier table: scores in place, interior list, edge counts
 // (scr[0, S) edges by step, scr[9] interior count, scr[10] positions seen)

@@ -219,3 +219,19 @@ def test_toot_large_boards_vs_oracle_digest(board, ranks):
     assert n == ref["positions"] and rec == ref["root_record"]
     assert [int(x) for x in ctx.tier_counts()] == ref["per_ply"]
     assert ctx.digest() == (ref["digest"], ref["positions"])
+
+
+@pytest.mark.parametrize("ranks", [1, 8])
+def test_toot_full_table_rerun(monkeypatch, ranks):
+    """A pinned, far too small distinct-child prediction fills every large tier
+    table: the insert pass must flag it and re-run into a larger table, and the
+    solve must still equal the C oracle's digest (Toot 4x4)."""
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["toot_4x4"]
+    monkeypatch.setenv("GM_TEST_DEDUP_RATIO", "0.02")
+    ctx = Context(TOOT, (4, 4), device=0)
+    if ranks > 1:
+        ctx.set_option(_lib.OPT_VIRTUAL_RANKS, ranks)
+    n, rec = ctx.solve(ctx.initial())
+    assert n == ref["positions"] and rec == ref["root_record"]
+    assert [int(x) for x in ctx.tier_counts()] == ref["per_ply"]
+    assert ctx.digest() == (ref["digest"], ref["positions"])
