@@ -148,6 +148,8 @@ def main():
     ap.add_argument("--cpu-heaps", type=int, default=8)
     ap.add_argument("--dist-batch", type=int, default=4, help="N>1: tiers per halo exchange")
     ap.add_argument("--dist-slots", type=int, default=4, help="N>1: halo buffers per split heap")
+    ap.add_argument("--dist-symmetry", type=int, default=1, choices=(0, 1),
+                    help="N>1: fill halo blocks that are a heap permutation of an own block locally")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     args = ap.parse_args()
@@ -187,6 +189,7 @@ def main():
     ctx.set_option(_lib.OPT_TIMING, 1)
     ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch)
     ctx.set_option(_lib.OPT_DIST_SLOTS, args.dist_slots)
+    ctx.set_option(_lib.OPT_DIST_SYMMETRY, args.dist_symmetry)
     if args.virtual_ranks > 1:
         ctx.set_option(_lib.OPT_VIRTUAL_RANKS, args.virtual_ranks)
     root = ctx.initial()
@@ -273,6 +276,7 @@ def main():
         "exchanged_bytes_per_step_rank0": st["exchanged_bytes"],
         "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
             "halo_batch_tiers": args.dist_batch, "halo_slots": args.dist_slots,
+            "halo_symmetric_fill": bool(args.dist_symmetry),
             "host_enqueue_ms_per_step_rank0": enqueue_ms / max(1, args.steps)},
         "cpu_baseline": None,
     }

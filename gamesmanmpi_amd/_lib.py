@@ -18,6 +18,7 @@ OPT_SUB_INTERLEAVE = 7
 OPT_SUB_ORDER = 8
 OPT_DIST_BATCH = 9
 OPT_DIST_SLOTS = 10
+OPT_DIST_SYMMETRY = 11
 BUF_DENSE_TABLE = 1
 REC_UNSOLVED = 0xFFFF
 

@@ -9,6 +9,17 @@
 // upper rank reads the two layers h = 6, 7 of its lower neighbour (tier t reads
 // the neighbour's tiers t-1 and t-2): a halo of <= 25 % of a rank per split heap.
 //
+// Symmetric fill (GM_OPT_DIST_SYMMETRY, default on).  The game is symmetric under
+// any permutation of heaps (DescSub: the same moves on every heap, one primitive
+// position), so a position's code equals that of any heap permutation of it.  A
+// halo block whose split nibble (6 or 7) can be swapped with an unsplit high
+// nibble >= 8 is that permutation of a block the upper rank owns, of the SAME
+// tier (a swap keeps the high sum), which the upper rank has just computed: it
+// copies it locally after that tier's launch instead of receiving it.  Only
+// halo blocks whose unsplit high nibbles are all <= 7 cross the link: 1/16, 1/8,
+// 1/4 of the halo at G = 2, 4, 8 (5 high nibbles).  Every position is still
+// computed by its owner; only the transfer is avoided.
+//
 // Schedule.  Tiers (high-nibble sums) are grouped in batches of B (GM_OPT_DIST_BATCH);
 // batch j is tiers [jB, jB+B).  Before batch j an upper rank needs its lower
 // neighbour's halo of tiers [jB-1, jB+B-2] -- message X_j, which the lower rank
@@ -40,7 +51,7 @@ namespace gm {
 constexpr int MAX_AXES = 3;
 
 enum EvKind { EV_PACKED = 0, EV_XCH = 1, EV_UNPACKED = 2, EV_KINDS = 3 };
-enum OpKind { OP_TIER, OP_PACK, OP_UNPACK, OP_SEND, OP_RECV, OP_RECORD, OP_WAIT };
+enum OpKind { OP_TIER, OP_PACK, OP_UNPACK, OP_SEND, OP_RECV, OP_RECORD, OP_WAIT, OP_FILL };
 
 struct Op {
     uint8_t kind, axis, ev, on_x;   // on_x: runs on X[axis], else on S
@@ -54,6 +65,8 @@ struct SubRank {
     bool owned = false;
     std::vector<uint32_t> off;          // per-tier offsets into dlist (owned blocks)
     uint32_t *dlist = nullptr;
+    std::vector<uint32_t> fill_off;     // per-tier offsets into dfill (symmetric fill)
+    uint32_t *dfill = nullptr;          // (dst, src) high parts, interleaved
     std::vector<uint32_t> send_off[MAX_AXES], recv_off[MAX_AXES];   // per-batch offsets
     uint32_t *dsend[MAX_AXES] = {}, *drecv[MAX_AXES] = {};
     uint8_t *sendbuf[MAX_AXES] = {}, *recvbuf[MAX_AXES] = {};       // rings of nslots slots
@@ -72,7 +85,7 @@ struct SubRank {
 struct DistSub {
     int heaps = 0, low = 0, high = 0, g = 0, G = 1, ntiers = 0, nt = 256;
     int batch = 4, nbatch = 0, nslots = 0;
-    int want_threads = 0, want_x4 = 0, want_order = 0, want_batch = 0, want_slots = 0;
+    int want_threads = 0, want_x4 = 0, want_order = 0, want_batch = 0, want_slots = 0, want_sym = 0;
     bool loopback = false;
     std::vector<SubRank> ranks;
     std::vector<int> lo, hi;            // per batch: tier range of X_j (empty if lo > hi)
@@ -96,6 +109,35 @@ static inline int owner_of(const DistSub *d, uint64_t H) {
 }
 
 static inline bool is_upper(int rank, int a) { return (rank >> a) & 1; }
+
+// Halo block H of axis a as a heap permutation of a block of the receiving (upper)
+// rank: swap the split nibble (6 or 7) with the first unsplit high nibble >= 8.
+// Returns false when every unsplit high nibble is <= 7 (the block is sent).
+static bool sym_source(const DistSub *d, uint64_t H, int a, uint64_t *src) {
+    const int ka = d->high - 1 - a;
+    for (int j = 0; j < d->high - d->g; j++) {
+        const uint64_t v = (uint64_t)nib(H, j);
+        if (v < 8) continue;
+        const uint64_t hv = (uint64_t)nib(H, ka);
+        *src = H - (v << (4 * j)) + (hv << (4 * j)) - (hv << (4 * ka)) + (v << (4 * ka));
+        return true;
+    }
+    return false;
+}
+
+// dst block <- src block for every (dst, src) pair: the symmetric halo fill
+__global__ void block_pair_copy_kernel(uint8_t *table, const uint32_t *__restrict__ pairs, int low) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint64_t bsz = 1ull << (4 * low);
+    const uint64_t dst = (uint64_t)pairs[2 * blockIdx.x] << (4 * low);
+    const uint64_t src = (uint64_t)pairs[2 * blockIdx.x + 1] << (4 * low);
+    if (bsz >= 16) {
+        for (uint64_t c = threadIdx.x; c < bsz / 16; c += blockDim.x)
+            *(u32x4 *)(table + dst + 16 * c) = *(const u32x4 *)(table + src + 16 * c);
+    } else {
+        for (uint64_t c = threadIdx.x; c < bsz; c += blockDim.x) table[dst + c] = table[src + c];
+    }
+}
 
 __global__ void block_copy_kernel(const uint8_t *__restrict__ src, const uint32_t *__restrict__ list,
                                   uint8_t *__restrict__ dst, int low, int pack) {
@@ -164,15 +206,29 @@ static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
     std::vector<int> xb(T, -1);   // halo message carrying tier t
     for (int j = 0; j < NB; j++)
         for (int t = d->lo[j]; t <= d->hi[j]; t++) xb[t] = j;
-    std::vector<std::vector<uint32_t>> own(T), Sd[MAX_AXES], Rv[MAX_AXES];
+    std::vector<std::vector<uint32_t>> own(T), Sd[MAX_AXES], Rv[MAX_AXES], fill(T);
     for (int a = 0; a < MAX_AXES; a++) { Sd[a].resize(NB); Rv[a].resize(NB); }
     for (uint64_t H = 0; H < nhigh; H++) {
         const int o = owner_of(d, H), t = tsum(H);
         for (int a = 0; a < d->g; a++) {
             const int h = nib(H, d->high - 1 - a);
             if ((h != 6 && h != 7) || xb[t] < 0) continue;
-            if (o == R.rank && !is_upper(R.rank, a)) Sd[a][xb[t]].push_back((uint32_t)H);
-            if (is_upper(R.rank, a) && o == (R.rank ^ (1 << a))) Rv[a][xb[t]].push_back((uint32_t)H);
+            uint64_t src = 0;
+            const bool sym = c->dist_symmetry && sym_source(d, H, a, &src);
+            if (o == R.rank && !is_upper(R.rank, a) && !sym) Sd[a][xb[t]].push_back((uint32_t)H);
+            if (is_upper(R.rank, a) && o == (R.rank ^ (1 << a))) {
+                if (!sym) {
+                    Rv[a][xb[t]].push_back((uint32_t)H);
+                } else {
+                    if (owner_of(d, src) != R.rank || tsum(src) != t) {
+                        set_error("symmetric halo source of block %llx is not an own block of its tier",
+                                  (unsigned long long)H);
+                        return GM_E_STATE;
+                    }
+                    fill[t].push_back((uint32_t)H);
+                    fill[t].push_back((uint32_t)src);
+                }
+            }
         }
         if (o == R.rank) {
             own[t].push_back((uint32_t)H);
@@ -193,6 +249,9 @@ static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
         flatten(own, R.off, flat);
         if (c->sub_order == 1) sort_tiers_morton(flat, R.off, d->high);
         GM_TRY(upload(flat, &R.dlist));
+        std::vector<uint32_t> ff;
+        flatten(fill, R.fill_off, ff);
+        GM_TRY(upload(ff, &R.dfill));
     }
     const uint64_t bb = 1ull << (4 * d->low);
     for (int a = 0; a < d->g; a++) {
@@ -251,6 +310,7 @@ static void build_ops(DistSub *d, SubRank &R) {
         }
         for (int t = j * B; t < std::min(T, j * B + B); t++) {
             op(OP_TIER, 0, 0, false, t, R.rank);
+            if (cnt(R.fill_off, t)) op(OP_FILL, 0, 0, false, t, R.rank);
             for (int jj : send_after[t])
                 for (int a = 0; a < d->g; a++) {
                     if (is_upper(R.rank, a) || !cnt(R.send_off[a], jj)) continue;
@@ -288,6 +348,7 @@ static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
     d->want_order = c->sub_order;
     d->want_batch = c->dist_batch;
     d->want_slots = c->dist_slots;
+    d->want_sym = c->dist_symmetry;
     if (!sub_kernel_exists(d->low, d->high, d->nt)) { set_error("no dense kernel"); return GM_E_GAME; }
     d->ntiers = 15 * d->high + 1;
     d->batch = std::max(1, std::min(c->dist_batch, d->ntiers));
@@ -356,6 +417,10 @@ static int exec_op(DistSub *d, SubRank &R, const Op &o) {
     switch (o.kind) {
     case OP_TIER:
         launch_sub_tier(d->low, d->high, d->nt, cnt(R.off, j), R.table, R.dlist + R.off[j], d->zero, st);
+        break;
+    case OP_FILL:   // fill_off counts u32 entries: two per block
+        hipLaunchKernelGGL(block_pair_copy_kernel, dim3(cnt(R.fill_off, j) / 2), dim3(256), 0, st, R.table,
+                           R.dfill + R.fill_off[j], d->low);
         break;
     case OP_PACK:
         copy_blocks(d, R.table, R.dsend[a] + R.send_off[a][j], cnt(R.send_off[a], j), send_ptr(d, R, a, j), true,
@@ -456,7 +521,7 @@ int dist_sub_solve(Ctx *c, uint64_t root) {
     DistSub *d = c->dist_sub;
     if (!d || d->heaps != c->sub.heaps || d->G != G || d->loopback != loopback ||
         d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave || d->want_order != c->sub_order ||
-        d->want_batch != c->dist_batch || d->want_slots != c->dist_slots ||
+        d->want_batch != c->dist_batch || d->want_slots != c->dist_slots || d->want_sym != c->dist_symmetry ||
         (!loopback && c->adopted_dense && d->ranks[0].table != c->adopted_dense)) {
         dist_sub_free(c);
         d = c->dist_sub = new DistSub();
@@ -588,6 +653,7 @@ void dist_sub_free(Ctx *c) {
     for (auto &R : d->ranks) {
         if (R.owned && R.table) (void)hipFree(R.table);
         if (R.dlist) (void)hipFree(R.dlist);
+        if (R.dfill) (void)hipFree(R.dfill);
         for (int a = 0; a < MAX_AXES; a++) {
             if (R.dsend[a]) (void)hipFree(R.dsend[a]);
             if (R.drecv[a]) (void)hipFree(R.drecv[a]);

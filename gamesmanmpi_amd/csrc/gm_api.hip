@@ -226,6 +226,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         if (v < 1 || v > 128) { set_error("dist_slots must be 1..128"); return GM_E_ARG; }
         c->dist_slots = (int)v;
         return GM_OK;
+    case GM_OPT_DIST_SYMMETRY:
+        if (v < 0 || v > 1) { set_error("dist_symmetry must be 0 or 1"); return GM_E_ARG; }
+        c->dist_symmetry = (int)v;
+        return GM_OK;
     case GM_OPT_VIRTUAL_RANKS:
         if (v < 1 || v > 64) { set_error("virtual ranks must be 1..64"); return GM_E_ARG; }
         c->virtual_ranks = (int)v;

@@ -87,6 +87,7 @@ struct Ctx {
     hipStream_t comm_stream = nullptr;
     int dist_batch = 4;      // sharded dense path: tiers per halo exchange
     int dist_slots = 4;      // sharded dense path: ring of exchange buffers, in batches
+    int dist_symmetry = 1;   // sharded dense path: halo blocks derivable by a heap swap are filled locally
 
     // results
     bool solved = false;

@@ -85,7 +85,9 @@ enum {
                                   4 = u16 image, 5 = u16 image + anti-diagonal pass B; 1 = one block */
     GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton (default) */
     GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
-    GM_OPT_DIST_SLOTS = 10  /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
+    GM_OPT_DIST_SLOTS = 10, /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
+    GM_OPT_DIST_SYMMETRY = 11 /* sharded SUBTRACT path: 1 (default) = fill halo blocks that are a heap
+                                 permutation of an own block locally, 0 = receive every halo block */
 };
 
 /* Buffer roles for gm_adopt_buffer. */

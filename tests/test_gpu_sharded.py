@@ -31,10 +31,11 @@ def _solve(game, params, ranks, root=None, engine=None, **opts):
     return ctx, n, rec
 
 
-@pytest.mark.parametrize("heaps,ranks", [(4, 2), (5, 2), (5, 4), (6, 2), (6, 4), (6, 8)])
-def test_dense_sharded_vs_oracle(oracle, heaps, ranks):
+@pytest.mark.parametrize("sym", [0, 1])
+@pytest.mark.parametrize("heaps,ranks", [(4, 2), (5, 2), (5, 4), (6, 2), (6, 4), (6, 8), (7, 2), (7, 4), (7, 8)])
+def test_dense_sharded_vs_oracle(oracle, heaps, ranks, sym):
     ref = oracle.subtract_dense(heaps)
-    ctx, n, rec = _solve(SUB, (heaps,), ranks)
+    ctx, n, rec = _solve(SUB, (heaps,), ranks, dist_symmetry=sym)
     assert ctx.stats()["engine"] == _lib.ENGINE_DIST_DENSE
     k, r = ctx.export()
     assert n == 16 ** heaps
@@ -45,7 +46,8 @@ def test_dense_sharded_vs_oracle(oracle, heaps, ranks):
 @pytest.mark.parametrize("batch,slots", [(1, 1), (1, 4), (2, 1), (3, 2), (4, 4), (8, 2), (16, 1), (100, 4)])
 @pytest.mark.parametrize("ranks", [2, 8])
 def test_dense_sharded_batches_and_rings(oracle, batch, slots, ranks):
-    """Every halo batch size and send-ring depth gives the oracle's table (6 heaps: 46 tiers)."""
+    """Every halo batch size and send-ring depth gives the oracle's table (6 heaps: 46 tiers;
+    at 2 ranks most halo blocks come from the symmetric fill, at 8 none)."""
     ref = oracle.subtract_dense(6)
     ctx, n, rec = _solve(SUB, (6,), ranks, dist_batch=batch, dist_slots=slots)
     k, r = ctx.export()
@@ -65,13 +67,17 @@ def test_dense_sharded_full_2_32_matches_single_gpu():
     single, n1, rec1 = _solve(SUB, (8,), 1)
     d1 = single.digest()
     single.close()
-    for ranks in (2, 8):
-        ctx, n, rec = _solve(SUB, (8,), ranks)
-        assert (n, rec) == (n1, rec1)
-        assert ctx.digest() == d1
-        st = ctx.stats()
-        assert st["exchanged_bytes"] > 0
-        ctx.close()
+    halo = {2: 512 << 20, 4: 2 * (512 << 20), 8: 3 * (512 << 20)}   # full halo bytes per solve, all ranks
+    for ranks in (2, 4, 8):
+        for sym in (1, 0):
+            ctx, n, rec = _solve(SUB, (8,), ranks, dist_symmetry=sym)
+            assert (n, rec) == (n1, rec1)
+            assert ctx.digest() == d1
+            sent = ctx.stats()["exchanged_bytes"]
+            # the symmetric fill leaves 1/16, 1/8, 1/4 of the halo to cross the link
+            want = halo[ranks] // {2: 16, 4: 8, 8: 4}[ranks] if sym else halo[ranks]
+            assert sent == want, (ranks, sym, sent, want)
+            ctx.close()
 
 
 @pytest.mark.parametrize("ranks", [2, 3, 8])
