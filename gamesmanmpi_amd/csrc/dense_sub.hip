@@ -54,6 +54,10 @@ struct DenseSub {
     uint64_t *d_acc = nullptr;          // digest / counters
     hipGraphExec_t graph = nullptr;
     hipStream_t graph_stream = nullptr;
+    // dataflow kernel (nt == -3): per-XCD item lists, heads, per-block flags
+    void *flow_items = nullptr;
+    uint32_t *flow_list_off = nullptr, *flow_heads = nullptr, *flow_flags = nullptr, *flow_abort = nullptr;
+    unsigned flow_grid = 0;
     std::vector<hipEvent_t> ev;         // timing events
 };
 
@@ -396,23 +400,17 @@ __device__ __forceinline__ uint32_t code_x4(uint32_t b) {   // parent_code on fo
 #ifndef GM_B4_WAVES
 #define GM_B4_WAVES 1
 #endif
-template <int HIGH>
-__global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *__restrict__ table,
-                                                          const uint32_t *__restrict__ blocks, uint32_t nblk,
-                                                          const uint8_t *__restrict__ zero) {
+// One workgroup solves the four blocks hp[0..3] (valid[k] false: slot unused).
+// CPOL = cache policy of the child loads and the stores (0 plain; CPOL_SC1 in the
+// dataflow kernel, whose consumers may sit on another XCD: write-through stores,
+// L1-bypassing loads -- MI355X_MICROARCH.md, inter-workgroup visibility).
+constexpr int CPOL_SC1 = 16;
+template <int HIGH, int CPOL, int LCPOL = CPOL>
+__device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint8_t *__restrict__ zero,
+                                         const uint32_t (&hp)[4], const bool (&valid)[4], uint32_t *s) {
     constexpr int NPOS = 4096, NCH = 256, NT = 256, K = 4;
     constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
-    __shared__ __attribute__((aligned(16))) uint32_t s[NPOS];   // 16 KiB
     const int tid = threadIdx.x;
-    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
-    uint32_t hp[K];
-    bool valid[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint32_t idx = grp * K + k;
-        valid[k] = idx < nblk;
-        hp[k] = valid[k] ? blocks[idx] : 0u;
-    }
     static_assert(NCH == NT, "one chunk per thread");
 
     // ---- pass A: chunk tid = positions 16 tid .. 16 tid + 15
@@ -425,7 +423,8 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *
             child_blocks<3, HIGH, NMAX>(table, zero, hp[k], valid[k], src);
             u32x4v v[NMAX];
 #pragma unroll
-            for (int m = 0; m < NMAX; m++) v[m] = load16(block_rsrc(src[m], NPOS), 16u * c);
+            for (int m = 0; m < NMAX; m++)
+                v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(block_rsrc(src[m], NPOS), 16u * c, 0, LCPOL));
             f[k] = fold16(v);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -496,11 +495,145 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *
             out[3][j] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);
         }
 #pragma unroll
-        for (int k = 0; k < K; k++) __builtin_amdgcn_raw_buffer_store_b128(out[k], wr[k], 16u * c, 0, 0);
+        for (int k = 0; k < K; k++) __builtin_amdgcn_raw_buffer_store_b128(out[k], wr[k], 16u * c, 0, CPOL);
+    }
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *__restrict__ table,
+                                                          const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                          const uint8_t *__restrict__ zero) {
+    constexpr int K = 4;
+    __shared__ __attribute__((aligned(16))) uint32_t s[4096];   // 16 KiB
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
+    uint32_t hp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = grp * K + k;
+        valid[k] = idx < nblk;
+        hp[k] = valid[k] ? blocks[idx] : 0u;
+    }
+    b4_solve<HIGH, 0>(table, zero, hp, valid, s);
+}
+
+// ---------------------------------------------------------------------------
+// Dataflow variant: the whole solve in ONE launch (GM_OPT_SUB_INTERLEAVE 7).
+// The tiered launches pay a fill/drain of ~12-16 us each (76 per solve): a tier's
+// last workgroups run on an almost idle chip.  Here every block still waits for
+// exactly its <= 10 child blocks, not for a whole tier:
+//   * items = groups of 4 blocks of one tier, in tier order, split into one list
+//     per XCD (the same contiguous Morton runs the tiered launch gives each XCD);
+//     a workgroup reads its XCD id and dequeues from that list with one atomic,
+//     then from the other lists once its own is empty;
+//   * before pass A one lane per child block polls the child's flag (sc1 loads);
+//     after pass C every wave drains its sc1 stores (s_waitcnt vmcnt(0)), the
+//     workgroup joins a barrier and lane k sets flag[hp[k]] (sc1 store).
+// No deadlock: lists are dequeued in tier order and a block only waits on lower
+// tiers, so along any chain of waits the tiers strictly decrease; a workgroup
+// waits only after it has dequeued, i.e. while running.  Waits are bounded in
+// time (GM_FLOW_WAIT_TICKS of the 100 MHz clock): a timeout raises `abort`,
+// every later wait is skipped, and the solve reports an error instead of hanging.
+constexpr uint64_t GM_FLOW_WAIT_TICKS = 5000000;   // 50 ms
+struct FlowItem {
+    uint32_t off;   // first block in the tier-sorted block list
+    uint32_t n;     // blocks in the group (1..4)
+};
+
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 7u;
+}
+
+#ifndef GM_FLOW_WAVES
+#define GM_FLOW_WAVES 1
+#endif
+#ifndef GM_FLOW_LOAD_CPOL
+#define GM_FLOW_LOAD_CPOL CPOL_SC1
+#endif
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_FLOW_WAVES) void sub_flow_kernel_b4(uint8_t *__restrict__ table,
+                                                          const uint32_t *__restrict__ blocks,
+                                                          const FlowItem *__restrict__ items,
+                                                          const uint32_t *__restrict__ list_off,
+                                                          uint32_t *heads, uint32_t *flags, uint32_t *abort_flag,
+                                                          const uint8_t *__restrict__ zero) {
+    constexpr int K = 4;
+    __shared__ __attribute__((aligned(16))) uint32_t s[4096];   // 16 KiB
+    __shared__ int item_sh;
+    const int tid = threadIdx.x;
+    const uint32_t home = xcc_id();
+    int list = (int)home, tries = 0;
+    for (;;) {
+        if (tid == 0) {
+            int got = -1;
+            while (tries < 8) {
+                const uint32_t len = list_off[list + 1] - list_off[list];
+                const uint32_t i = atomicAdd(&heads[list], 1u);
+                if (i < len) { got = (int)(list_off[list] + i); break; }
+                list = (list + 1) & 7;
+                tries++;
+            }
+            item_sh = got;
+        }
+        __syncthreads();
+        const int it = item_sh;
+        if (it < 0) break;
+        const FlowItem item = items[it];
+        uint32_t hp[K];
+        bool valid[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            valid[k] = (uint32_t)k < item.n;
+            hp[k] = valid[k] ? blocks[item.off + k] : 0u;
+        }
+        // wait for the child blocks: lane 10k + m of wave 0 polls child m of block k
+        if (tid < 64) {
+            const int k = tid / 10, m = tid % 10, j = m >> 1, sub = (m & 1) + 1;
+            bool need = false;
+            uint32_t child = 0;
+            if (k < K && j < HIGH) {
+                const uint32_t h = (hp[k] >> (4 * j)) & 15u;
+                need = valid[k] && h >= (uint32_t)sub;
+                child = hp[k] - ((uint32_t)sub << (4 * j));
+            }
+            if (need && __hip_atomic_load(&flags[child], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__hip_atomic_load(&flags[child], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+                    if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > GM_FLOW_WAIT_TICKS) {
+                        __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        b4_solve<HIGH, CPOL_SC1, GM_FLOW_LOAD_CPOL>(table, zero, hp, valid, s);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid < K && valid[tid]) __hip_atomic_store(&flags[hp[tid]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 typedef void (*tier_kernel_t)(uint8_t *, const uint32_t *, uint32_t, const uint8_t *);
+typedef void (*flow_kernel_t)(uint8_t *, const uint32_t *, const FlowItem *, const uint32_t *, uint32_t *, uint32_t *,
+                              uint32_t *, const uint8_t *);
+
+static flow_kernel_t pick_flow(int high) {
+    switch (high) {
+    case 0: return sub_flow_kernel_b4<0>;
+    case 1: return sub_flow_kernel_b4<1>;
+    case 2: return sub_flow_kernel_b4<2>;
+    case 3: return sub_flow_kernel_b4<3>;
+    case 4: return sub_flow_kernel_b4<4>;
+    case 5: return sub_flow_kernel_b4<5>;
+    }
+    return nullptr;
+}
 
 static tier_kernel_t pick_b4(int high) {
     switch (high) {
@@ -567,6 +700,7 @@ static tier_kernel_t pick_interleaved(int high, int nt) {
 }
 
 bool sub_kernel_exists(int low, int high, int nt) {
+    if (nt == -3) return low == 3 && pick_flow(high) != nullptr;
     return nt <= 0 ? (low == 3 && pick_interleaved(high, nt) != nullptr) : pick_kernel(low, high, nt) != nullptr;
 }
 
@@ -584,6 +718,7 @@ int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 4) return 0;
     if (low == 3 && c->sub_interleave == 5) return -1;
     if (low == 3 && c->sub_interleave == 6) return -2;
+    if (low == 3 && c->sub_interleave == 7) return -3;
     return c->sub_threads;
 }
 
@@ -663,6 +798,41 @@ static int prepare(Ctx *c, DenseSub *d) {
     GM_HIP(hipMalloc(&d->zero, zbytes));
     GM_HIP(hipMemset(d->zero, 0, zbytes));
     GM_HIP(hipMalloc(&d->d_acc, 2 * sizeof(uint64_t)));
+    if (nt == -3) {
+        // per-XCD item lists: each tier's 4-block groups split into the same 8
+        // contiguous runs that xcd_order gives the tiered launch
+        std::vector<FlowItem> lists[8];
+        for (size_t t = 0; t + 1 < d->tier_off.size(); t++) {
+            const uint32_t nb = d->tier_off[t + 1] - d->tier_off[t], ng = (nb + 3) / 4, q = ng >> 3, r = ng & 7;
+            for (uint32_t x = 0; x < 8; x++) {
+                const uint32_t g0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, len = x < r ? q + 1 : q;
+                for (uint32_t g = g0; g < g0 + len; g++)
+                    lists[x].push_back(FlowItem{d->tier_off[t] + 4 * g, std::min(4u, nb - 4 * g)});
+            }
+        }
+        std::vector<FlowItem> all;
+        std::vector<uint32_t> off(9, 0);
+        for (int x = 0; x < 8; x++) {
+            off[x] = (uint32_t)all.size();
+            all.insert(all.end(), lists[x].begin(), lists[x].end());
+        }
+        off[8] = (uint32_t)all.size();
+        GM_HIP(hipMalloc(&d->flow_items, all.size() * sizeof(FlowItem)));
+        GM_HIP(hipMemcpy(d->flow_items, all.data(), all.size() * sizeof(FlowItem), hipMemcpyHostToDevice));
+        GM_HIP(hipMalloc(&d->flow_list_off, 9 * 4));
+        GM_HIP(hipMemcpy(d->flow_list_off, off.data(), 9 * 4, hipMemcpyHostToDevice));
+        GM_HIP(hipMalloc(&d->flow_heads, 8 * 4));
+        GM_HIP(hipMalloc(&d->flow_abort, 4));
+        GM_HIP(hipMalloc(&d->flow_flags, nhigh * 4));
+        int per_cu = 0, dev = 0;
+        GM_HIP(hipGetDevice(&dev));
+        hipDeviceProp_t prop;
+        GM_HIP(hipGetDeviceProperties(&prop, dev));
+        GM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(pick_flow(high)),
+                                                            256, 0));
+        d->flow_grid = (unsigned)std::max(1, per_cu) * (unsigned)prop.multiProcessorCount;
+        d->flow_grid = std::min<unsigned>(d->flow_grid, (unsigned)all.size());
+    }
     uint64_t bytes = d->slots;
     if (c->adopted_dense) {
         if (c->adopted_dense_bytes < bytes) {
@@ -694,6 +864,19 @@ static int ensure_events(DenseSub *d) {
 
 static int launch_tiers(Ctx *c, DenseSub *d, bool timed) {
     int ntiers = (int)d->tier_off.size() - 1;
+    if (d->nt == -3) {
+        const uint64_t nhigh = 1ull << (4 * d->high);
+        if (timed) GM_HIP(hipEventRecord(d->ev[0], c->stream));
+        GM_HIP(hipMemsetAsync(d->flow_heads, 0, 8 * 4, c->stream));
+        GM_HIP(hipMemsetAsync(d->flow_abort, 0, 4, c->stream));
+        GM_HIP(hipMemsetAsync(d->flow_flags, 0, nhigh * 4, c->stream));
+        hipLaunchKernelGGL(pick_flow(d->high), dim3(d->flow_grid), dim3(256), 0, c->stream, d->table, d->d_blocks,
+                           (const FlowItem *)d->flow_items, d->flow_list_off, d->flow_heads, d->flow_flags,
+                           d->flow_abort, d->zero);
+        if (timed) GM_HIP(hipEventRecord(d->ev[1], c->stream));
+        GM_HIP(hipGetLastError());
+        return GM_OK;
+    }
     for (int t = 0; t < ntiers; t++) {
         uint32_t nb = d->tier_off[t + 1] - d->tier_off[t];
         if (!nb) continue;
@@ -741,9 +924,15 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
         GM_TRY(launch_tiers(c, d, timed));
     }
     uint8_t rs;
+    uint32_t aborted = 0;
     GM_HIP(hipMemcpyAsync(&rs, d->table + root, 1, hipMemcpyDeviceToHost, c->stream));
+    if (d->nt == -3) GM_HIP(hipMemcpyAsync(&aborted, d->flow_abort, 4, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     double t1 = now_ms();
+    if (aborted) {
+        set_error("dataflow solve: a wait for a child block timed out");
+        return GM_E_STATE;
+    }
 
     c->root_record = record_of_code(rs);
     uint64_t n = 1;
@@ -773,7 +962,7 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
     if (timed) {
         float total = 0;
         int launches = 0;
-        for (int t = 0; t < ntiers; t++) {
+        for (int t = 0; t < ntiers && d->nt != -3; t++) {
             if (d->tier_off[t + 1] == d->tier_off[t]) continue;
             launches++;
             if (c->use_graph) continue;
@@ -781,7 +970,8 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
             GM_HIP(hipEventElapsedTime(&ms, d->ev[2 * t], d->ev[2 * t + 1]));
             total += ms;
         }
-        if (c->use_graph) GM_HIP(hipEventElapsedTime(&total, d->ev[0], d->ev[1]));
+        if (d->nt == -3) launches = 1;
+        if (c->use_graph || d->nt == -3) GM_HIP(hipEventElapsedTime(&total, d->ev[0], d->ev[1]));
         c->stats.kernel_ms = total;
         c->stats.kernel_launches = launches;
     }
@@ -856,6 +1046,9 @@ void dense_sub_free(Ctx *c) {
     if (d->zero) (void)hipFree(d->zero);
     if (d->d_blocks) (void)hipFree(d->d_blocks);
     if (d->d_acc) (void)hipFree(d->d_acc);
+    for (void *p : {(void *)d->flow_items, (void *)d->flow_list_off, (void *)d->flow_heads, (void *)d->flow_flags,
+                    (void *)d->flow_abort})
+        if (p) (void)hipFree(p);
     delete d;
     c->dsub = nullptr;
 }

@@ -343,6 +343,7 @@ static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
         return GM_E_ARG;
     }
     d->nt = sub_kernel_threads(c, d->low);
+    if (d->nt == -3) d->nt = -2;   // the dataflow kernel is single-GPU: ranks run the tiered byte-image kernel
     d->want_threads = c->sub_threads;
     d->want_x4 = c->sub_interleave;
     d->want_order = c->sub_order;

@@ -211,7 +211,7 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sub_threads = (int)v;
         return GM_OK;
     case GM_OPT_SUB_INTERLEAVE:
-        if (v != 1 && (v < 4 || v > 6)) { set_error("sub_interleave must be 1, 4, 5 or 6"); return GM_E_ARG; }
+        if (v != 1 && (v < 4 || v > 7)) { set_error("sub_interleave must be 1, 4, 5, 6 or 7"); return GM_E_ARG; }
         c->sub_interleave = (int)v;
         return GM_OK;
     case GM_OPT_SUB_ORDER:
