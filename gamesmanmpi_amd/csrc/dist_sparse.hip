@@ -61,13 +61,16 @@ constexpr int MAXBINS = 64 * 3;
 // COUNT: LDS histogram, one global atomic per bin per workgroup.  SCATTER: the
 // workgroup reserves a range per bin and a second visit writes the keys (and, in
 // the backward pass, the parent's interior index).  BACK: primitive children are
-// folded locally (never sent) and the local best initialises best[i].
+// folded locally (never sent) and the local best initialises best[i].  The forward
+// scatter marks parents with a LOSS-in-0 child (iwon); the backward pass sends
+// nothing for them (their value is final: WIN in 1).
 template <class D, bool SCATTER, bool BACK>
 __global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n, int G,
                                                      unsigned long long *hist,
                                                      const unsigned long long *__restrict__ seg,
                                                      unsigned long long *cursor, uint64_t *out_keys,
-                                                     uint32_t *out_parent, uint32_t *best, uint32_t *err) {
+                                                     uint32_t *out_parent, uint32_t *best, uint8_t *iwon,
+                                                     uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
     __shared__ unsigned int lh[MAXBINS], lh2[MAXBINS];
     __shared__ unsigned long long lbase[MAXBINS];
@@ -76,14 +79,17 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__rest
         for (int b = threadIdx.x; b < nb; b += blockDim.x) lh[b] = lh2[b] = 0;
         __syncthreads();
         const uint64_t i = base + threadIdx.x;
-        const bool live = i < n;
+        const bool won_before = BACK && i < n && iwon[i];
+        const bool live = i < n && !won_before;
         const uint64_t k = live ? ikeys[i] : 0;
         const int64_t tk = live ? d.tier(k) : 0;
         // one pass over the children; `emit(c, bin)` is called for the ones that leave this thread
+        bool won = false;
         auto walk = [&](auto emit) -> uint32_t {
             uint32_t local = 0;
             if (!live) return local;
             d.visit(k, [&](uint64_t c) {
+                if (SCATTER && !BACK && !won) won = d.primitive(c) == LOSS;
                 if (BACK) {
                     const int p = d.primitive(c);
                     if (p != UNDECIDED) {
@@ -113,6 +119,8 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__rest
                 if (BACK) out_parent[at] = (uint32_t)i;
             });
             if (BACK && live) best[i] = local;
+            if (BACK && won_before) best[i] = 0xFFFFu;
+            if (!BACK && live) iwon[i] = won ? 1 : 0;
         }
         __syncthreads();
     }
@@ -202,7 +210,7 @@ static void run_bucket(Ctx *c, DistSparse *d, const D &desc, SpRank &R, size_t t
     SpTier &T = R.tiers[t];
     if (!T.ni) return;
     hipLaunchKernelGGL((bucket_kernel<D, SCATTER, BACK>), dim3(grid_for(T.ni)), dim3(256), 0, c->stream, desc, T.ikeys,
-                       T.ni, d->G, R.d_hist, R.d_seg, R.d_cursor, R.sendk, R.sendp, best, R.d_err);
+                       T.ni, d->G, R.d_hist, R.d_seg, R.d_cursor, R.sendk, R.sendp, best, T.iwon, R.d_err);
 }
 
 // counts[r][dest*S+dt] for all ranks -> host matrix (G x G*S)
@@ -526,7 +534,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     uint64_t n = 0, tb = 0;
     for (auto v : d->gcount) n += v;
     for (auto &R : d->ranks)
-        for (auto &T : R.tiers) tb += T.cap * sizeof(RSlot) + T.ni * 12;
+        for (auto &T : R.tiers) tb += T.cap * sizeof(RSlot) + T.ni * 13;
     c->n_positions = n;
     c->tier_counts = d->gcount;
     c->stats.n_positions = n;

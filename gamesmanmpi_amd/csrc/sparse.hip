@@ -36,9 +36,12 @@ struct Sparse {
 };
 
 // ----------------------------------------------------------------- kernels
+// Also marks the parents with a LOSS-in-0 child (a move that wins at once): their
+// value is final here (WIN in 1), so the retrograde pass skips their lookups.
 template <class D>
 __global__ __launch_bounds__(256) void expand_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n,
-                                                     Fronts<D::MAX_SKIP> next, uint32_t *err) {
+                                                     Fronts<D::MAX_SKIP> next, uint8_t *__restrict__ iwon,
+                                                     uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
     uint64_t fresh[S];
 #pragma unroll
@@ -48,13 +51,16 @@ __global__ __launch_bounds__(256) void expand_kernel(D d, const uint64_t *__rest
         if (*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL) break;   // the pass is re-run into larger tables
         const uint64_t k = ikeys[i];
         const int64_t tk = d.tier(k);
+        bool won = false;
         d.visit(k, [&](uint64_t c) {
             const int64_t dt = d.tier(c) - tk;
 #pragma unroll
             for (int s = 0; s < S; s++)
                 if (dt == s + 1 && front_insert(next.t[s], c, err)) fresh[s]++;
+            if (!won) won = d.primitive(c) == LOSS;
             return true;
         });
+        iwon[i] = won ? 1 : 0;
     }
 #pragma unroll
     for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
@@ -62,11 +68,16 @@ __global__ __launch_bounds__(256) void expand_kernel(D d, const uint64_t *__rest
 
 template <class D>
 __global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restrict__ ikeys,
-                                                    const uint32_t *__restrict__ islot, uint64_t n, ResRef self,
+                                                    const uint32_t *__restrict__ islot,
+                                                    const uint8_t *__restrict__ iwon, uint64_t n, ResRef self,
                                                     Ress<D::MAX_SKIP> next, uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
+        if (iwon[i]) {   // a LOSS-in-0 child: nothing beats it, no lookup needed
+            self.s[islot[i]].score = parent_score(0xFFFFu);
+            continue;
+        }
         const uint64_t k = ikeys[i];
         const int64_t tk = d.tier(k);
         uint32_t best = 0;
@@ -178,7 +189,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
             Fronts<S> nx;
             for (int s = 0; s < S; s++) nx.t[s] = front_ref(sp, t + 1 + s);
             hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(sp->tiers[t].ni)), dim3(256), 0, c->stream, d,
-                               sp->tiers[t].ikeys, sp->tiers[t].ni, nx, sp->d_err);
+                               sp->tiers[t].ikeys, sp->tiers[t].ni, nx, sp->tiers[t].iwon, sp->d_err);
             GM_HIP(hipGetLastError());
             uint32_t e;
             GM_HIP(hipMemcpyAsync(&e, sp->d_err, 4, hipMemcpyDeviceToHost, c->stream));
@@ -220,8 +231,8 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
             const size_t u = tt + 1 + s;
             nx.t[s] = u < sp->tiers.size() ? res_ref(sp, u) : ResRef{nullptr, 0};
         }
-        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, d, T.ikeys, T.islot, T.ni,
-                           res_ref(sp, tt), nx, sp->d_err);
+        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, d, T.ikeys, T.islot,
+                           T.iwon, T.ni, res_ref(sp, tt), nx, sp->d_err);
     }
     GM_HIP(hipGetLastError());
     GM_TRY(read_err(c, sp));
@@ -238,7 +249,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     for (auto &T : sp->tiers) {
         n += T.count;
         c->tier_counts.push_back(T.count);
-        tb += T.cap * sizeof(RSlot) + T.ni * 12;
+        tb += T.cap * sizeof(RSlot) + T.ni * 13;
     }
     c->n_positions = n;
     c->stats.n_positions = n;

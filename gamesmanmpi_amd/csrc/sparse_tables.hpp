@@ -54,6 +54,7 @@ struct SpTier {
     uint64_t count = 0;          // positions of the tier once classified
     uint64_t *ikeys = nullptr;   // interior (undecided) positions and their slots
     uint32_t *islot = nullptr;
+    uint8_t *iwon = nullptr;     // per interior position: 1 = has a LOSS-in-0 child (set by expand)
     uint64_t ni = 0;
 };
 
@@ -293,6 +294,7 @@ inline int classify_tier_table(Ctx *c, const D &d, SpTier &T, unsigned long long
     const uint64_t n = T.fcount;
     GM_TRY(dev_alloc(c, (void **)&T.ikeys, std::max<uint64_t>(n, 1) * 8));
     GM_TRY(dev_alloc(c, (void **)&T.islot, std::max<uint64_t>(n, 1) * 4));
+    GM_TRY(dev_alloc(c, (void **)&T.iwon, std::max<uint64_t>(n, 1)));
     GM_HIP(hipMemsetAsync(scr, 0, 16 * sizeof(unsigned long long), c->stream));
     hipLaunchKernelGGL(classify_kernel<D>, dim3(grid_for(T.cap / CROWS + 1)), dim3(256), 0, c->stream, d, T.slots,
                        T.cap, T.ikeys, T.islot, scr + 9, scr, scr + 10, d_err);
@@ -301,7 +303,7 @@ inline int classify_tier_table(Ctx *c, const D &d, SpTier &T, unsigned long long
 }
 
 inline void free_tier(Ctx *c, SpTier &T) {
-    for (void *p : {(void *)T.slots, (void *)T.ikeys, (void *)T.islot}) dev_free(c, p);
+    for (void *p : {(void *)T.slots, (void *)T.ikeys, (void *)T.islot, (void *)T.iwon}) dev_free(c, p);
     T = SpTier{};
 }
 
