@@ -20,6 +20,7 @@ OPT_DIST_BATCH = 9
 OPT_DIST_SLOTS = 10
 OPT_DIST_SYMMETRY = 11
 BUF_DENSE_TABLE = 1
+PLAN_SHAPE, PLAN_OWN, PLAN_FILL, PLAN_SEND, PLAN_RECV, PLAN_OPS = 0, 1, 2, 3, 4, 5
 REC_UNSOLVED = 0xFFFF
 
 ERRORS = {
@@ -31,7 +32,7 @@ ERRORS = {
 SYMBOLS = ("gm_version", "gm_last_error", "gm_device_count", "gm_open", "gm_set_stream",
            "gm_set_option", "gm_pack_initial", "gm_expand_host", "gm_comm_unique_id",
            "gm_set_comm", "gm_solve", "gm_solve_graph", "gm_export", "gm_query", "gm_digest", "gm_stats",
-           "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_close")
+           "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_dist_plan", "gm_close")
 
 
 class GMError(RuntimeError):
@@ -99,6 +100,8 @@ def lib():
         "gm_tier_counts": (ctypes.c_int, [vp, vp, ctypes.c_int, P(ctypes.c_int)]),
         "gm_adopt_buffer": (ctypes.c_int, [vp, ctypes.c_int, vp, u64]),
         "gm_dense_table": (ctypes.c_int, [vp, P(vp), P(u64)]),
+        "gm_dist_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
+                                        vp, u64, P(u64), vp, u64, P(u64)]),
         "gm_close": (None, [vp]),
     }
     for name, (res, args) in sig.items():
@@ -114,3 +117,18 @@ def check(rc):
         msg = lib().gm_last_error()
         raise GMError(rc, msg.decode() if msg else "")
     return rc
+
+
+def dist_plan(heaps, world, rank, what, axis=0, batch=4, slots=4, symmetry=1):
+    """gm_dist_plan -> (off, data) as uint32 numpy arrays (host only, no GPU)."""
+    import numpy as np
+    L = lib()
+    opts = (ctypes.c_int32 * 3)(batch, slots, symmetry)
+    n_off, n_data = ctypes.c_uint64(), ctypes.c_uint64()
+    check(L.gm_dist_plan(heaps, world, rank, opts, what, axis, None, 0, ctypes.byref(n_off), None, 0,
+                         ctypes.byref(n_data)))
+    off = np.zeros(max(1, n_off.value), dtype=np.uint32)
+    data = np.zeros(max(1, n_data.value), dtype=np.uint32)
+    check(L.gm_dist_plan(heaps, world, rank, opts, what, axis, off.ctypes.data, len(off), ctypes.byref(n_off),
+                         data.ctypes.data, len(data), ctypes.byref(n_data)))
+    return off[:n_off.value], data[:n_data.value]

@@ -197,9 +197,17 @@ static uint32_t cnt(const std::vector<uint32_t> &off, int i) {
     return (i < 0 || i + 1 >= (int)off.size()) ? 0 : off[i + 1] - off[i];
 }
 
-// Build rank R's block lists (identical enumeration on every rank, so a sender's
-// halo list and its receiver's list agree block for block).
-static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
+// Rank `rank`'s block lists, host only: own blocks per tier, symmetric-fill
+// (dst, src) pairs per tier, halo blocks sent / received per batch and split heap.
+struct Plan {
+    std::vector<uint32_t> off, own, fill_off, fill;
+    std::vector<uint32_t> send_off[MAX_AXES], send[MAX_AXES], recv_off[MAX_AXES], recv[MAX_AXES];
+    uint64_t own_blocks = 0;
+};
+
+// Identical enumeration on every rank, so a sender's halo list and its
+// receiver's list agree block for block.
+static int plan_lists(const Ctx *c, const DistSub *d, int rank, Plan &P) {
     const int T = d->ntiers, NB = d->nbatch;
     const uint64_t nhigh = 1ull << (4 * d->high);
     auto tsum = [&](uint64_t H) { int s = 0; for (int k = 0; k < d->high; k++) s += nib(H, k); return s; };
@@ -215,12 +223,12 @@ static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
             if ((h != 6 && h != 7) || xb[t] < 0) continue;
             uint64_t src = 0;
             const bool sym = c->dist_symmetry && sym_source(d, H, a, &src);
-            if (o == R.rank && !is_upper(R.rank, a) && !sym) Sd[a][xb[t]].push_back((uint32_t)H);
-            if (is_upper(R.rank, a) && o == (R.rank ^ (1 << a))) {
+            if (o == rank && !is_upper(rank, a) && !sym) Sd[a][xb[t]].push_back((uint32_t)H);
+            if (is_upper(rank, a) && o == (rank ^ (1 << a))) {
                 if (!sym) {
                     Rv[a][xb[t]].push_back((uint32_t)H);
                 } else {
-                    if (owner_of(d, src) != R.rank || tsum(src) != t) {
+                    if (owner_of(d, src) != rank || tsum(src) != t) {
                         set_error("symmetric halo source of block %llx is not an own block of its tier",
                                   (unsigned long long)H);
                         return GM_E_STATE;
@@ -230,9 +238,9 @@ static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
                 }
             }
         }
-        if (o == R.rank) {
+        if (o == rank) {
             own[t].push_back((uint32_t)H);
-            R.own_blocks++;
+            P.own_blocks++;
         }
     }
     auto flatten = [&](std::vector<std::vector<uint32_t>> &L, std::vector<uint32_t> &off,
@@ -244,22 +252,32 @@ static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
         }
         off[L.size()] = (uint32_t)flat.size();
     };
-    {
-        std::vector<uint32_t> flat;
-        flatten(own, R.off, flat);
-        if (c->sub_order == 1) sort_tiers_morton(flat, R.off, d->high);
-        GM_TRY(upload(flat, &R.dlist));
-        std::vector<uint32_t> ff;
-        flatten(fill, R.fill_off, ff);
-        GM_TRY(upload(ff, &R.dfill));
+    flatten(own, P.off, P.own);
+    if (c->sub_order == 1) sort_tiers_morton(P.own, P.off, d->high);
+    flatten(fill, P.fill_off, P.fill);
+    for (int a = 0; a < d->g; a++) {
+        flatten(Sd[a], P.send_off[a], P.send[a]);
+        flatten(Rv[a], P.recv_off[a], P.recv[a]);
     }
+    return GM_OK;
+}
+
+// Plan rank R's lists and put them on the device with its exchange buffers and events.
+static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
+    const int NB = d->nbatch;
+    Plan P;
+    GM_TRY(plan_lists(c, d, R.rank, P));
+    R.own_blocks = P.own_blocks;
+    R.off = P.off;
+    R.fill_off = P.fill_off;
+    GM_TRY(upload(P.own, &R.dlist));
+    GM_TRY(upload(P.fill, &R.dfill));
     const uint64_t bb = 1ull << (4 * d->low);
     for (int a = 0; a < d->g; a++) {
-        std::vector<uint32_t> fs, fr;
-        flatten(Sd[a], R.send_off[a], fs);
-        flatten(Rv[a], R.recv_off[a], fr);
-        GM_TRY(upload(fs, &R.dsend[a]));
-        GM_TRY(upload(fr, &R.drecv[a]));
+        R.send_off[a] = P.send_off[a];
+        R.recv_off[a] = P.recv_off[a];
+        GM_TRY(upload(P.send[a], &R.dsend[a]));
+        GM_TRY(upload(P.recv[a], &R.drecv[a]));
         uint64_t ms = 0, mr = 0;
         for (int j = 0; j < NB; j++) {
             ms = std::max<uint64_t>(ms, cnt(R.send_off[a], j));
@@ -330,7 +348,8 @@ static void build_ops(DistSub *d, SubRank &R) {
     }
 }
 
-static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
+// The partition's shape (block split, tiers, batches, ring depth), host only.
+static int plan_shape(const Ctx *c, DistSub *d, int G, bool loopback) {
     d->heaps = c->sub.heaps;
     d->low = std::min(3, d->heaps);
     d->high = d->heaps - d->low;
@@ -361,6 +380,11 @@ static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
         d->lo[j] = std::max(0, j * d->batch - 1);
         d->hi[j] = std::min(d->ntiers - 2, j * d->batch + d->batch - 2);
     }
+    return GM_OK;
+}
+
+static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
+    GM_TRY(plan_shape(c, d, G, loopback));
     size_t zb = std::max<size_t>(16, 1ull << (4 * d->low));
     GM_HIP(hipMalloc(&d->zero, zb));
     GM_HIP(hipMemset(d->zero, 0, zb));
@@ -676,6 +700,72 @@ void dist_sub_free(Ctx *c) {
     if (d->d_root) (void)hipFree(d->d_root);
     delete d;
     c->dist_sub = nullptr;
+}
+
+// gm_dist_plan: the plan one rank of an RCCL-mode solve executes, built by the
+// same host code as dist_sub_solve (plan_shape, plan_lists, build_ops) but with
+// no device or communicator call.
+int dist_sub_plan(int heaps, int world, int rank, const int32_t *opts, int what, int axis, uint32_t *off,
+                  uint64_t off_cap, uint64_t *n_off, uint32_t *data, uint64_t data_cap, uint64_t *n_data) {
+    if (heaps < 1 || heaps > 8 || rank < 0 || rank >= world || !n_off || !n_data) {
+        set_error("gm_dist_plan: bad heaps / rank / world");
+        return GM_E_ARG;
+    }
+    Ctx c;
+    c.game = GM_GAME_SUBTRACT;
+    c.sub.heaps = heaps;
+    if (opts) {
+        c.dist_batch = std::max(1, (int)opts[0]);
+        c.dist_slots = std::max(1, (int)opts[1]);
+        c.dist_symmetry = opts[2] ? 1 : 0;
+    }
+    DistSub d;
+    GM_TRY(plan_shape(&c, &d, world, false));
+    if (axis < 0 || axis >= std::max(1, d.g)) { set_error("gm_dist_plan: axis out of range"); return GM_E_ARG; }
+    std::vector<uint32_t> O, D;
+    if (what == GM_PLAN_SHAPE) {
+        D = {(uint32_t)d.low, (uint32_t)d.high, (uint32_t)d.ntiers, (uint32_t)d.batch, (uint32_t)d.nbatch,
+             (uint32_t)d.nslots, (uint32_t)d.g};
+        for (int j = 0; j < d.nbatch; j++) { O.push_back((uint32_t)d.lo[j]); O.push_back((uint32_t)d.hi[j]); }
+    } else {
+        Plan P;
+        GM_TRY(plan_lists(&c, &d, rank, P));
+        switch (what) {
+        case GM_PLAN_OWN: O = P.off; D = P.own; break;
+        case GM_PLAN_FILL: O = P.fill_off; D = P.fill; break;
+        case GM_PLAN_SEND: O = P.send_off[axis]; D = P.send[axis]; break;
+        case GM_PLAN_RECV: O = P.recv_off[axis]; D = P.recv[axis]; break;
+        case GM_PLAN_OPS: {
+            SubRank R;
+            R.rank = rank;
+            R.off = P.off;
+            R.fill_off = P.fill_off;
+            for (int a = 0; a < d.g; a++) { R.send_off[a] = P.send_off[a]; R.recv_off[a] = P.recv_off[a]; }
+            build_ops(&d, R);
+            for (const Op &o : R.ops) {
+                D.push_back(o.kind);
+                D.push_back(o.axis);
+                D.push_back(o.ev);
+                D.push_back(o.on_x);
+                D.push_back((uint32_t)o.arg);
+                D.push_back((uint32_t)o.peer);
+            }
+            break;
+        }
+        default: set_error("gm_dist_plan: unknown `what` %d", what); return GM_E_ARG;
+        }
+    }
+    *n_off = O.size();
+    *n_data = D.size();
+    if (off) {
+        if (off_cap < O.size()) { set_error("gm_dist_plan: off buffer too small"); return GM_E_CAP; }
+        std::copy(O.begin(), O.end(), off);
+    }
+    if (data) {
+        if (data_cap < D.size()) { set_error("gm_dist_plan: data buffer too small"); return GM_E_CAP; }
+        std::copy(D.begin(), D.end(), data);
+    }
+    return GM_OK;
 }
 
 }  // namespace gm

@@ -449,6 +449,11 @@ int gm_dense_table(gm_ctx *h, void **p, uint64_t *bytes) {
     return dense_sub_table(&h->c, p, bytes);
 }
 
+int gm_dist_plan(int heaps, int world, int rank, const int32_t *opts, int what, int axis, uint32_t *off,
+                 uint64_t off_cap, uint64_t *n_off, uint32_t *data, uint64_t data_cap, uint64_t *n_data) {
+    return dist_sub_plan(heaps, world, rank, opts, what, axis, off, off_cap, n_off, data, data_cap, n_data);
+}
+
 void gm_close(gm_ctx *h) {
     if (!h) return;
     Ctx *c = &h->c;

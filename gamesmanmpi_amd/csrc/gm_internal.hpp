@@ -134,6 +134,8 @@ int dist_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64
 int dist_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
 int dist_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n);
 void dist_sub_free(Ctx *c);
+int dist_sub_plan(int heaps, int world, int rank, const int32_t *opts, int what, int axis, uint32_t *off,
+                  uint64_t off_cap, uint64_t *n_off, uint32_t *data, uint64_t data_cap, uint64_t *n_data);
 
 int dist_sparse_solve(Ctx *c, uint64_t root);
 int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);

@@ -203,6 +203,28 @@ int gm_adopt_buffer(gm_ctx *ctx, int role, void *dev_ptr, uint64_t bytes);
  * its slots hold 1-byte order-preserving codes ("HBM layout"), not records. */
 int gm_dense_table(gm_ctx *ctx, void **dev_ptr, uint64_t *bytes);
 
+/* Host only -- makes no HIP or RCCL call, so it runs without a GPU: the plan
+ * that rank `rank` of a `world`-rank sharded SUBTRACT solve executes, built by
+ * the same code gm_solve uses (block-owner partition, halo lists, op list;
+ * DESIGN.md §5).  For tests and tooling that check the multi-GPU schedule on the
+ * CPU.  The reference has no counterpart: its schedule is the dynamic mpi4py job
+ * queue (src/new_process.py:37-60, :145-187).  `opts` = {GM_OPT_DIST_BATCH,
+ * GM_OPT_DIST_SLOTS, GM_OPT_DIST_SYMMETRY} values, NULL = defaults.
+ *   GM_PLAN_SHAPE  data = {low, high, ntiers, batch, nbatch, nslots, g};
+ *                  off = (lo, hi) tier range of each batch's halo message
+ *   GM_PLAN_OWN    data = high parts this rank computes; off[t]..off[t+1] = tier t
+ *   GM_PLAN_FILL   data = (dst, src) pairs filled locally after tier t (off in u32 entries)
+ *   GM_PLAN_SEND   data = halo high parts sent on split heap `axis`; off per batch
+ *   GM_PLAN_RECV   data = halo high parts received on split heap `axis`; off per batch
+ *   GM_PLAN_OPS    data = 6 u32 per op {kind, axis, event, on_exchange_stream, tier|batch, peer},
+ *                  kind: 0 tier launch, 1 pack, 2 unpack, 3 send, 4 recv, 5 event record,
+ *                  6 event wait, 7 symmetric fill; event: 0 packed, 1 exchanged, 2 unpacked
+ * With off / data NULL only *n_off / *n_data are set. */
+enum { GM_PLAN_SHAPE = 0, GM_PLAN_OWN = 1, GM_PLAN_FILL = 2, GM_PLAN_SEND = 3, GM_PLAN_RECV = 4, GM_PLAN_OPS = 5 };
+int gm_dist_plan(int heaps, int world, int rank, const int32_t *opts, int what, int axis,
+                 uint32_t *off, uint64_t off_cap, uint64_t *n_off,
+                 uint32_t *data, uint64_t data_cap, uint64_t *n_data);
+
 /* Release everything. */
 void gm_close(gm_ctx *ctx);
 

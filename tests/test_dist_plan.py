@@ -1,0 +1,136 @@
+"""The multi-GPU dense path's schedule, checked on the CPU (no GPU needed).
+
+Each rank's plan -- block-owner partition, halo lists, op list -- comes from the
+product through gm_dist_plan (the host code gm_solve runs; csrc/dist_sub.hip).
+tests/dist_sim.py executes the RCCL-mode op lists of all ranks under HIP stream /
+event and RCCL point-to-point semantics in random interleavings, and, over
+torch.distributed gloo with one process per rank, moves the halos as real
+messages carrying the C oracle's values.  The GPU side of the same schedule is
+tests/test_gpu_sharded.py (loopback ranks on one device).
+"""
+import multiprocessing as mp
+import socket
+
+import numpy as np
+import pytest
+
+import dist_sim as S
+from gamesmanmpi_amd import _lib, GMError
+
+
+def plans(heaps, world, batch=4, slots=4, symmetry=1):
+    return [S.load_plan(heaps, world, r, batch, slots, symmetry) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("batch,slots,symmetry", [(4, 4, 1), (4, 4, 0), (1, 1, 1), (1, 1, 0), (2, 1, 1),
+                                                  (3, 2, 0), (100, 2, 1)])
+def test_schedule_is_deadlock_free_and_race_free(world, batch, slots, symmetry):
+    P = plans(6, world, batch, slots, symmetry)
+    for seed in range(3):
+        assert S.simulate(P, seed=seed)
+
+
+def test_schedule_full_size_8_ranks():
+    """The bench configuration: 2^32 positions, 8 ranks, default batch / ring / fill."""
+    P = plans(8, 8)
+    shape = P[0]
+    assert (shape["low"], shape["high"], shape["ntiers"], shape["nbatch"], shape["g"]) == (3, 5, 76, 19, 3)
+    assert S.simulate(P, seed=1)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_partition_and_halo_volume(world):
+    """Every block has one owner, ranks own equal shares, and the symmetric fill cuts the
+    halo that crosses a link to 1/16, 1/8, 1/4 of the split-heap layers."""
+    heaps = 8
+    g = world.bit_length() - 1
+    sent = {}
+    for sym in (0, 1):
+        total = 0
+        owned = np.zeros(1 << 20, dtype=np.int64)
+        for r in range(world):
+            _, own = _lib.dist_plan(heaps, world, r, _lib.PLAN_OWN, symmetry=sym)
+            owned[own] += 1
+            assert len(own) == (1 << 20) // world
+            for a in range(g):
+                total += len(_lib.dist_plan(heaps, world, r, _lib.PLAN_SEND, axis=a, symmetry=sym)[1])
+        assert (owned == 1).all()
+        sent[sym] = total * 4096
+    assert sent[0] == g * (512 << 20)           # 2 of 16 layers of the 4 GiB table per split heap
+    assert sent[1] == {2: 32, 4: 128, 8: 384}[world] << 20
+
+
+def test_plan_rejects_impossible_splits():
+    with pytest.raises(GMError):
+        _lib.dist_plan(5, 8, 0, _lib.PLAN_SHAPE)      # 2 block heaps cannot split 8 ways
+    with pytest.raises(GMError):
+        _lib.dist_plan(8, 3, 0, _lib.PLAN_SHAPE)      # world must be 2, 4 or 8
+    with pytest.raises(GMError):
+        _lib.dist_plan(8, 2, 2, _lib.PLAN_OWN)        # rank out of range
+
+
+def _mutate(P, rank, pred, action):
+    """Copy of the plans with the first op of `rank` matching pred dropped or moved."""
+    Q = [dict(p) for p in P]
+    ops = Q[rank]["ops"].tolist()
+    i = next(k for k, o in enumerate(ops) if pred(o))
+    o = ops.pop(i)
+    if action == "later":
+        ops.insert(min(len(ops), i + 3), o)
+    Q[rank]["ops"] = np.array(ops, dtype=np.int64).reshape(-1, 6)
+    return Q
+
+
+@pytest.mark.parametrize("what", ["unpack_wait", "fill", "pack_after_tier", "recv"])
+def test_simulator_catches_broken_schedules(what):
+    """The checker bites: each injected schedule bug is reported."""
+    P = plans(6, 4, batch=2, slots=1, symmetry=1)
+    upper = 3
+    if what == "unpack_wait":      # S no longer waits for the receive before unpacking
+        Q = _mutate(P, upper, lambda o: o[0] == S.OP_WAIT and o[2] == S.EV_XCH and o[3] == 0, "drop")
+    elif what == "fill":           # a symmetric fill is lost
+        Q = _mutate(P, upper, lambda o: o[0] == S.OP_FILL, "drop")
+    elif what == "pack_after_tier":    # the lower rank packs before computing the halo's last tier
+        Q = [dict(p) for p in P]
+        ops = Q[0]["ops"].tolist()
+        i = next(k for k, o in enumerate(ops) if o[0] == S.OP_PACK)
+        ops.insert(i - 1, ops.pop(i))
+        Q[0]["ops"] = np.array(ops, dtype=np.int64).reshape(-1, 6)
+    else:                          # a receive is dropped: its send never matches
+        Q = _mutate(P, upper, lambda o: o[0] == S.OP_RECV, "drop")
+    caught = 0
+    for seed in range(6):
+        try:
+            S.simulate(Q, seed=seed)
+        except S.SimError:
+            caught += 1
+    assert caught > 0
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,batch,slots,symmetry", [(2, 4, 4, 1), (2, 1, 1, 0), (4, 4, 4, 1), (4, 2, 1, 0)])
+def test_gloo_ranks_exchange_halos(world, batch, slots, symmetry):
+    """world_size > 1 over torch.distributed gloo: every rank runs its own RCCL-mode op
+    list as a host program; after the solve every own and every halo block it holds
+    equals the oracle's (6 heaps, 16.7 M positions)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=S.gloo_main, args=(r, world, port, 6, batch, slots, symmetry, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all("error" not in r for r in res), res
+    assert sorted(r["rank"] for r in res) == list(range(world))
+    assert all(r["own_ok"] and r["held_ok"] for r in res), res
+    assert sum(r["own_blocks"] for r in res) == 1 << 12
+    assert any(r["halo_blocks"] > 0 for r in res)
