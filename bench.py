@@ -17,8 +17,12 @@ Prints ONE JSON line on rank 0 (driver contract), including
                 positions per launch) / its average launch time, from
                 HIP events recorded around every launch on the launch stream;
                 traffic = rocprofv3 PMC bytes per launch from profiles/ when present;
-  cpu_baseline  the C oracle's dense solver (oracle/gm_oracle.c, 1 thread) on a
-                bounded sample (7 heaps = 2^28 positions) on this host.
+  cpu_baseline  the C oracle's dense solver (oracle/gm_oracle.c), OpenMP over
+                the host threads the box gives the process, on the full 2^32
+                workload (a 7-heap sample if the full one would exceed ~30 s);
+  other_configs config 3 (Toot-and-Otto 6x4) and config 4 (Othello 4x4) on the
+                sparse engine, hash-sharded over the same N ranks when N > 1
+                (reported beside the headline, not the metric).
 """
 import argparse
 import ctypes
@@ -89,25 +93,96 @@ def cpu_baseline(heaps=8):
                       "nproc %d" % (heaps, n, dt, threads, cpu, os.cpu_count())}
 
 
-def toot_6x4(repeats=2):
-    """Config 3 beside the headline: Toot-and-Otto 6x4 strong solve on this GPU
-    (sparse engine); reported, not the metric.  Per-ply counts are checked
-    against SURVEY Appendix D's total."""
+TOOT_6X4_PER_PLY = [1, 12, 114, 748, 4266, 19692, 81140, 285708, 928196, 2665424, 7098172, 17010952,
+                    37792450, 64636776, 100084356, 136321692, 169785424, 180777508, 172831136,
+                    135153280, 91440950, 45953432, 19196602, 4537828, 606968]
+
+
+def sparse_config(name, game, params, rank, world, dist, torch, repeats=2):
+    """Config 3 / 4 on the sparse engine, hash-sharded over the job's ranks (RCCL p2p,
+    csrc/dist_sparse.hip) when world > 1.  Checked: position count and root record
+    (Othello 4x4: SURVEY §8a, 54,089 positions, LOSS in 12; Toot 6x4: Appendix D's
+    per-ply counts).  Othello 4x4 at world > 1 also compares the all-reduced
+    full-table digest with a one-GPU solve of the same game.  Time = max over ranks."""
     from gamesmanmpi_amd import Context, _lib
-    ctx = Context(_lib.GAME_TOOT, (6, 4), device=0)
+    ctx = Context(game, params, device=int(os.environ.get("LOCAL_RANK", 0)))
+    if world > 1:
+        uid = [None]
+        if rank == 0:
+            buf = ctypes.create_string_buffer(128)
+            _lib.check(_lib.lib().gm_comm_unique_id(buf, 128))
+            uid[0] = buf.raw
+        dist.broadcast_object_list(uid, src=0)
+        ctx.set_comm(rank, world, uid[0])
     root = ctx.initial()
     best = None
     for _ in range(repeats):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         n, rec = ctx.solve(root)
+        torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
         best = dt if best is None else min(best, dt)
     st = ctx.stats()
+    out = {"positions": n, "root_record": rec, "solve_ms": best * 1e3, "positions_per_s": n / best,
+           "ranks": world, "exchanged_bytes_rank%d" % rank: st["exchanged_bytes"]}
+    if name == "toot_6x4":
+        out["workload"] = "Toot-and-Otto 6x4 (config 3), sparse engine" + (", hash-sharded" if world > 1 else "")
+        out["per_ply_counts_match_appendix_d"] = [int(x) for x in ctx.tier_counts()] == TOOT_6X4_PER_PLY
+        out["ok"] = n == 1187212827 and out["per_ply_counts_match_appendix_d"]
+        out["edges"] = st["n_edges"]
+        out["algo_bytes_per_position"] = st["algo_bytes"] / n
+    else:
+        out["workload"] = "Othello 4x4 (config 4), sparse engine" + (", hash-sharded" if world > 1 else "")
+        out["ok"] = n == 54089 and (rec >> 14) == 1 and (rec & 0x3FFF) == 12
+        if world > 1:
+            d, m = ctx.digest()
+            v = torch.tensor([d - (1 << 64) if d >= (1 << 63) else d, m], dtype=torch.int64, device="cuda")
+            dist.all_reduce(v)
+            dsum, msum = int(v[0].item()) & ((1 << 64) - 1), int(v[1].item())
+            one = Context(game, params, device=int(os.environ.get("LOCAL_RANK", 0)))
+            one.solve(one.initial())
+            out["digest_matches_one_gpu"] = (dsum, msum) == one.digest()
+            out["ok"] = out["ok"] and out["digest_matches_one_gpu"]
+            one.close()
     ctx.close()
-    assert n == 1187212827, n
-    return {"workload": "Toot-and-Otto 6x4 (config 3), sparse engine", "positions": n, "root_record": rec,
-            "solve_ms": best * 1e3, "positions_per_s": n / best, "edges": st["n_edges"],
-            "algo_bytes_per_position": st["algo_bytes"] / n}
+    return out
+
+
+def other_configs(rank, world, dist, torch, budget_s=150.0, emit=None):
+    """Run the side configs under a watchdog: if the ranks have not finished within
+    budget_s (a sharded exchange that never completes), every rank prints what it
+    has (rank 0 the headline line via emit) and leaves with status 0, so the
+    headline measurement is never lost to a side measurement."""
+    import threading
+    from gamesmanmpi_amd import _lib
+    res = {}
+
+    def expire():
+        res["error"] = "watchdog: side configs did not finish within %.0f s" % budget_s
+        if emit is not None:
+            emit(res)
+        sys.stdout.flush()
+        os._exit(0)
+
+    timer = threading.Timer(budget_s, expire)
+    timer.daemon = True
+    timer.start()
+    for name, game, params in (("othello_4x4", _lib.GAME_OTHELLO, (4, 4)), ("toot_6x4", _lib.GAME_TOOT, (6, 4))):
+        try:
+            res[name] = sparse_config(name, game, params, rank, world, dist, torch)
+        except Exception as e:  # reported in the line; a rank that fails here leaves the others to the watchdog
+            res[name] = {"error": "%s: %s" % (type(e).__name__, e)}
+            if world > 1:
+                break
+    timer.cancel()
+    return res
 
 
 def pmc_traffic(heaps):
@@ -144,7 +219,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--heaps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-toot", action="store_true", help="skip the config-3 side measurement")
+    ap.add_argument("--no-toot", action="store_true", help="skip the config-3/4 side measurements")
     ap.add_argument("--cpu-heaps", type=int, default=8)
     ap.add_argument("--dist-batch", type=int, default=4, help="N>1: tiers per halo exchange")
     ap.add_argument("--dist-slots", type=int, default=4, help="N>1: halo buffers per split heap")
@@ -283,10 +358,16 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_heaps)
     ctx.close()
-    if rank == 0 and world == 1 and args.virtual_ranks == 1 and not args.no_toot:
+    if args.virtual_ranks == 1 and not args.no_toot:
         del table
         torch.cuda.empty_cache()
-        out["other_configs"] = {"toot_6x4": toot_6x4()}
+
+        def emit(partial):
+            if rank == 0:
+                out["other_configs"] = partial
+                print(json.dumps(out), flush=True)
+
+        out["other_configs"] = other_configs(rank, world, dist, torch, emit=emit)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -405,9 +405,14 @@ __device__ __forceinline__ uint32_t code_x4(uint32_t b) {   // parent_code on fo
 // dataflow kernel, whose consumers may sit on another XCD: write-through stores,
 // L1-bypassing loads -- MI355X_MICROARCH.md, inter-workgroup visibility).
 constexpr int CPOL_SC1 = 16;
-template <int HIGH, int CPOL, int LCPOL = CPOL>
+// XD (sharded solve): block k also goes to the extra destinations xdst[xoff[idx0 + k] ..
+// xoff[idx0 + k + 1]) -- symmetric-fill images in the table and halo ring slots --
+// from the same registers, so no separate fill / pack launch follows the tier.
+template <int HIGH, int CPOL, int LCPOL = CPOL, bool XD = false>
 __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint8_t *__restrict__ zero,
-                                         const uint32_t (&hp)[4], const bool (&valid)[4], uint32_t *s) {
+                                         const uint32_t (&hp)[4], const bool (&valid)[4], uint32_t *s,
+                                         const uint32_t *__restrict__ xoff = nullptr,
+                                         const uint64_t *__restrict__ xdst = nullptr, uint32_t idx0 = 0) {
     constexpr int NPOS = 4096, NCH = 256, NT = 256, K = 4;
     constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
     const int tid = threadIdx.x;
@@ -496,6 +501,15 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
         }
 #pragma unroll
         for (int k = 0; k < K; k++) __builtin_amdgcn_raw_buffer_store_b128(out[k], wr[k], 16u * c, 0, CPOL);
+        if constexpr (XD) {
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                if (!valid[k]) continue;
+                const uint32_t m1 = xoff[idx0 + k + 1];
+                for (uint32_t m = xoff[idx0 + k]; m < m1; m++)
+                    __builtin_amdgcn_raw_buffer_store_b128(out[k], block_rsrc((uint8_t *)xdst[m], NPOS), 16u * c, 0, 0);
+            }
+        }
     }
 }
 
@@ -515,6 +529,28 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *
         hp[k] = valid[k] ? blocks[idx] : 0u;
     }
     b4_solve<HIGH, 0>(table, zero, hp, valid, s);
+}
+
+// The sharded solve's tier kernel (csrc/dist_sub.hip): as above, plus each block's
+// extra destinations (xoff / xdst indexed like `blocks`).
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t *__restrict__ table,
+                                                           const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                           const uint8_t *__restrict__ zero,
+                                                           const uint32_t *__restrict__ xoff,
+                                                           const uint64_t *__restrict__ xdst) {
+    constexpr int K = 4;
+    __shared__ __attribute__((aligned(16))) uint32_t s[4096];   // 16 KiB
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
+    uint32_t hp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = grp * K + k;
+        valid[k] = idx < nblk;
+        hp[k] = valid[k] ? blocks[idx] : 0u;
+    }
+    b4_solve<HIGH, 0, 0, true>(table, zero, hp, valid, s, xoff, xdst, grp * K);
 }
 
 // ---------------------------------------------------------------------------
@@ -712,6 +748,28 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
                            zero);
     else
         hipLaunchKernelGGL(pick_kernel(low, high, nt), dim3(nblocks), dim3(nt), 0, s, table, list, nblocks, zero);
+}
+
+typedef void (*tier_kernel_x_t)(uint8_t *, const uint32_t *, uint32_t, const uint8_t *, const uint32_t *,
+                                const uint64_t *);
+static tier_kernel_x_t pick_b4x(int high) {
+    switch (high) {
+    case 1: return sub_tier_kernel_b4x<1>;
+    case 2: return sub_tier_kernel_b4x<2>;
+    case 3: return sub_tier_kernel_b4x<3>;
+    case 4: return sub_tier_kernel_b4x<4>;
+    case 5: return sub_tier_kernel_b4x<5>;
+    }
+    return nullptr;
+}
+
+bool sub_kernel_x_exists(int high) { return pick_b4x(high) != nullptr; }
+
+void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
+                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s) {
+    if (!nblocks) return;
+    hipLaunchKernelGGL(pick_b4x(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero, xoff,
+                       xdst);
 }
 
 int sub_kernel_threads(const Ctx *c, int low) {

@@ -35,8 +35,15 @@
 // stream never holds both a send and a receive, and a lower rank waits for an
 // upper one only when its ring of K send buffers (GM_OPT_DIST_SLOTS) is full.
 //
-// Every rank's work is a precomputed list of ops (tier launch, pack, unpack,
-// send, receive, event record / wait).  RCCL mode runs its list in order.  The
+// Every rank's work is a precomputed list of ops (tier launch, unpack, send,
+// receive, event record / wait).  The compute stream S carries only the tier
+// launches and event waits/records: the tier kernel itself (sub_tier_kernel_b4x)
+// writes each block, from the registers that hold it, also to the block's extra
+// destinations -- its symmetric-fill images in the table and its slot in the
+// halo message of every split heap it is sent on -- so no fill or pack kernel
+// sits between two tiers, and the unpack of a received halo runs on X[a].  A
+// tier that writes into a ring slot first waits until the slot's previous
+// message has left.  RCCL mode runs its list in order.  The
 // loopback mode (GM_OPT_VIRTUAL_RANKS: G ranks inside one context on one GPU,
 // for testing the partition without a second GPU) runs the same lists on per-rank
 // streams, a receive being a device copy from the sender's ring slot after the
@@ -65,10 +72,13 @@ struct SubRank {
     bool owned = false;
     std::vector<uint32_t> off;          // per-tier offsets into dlist (owned blocks)
     uint32_t *dlist = nullptr;
-    std::vector<uint32_t> fill_off;     // per-tier offsets into dfill (symmetric fill)
-    uint32_t *dfill = nullptr;          // (dst, src) high parts, interleaved
+    std::vector<uint32_t> fill_off;     // per-tier offsets into the fill pairs (symmetric fill; plan only)
+    std::vector<uint32_t> xoff;         // per own block (dlist order): its extra destinations in xd
+    std::vector<uint32_t> xd;           // (kind, value) pairs: XD_TABLE high part | XD_SEND + axis, (batch, index)
+    uint32_t *dxoff = nullptr;
+    uint64_t *dxdst = nullptr;          // xd resolved to device addresses (table / ring slots)
     std::vector<uint32_t> send_off[MAX_AXES], recv_off[MAX_AXES];   // per-batch offsets
-    uint32_t *dsend[MAX_AXES] = {}, *drecv[MAX_AXES] = {};
+    uint32_t *drecv[MAX_AXES] = {};
     uint8_t *sendbuf[MAX_AXES] = {}, *recvbuf[MAX_AXES] = {};       // rings of nslots slots
     uint64_t send_slot[MAX_AXES] = {}, recv_slot[MAX_AXES] = {};    // bytes per slot
     std::vector<hipEvent_t> ev[EV_KINDS][MAX_AXES];                 // nslots each
@@ -110,6 +120,9 @@ static inline int owner_of(const DistSub *d, uint64_t H) {
 
 static inline bool is_upper(int rank, int a) { return (rank >> a) & 1; }
 
+// extra destinations of an own block (written by the tier kernel from the same registers)
+enum XdKind { XD_TABLE = 0, XD_SEND = 1 };   // XD_SEND + axis; value = batch << 16 | index in the message
+
 // Halo block H of axis a as a heap permutation of a block of the receiving (upper)
 // rank: swap the split nibble (6 or 7) with the first unsplit high nibble >= 8.
 // Returns false when every unsplit high nibble is <= 7 (the block is sent).
@@ -123,20 +136,6 @@ static bool sym_source(const DistSub *d, uint64_t H, int a, uint64_t *src) {
         return true;
     }
     return false;
-}
-
-// dst block <- src block for every (dst, src) pair: the symmetric halo fill
-__global__ void block_pair_copy_kernel(uint8_t *table, const uint32_t *__restrict__ pairs, int low) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const uint64_t bsz = 1ull << (4 * low);
-    const uint64_t dst = (uint64_t)pairs[2 * blockIdx.x] << (4 * low);
-    const uint64_t src = (uint64_t)pairs[2 * blockIdx.x + 1] << (4 * low);
-    if (bsz >= 16) {
-        for (uint64_t c = threadIdx.x; c < bsz / 16; c += blockDim.x)
-            *(u32x4 *)(table + dst + 16 * c) = *(const u32x4 *)(table + src + 16 * c);
-    } else {
-        for (uint64_t c = threadIdx.x; c < bsz; c += blockDim.x) table[dst + c] = table[src + c];
-    }
 }
 
 __global__ void block_copy_kernel(const uint8_t *__restrict__ src, const uint32_t *__restrict__ list,
@@ -200,7 +199,7 @@ static uint32_t cnt(const std::vector<uint32_t> &off, int i) {
 // Rank `rank`'s block lists, host only: own blocks per tier, symmetric-fill
 // (dst, src) pairs per tier, halo blocks sent / received per batch and split heap.
 struct Plan {
-    std::vector<uint32_t> off, own, fill_off, fill;
+    std::vector<uint32_t> off, own, fill_off, fill, xoff, xd;
     std::vector<uint32_t> send_off[MAX_AXES], send[MAX_AXES], recv_off[MAX_AXES], recv[MAX_AXES];
     uint64_t own_blocks = 0;
 };
@@ -259,6 +258,25 @@ static int plan_lists(const Ctx *c, const DistSub *d, int rank, Plan &P) {
         flatten(Sd[a], P.send_off[a], P.send[a]);
         flatten(Rv[a], P.recv_off[a], P.recv[a]);
     }
+    // each own block's extra destinations, in the own list's (possibly Morton) order
+    std::vector<std::vector<uint32_t>> ex(nhigh);
+    for (size_t i = 0; i + 1 < P.fill.size(); i += 2) {
+        ex[P.fill[i + 1]].push_back(XD_TABLE);
+        ex[P.fill[i + 1]].push_back(P.fill[i]);
+    }
+    for (int a = 0; a < d->g; a++)
+        for (int j = 0; j < NB; j++)
+            for (int k = 0; k < (int)Sd[a][j].size(); k++) {
+                if (k >= (1 << 16) || j >= (1 << 16)) { set_error("halo message too large"); return GM_E_STATE; }
+                ex[Sd[a][j][k]].push_back(XD_SEND + a);
+                ex[Sd[a][j][k]].push_back((uint32_t)j << 16 | (uint32_t)k);
+            }
+    P.xoff.assign(P.own.size() + 1, 0);
+    for (size_t i = 0; i < P.own.size(); i++) {
+        P.xoff[i] = (uint32_t)(P.xd.size() / 2);
+        P.xd.insert(P.xd.end(), ex[P.own[i]].begin(), ex[P.own[i]].end());
+    }
+    P.xoff[P.own.size()] = (uint32_t)(P.xd.size() / 2);
     return GM_OK;
 }
 
@@ -270,13 +288,14 @@ static int build_lists(Ctx *c, DistSub *d, SubRank &R) {
     R.own_blocks = P.own_blocks;
     R.off = P.off;
     R.fill_off = P.fill_off;
+    R.xoff = P.xoff;
+    R.xd = P.xd;
     GM_TRY(upload(P.own, &R.dlist));
-    GM_TRY(upload(P.fill, &R.dfill));
+    GM_TRY(upload(P.xoff, &R.dxoff));
     const uint64_t bb = 1ull << (4 * d->low);
     for (int a = 0; a < d->g; a++) {
         R.send_off[a] = P.send_off[a];
         R.recv_off[a] = P.recv_off[a];
-        GM_TRY(upload(P.send[a], &R.dsend[a]));
         GM_TRY(upload(P.recv[a], &R.drecv[a]));
         uint64_t ms = 0, mr = 0;
         for (int j = 0; j < NB; j++) {
@@ -303,44 +322,67 @@ static uint8_t *recv_ptr(const DistSub *d, const SubRank &R, int a, int j) {
     return R.recvbuf[a] + (uint64_t)(j % d->nslots) * R.recv_slot[a];
 }
 
+// R.xd -> device addresses, once the table and the send rings exist
+static int upload_xdst(DistSub *d, SubRank &R) {
+    const uint64_t bb = 1ull << (4 * d->low);
+    std::vector<uint64_t> a64(std::max<size_t>(1, R.xd.size() / 2), 0);
+    for (size_t i = 0; i < R.xd.size() / 2; i++) {
+        const uint32_t kind = R.xd[2 * i], v = R.xd[2 * i + 1];
+        if (kind == XD_TABLE) {
+            a64[i] = (uint64_t)(uintptr_t)(R.table + ((uint64_t)v << (4 * d->low)));
+        } else {
+            const int a = (int)kind - XD_SEND, j = (int)(v >> 16), k = (int)(v & 0xFFFFu);
+            a64[i] = (uint64_t)(uintptr_t)(send_ptr(d, R, a, j) + (uint64_t)k * bb);
+        }
+    }
+    GM_HIP(hipMalloc(&R.dxdst, a64.size() * 8));
+    GM_HIP(hipMemcpy(R.dxdst, a64.data(), a64.size() * 8, hipMemcpyHostToDevice));
+    return GM_OK;
+}
+
 // The op list of rank R for one solve (see the file comment).
 static void build_ops(DistSub *d, SubRank &R) {
     const int T = d->ntiers, NB = d->nbatch, B = d->batch, NS = d->nslots;
     auto op = [&](int kind, int axis, int ev, bool on_x, int arg, int peer) {
         R.ops.push_back(Op{(uint8_t)kind, (uint8_t)axis, (uint8_t)ev, (uint8_t)on_x, arg, peer});
     };
-    std::vector<std::vector<int>> send_after(T);   // halo messages a lower rank sends after tier t
+    std::vector<std::vector<int>> send_after(T), send_from(T);   // halo messages ending / starting at tier t
     for (int j = 0; j < NB; j++)
-        if (d->lo[j] <= d->hi[j]) send_after[d->hi[j]].push_back(j);
+        if (d->lo[j] <= d->hi[j]) {
+            send_after[d->hi[j]].push_back(j);
+            send_from[d->lo[j]].push_back(j);
+        }
     R.ops.clear();
     for (int j = 0; j < NB; j++) {
-        // receive X_j on every axis where this rank is the upper side
+        // receive X_j on every axis where this rank is the upper side; X[a] unpacks it
+        // (the previous message in its ring slot was unpacked earlier on the same stream)
         for (int a = 0; a < d->g; a++) {
             if (!is_upper(R.rank, a) || !cnt(R.recv_off[a], j)) continue;
             const int lower = R.rank ^ (1 << a);
-            if (j >= NS && cnt(R.recv_off[a], j - NS)) op(OP_WAIT, a, EV_UNPACKED, true, j - NS, R.rank);
             if (d->loopback) op(OP_WAIT, a, EV_PACKED, true, j, lower);
             op(OP_RECV, a, 0, true, j, lower);
             op(OP_RECORD, a, EV_XCH, true, j, R.rank);
-            op(OP_WAIT, a, EV_XCH, false, j, R.rank);
-            op(OP_UNPACK, a, 0, false, j, R.rank);
-            op(OP_RECORD, a, EV_UNPACKED, false, j, R.rank);
+            op(OP_UNPACK, a, 0, true, j, R.rank);
+            op(OP_RECORD, a, EV_UNPACKED, true, j, R.rank);
+            op(OP_WAIT, a, EV_UNPACKED, false, j, R.rank);
         }
         for (int t = j * B; t < std::min(T, j * B + B); t++) {
+            // the tier kernel writes the halo blocks of messages starting here into their
+            // ring slots: the slot's previous message (jj - NS) must have left
+            for (int jj : send_from[t])
+                for (int a = 0; a < d->g; a++) {
+                    if (is_upper(R.rank, a) || !cnt(R.send_off[a], jj)) continue;
+                    if (jj >= NS && cnt(R.send_off[a], jj - NS))
+                        op(OP_WAIT, a, EV_XCH, false, jj - NS, d->loopback ? (R.rank ^ (1 << a)) : R.rank);
+                }
             op(OP_TIER, 0, 0, false, t, R.rank);
-            if (cnt(R.fill_off, t)) op(OP_FILL, 0, 0, false, t, R.rank);
             for (int jj : send_after[t])
                 for (int a = 0; a < d->g; a++) {
                     if (is_upper(R.rank, a) || !cnt(R.send_off[a], jj)) continue;
-                    const int upper = R.rank ^ (1 << a);
-                    // ring slot jj % NS last carried batch jj-NS: wait until it has left
-                    if (jj >= NS && cnt(R.send_off[a], jj - NS))
-                        op(OP_WAIT, a, EV_XCH, false, jj - NS, d->loopback ? upper : R.rank);
-                    op(OP_PACK, a, 0, false, jj, upper);
                     op(OP_RECORD, a, EV_PACKED, false, jj, R.rank);
                     if (!d->loopback) {
                         op(OP_WAIT, a, EV_PACKED, true, jj, R.rank);
-                        op(OP_SEND, a, 0, true, jj, upper);
+                        op(OP_SEND, a, 0, true, jj, R.rank ^ (1 << a));
                         op(OP_RECORD, a, EV_XCH, true, jj, R.rank);
                     }
                 }
@@ -361,15 +403,14 @@ static int plan_shape(const Ctx *c, DistSub *d, int G, bool loopback) {
         set_error("%d heaps leave %d block heaps; cannot split %d ways", d->heaps, d->high, G);
         return GM_E_ARG;
     }
-    d->nt = sub_kernel_threads(c, d->low);
-    if (d->nt == -3) d->nt = -2;   // the dataflow kernel is single-GPU: ranks run the tiered byte-image kernel
+    d->nt = -2;   // ranks always run the byte-image tier kernel (its extra-destination variant)
     d->want_threads = c->sub_threads;
     d->want_x4 = c->sub_interleave;
     d->want_order = c->sub_order;
     d->want_batch = c->dist_batch;
     d->want_slots = c->dist_slots;
     d->want_sym = c->dist_symmetry;
-    if (!sub_kernel_exists(d->low, d->high, d->nt)) { set_error("no dense kernel"); return GM_E_GAME; }
+    if (d->low != 3 || !sub_kernel_x_exists(d->high)) { set_error("no sharded dense kernel"); return GM_E_GAME; }
     d->ntiers = 15 * d->high + 1;
     d->batch = std::max(1, std::min(c->dist_batch, d->ntiers));
     d->nbatch = (d->ntiers + d->batch - 1) / d->batch;
@@ -424,6 +465,7 @@ static int prepare(Ctx *c, DistSub *d, int G, bool loopback) {
             R.own_S = true;
         }
         for (int a = 0; a < d->g; a++) GM_HIP(hipStreamCreateWithFlags(&R.X[a], hipStreamNonBlocking));
+        GM_TRY(upload_xdst(d, R));
         build_ops(d, R);
     }
     return GM_OK;
@@ -441,17 +483,13 @@ static int exec_op(DistSub *d, SubRank &R, const Op &o) {
     hipStream_t st = o.on_x ? R.X[a] : R.S;
     switch (o.kind) {
     case OP_TIER:
-        launch_sub_tier(d->low, d->high, d->nt, cnt(R.off, j), R.table, R.dlist + R.off[j], d->zero, st);
+        launch_sub_tier_x(d->high, cnt(R.off, j), R.table, R.dlist + R.off[j], d->zero, R.dxoff + R.off[j], R.dxdst,
+                          st);
         break;
-    case OP_FILL:   // fill_off counts u32 entries: two per block
-        hipLaunchKernelGGL(block_pair_copy_kernel, dim3(cnt(R.fill_off, j) / 2), dim3(256), 0, st, R.table,
-                           R.dfill + R.fill_off[j], d->low);
-        break;
-    case OP_PACK:
-        copy_blocks(d, R.table, R.dsend[a] + R.send_off[a][j], cnt(R.send_off[a], j), send_ptr(d, R, a, j), true,
-                    st);
-        d->sent += cnt(R.send_off[a], j) * bb;
-        break;
+    case OP_FILL:
+    case OP_PACK:   // folded into OP_TIER (extra destinations); not in the lists
+        set_error("unexpected op %d", (int)o.kind);
+        return GM_E_STATE;
     case OP_UNPACK:
         copy_blocks(d, recv_ptr(d, R, a, j), R.drecv[a] + R.recv_off[a][j], cnt(R.recv_off[a], j), R.table, false,
                     st);
@@ -471,6 +509,7 @@ static int exec_op(DistSub *d, SubRank &R, const Op &o) {
         break;
     }
     case OP_RECORD:
+        if (o.ev == EV_PACKED) d->sent += cnt(R.send_off[a], j) * bb;   // message j complete in its slot
         GM_HIP(hipEventRecord(R.ev[o.ev][a][j % d->nslots], st));
         R.recorded[o.ev][a] = j + 1;
         break;
@@ -486,7 +525,15 @@ static int exec_op(DistSub *d, SubRank &R, const Op &o) {
 // Enqueue one whole solve.  RCCL mode: the single rank's list in order.
 // Loopback: round-robin over the ranks, each running until its next op waits on
 // an event another rank has not enqueued yet.
-static int enqueue_solve(DistSub *d) {
+static int enqueue_solve(DistSub *d, int solo) {
+    if (solo > 0) {   // diagnostic: one rank's tier launches back to back (results invalid)
+        if (!d->loopback || solo > (int)d->ranks.size()) { set_error("dist_solo needs loopback ranks"); return GM_E_ARG; }
+        SubRank &R = d->ranks[solo - 1];
+        for (const Op &o : R.ops)
+            if (o.kind == OP_TIER) GM_TRY(exec_op(d, R, o));
+        GM_HIP(hipGetLastError());
+        return GM_OK;
+    }
     for (auto &R : d->ranks) {
         R.pc = 0;
         for (auto &k : R.recorded)
@@ -525,7 +572,7 @@ static int run_solve(Ctx *c, DistSub *d) {
         if (R.S != H) GM_HIP(hipStreamWaitEvent(R.S, d->ev_fork, 0));
         for (int a = 0; a < d->g; a++) GM_HIP(hipStreamWaitEvent(R.X[a], d->ev_fork, 0));
     }
-    GM_TRY(enqueue_solve(d));
+    GM_TRY(enqueue_solve(d, c->dist_solo));
     for (auto &R : d->ranks) {
         for (int a = 0; a < d->g; a++) {
             GM_HIP(hipEventRecord(R.ev_join[a], R.X[a]));
@@ -678,9 +725,9 @@ void dist_sub_free(Ctx *c) {
     for (auto &R : d->ranks) {
         if (R.owned && R.table) (void)hipFree(R.table);
         if (R.dlist) (void)hipFree(R.dlist);
-        if (R.dfill) (void)hipFree(R.dfill);
+        if (R.dxoff) (void)hipFree(R.dxoff);
+        if (R.dxdst) (void)hipFree(R.dxdst);
         for (int a = 0; a < MAX_AXES; a++) {
-            if (R.dsend[a]) (void)hipFree(R.dsend[a]);
             if (R.drecv[a]) (void)hipFree(R.drecv[a]);
             if (R.sendbuf[a]) (void)hipFree(R.sendbuf[a]);
             if (R.recvbuf[a]) (void)hipFree(R.recvbuf[a]);
@@ -735,6 +782,7 @@ int dist_sub_plan(int heaps, int world, int rank, const int32_t *opts, int what,
         case GM_PLAN_FILL: O = P.fill_off; D = P.fill; break;
         case GM_PLAN_SEND: O = P.send_off[axis]; D = P.send[axis]; break;
         case GM_PLAN_RECV: O = P.recv_off[axis]; D = P.recv[axis]; break;
+        case GM_PLAN_XDEST: O = P.xoff; D = P.xd; break;
         case GM_PLAN_OPS: {
             SubRank R;
             R.rank = rank;

@@ -230,6 +230,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         if (v < 0 || v > 1) { set_error("dist_symmetry must be 0 or 1"); return GM_E_ARG; }
         c->dist_symmetry = (int)v;
         return GM_OK;
+    case GM_OPT_DIST_SOLO:
+        if (v < 0 || v > 64) { set_error("dist_solo must be 0..64"); return GM_E_ARG; }
+        c->dist_solo = (int)v;
+        return GM_OK;
     case GM_OPT_VIRTUAL_RANKS:
         if (v < 1 || v > 64) { set_error("virtual ranks must be 1..64"); return GM_E_ARG; }
         c->virtual_ranks = (int)v;

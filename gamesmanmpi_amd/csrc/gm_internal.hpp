@@ -87,6 +87,7 @@ struct Ctx {
     hipStream_t comm_stream = nullptr;
     int dist_batch = 4;      // sharded dense path: tiers per halo exchange
     int dist_slots = 4;      // sharded dense path: ring of exchange buffers, in batches
+    int dist_solo = 0;       // diagnostic (loopback): enqueue only rank dist_solo-1's tier launches
     int dist_symmetry = 1;   // sharded dense path: halo blocks derivable by a heap swap are filled locally
 
     // results
@@ -125,6 +126,10 @@ int dense_sub_table(Ctx *c, void **p, uint64_t *bytes);
 bool sub_kernel_exists(int low, int high, int nt);
 void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table, const uint32_t *list,
                      const uint8_t *zero, hipStream_t s);
+// the sharded solve's byte-image tier kernel with per-block extra destinations (LOW = 3)
+bool sub_kernel_x_exists(int high);
+void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
+                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s);
 int sub_kernel_threads(const Ctx *c, int low);   // 0 = the 4-block interleaved kernel
 void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &tier_off, int high);
 

@@ -87,6 +87,9 @@ enum {
     GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton (default) */
     GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
     GM_OPT_DIST_SLOTS = 10, /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
+    GM_OPT_DIST_SOLO = 12,  /* diagnostic, loopback sharded SUBTRACT path: r + 1 = enqueue only rank r's
+                               tier launches (no exchange, no waits), to time one rank's compute
+                               critical path; the results are NOT valid.  0 (default) = off. */
     GM_OPT_DIST_SYMMETRY = 11 /* sharded SUBTRACT path: 1 (default) = fill halo blocks that are a heap
                                  permutation of an own block locally, 0 = receive every halo block */
 };
@@ -213,14 +216,22 @@ int gm_dense_table(gm_ctx *ctx, void **dev_ptr, uint64_t *bytes);
  *   GM_PLAN_SHAPE  data = {low, high, ntiers, batch, nbatch, nslots, g};
  *                  off = (lo, hi) tier range of each batch's halo message
  *   GM_PLAN_OWN    data = high parts this rank computes; off[t]..off[t+1] = tier t
- *   GM_PLAN_FILL   data = (dst, src) pairs filled locally after tier t (off in u32 entries)
+ *   GM_PLAN_FILL   data = (dst, src) pairs of tier t filled locally (off in u32 entries)
  *   GM_PLAN_SEND   data = halo high parts sent on split heap `axis`; off per batch
  *   GM_PLAN_RECV   data = halo high parts received on split heap `axis`; off per batch
  *   GM_PLAN_OPS    data = 6 u32 per op {kind, axis, event, on_exchange_stream, tier|batch, peer},
- *                  kind: 0 tier launch, 1 pack, 2 unpack, 3 send, 4 recv, 5 event record,
- *                  6 event wait, 7 symmetric fill; event: 0 packed, 1 exchanged, 2 unpacked
+ *                  kind: 0 tier launch (also writes every block's extra destinations:
+ *                  its symmetric-fill images and its halo ring slots), 2 unpack, 3 send,
+ *                  4 recv, 5 event record, 6 event wait (kinds 1 pack and 7 fill are
+ *                  folded into 0); event: 0 message complete in its slot, 1 exchanged,
+ *                  2 unpacked
+ *   GM_PLAN_XDEST  per own block (GM_PLAN_OWN order) its extra destinations:
+ *                  off[i]..off[i+1] index (kind, value) u32 pairs of data; kind 0 =
+ *                  table block (value = high part), 1 + axis = halo message slot
+ *                  (value = batch << 16 | index in the message)
  * With off / data NULL only *n_off / *n_data are set. */
-enum { GM_PLAN_SHAPE = 0, GM_PLAN_OWN = 1, GM_PLAN_FILL = 2, GM_PLAN_SEND = 3, GM_PLAN_RECV = 4, GM_PLAN_OPS = 5 };
+enum { GM_PLAN_SHAPE = 0, GM_PLAN_OWN = 1, GM_PLAN_FILL = 2, GM_PLAN_SEND = 3, GM_PLAN_RECV = 4, GM_PLAN_OPS = 5,
+       GM_PLAN_XDEST = 6 };
 int gm_dist_plan(int heaps, int world, int rank, const int32_t *opts, int what, int axis,
                  uint32_t *off, uint64_t off_cap, uint64_t *n_off,
                  uint32_t *data, uint64_t data_cap, uint64_t *n_data);

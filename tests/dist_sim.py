@@ -9,10 +9,12 @@ relies on -- one FIFO per HIP stream (S, X[axis]), hipStreamWaitEvent binding to
 the latest record of that event enqueued before it, and rendezvous matching of
 the k-th ncclSend/ncclRecv per (communicator, peer) -- in a random interleaving of
 whatever is ready, and tracks which blocks each rank's table holds final values
-for.  It fails on a deadlock, on a tier launch whose child blocks are not final
-in that rank's table, on a pack of a non-final block, on a ring slot reused
-before its previous batch left or was unpacked, and on sender / receiver halo
-lists that disagree.
+for.  A tier launch also writes its blocks' extra destinations (GM_PLAN_XDEST:
+symmetric-fill images, halo ring slots), as the tier kernel does.  It fails on a
+deadlock, on a tier launch whose child blocks are not final in that rank's table,
+on a send of a message whose blocks are not all written, on a ring slot written
+before its previous message left or received over before it was unpacked, and on
+sender / receiver halo lists that disagree.
 
 ``gloo_rank`` runs one rank's op list as a host program over torch.distributed
 (gloo) -- the same messages, peers and ordering as RCCL mode, with the oracle's
@@ -42,7 +44,32 @@ def load_plan(heaps, world, rank, batch=4, slots=4, symmetry=1):
         p["send"].append(_lib.dist_plan(heaps, world, rank, _lib.PLAN_SEND, axis=a, **kw))
         p["recv"].append(_lib.dist_plan(heaps, world, rank, _lib.PLAN_RECV, axis=a, **kw))
     p["ops"] = _lib.dist_plan(heaps, world, rank, _lib.PLAN_OPS, **kw)[1].reshape(-1, 6).astype(np.int64)
+    p["xoff"], p["xd"] = _lib.dist_plan(heaps, world, rank, _lib.PLAN_XDEST, **kw)
     return p
+
+
+def message_of_tier(p):
+    """tier -> the batch whose halo message carries it (-1: none)."""
+    m = np.full(p["ntiers"], -1, dtype=np.int64)
+    for j, (lo, hi) in enumerate(p["halo_range"].tolist()):
+        if lo <= hi:
+            m[lo:hi + 1] = j
+    return m
+
+
+def tier_writes(p, t):
+    """What tier t's launch writes besides its own blocks: (fill pairs, {axis: (batch, blocks, indices)})."""
+    pairs = seg(p["fill_off"], p["fill"], t).reshape(-1, 2)
+    sends = {}
+    j = message_of_tier(p)[t]
+    if j >= 0:
+        for a in range(p["g"]):
+            blocks = seg(*p["send"][a], j)
+            if len(blocks):
+                k = np.nonzero(tier_of(blocks, p["high"]) == t)[0]
+                if len(k):
+                    sends[a] = (int(j), blocks[k], k)
+    return pairs, sends
 
 
 def seg(off, data, i):
@@ -155,23 +182,24 @@ def simulate(plans, seed=0):
                 if final[r][own].any():
                     raise SimError("rank %d computes block %x twice" % (r, int(own[final[r][own]][0])))
                 final[r][own] = True
-        elif kind == OP_FILL:
-            pairs = seg(p["fill_off"], p["fill"], arg).reshape(-1, 2)
+            pairs, sends = tier_writes(p, arg)
             if not final[r][pairs[:, 1]].all():
-                raise SimError("rank %d fill after tier %d from a non-final block" % (r, arg))
+                raise SimError("rank %d tier %d fills from a block it did not compute" % (r, arg))
             final[r][pairs[:, 0]] = True
-        elif kind == OP_PACK:
-            blocks = seg(*p["send"][axis], arg)
-            if not final[r][blocks].all():
-                raise SimError("rank %d packs batch %d on axis %d before its blocks are final" % (r, arg, axis))
-            prev = send_slot[r][(axis, arg % ns)]
-            if prev is not None and not prev[1]:
-                raise SimError("rank %d overwrites send slot of batch %d before it was sent" % (r, prev[0]))
-            send_slot[r][(axis, arg % ns)] = [arg, False]
+            for a, (j, blocks, _) in sends.items():
+                prev = send_slot[r][(a, j % ns)]
+                if prev is not None and prev[0] != j and not prev[1]:
+                    raise SimError("rank %d writes batch %d into the send slot of batch %d before it was sent"
+                                   % (r, j, prev[0]))
+                if prev is None or prev[0] != j:
+                    send_slot[r][(a, j % ns)] = [j, False, set()]
+                send_slot[r][(a, j % ns)][2].update(blocks.tolist())
         elif kind == OP_SEND:
             cur = send_slot[r][(axis, arg % ns)]
             if cur is None or cur[0] != arg:
-                raise SimError("rank %d sends batch %d from a slot holding %s" % (r, arg, cur))
+                raise SimError("rank %d sends batch %d from a slot holding %s" % (r, arg, cur and cur[:2]))
+            if cur[2] != set(seg(*p["send"][axis], arg).tolist()):
+                raise SimError("rank %d sends batch %d on axis %d before all its blocks are written" % (r, arg, axis))
             cur[1] = True
         elif kind == OP_RECV:
             prev = recv_slot[r][(axis, arg % ns)]
@@ -180,7 +208,7 @@ def simulate(plans, seed=0):
             sender = plans[peer]
             got = send_slot[peer][(axis, arg % ns)]
             if got is None or got[0] != arg:
-                raise SimError("rank %d receives batch %d but rank %d's slot holds %s" % (r, arg, peer, got))
+                raise SimError("rank %d receives batch %d but rank %d's slot holds %s" % (r, arg, peer, got and got[:2]))
             mine, theirs = seg(*p["recv"][axis], arg), seg(*sender["send"][axis], arg)
             if not np.array_equal(mine, theirs):
                 raise SimError("axis %d batch %d: rank %d expects other blocks than rank %d sends" %
@@ -253,18 +281,24 @@ def gloo_rank(rank, world, heaps, batch, slots, symmetry, oracle_codes, result):
                 for H in own.tolist():
                     table[H * bsz:(H + 1) * bsz] = oracle_codes[H * bsz:(H + 1) * bsz]
                 have[own] = True
-        elif kind == OP_FILL:
-            for dst, src in seg(p["fill_off"], p["fill"], arg).reshape(-1, 2).tolist():
+            # the tier kernel's extra destinations: fill images, halo ring slots
+            pairs, sends = tier_writes(p, arg)
+            for dst, src in pairs.tolist():
                 assert have[src]
                 table[dst * bsz:(dst + 1) * bsz] = table[src * bsz:(src + 1) * bsz]
                 have[dst] = True
-        elif kind == OP_PACK:
-            blocks = seg(*p["send"][axis], arg)
-            assert have[blocks].all()
-            sendbuf[(axis, arg % ns)] = torch.from_numpy(
-                np.concatenate([table[H * bsz:(H + 1) * bsz] for H in blocks.tolist()] or [np.zeros(0, np.uint8)]))
+            for a, (j, blocks, idx) in sends.items():
+                n = len(seg(*p["send"][a], j))
+                key = (a, j % ns)
+                if key not in sendbuf or sendbuf[key][0] != j:
+                    assert ("s", a, j - ns) not in pending, "ring slot reused before its send left"
+                    sendbuf[key] = (j, np.zeros(n * bsz, dtype=np.uint8))
+                for H, k in zip(blocks.tolist(), idx.tolist()):
+                    sendbuf[key][1][k * bsz:(k + 1) * bsz] = table[H * bsz:(H + 1) * bsz]
         elif kind == OP_SEND:
-            buf = sendbuf[(axis, arg % ns)]
+            j, data = sendbuf[(axis, arg % ns)]
+            assert j == arg
+            buf = torch.from_numpy(data.copy())
             pending[("s", axis, arg)] = (dist.isend(buf, dst=peer), buf)
         elif kind == OP_RECV:
             n = len(seg(*p["recv"][axis], arg)) * bsz

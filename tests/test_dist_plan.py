@@ -61,6 +61,31 @@ def test_partition_and_halo_volume(world):
     assert sent[1] == {2: 32, 4: 128, 8: 384}[world] << 20
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tier_kernel_destinations_match_the_lists(world):
+    """GM_PLAN_XDEST (what the tier kernel writes besides each own block) is exactly the
+    symmetric-fill images and the halo ring slots of the plan's fill and send lists."""
+    for r in range(world):
+        p = S.load_plan(7, world, r)
+        want = {}
+        for dst, src in p["fill"].reshape(-1, 2).tolist():
+            want.setdefault(src, set()).add((0, dst))
+        for a in range(p["g"]):
+            off, blocks = p["send"][a]
+            for j in range(len(off) - 1):
+                for k, H in enumerate(blocks[off[j]:off[j + 1]].tolist()):
+                    want.setdefault(H, set()).add((1 + a, j << 16 | k))
+        got = {}
+        xoff, xd = p["xoff"], p["xd"].reshape(-1, 2)
+        assert len(xoff) == len(p["own"]) + 1
+        for i, H in enumerate(p["own"].tolist()):
+            d = {tuple(v) for v in xd[xoff[i]:xoff[i + 1]].tolist()}
+            if d:
+                got[H] = d
+        assert got == want
+        assert sum(len(v) for v in want.values()) == len(xd)
+
+
 def test_plan_rejects_impossible_splits():
     with pytest.raises(GMError):
         _lib.dist_plan(5, 8, 0, _lib.PLAN_SHAPE)      # 2 block heaps cannot split 8 ways
@@ -82,25 +107,35 @@ def _mutate(P, rank, pred, action):
     return Q
 
 
-@pytest.mark.parametrize("what", ["unpack_wait", "fill", "pack_after_tier", "recv"])
+@pytest.mark.parametrize("what", ["unpack_wait", "fill", "send_before_tier", "slot_wait", "recv"])
 def test_simulator_catches_broken_schedules(what):
     """The checker bites: each injected schedule bug is reported."""
     P = plans(6, 4, batch=2, slots=1, symmetry=1)
     upper = 3
-    if what == "unpack_wait":      # S no longer waits for the receive before unpacking
-        Q = _mutate(P, upper, lambda o: o[0] == S.OP_WAIT and o[2] == S.EV_XCH and o[3] == 0, "drop")
-    elif what == "fill":           # a symmetric fill is lost
-        Q = _mutate(P, upper, lambda o: o[0] == S.OP_FILL, "drop")
-    elif what == "pack_after_tier":    # the lower rank packs before computing the halo's last tier
+    if what == "unpack_wait":      # S no longer waits for the halo's unpack before its tiers
+        mid = P[upper]["nbatch"] // 2  # a batch whose tiers need the halo (rank 3's blocks start at tier 16)
+        Q = _mutate(P, upper, lambda o: o[0] == S.OP_WAIT and o[2] == S.EV_UNPACKED and o[3] == 0 and o[4] == mid,
+                    "drop")
+    elif what == "fill":           # the symmetric fill of one tier is lost
+        Q = [dict(p) for p in P]
+        fo = Q[upper]["fill_off"].astype(np.int64)
+        t = next(t for t in range(len(fo) - 1) if fo[t + 1] > fo[t])
+        Q[upper]["fill"] = np.delete(Q[upper]["fill"], np.arange(fo[t], fo[t + 1]))
+        fo[t + 1:] -= fo[t + 1] - fo[t]
+        Q[upper]["fill_off"] = fo
+    elif what == "send_before_tier":   # the lower rank marks a message complete before its last tier
         Q = [dict(p) for p in P]
         ops = Q[0]["ops"].tolist()
-        i = next(k for k, o in enumerate(ops) if o[0] == S.OP_PACK)
+        i = next(k for k, o in enumerate(ops) if o[0] == S.OP_RECORD and o[2] == S.EV_PACKED and o[3] == 0)
         ops.insert(i - 1, ops.pop(i))
         Q[0]["ops"] = np.array(ops, dtype=np.int64).reshape(-1, 6)
+    elif what == "slot_wait":      # a tier writes a ring slot without waiting for its previous send
+        Q = _mutate(P, 0, lambda o: o[0] == S.OP_WAIT and o[2] == S.EV_XCH and o[3] == 0 and o[1] == 1 and o[4] == 4,
+                    "drop")
     else:                          # a receive is dropped: its send never matches
         Q = _mutate(P, upper, lambda o: o[0] == S.OP_RECV, "drop")
     caught = 0
-    for seed in range(6):
+    for seed in range(20):          # a race shows only in some interleavings (the seeds are fixed)
         try:
             S.simulate(Q, seed=seed)
         except S.SimError:
