@@ -397,6 +397,9 @@ __device__ __forceinline__ uint32_t code_x4(uint32_t b) {   // parent_code on fo
     return ~b + ((b >> 6) & 0x02020202u);
 }
 
+#ifndef GM_PASSB_REG
+#define GM_PASSB_REG 1   // pass B children (a0-1, a0-2) by DPP and (c-1, c-2) from registers
+#endif
 #ifndef GM_B4_WAVES
 #define GM_B4_WAVES 1
 #endif
@@ -458,12 +461,42 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
 #else
     constexpr int TAU_END = 45;
 #endif
+    uint32_t p1 = 0, p2 = 0;   // this thread's codes of the last two steps: (a0, a1, c-1), (a0, a1, c-2)
     if (tid == 0) {
         uint32_t r = code_x4(s[0]);
         if (valid[0] && hp[0] == 0) r = (r & 0xFFFFFF00u) | 255u;   // all heaps empty: LOSS in 0
         s[0] = r;
+        p1 = r;
     }
     __syncthreads();
+#if GM_PASSB_REG
+    // Children inside the block, by where they live: (a0-1 | a0-2, a1, c) are the codes
+    // lanes tid-1 / tid-2 (same 16-lane DPP row) produced one / two steps ago, moved
+    // with row_shr (an invalid child reads 0, which max ignores: every position but
+    // the primitive has a child); (a0, a1, c-1 | c-2) are this thread's own last two
+    // codes; only (a0, a1-1 | a1-2, c), written by other waves, and the child-block
+    // fold s[o] come from LDS.  So a step issues 3 LDS reads instead of 7.
+    for (int tau = 1; tau <= TAU_END; tau++) {
+        const uint32_t n1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p1, 0x111, 0xF, 0xF, true);   // row_shr:1
+        const uint32_t n2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)p2, 0x112, 0xF, 0xF, true);   // row_shr:2
+        const int c = tau - s0;
+        uint32_t r = 0;
+        if (c >= 0 && c <= 15) {
+            const uint32_t o = (uint32_t)(tid + 256 * c);
+            const uint32_t v0 = s[o], v3 = s[o - d11], v4 = s[o - d12];
+            const uint32_t q1 = c >= 1 ? p1 : 0u, q2 = c >= 2 ? p2 : 0u;
+            const uint32_t e = pk_max(pk_max(pk_max(even_bytes(v0), even_bytes(v3)), pk_max(even_bytes(v4), even_bytes(n1))),
+                                      pk_max(pk_max(even_bytes(n2), even_bytes(q1)), even_bytes(q2)));
+            const uint32_t od = pk_max(pk_max(pk_max(odd_bytes(v0), odd_bytes(v3)), pk_max(odd_bytes(v4), odd_bytes(n1))),
+                                       pk_max(pk_max(odd_bytes(n2), odd_bytes(q1)), odd_bytes(q2)));
+            r = code_x4(__builtin_amdgcn_perm(od, e, 0x06020400u));
+            s[o] = r;
+        }
+        p2 = p1;
+        p1 = r;
+        __syncthreads();
+    }
+#else
     for (int tau = 1; tau <= TAU_END; tau++) {
         const int c = tau - s0;
         if (c >= 0 && c <= 15) {
@@ -479,6 +512,7 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
         }
         __syncthreads();
     }
+#endif
 
     // ---- pass C: back to four 16-byte rows per chunk
     __amdgpu_buffer_rsrc_t wr[K];
