@@ -290,10 +290,17 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    per_rank = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # each rank's own view per step: GPU time of its sharded solve (HIP events on its
+        # stream, halo waits included) and host time spent enqueueing it
+        mine = torch.tensor([kernel_ms / args.steps, enqueue_ms / args.steps], dtype=torch.float64, device="cuda")
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [[round(float(x), 4) for x in a.tolist()] for a in allr]
 
     # closed-form check of the root: LOSS iff xor over heaps of (h mod 3) == 0
     g = 0
@@ -352,7 +359,8 @@ def main():
         "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
             "halo_batch_tiers": args.dist_batch, "halo_slots": args.dist_slots,
             "halo_symmetric_fill": bool(args.dist_symmetry),
-            "host_enqueue_ms_per_step_rank0": enqueue_ms / max(1, args.steps)},
+            "host_enqueue_ms_per_step_rank0": enqueue_ms / max(1, args.steps),
+            "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
