@@ -49,6 +49,8 @@ struct DistSparse {
     std::vector<uint64_t> gcount;            // global positions per tier
     size_t cnt_cap = 0;
     unsigned long long *d_mat = nullptr;     // all-gathered G*G*S counts (RCCL mode)
+    unsigned long long *d_tot = nullptr;     // per-tier totals, all-reduced (RCCL mode)
+    size_t tot_cap = 0;
     uint32_t *d_root = nullptr;
     uint64_t sent_bytes = 0, edges = 0;
     DedupEstimate est;
@@ -194,12 +196,18 @@ static FrontRef fref(SpRank &R, size_t t) {
 // Cross-rank exchange of G-segmented arrays (RCCL mode; loopback copies are done by the caller).
 static int sendrecv(Ctx *c, DistSparse *d, const void *send, const uint64_t *send_off, void *recv,
                     const uint64_t *recv_off, size_t elem) {
+    // messages go in pieces of <= 1 GiB (the k-th piece to a peer matches its k-th receive)
+    constexpr uint64_t PIECE = 1ull << 30;
     GM_NCCL(ncclGroupStart());
     for (int p = 0; p < d->G; p++) {
-        const uint64_t sn = send_off[p + 1] - send_off[p], rn = recv_off[p + 1] - recv_off[p];
-        if (sn) GM_NCCL(ncclSend((const char *)send + send_off[p] * elem, sn * elem, ncclUint8, p, c->comm, c->stream));
-        if (rn) GM_NCCL(ncclRecv((char *)recv + recv_off[p] * elem, rn * elem, ncclUint8, p, c->comm, c->stream));
-        if (p != c->rank) d->sent_bytes += sn * elem;
+        const uint64_t sb = (send_off[p + 1] - send_off[p]) * elem, rb = (recv_off[p + 1] - recv_off[p]) * elem;
+        const char *sp = (const char *)send + send_off[p] * elem;
+        char *rp = (char *)recv + recv_off[p] * elem;
+        for (uint64_t o = 0; o < sb; o += PIECE)
+            GM_NCCL(ncclSend(sp + o, std::min(PIECE, sb - o), ncclUint8, p, c->comm, c->stream));
+        for (uint64_t o = 0; o < rb; o += PIECE)
+            GM_NCCL(ncclRecv(rp + o, std::min(PIECE, rb - o), ncclUint8, p, c->comm, c->stream));
+        if (p != c->rank) d->sent_bytes += sb;
     }
     GM_NCCL(ncclGroupEnd());
     return GM_OK;
@@ -345,6 +353,10 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     d->S = D::MAX_SKIP;
     d->t_root = desc.tier(root);
     const int G = d->G, S = d->S, nb = G * S;
+    if (!d->loopback && !c->comm) {
+        set_error("the sharded sparse engine needs a communicator (gm_set_comm) or virtual ranks");
+        return GM_E_ARG;
+    }
     if (nb > MAXBINS) { set_error("too many ranks for the sharded sparse engine"); return GM_E_ARG; }
     d->ranks.resize(d->loopback ? G : 1);
     for (size_t i = 0; i < d->ranks.size(); i++) {
@@ -450,9 +462,14 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
             }
         }
         if (!d->loopback) {
-            GM_HIP(hipMemcpyAsync(d->d_mat, local.data(), need * 8, hipMemcpyHostToDevice, c->stream));
-            GM_NCCL(ncclAllReduce(d->d_mat, d->d_mat, need, ncclUint64, ncclSum, c->comm, c->stream));
-            GM_HIP(hipMemcpyAsync(local.data(), d->d_mat, need * 8, hipMemcpyDeviceToHost, c->stream));
+            if (need > d->tot_cap) {   // the tier count grows past the G*G*S count matrix
+                if (d->d_tot) dev_free(c, d->d_tot);
+                d->tot_cap = std::max<size_t>(64, 2 * need);
+                GM_TRY(dev_alloc(c, (void **)&d->d_tot, d->tot_cap * 8));
+            }
+            GM_HIP(hipMemcpyAsync(d->d_tot, local.data(), need * 8, hipMemcpyHostToDevice, c->stream));
+            GM_NCCL(ncclAllReduce(d->d_tot, d->d_tot, need, ncclUint64, ncclSum, c->comm, c->stream));
+            GM_HIP(hipMemcpyAsync(local.data(), d->d_tot, need * 8, hipMemcpyDeviceToHost, c->stream));
             GM_HIP(hipStreamSynchronize(c->stream));
         }
         for (size_t u = t + 1; u < need; u++) d->gcount[u] = local[u];
@@ -671,6 +688,7 @@ void dist_sparse_free(Ctx *c) {
             dev_free(c, p);
     }
     dev_free(c, d->d_mat);
+    if (d->d_tot) dev_free(c, d->d_tot);
     dev_free(c, d->d_root);
     (void)hipStreamSynchronize(c->stream);
     delete d;

@@ -197,7 +197,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
     Ctx *c = &h->c;
     switch (opt) {
     case GM_OPT_ENGINE:
-        if (v < GM_ENGINE_AUTO || v > GM_ENGINE_SPARSE) { set_error("bad engine"); return GM_E_ARG; }
+        if (v < GM_ENGINE_AUTO || (v > GM_ENGINE_SPARSE && v != GM_ENGINE_DIST_SPARSE)) {
+            set_error("bad engine");
+            return GM_E_ARG;
+        }
         c->engine_opt = (int)v;
         return GM_OK;
     case GM_OPT_SUB_LOW:
@@ -302,7 +305,7 @@ int gm_set_comm(gm_ctx *h, int rank, int world, const void *uid, int bytes) {
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
     c->rank = rank;
     c->world = world;
-    if (world == 1) return GM_OK;
+    if (world == 1 && (!uid || bytes <= 0)) return GM_OK;   // no communicator needed
     if (!uid || bytes < (int)sizeof(ncclUniqueId)) { set_error("uid must hold %d bytes", (int)sizeof(ncclUniqueId)); return GM_E_ARG; }
     if (c->device < 0) { set_error("no HIP device"); return GM_E_HIP; }
     ncclUniqueId id;
@@ -326,13 +329,16 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     c->stats.world = c->world;
     c->root = root;
     int eng = engine_for(c);
-    bool sharded = c->world > 1 || c->virtual_ranks > 1;
+    // GM_ENGINE_DIST_SPARSE forces the hash-sharded engine, e.g. over a one-rank communicator
+    const bool force_dist_sparse = c->engine_opt == GM_ENGINE_DIST_SPARSE;
+    bool sharded = c->world > 1 || c->virtual_ranks > 1 || force_dist_sparse;
     if (sharded && c->world > 1 && c->virtual_ranks > 1) {
         set_error("virtual ranks and a multi-process communicator are exclusive");
         return GM_E_ARG;
     }
-    if (sharded) eng = (eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT) ? GM_ENGINE_DIST_DENSE
-                                                                              : GM_ENGINE_DIST_SPARSE;
+    if (sharded) eng = (!force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT)
+                           ? GM_ENGINE_DIST_DENSE
+                           : GM_ENGINE_DIST_SPARSE;
     int rc;
     switch (eng) {
     case GM_ENGINE_DENSE:

@@ -68,7 +68,8 @@ enum {
     GM_ENGINE_DENSE = 1,
     GM_ENGINE_SPARSE = 2,
     GM_ENGINE_DIST_DENSE = 3,   /* reported in gm_stats_t.engine: sharded dense path */
-    GM_ENGINE_DIST_SPARSE = 4,  /* reported in gm_stats_t.engine: sharded sparse path */
+    GM_ENGINE_DIST_SPARSE = 4,  /* reported in gm_stats_t.engine: sharded sparse path; as GM_OPT_ENGINE it
+                                   forces that path (needs gm_set_comm or GM_OPT_VIRTUAL_RANKS) */
     GM_ENGINE_GRAPH = 5         /* reported in gm_stats_t.engine: explicit graph (gm_solve_graph) */
 };
 
@@ -154,7 +155,10 @@ int gm_expand_host(gm_ctx *ctx, uint64_t key, uint64_t *children, int cap,
 /* Multi-GPU: join a solve of `world` ranks (one process per GPU).  `uid` is a
  * 128-byte ncclUniqueId produced by gm_comm_unique_id on rank 0 and shared by
  * the caller (e.g. over torch.distributed).  Replaces the mpi4py COMM_WORLD the
- * reference passes to Process (solver_launcher.py:47-52, :132-140). */
+ * reference passes to Process (solver_launcher.py:47-52, :132-140).  With
+ * world = 1 and a uid, a one-rank communicator is created: with GM_OPT_ENGINE =
+ * GM_ENGINE_DIST_SPARSE the hash-sharded engine then runs its RCCL transport on
+ * one GPU (self send/recv, all-gather, all-reduce), which tests use. */
 int gm_comm_unique_id(void *uid, int bytes);
 int gm_set_comm(gm_ctx *ctx, int rank, int world, const void *uid, int bytes);
 

@@ -5,6 +5,8 @@ lists, halo / all-to-all schedule and kernels as the one-process-per-GPU RCCL
 path, with the exchanges done by device copies (dist_sub.hip, dist_sparse.hip).
 Every sharded result must be bit-identical to the single-rank result.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -109,3 +111,41 @@ def test_sparse_sharded_toot_6x4_matches_single_gpu():
     assert (n, rec) == (n1, rec1) and n == 1187212827
     assert ctx.tier_counts().tolist() == counts1
     assert ctx.digest() == d1
+
+
+def _rccl_one_rank(game, params):
+    ctx = Context(game, params, device=0)
+    buf = ctypes.create_string_buffer(128)
+    _lib.check(_lib.lib().gm_comm_unique_id(buf, 128))
+    ctx.set_comm(0, 1, buf.raw)
+    ctx.set_option(_lib.OPT_ENGINE, _lib.ENGINE_DIST_SPARSE)
+    n, rec = ctx.solve(ctx.initial())
+    assert ctx.stats()["engine"] == _lib.ENGINE_DIST_SPARSE
+    return ctx, n, rec
+
+
+@pytest.mark.parametrize("name,game,params", [("othello_4x4", OTH, (4, 4)), ("toot_4x3", TOOT, (4, 3)),
+                                              ("ttt", TTT, ())])
+def test_sparse_rccl_transport_one_rank(name, game, params):
+    """The hash-sharded engine's RCCL transport on one GPU: over a one-rank communicator
+    every exchange is a real ncclGroup of self send/recv, the counts an ncclAllGather and
+    the tier totals an ncclAllReduce; the table equals the reference plugin's golden one."""
+    ctx, n, rec = _rccl_one_rank(game, params)
+    keys, recs = golden(name)
+    k, r = ctx.export()
+    assert n == len(keys)
+    assert np.array_equal(k, keys) and np.array_equal(r, recs)
+    ctx.close()
+
+
+def test_sparse_rccl_transport_one_rank_toot_6x4():
+    """Config 3 at full size through the RCCL transport (one rank): per-ply counts and the
+    full-table digest equal the one-GPU engine's."""
+    single, n1, rec1 = _solve(TOOT, (6, 4), 1)
+    d1, c1 = single.digest(), single.tier_counts().tolist()
+    single.close()
+    ctx, n, rec = _rccl_one_rank(TOOT, (6, 4))
+    assert (n, rec) == (n1, rec1) and n == 1187212827
+    assert ctx.tier_counts().tolist() == c1
+    assert ctx.digest() == d1
+    ctx.close()
