@@ -221,7 +221,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-toot", action="store_true", help="skip the config-3/4 side measurements")
     ap.add_argument("--cpu-heaps", type=int, default=8)
-    ap.add_argument("--dist-batch", type=int, default=4, help="N>1: tiers per halo exchange")
+    ap.add_argument("--dist-batch", type=int, default=None,
+                    help="N>1: tiers per halo exchange (default: chosen in warmup from 1, 2, 4, 8 by the "
+                         "max-over-ranks solve time; 4 for virtual ranks)")
     ap.add_argument("--dist-slots", type=int, default=4, help="N>1: halo buffers per split heap")
     ap.add_argument("--dist-symmetry", type=int, default=1, choices=(0, 1),
                     help="N>1: fill halo blocks that are a heap permutation of an own block locally")
@@ -262,7 +264,7 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_option(_lib.OPT_TIMING, 1)
-    ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch)
+    ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch or 4)
     ctx.set_option(_lib.OPT_DIST_SLOTS, args.dist_slots)
     ctx.set_option(_lib.OPT_DIST_SYMMETRY, args.dist_symmetry)
     if args.virtual_ranks > 1:
@@ -273,6 +275,27 @@ def main():
         if world > 1:
             dist.barrier()
 
+    autotune = None
+    if world > 1 and args.dist_batch is None:
+        # untimed: the halo batch trades the upper ranks' lag (B - 1 tiers) against the
+        # number of RCCL messages; every rank measures the same candidates and takes the
+        # same argmin of the max-over-ranks time, so all ranks keep one schedule
+        autotune = {}
+        for b in (1, 2, 4, 8):
+            ctx.set_option(_lib.OPT_DIST_BATCH, b)
+            ctx.solve(root)
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                ctx.solve(root)
+            torch.cuda.synchronize()
+            dt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3], dtype=torch.float64, device="cuda")
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            autotune[b] = round(float(dt.item()), 4)
+        args.dist_batch = min(autotune, key=lambda b: (autotune[b], b))
+        ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch)
+    args.dist_batch = args.dist_batch or 4
     for _ in range(args.warmup):
         n, rec = ctx.solve(root)
     barrier()
@@ -357,7 +380,7 @@ def main():
                                 "HIP events around rank 0's whole sharded solve (includes halo waits)")},
         "exchanged_bytes_per_step_rank0": st["exchanged_bytes"],
         "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
-            "halo_batch_tiers": args.dist_batch, "halo_slots": args.dist_slots,
+            "halo_batch_tiers": args.dist_batch, "halo_batch_autotune_ms": autotune, "halo_slots": args.dist_slots,
             "halo_symmetric_fill": bool(args.dist_symmetry),
             "host_enqueue_ms_per_step_rank0": enqueue_ms / max(1, args.steps),
             "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank},
