@@ -227,6 +227,9 @@ def main():
     ap.add_argument("--dist-slots", type=int, default=4, help="N>1: halo buffers per split heap")
     ap.add_argument("--dist-symmetry", type=int, default=1, choices=(0, 1),
                     help="N>1: fill halo blocks that are a heap permutation of an own block locally")
+    ap.add_argument("--dist-owner", type=int, default=None, choices=(0, 1),
+                    help="N>1: block owner, 0 = split heaps in halves, 1 = tier-balanced (default: chosen "
+                         "in warmup with the halo batch; 0 for virtual ranks)")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     args = ap.parse_args()
@@ -267,6 +270,7 @@ def main():
     ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch or 4)
     ctx.set_option(_lib.OPT_DIST_SLOTS, args.dist_slots)
     ctx.set_option(_lib.OPT_DIST_SYMMETRY, args.dist_symmetry)
+    ctx.set_option(_lib.OPT_DIST_OWNER, args.dist_owner or 0)
     if args.virtual_ranks > 1:
         ctx.set_option(_lib.OPT_VIRTUAL_RANKS, args.virtual_ranks)
     root = ctx.initial()
@@ -276,12 +280,18 @@ def main():
             dist.barrier()
 
     autotune = None
-    if world > 1 and args.dist_batch is None:
+    if world > 1 and (args.dist_batch is None or args.dist_owner is None):
         # untimed: the halo batch trades the upper ranks' lag (B - 1 tiers) against the
-        # number of RCCL messages; every rank measures the same candidates and takes the
-        # same argmin of the max-over-ranks time, so all ranks keep one schedule
+        # number of RCCL messages, the owner function the ranks' tier balance against
+        # the symmetric-fill writes; every rank measures the same candidates and takes
+        # the same argmin of the max-over-ranks time, so all ranks keep one schedule
         autotune = {}
-        for b in (1, 2, 4, 8):
+        owners = (0, 1) if args.dist_owner is None else (args.dist_owner,)
+        batches = (1, 2, 4, 8) if args.dist_batch is None else (args.dist_batch,)
+        for o, b in [(o, b) for o in owners for b in batches]:
+            if o == 1 and not args.dist_symmetry:
+                continue
+            ctx.set_option(_lib.OPT_DIST_OWNER, o)
             ctx.set_option(_lib.OPT_DIST_BATCH, b)
             ctx.solve(root)
             barrier()
@@ -292,10 +302,13 @@ def main():
             torch.cuda.synchronize()
             dt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3], dtype=torch.float64, device="cuda")
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            autotune[b] = round(float(dt.item()), 4)
-        args.dist_batch = min(autotune, key=lambda b: (autotune[b], b))
+            autotune["owner%d_batch%d" % (o, b)] = (round(float(dt.item()), 4), o, b)
+        _, args.dist_owner, args.dist_batch = min(autotune.values())
+        autotune = {k: v[0] for k, v in autotune.items()}
+        ctx.set_option(_lib.OPT_DIST_OWNER, args.dist_owner)
         ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch)
     args.dist_batch = args.dist_batch or 4
+    args.dist_owner = args.dist_owner or 0
     for _ in range(args.warmup):
         n, rec = ctx.solve(root)
     barrier()
@@ -382,6 +395,7 @@ def main():
         "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
             "halo_batch_tiers": args.dist_batch, "halo_batch_autotune_ms": autotune, "halo_slots": args.dist_slots,
             "halo_symmetric_fill": bool(args.dist_symmetry),
+            "block_owner": ("split heaps in halves", "tier-balanced")[args.dist_owner],
             "host_enqueue_ms_per_step_rank0": enqueue_ms / max(1, args.steps),
             "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank},
         "cpu_baseline": None,

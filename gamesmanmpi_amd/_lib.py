@@ -20,6 +20,7 @@ OPT_DIST_BATCH = 9
 OPT_DIST_SLOTS = 10
 OPT_DIST_SYMMETRY = 11
 OPT_DIST_SOLO = 12
+OPT_DIST_OWNER = 13
 BUF_DENSE_TABLE = 1
 PLAN_SHAPE, PLAN_OWN, PLAN_FILL, PLAN_SEND, PLAN_RECV, PLAN_OPS, PLAN_XDEST = 0, 1, 2, 3, 4, 5, 6
 REC_UNSOLVED = 0xFFFF
@@ -120,11 +121,11 @@ def check(rc):
     return rc
 
 
-def dist_plan(heaps, world, rank, what, axis=0, batch=4, slots=4, symmetry=1):
+def dist_plan(heaps, world, rank, what, axis=0, batch=4, slots=4, symmetry=1, owner=0):
     """gm_dist_plan -> (off, data) as uint32 numpy arrays (host only, no GPU)."""
     import numpy as np
     L = lib()
-    opts = (ctypes.c_int32 * 3)(batch, slots, symmetry)
+    opts = (ctypes.c_int32 * 3)(batch, slots, symmetry | owner << 1)
     n_off, n_data = ctypes.c_uint64(), ctypes.c_uint64()
     check(L.gm_dist_plan(heaps, world, rank, opts, what, axis, None, 0, ctypes.byref(n_off), None, 0,
                          ctypes.byref(n_data)))

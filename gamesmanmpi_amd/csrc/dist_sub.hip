@@ -20,6 +20,16 @@
 // 1/4 of the halo at G = 2, 4, 8 (5 high nibbles).  Every position is still
 // computed by its owner; only the transfer is avoided.
 //
+// Tier-balanced owner (GM_OPT_DIST_OWNER 1).  Owner 0 staggers the ranks: rank r's
+// blocks start at tier 8*popcount(r), so at a given tier one rank holds far more
+// than 1/G of it and the job spans the whole 76-tier chain.  Owner 1 makes rank
+// bits compare two heaps, [h_x < h_y]; a heap swap maps the two classes onto each
+// other and keeps the tier, so every rank holds a share of every tier.  A child
+// crossing into the other class is a permutation of a block its own rank owns
+// (filled locally, any high-nibble permutation is searched), except the ties
+// h_x == h_y, which only the [h_x < h_y] side needs: one direction per axis, as
+// with owner 0, so the same lower/upper schedule carries them.
+//
 // Schedule.  Tiers (high-nibble sums) are grouped in batches of B (GM_OPT_DIST_BATCH);
 // batch j is tiers [jB, jB+B).  Before batch j an upper rank needs its lower
 // neighbour's halo of tiers [jB-1, jB+B-2] -- message X_j, which the lower rank
@@ -96,6 +106,7 @@ struct DistSub {
     int heaps = 0, low = 0, high = 0, g = 0, G = 1, ntiers = 0, nt = 256;
     int batch = 4, nbatch = 0, nslots = 0;
     int want_threads = 0, want_x4 = 0, want_order = 0, want_batch = 0, want_slots = 0, want_sym = 0;
+    int owner = 0, npair = 0;           // owner function (GM_OPT_DIST_OWNER); axes 0..npair-1 compare two heaps
     bool loopback = false;
     std::vector<SubRank> ranks;
     std::vector<int> lo, hi;            // per batch: tier range of X_j (empty if lo > hi)
@@ -110,12 +121,42 @@ struct DistSub {
 
 static inline int nib(uint64_t v, int k) { return (int)((v >> (4 * k)) & 15u); }
 
-// rank owning high part H (axis a = high nibble high-1-a)
+// rank owning high part H.  Owner 0: rank bit a = [nibble high-1-a >= 8].  Owner 1
+// (tier-balanced): for a < npair, bit a = [nibble high-1-2a < nibble high-2-2a];
+// the remaining axes take [nibble >= 8] on the next unused nibbles.  A move lowers
+// one nibble, so a child's owner differs from its parent's in at most one bit.
 static inline int owner_of(const DistSub *d, uint64_t H) {
     int r = 0;
-    for (int a = 0; a < d->g; a++)
-        if (nib(H, d->high - 1 - a) >= 8) r |= 1 << a;
+    if (d->owner == 0) {
+        for (int a = 0; a < d->g; a++)
+            if (nib(H, d->high - 1 - a) >= 8) r |= 1 << a;
+        return r;
+    }
+    for (int a = 0; a < d->npair; a++)
+        if (nib(H, d->high - 1 - 2 * a) < nib(H, d->high - 2 - 2 * a)) r |= 1 << a;
+    for (int a = d->npair; a < d->g; a++)
+        if (nib(H, d->high - 1 - d->npair - a) >= 8) r |= 1 << a;
     return r;
+}
+
+// Some block of rank q has H as a child block (H + 1 or + 2 on one nibble is q's).
+static bool needed_by(const DistSub *d, uint64_t H, int q) {
+    for (int k = 0; k < d->high; k++)
+        for (uint64_t s = 1; s <= 2; s++)
+            if ((uint64_t)nib(H, k) + s <= 15 && owner_of(d, H + (s << (4 * k))) == q) return true;
+    return false;
+}
+
+// Owner 1: the first high-nibble permutation of H (lexicographic) that rank q owns.
+static bool perm_source(const DistSub *d, uint64_t H, int q, uint64_t *src) {
+    int idx[8];
+    for (int k = 0; k < d->high; k++) idx[k] = k;
+    while (std::next_permutation(idx, idx + d->high)) {
+        uint64_t P = 0;
+        for (int k = 0; k < d->high; k++) P |= (uint64_t)nib(H, idx[k]) << (4 * k);
+        if (owner_of(d, P) == q) { *src = P; return true; }
+    }
+    return false;
 }
 
 static inline bool is_upper(int rank, int a) { return (rank >> a) & 1; }
@@ -218,10 +259,28 @@ static int plan_lists(const Ctx *c, const DistSub *d, int rank, Plan &P) {
     for (uint64_t H = 0; H < nhigh; H++) {
         const int o = owner_of(d, H), t = tsum(H);
         for (int a = 0; a < d->g; a++) {
-            const int h = nib(H, d->high - 1 - a);
-            if ((h != 6 && h != 7) || xb[t] < 0) continue;
+            if (xb[t] < 0) continue;
+            const int q = o ^ (1 << a);   // the rank across axis a
             uint64_t src = 0;
-            const bool sym = c->dist_symmetry && sym_source(d, H, a, &src);
+            bool sym;
+            if (d->owner == 0) {
+                const int h = nib(H, d->high - 1 - a);
+                if (h != 6 && h != 7) continue;
+                sym = c->dist_symmetry && sym_source(d, H, a, &src);
+            } else {
+                if ((q != rank && o != rank) || !needed_by(d, H, q)) continue;
+                sym = perm_source(d, H, q, &src);
+                if (!is_upper(q, a)) {
+                    // a lower rank needing an upper rank's block: always a permutation of its own
+                    if (!sym) {
+                        set_error("tier-balanced owner: block %llx would cross axis %d downwards",
+                                  (unsigned long long)H, a);
+                        return GM_E_STATE;
+                    }
+                    if (q == rank) { fill[t].push_back((uint32_t)H); fill[t].push_back((uint32_t)src); }
+                    continue;
+                }
+            }
             if (o == rank && !is_upper(rank, a) && !sym) Sd[a][xb[t]].push_back((uint32_t)H);
             if (is_upper(rank, a) && o == (rank ^ (1 << a))) {
                 if (!sym) {
@@ -372,8 +431,11 @@ static void build_ops(DistSub *d, SubRank &R) {
             for (int jj : send_from[t])
                 for (int a = 0; a < d->g; a++) {
                     if (is_upper(R.rank, a) || !cnt(R.send_off[a], jj)) continue;
-                    if (jj >= NS && cnt(R.send_off[a], jj - NS))
-                        op(OP_WAIT, a, EV_XCH, false, jj - NS, d->loopback ? (R.rank ^ (1 << a)) : R.rank);
+                    // the slot's last non-empty message (empty ones record nothing; with
+                    // owner 1 a batch's message can be empty between two that are not)
+                    int jp = jj - NS;
+                    while (jp >= 0 && !cnt(R.send_off[a], jp)) jp -= NS;
+                    if (jp >= 0) op(OP_WAIT, a, EV_XCH, false, jp, d->loopback ? (R.rank ^ (1 << a)) : R.rank);
                 }
             op(OP_TIER, 0, 0, false, t, R.rank);
             for (int jj : send_after[t])
@@ -410,6 +472,15 @@ static int plan_shape(const Ctx *c, DistSub *d, int G, bool loopback) {
     d->want_batch = c->dist_batch;
     d->want_slots = c->dist_slots;
     d->want_sym = c->dist_symmetry;
+    d->owner = c->dist_owner;
+    if (d->owner == 1) {
+        // as many two-heap comparisons as leave a nibble for every remaining axis
+        d->npair = std::max(0, std::min(d->g, d->high - d->g));
+        if (!c->dist_symmetry) {
+            set_error("the tier-balanced owner needs GM_OPT_DIST_SYMMETRY 1 (its downward halo is all fills)");
+            return GM_E_ARG;
+        }
+    }
     if (d->low != 3 || !sub_kernel_x_exists(d->high)) { set_error("no sharded dense kernel"); return GM_E_GAME; }
     d->ntiers = 15 * d->high + 1;
     d->batch = std::max(1, std::min(c->dist_batch, d->ntiers));
@@ -594,6 +665,7 @@ int dist_sub_solve(Ctx *c, uint64_t root) {
     if (!d || d->heaps != c->sub.heaps || d->G != G || d->loopback != loopback ||
         d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave || d->want_order != c->sub_order ||
         d->want_batch != c->dist_batch || d->want_slots != c->dist_slots || d->want_sym != c->dist_symmetry ||
+        d->owner != c->dist_owner ||
         (!loopback && c->adopted_dense && d->ranks[0].table != c->adopted_dense)) {
         dist_sub_free(c);
         d = c->dist_sub = new DistSub();
@@ -764,7 +836,8 @@ int dist_sub_plan(int heaps, int world, int rank, const int32_t *opts, int what,
     if (opts) {
         c.dist_batch = std::max(1, (int)opts[0]);
         c.dist_slots = std::max(1, (int)opts[1]);
-        c.dist_symmetry = opts[2] ? 1 : 0;
+        c.dist_symmetry = opts[2] & 1;
+        c.dist_owner = (opts[2] >> 1) & 1;
     }
     DistSub d;
     GM_TRY(plan_shape(&c, &d, world, false));
@@ -775,8 +848,17 @@ int dist_sub_plan(int heaps, int world, int rank, const int32_t *opts, int what,
              (uint32_t)d.nslots, (uint32_t)d.g};
         for (int j = 0; j < d.nbatch; j++) { O.push_back((uint32_t)d.lo[j]); O.push_back((uint32_t)d.hi[j]); }
     } else {
-        Plan P;
-        GM_TRY(plan_lists(&c, &d, rank, P));
+        // the last plan is kept: a caller reads one rank's lists with several calls
+        static std::vector<int> last_key;
+        static Plan last;
+        const std::vector<int> key = {heaps, world, rank, d.batch, d.nslots, c.dist_symmetry, c.dist_owner};
+        if (key != last_key) {
+            last_key.clear();
+            last = Plan();
+            GM_TRY(plan_lists(&c, &d, rank, last));
+            last_key = key;
+        }
+        const Plan &P = last;
         switch (what) {
         case GM_PLAN_OWN: O = P.off; D = P.own; break;
         case GM_PLAN_FILL: O = P.fill_off; D = P.fill; break;

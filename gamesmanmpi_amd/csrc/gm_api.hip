@@ -233,6 +233,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         if (v < 0 || v > 1) { set_error("dist_symmetry must be 0 or 1"); return GM_E_ARG; }
         c->dist_symmetry = (int)v;
         return GM_OK;
+    case GM_OPT_DIST_OWNER:
+        if (v < 0 || v > 1) { set_error("dist_owner must be 0 or 1"); return GM_E_ARG; }
+        c->dist_owner = (int)v;
+        return GM_OK;
     case GM_OPT_DIST_SOLO:
         if (v < 0 || v > 64) { set_error("dist_solo must be 0..64"); return GM_E_ARG; }
         c->dist_solo = (int)v;

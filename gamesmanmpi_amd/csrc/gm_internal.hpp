@@ -89,6 +89,7 @@ struct Ctx {
     int dist_slots = 4;      // sharded dense path: ring of exchange buffers, in batches
     int dist_solo = 0;       // diagnostic (loopback): enqueue only rank dist_solo-1's tier launches
     int dist_symmetry = 1;   // sharded dense path: halo blocks derivable by a heap swap are filled locally
+    int dist_owner = 0;      // sharded dense path: 0 = split heaps in halves, 1 = tier-balanced comparisons
 
     // results
     bool solved = false;

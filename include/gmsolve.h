@@ -91,8 +91,12 @@ enum {
     GM_OPT_DIST_SOLO = 12,  /* diagnostic, loopback sharded SUBTRACT path: r + 1 = enqueue only rank r's
                                tier launches (no exchange, no waits), to time one rank's compute
                                critical path; the results are NOT valid.  0 (default) = off. */
-    GM_OPT_DIST_SYMMETRY = 11 /* sharded SUBTRACT path: 1 (default) = fill halo blocks that are a heap
+    GM_OPT_DIST_SYMMETRY = 11, /* sharded SUBTRACT path: 1 (default) = fill halo blocks that are a heap
                                  permutation of an own block locally, 0 = receive every halo block */
+    GM_OPT_DIST_OWNER = 13  /* sharded SUBTRACT path, block owner: 0 = split the top heaps in halves
+                               (rank bit a = [heap >= 8]); 1 = tier-balanced: rank bits compare two
+                               heaps ([h_x < h_y]) while enough heaps remain, [heap >= 8] after, so
+                               every rank holds a share of every tier (needs GM_OPT_DIST_SYMMETRY 1) */
 };
 
 /* Buffer roles for gm_adopt_buffer. */
@@ -216,7 +220,7 @@ int gm_dense_table(gm_ctx *ctx, void **dev_ptr, uint64_t *bytes);
  * DESIGN.md §5).  For tests and tooling that check the multi-GPU schedule on the
  * CPU.  The reference has no counterpart: its schedule is the dynamic mpi4py job
  * queue (src/new_process.py:37-60, :145-187).  `opts` = {GM_OPT_DIST_BATCH,
- * GM_OPT_DIST_SLOTS, GM_OPT_DIST_SYMMETRY} values, NULL = defaults.
+ * GM_OPT_DIST_SLOTS, GM_OPT_DIST_SYMMETRY | GM_OPT_DIST_OWNER << 1} values, NULL = defaults.
  *   GM_PLAN_SHAPE  data = {low, high, ntiers, batch, nbatch, nslots, g};
  *                  off = (lo, hi) tier range of each batch's halo message
  *   GM_PLAN_OWN    data = high parts this rank computes; off[t]..off[t+1] = tier t

@@ -31,8 +31,8 @@ OP_TIER, OP_PACK, OP_UNPACK, OP_SEND, OP_RECV, OP_RECORD, OP_WAIT, OP_FILL = ran
 EV_PACKED, EV_XCH, EV_UNPACKED = range(3)
 
 
-def load_plan(heaps, world, rank, batch=4, slots=4, symmetry=1):
-    kw = dict(batch=batch, slots=slots, symmetry=symmetry)
+def load_plan(heaps, world, rank, batch=4, slots=4, symmetry=1, owner=0):
+    kw = dict(batch=batch, slots=slots, symmetry=symmetry, owner=owner)
     shape_off, shape = _lib.dist_plan(heaps, world, rank, _lib.PLAN_SHAPE, **kw)
     low, high, ntiers, b, nbatch, nslots, g = (int(v) for v in shape)
     p = {"rank": rank, "low": low, "high": high, "ntiers": ntiers, "batch": b, "nbatch": nbatch,
@@ -260,13 +260,13 @@ def simulate(plans, seed=0):
     return True
 
 
-def gloo_rank(rank, world, heaps, batch, slots, symmetry, oracle_codes, result):
+def gloo_rank(rank, world, heaps, batch, slots, symmetry, oracle_codes, result, owner=0):
     """One rank of the RCCL-mode op list executed on the host over torch.distributed
     (gloo): halos travel as real messages; a tier launch copies the oracle's codes for
     its own blocks after checking their child blocks arrived."""
     import torch
     import torch.distributed as dist
-    p = load_plan(heaps, world, rank, batch, slots, symmetry)
+    p = load_plan(heaps, world, rank, batch, slots, symmetry, owner)
     low, high, ns = p["low"], p["high"], p["nslots"]
     bsz = 1 << (4 * low)
     table = np.zeros(1 << (4 * heaps), dtype=np.uint8)
@@ -334,7 +334,7 @@ def oracle_codes(heaps):
     return np.where(val == 0, rem + 1, 255 - rem).astype(np.uint8)
 
 
-def gloo_main(rank, world, port, heaps, batch, slots, symmetry, queue):
+def gloo_main(rank, world, port, heaps, batch, slots, symmetry, queue, owner=0):
     """Process entry of the world-size-N gloo test (tests/test_dist_plan.py)."""
     import os
     import sys
@@ -346,7 +346,7 @@ def gloo_main(rank, world, port, heaps, batch, slots, symmetry, queue):
     try:
         dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
         res = {}
-        gloo_rank(rank, world, heaps, batch, slots, symmetry, oracle_codes(heaps), res)
+        gloo_rank(rank, world, heaps, batch, slots, symmetry, oracle_codes(heaps), res, owner)
         dist.barrier()
         dist.destroy_process_group()
         queue.put(res)

@@ -18,8 +18,8 @@ import dist_sim as S
 from gamesmanmpi_amd import _lib, GMError
 
 
-def plans(heaps, world, batch=4, slots=4, symmetry=1):
-    return [S.load_plan(heaps, world, r, batch, slots, symmetry) for r in range(world)]
+def plans(heaps, world, batch=4, slots=4, symmetry=1, owner=0):
+    return [S.load_plan(heaps, world, r, batch, slots, symmetry, owner) for r in range(world)]
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
@@ -61,12 +61,13 @@ def test_partition_and_halo_volume(world):
     assert sent[1] == {2: 32, 4: 128, 8: 384}[world] << 20
 
 
+@pytest.mark.parametrize("owner", [0, 1])
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_tier_kernel_destinations_match_the_lists(world):
+def test_tier_kernel_destinations_match_the_lists(world, owner):
     """GM_PLAN_XDEST (what the tier kernel writes besides each own block) is exactly the
     symmetric-fill images and the halo ring slots of the plan's fill and send lists."""
     for r in range(world):
-        p = S.load_plan(7, world, r)
+        p = S.load_plan(7, world, r, owner=owner)
         want = {}
         for dst, src in p["fill"].reshape(-1, 2).tolist():
             want.setdefault(src, set()).add((0, dst))
@@ -84,6 +85,49 @@ def test_tier_kernel_destinations_match_the_lists(world):
                 got[H] = d
         assert got == want
         assert sum(len(v) for v in want.values()) == len(xd)
+
+
+@pytest.mark.parametrize("heaps,world", [(6, 2), (6, 4), (7, 4), (7, 8)])
+@pytest.mark.parametrize("batch,slots", [(4, 4), (1, 1), (2, 1), (100, 2)])
+def test_tier_balanced_schedule_is_deadlock_free_and_race_free(heaps, world, batch, slots):
+    """GM_OPT_DIST_OWNER 1: the same checks on the tier-balanced partition (its halo is
+    the tie blocks and whatever no heap permutation maps onto the receiver)."""
+    P = plans(heaps, world, batch, slots, owner=1)
+    for seed in range(2):
+        assert S.simulate(P, seed=seed)
+
+
+def test_tier_balanced_full_size_8_ranks():
+    P = plans(8, 8, owner=1)
+    assert S.simulate(P, seed=1)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tier_balanced_partition(world):
+    """Owner 1 at 2^32: every block has one owner; summed over tiers, the largest rank
+    share of a tier (the tier chain's critical path) drops against owner 0; the
+    halo that crosses a link is the blocks no heap permutation can fill."""
+    heaps, g = 8, world.bit_length() - 1
+    crit, sent = {}, {}
+    for owner in (0, 1):
+        owned = np.zeros(1 << 20, dtype=np.int64)
+        per_tier, total = [], 0
+        for r in range(world):
+            off, own = _lib.dist_plan(heaps, world, r, _lib.PLAN_OWN, owner=owner)
+            owned[own] += 1
+            per_tier.append(np.diff(off.astype(np.int64)))
+            for a in range(g):
+                total += len(_lib.dist_plan(heaps, world, r, _lib.PLAN_SEND, axis=a, owner=owner)[1])
+        assert (owned == 1).all()
+        crit[owner] = int(np.array(per_tier).max(0).sum())
+        sent[owner] = total
+    assert crit == {2: {0: 690152, 1: 557056}, 4: {0: 442952, 1: 295936}, 8: {0: 282320, 1: 193568}}[world]
+    assert sent[1] == {2: 15, 4: 480, 8: 12896}[world]
+
+
+def test_tier_balanced_needs_symmetric_fill():
+    with pytest.raises(GMError):
+        _lib.dist_plan(8, 2, 0, _lib.PLAN_OWN, symmetry=0, owner=1)
 
 
 def test_plan_rejects_impossible_splits():
@@ -149,15 +193,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,batch,slots,symmetry", [(2, 4, 4, 1), (2, 1, 1, 0), (4, 4, 4, 1), (4, 2, 1, 0)])
-def test_gloo_ranks_exchange_halos(world, batch, slots, symmetry):
+@pytest.mark.parametrize("world,batch,slots,symmetry,owner", [(2, 4, 4, 1, 0), (2, 1, 1, 0, 0), (4, 4, 4, 1, 0),
+                                                               (4, 2, 1, 0, 0), (2, 1, 1, 1, 1), (4, 4, 2, 1, 1)])
+def test_gloo_ranks_exchange_halos(world, batch, slots, symmetry, owner):
     """world_size > 1 over torch.distributed gloo: every rank runs its own RCCL-mode op
     list as a host program; after the solve every own and every halo block it holds
     equals the oracle's (6 heaps, 16.7 M positions)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=S.gloo_main, args=(r, world, port, 6, batch, slots, symmetry, q))
+    procs = [ctx.Process(target=S.gloo_main, args=(r, world, port, 6, batch, slots, symmetry, q, owner))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -56,6 +56,30 @@ def test_dense_sharded_batches_and_rings(oracle, batch, slots, ranks):
     assert np.array_equal(r, ref)
 
 
+@pytest.mark.parametrize("heaps,ranks", [(5, 2), (6, 2), (6, 4), (7, 2), (7, 4), (7, 8)])
+def test_dense_tier_balanced_vs_oracle(oracle, heaps, ranks):
+    """GM_OPT_DIST_OWNER 1 (tier-balanced owner) gives the oracle's table."""
+    ref = oracle.subtract_dense(heaps)
+    ctx, n, rec = _solve(SUB, (heaps,), ranks, dist_owner=1)
+    k, r = ctx.export()
+    assert np.array_equal(k, np.arange(16 ** heaps, dtype=np.uint64))
+    assert np.array_equal(r, ref)
+
+
+@pytest.mark.parametrize("batch,slots", [(1, 1), (2, 4), (8, 2)])
+def test_dense_tier_balanced_full_2_32_matches_single_gpu(batch, slots):
+    single, n1, rec1 = _solve(SUB, (8,), 1)
+    d1 = single.digest()
+    single.close()
+    for ranks in (2, 4, 8):
+        ctx, n, rec = _solve(SUB, (8,), ranks, dist_owner=1, dist_batch=batch, dist_slots=slots)
+        assert (n, rec) == (n1, rec1)
+        assert ctx.digest() == d1
+        # the halo blocks no heap permutation fills (tests/test_dist_plan.py pins the counts)
+        assert ctx.stats()["exchanged_bytes"] == {2: 15, 4: 480, 8: 12896}[ranks] * 4096
+        ctx.close()
+
+
 def test_dense_sharded_custom_root(oracle):
     root = 0x3F0A5C
     ok, orec = oracle.solve(SUB, (6,), root=root)
