@@ -12,16 +12,25 @@ timed region starts.  Synthetic by construction: the game is the input.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Prints ONE JSON line on rank 0 (driver contract), including
-  roofline      the tier kernel's algorithmic bytes per launch (SURVEY §8d edge
-                model with 1-byte records: 1 + 14.5 = 15.5 B per position, x
-                positions per launch) / its average launch time, from
-                HIP events recorded around every launch on the launch stream;
-                traffic = rocprofv3 PMC bytes per launch from profiles/ when present;
+  roofline      bound "hbm": achieved = the tier kernel's COMPULSORY bytes per
+                launch (1 B written + 2 producer-tier reads = 3 B per
+                position, x positions per launch) / its average launch time from
+                HIP events on the launch stream; frac = achieved / 8 TB/s;
+                traffic = rocprofv3 PMC HBM-side bytes per launch (profiles/), with
+                traffic_frac beside it; the SURVEY edge model (15.5 B/position) is
+                kept only as a diagnostic field, it is not an HBM bound for a
+                kernel that serves 6 of 14.5 child edges from LDS;
+  parity        the solved 2^32 table's gm_digest (all ranks summed) against the C
+                oracle's digest of the same table -- live from the cpu_baseline
+                leg at N = 1, and the committed oracle value
+                (tests/golden/oracle_digests.json) at every N;
   cpu_baseline  the C oracle's dense solver (oracle/gm_oracle.c), OpenMP over
                 the host threads the box gives the process, on the full 2^32
                 workload (a 7-heap sample if the full one would exceed ~30 s);
   other_configs config 3 (Toot-and-Otto 6x4) and config 4 (Othello 4x4) on the
-                sparse engine, hash-sharded over the same N ranks when N > 1
+                sparse engine, hash-sharded over the same N ranks when N > 1,
+                each with its oracle digest check and (rank 0, N = 1) a CPU
+                baseline from the C oracle's sorted-layer OpenMP solver
                 (reported beside the headline, not the metric).
 """
 import argparse
@@ -35,24 +44,55 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-ALGO_BYTES_PER_POSITION = 15.5  # SURVEY §8d edge model at 8 heaps, 1-B records: 1 write + 14.5 child reads
+EDGE_MODEL_BYTES_PER_POSITION = 15.5  # SURVEY §8d edge model, 1-B records: 1 write + 14.5 child reads (diagnostic)
 COMPULSORY_BYTES_PER_POSITION = 3.0  # SURVEY §8d compulsory bound with 1-B records: 1 write + 2 producer-tier reads
+ORACLE_DIGESTS = os.path.join(REPO, "tests", "golden", "oracle_digests.json")
 METRIC = "positions solved/sec (node) at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
 
 
-def cpu_baseline(heaps=8):
-    """The C oracle's dense solver on the host cores (positions/s).
-
-    OpenMP over every thread the box gives the process (OMP_NUM_THREADS), in the
-    GPU's block/tier decomposition (oracle/gm_oracle.c oracle_subtract_dense_mt).
-    The full 8-heap workload takes ~5-20 s on 16 cores; if a 7-heap probe says it
-    would exceed ~30 s, the 7-heap sample is reported instead."""
+def _oracle():
+    """ctypes view of the C oracle (test infrastructure: the checker and the CPU baseline)."""
     path = os.path.join(REPO, "oracle", "_build", "liboracle.so")
     if not os.path.exists(path):
         return None
-    import numpy as np
     L = ctypes.CDLL(path)
+    P = ctypes.POINTER
     L.oracle_subtract_dense_mt.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    L.oracle_dense_digest.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, P(ctypes.c_uint64)]
+    L.oracle_initial.argtypes = [ctypes.c_int, P(ctypes.c_int32), ctypes.c_int, P(ctypes.c_uint64)]
+    L.oracle_solve_layered.argtypes = [ctypes.c_int, P(ctypes.c_int32), ctypes.c_int, ctypes.c_uint64,
+                                       ctypes.c_int, P(ctypes.c_uint64), P(ctypes.c_uint64),
+                                       P(ctypes.c_uint16), P(ctypes.c_uint64), ctypes.c_int, P(ctypes.c_int)]
+    return L
+
+
+def _cpu_name():
+    import platform
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), cpu)
+    except OSError:
+        pass
+    return cpu
+
+
+THREAD_NOTE = ("threads = OMP_NUM_THREADS, the host-CPU share the box grants one GPU (nproc counts the "
+               "whole machine)")
+
+
+def cpu_baseline(heaps=8):
+    """The C oracle's dense solver on the host cores (positions/s), plus the oracle
+    digest of the table it built (the headline's live parity check).
+
+    OpenMP over every thread the box gives the process (OMP_NUM_THREADS), in the
+    GPU's block/tier decomposition (oracle/gm_oracle.c oracle_subtract_dense_mt).
+    The full 8-heap workload takes ~4 s on 16 cores; if a 7-heap probe says it
+    would exceed ~30 s, the 7-heap sample is reported instead."""
+    L = _oracle()
+    if L is None:
+        return None, None
+    import numpy as np
     threads = L.oracle_threads()
 
     def run(h):
@@ -64,33 +104,70 @@ def cpu_baseline(heaps=8):
 
     dt, _ = run(heaps - 1)
     if dt is None:
-        return None
+        return None, None
+    digest = None
     if dt * 16 < 30.0:
         dt8, out = run(heaps)
         if dt8 is not None:
-            # spot check against the closed form: LOSS iff xor of (h mod 3) == 0
-            k = 0xFFFFFFFF >> (4 * (8 - heaps))
-            g = 0
-            for i in range(heaps):
-                g ^= ((k >> (4 * i)) & 15) % 3
-            assert (int(out[k]) >> 14) == (1 if g == 0 else 0)
-            dt, heaps = dt8, heaps
+            d = ctypes.c_uint64()
+            L.oracle_dense_digest(out.ctypes.data, ctypes.c_uint64(len(out)), 0, ctypes.byref(d))
+            digest = d.value
+            dt = dt8
         else:
             heaps -= 1
+        del out
     else:
         heaps -= 1
     n = 1 << (4 * heaps)
-    import platform
-    cpu = platform.processor() or platform.machine()
+    return ({"value": n / dt, "unit": "positions/s", "cores": threads, "kind": "port",
+             "sample": "%d-heap subtraction game, all %d positions, %.2f s; C oracle dense retrograde "
+                       "(oracle/gm_oracle.c oracle_subtract_dense_mt), OpenMP %d threads on %s; %s, nproc %d"
+                       % (heaps, n, dt, threads, _cpu_name(), THREAD_NOTE, os.cpu_count())},
+            digest if heaps == 8 else None)
+
+
+def sparse_cpu_baseline(game, params):
+    """C oracle's sorted-layer OpenMP solver (oracle_solve_layered) on the host cores:
+    positions/s of one complete strong solve of `game` at `params`."""
+    L = _oracle()
+    if L is None:
+        return None
+    arr = (ctypes.c_int32 * len(params))(*params)
+    root = ctypes.c_uint64()
+    L.oracle_initial(game, arr, len(params), ctypes.byref(root))
+    npos, dg, rr, nt = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint16(), ctypes.c_int()
+    t0 = time.perf_counter()
+    rc = L.oracle_solve_layered(game, arr, len(params), root, 0, ctypes.byref(npos), ctypes.byref(dg),
+                                ctypes.byref(rr), None, 0, ctypes.byref(nt))
+    dt = time.perf_counter() - t0
+    if rc != 0:
+        return None
+    return {"value": npos.value / dt, "unit": "positions/s", "cores": L.oracle_threads(), "kind": "port",
+            "positions": npos.value, "seconds": dt, "digest": dg.value,
+            "sample": "%s %s, all %d positions, %.2f s; C oracle sorted-layer retrograde "
+                      "(oracle/gm_oracle.c oracle_solve_layered), OpenMP %d threads on %s; %s"
+                      % ({3: "Toot-and-Otto", 4: "Othello"}[game], "x".join(map(str, params)), npos.value, dt,
+                         L.oracle_threads(), _cpu_name(), THREAD_NOTE)}
+
+
+def committed_digest(name):
+    """Oracle digest of a full table from tests/golden/oracle_digests.json (made by
+    tests/golden/make_oracle_digests.py with the C oracle), or None."""
     try:
-        with open("/proc/cpuinfo") as f:
-            cpu = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), cpu)
-    except OSError:
-        pass
-    return {"value": n / dt, "unit": "positions/s", "cores": threads, "kind": "port",
-            "sample": "%d-heap subtraction game, all %d positions, %.2f s; C oracle dense retrograde "
-                      "(oracle/gm_oracle.c oracle_subtract_dense_mt), OpenMP %d threads on %s, "
-                      "nproc %d" % (heaps, n, dt, threads, cpu, os.cpu_count())}
+        with open(ORACLE_DIGESTS) as f:
+            return json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def summed_digest(ctx, world, dist, torch):
+    """gm_digest of this rank's table, summed over ranks (mod 2^64) when world > 1."""
+    d, m = ctx.digest()
+    if world > 1:
+        v = torch.tensor([d - (1 << 64) if d >= (1 << 63) else d, m], dtype=torch.int64, device="cuda")
+        dist.all_reduce(v)
+        d, m = int(v[0].item()) & ((1 << 64) - 1), int(v[1].item())
+    return d, m
 
 
 TOOT_6X4_PER_PLY = [1, 12, 114, 748, 4266, 19692, 81140, 285708, 928196, 2665424, 7098172, 17010952,
@@ -100,10 +177,10 @@ TOOT_6X4_PER_PLY = [1, 12, 114, 748, 4266, 19692, 81140, 285708, 928196, 2665424
 
 def sparse_config(name, game, params, rank, world, dist, torch, repeats=2):
     """Config 3 / 4 on the sparse engine, hash-sharded over the job's ranks (RCCL p2p,
-    csrc/dist_sparse.hip) when world > 1.  Checked: position count and root record
-    (Othello 4x4: SURVEY §8a, 54,089 positions, LOSS in 12; Toot 6x4: Appendix D's
-    per-ply counts).  Othello 4x4 at world > 1 also compares the all-reduced
-    full-table digest with a one-GPU solve of the same game.  Time = max over ranks."""
+    csrc/dist_sparse.hip) when world > 1.  Checked: position count, root record,
+    per-ply counts (Toot 6x4: SURVEY Appendix D) and the full-table digest summed
+    over ranks against the C oracle's (tests/golden/oracle_digests.json).  Time =
+    max over ranks."""
     from gamesmanmpi_amd import Context, _lib
     ctx = Context(game, params, device=int(os.environ.get("LOCAL_RANK", 0)))
     if world > 1:
@@ -132,30 +209,29 @@ def sparse_config(name, game, params, rank, world, dist, torch, repeats=2):
     st = ctx.stats()
     out = {"positions": n, "root_record": rec, "solve_ms": best * 1e3, "positions_per_s": n / best,
            "ranks": world, "exchanged_bytes_rank%d" % rank: st["exchanged_bytes"]}
+    ref = committed_digest(name)
+    d, m = summed_digest(ctx, world, dist, torch)
+    out["digest"] = "%#018x" % d
+    out["digest_matches_oracle"] = (ref is not None and (d, m) == (ref["digest"], ref["positions"])
+                                    and rec == ref["root_record"])
     if name == "toot_6x4":
         out["workload"] = "Toot-and-Otto 6x4 (config 3), sparse engine" + (", hash-sharded" if world > 1 else "")
         out["per_ply_counts_match_appendix_d"] = [int(x) for x in ctx.tier_counts()] == TOOT_6X4_PER_PLY
-        out["ok"] = n == 1187212827 and out["per_ply_counts_match_appendix_d"]
+        out["ok"] = n == 1187212827 and out["per_ply_counts_match_appendix_d"] and out["digest_matches_oracle"]
         out["edges"] = st["n_edges"]
         out["algo_bytes_per_position"] = st["algo_bytes"] / n
     else:
         out["workload"] = "Othello 4x4 (config 4), sparse engine" + (", hash-sharded" if world > 1 else "")
-        out["ok"] = n == 54089 and (rec >> 14) == 1 and (rec & 0x3FFF) == 12
-        if world > 1:
-            d, m = ctx.digest()
-            v = torch.tensor([d - (1 << 64) if d >= (1 << 63) else d, m], dtype=torch.int64, device="cuda")
-            dist.all_reduce(v)
-            dsum, msum = int(v[0].item()) & ((1 << 64) - 1), int(v[1].item())
-            one = Context(game, params, device=int(os.environ.get("LOCAL_RANK", 0)))
-            one.solve(one.initial())
-            out["digest_matches_one_gpu"] = (dsum, msum) == one.digest()
-            out["ok"] = out["ok"] and out["digest_matches_one_gpu"]
-            one.close()
+        out["ok"] = n == 54089 and (rec >> 14) == 1 and (rec & 0x3FFF) == 12 and out["digest_matches_oracle"]
     ctx.close()
     return out
 
 
-def other_configs(rank, world, dist, torch, budget_s=150.0, emit=None):
+SPARSE_CPU_SAMPLE = {"othello_4x4": (4, (4, 4)),    # the whole config-4 workload
+                     "toot_6x4": (3, (5, 4))}        # bounded sample: the 5x4 board (70 M positions, ~10-20 s)
+
+
+def other_configs(rank, world, dist, torch, budget_s=240.0, emit=None):
     """Run the side configs under a watchdog: if the ranks have not finished within
     budget_s (a sharded exchange that never completes), every rank prints what it
     has (rank 0 the headline line via emit) and leaves with status 0, so the
@@ -181,6 +257,12 @@ def other_configs(rank, world, dist, torch, budget_s=150.0, emit=None):
             res[name] = {"error": "%s: %s" % (type(e).__name__, e)}
             if world > 1:
                 break
+        if rank == 0 and world == 1 and "error" not in res[name]:
+            g, p = SPARSE_CPU_SAMPLE[name]
+            cb = sparse_cpu_baseline(g, p)
+            if cb is not None:
+                res[name]["cpu_baseline"] = cb
+                res[name]["speedup_vs_cpu_baseline"] = res[name]["positions_per_s"] / cb["value"]
     timer.cancel()
     return res
 
@@ -227,18 +309,40 @@ def main():
     ap.add_argument("--dist-slots", type=int, default=4, help="N>1: halo buffers per split heap")
     ap.add_argument("--dist-symmetry", type=int, default=1, choices=(0, 1),
                     help="N>1: fill halo blocks that are a heap permutation of an own block locally")
-    ap.add_argument("--dist-owner", type=int, default=None, choices=(0, 1),
-                    help="N>1: block owner, 0 = split heaps in halves, 1 = tier-balanced (default: chosen "
-                         "in warmup with the halo batch; 0 for virtual ranks)")
+    ap.add_argument("--dist-owner", type=int, default=0, choices=(0, 1),
+                    help="N>1: block owner, 0 = split heaps in halves (default), 1 = tier-balanced (measured "
+                         "slower per rank on one GPU, DESIGN.md §5)")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
+    ap.add_argument("--watchdog", type=float, default=None,
+                    help="seconds before the headline solve is declared hung (default 240 + 2 s per step)")
     args = ap.parse_args()
+    if args.dist_owner == 1 and not args.dist_symmetry:
+        ap.error("--dist-owner 1 needs --dist-symmetry 1 (the tier-balanced owner relies on the symmetric fill)")
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+
+    # Headline watchdog: a sharded solve whose exchange never completes must end the
+    # job with a non-zero status (never a re-exec), not hang until the driver's limit.
+    import threading
+    budget = args.watchdog or (240.0 + 2.0 * (args.steps + args.warmup))
+
+    def expire():
+        sys.stderr.write("bench.py rank %d: watchdog: the headline solve did not finish within %.0f s\n"
+                         % (rank, budget))
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "error": "watchdog expired after %.0f s" % budget}),
+                  flush=True)
+        sys.stderr.flush()
+        os._exit(3)
+
+    watchdog = threading.Timer(budget, expire)
+    watchdog.daemon = True
+    watchdog.start()
 
     import torch
     import torch.distributed as dist
@@ -270,7 +374,7 @@ def main():
     ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch or 4)
     ctx.set_option(_lib.OPT_DIST_SLOTS, args.dist_slots)
     ctx.set_option(_lib.OPT_DIST_SYMMETRY, args.dist_symmetry)
-    ctx.set_option(_lib.OPT_DIST_OWNER, args.dist_owner or 0)
+    ctx.set_option(_lib.OPT_DIST_OWNER, args.dist_owner)
     if args.virtual_ranks > 1:
         ctx.set_option(_lib.OPT_VIRTUAL_RANKS, args.virtual_ranks)
     root = ctx.initial()
@@ -280,18 +384,12 @@ def main():
             dist.barrier()
 
     autotune = None
-    if world > 1 and (args.dist_batch is None or args.dist_owner is None):
+    if world > 1 and args.dist_batch is None:
         # untimed: the halo batch trades the upper ranks' lag (B - 1 tiers) against the
-        # number of RCCL messages, the owner function the ranks' tier balance against
-        # the symmetric-fill writes; every rank measures the same candidates and takes
+        # number of RCCL messages; every rank measures the same candidates and takes
         # the same argmin of the max-over-ranks time, so all ranks keep one schedule
         autotune = {}
-        owners = (0, 1) if args.dist_owner is None else (args.dist_owner,)
-        batches = (1, 2, 4, 8) if args.dist_batch is None else (args.dist_batch,)
-        for o, b in [(o, b) for o in owners for b in batches]:
-            if o == 1 and not args.dist_symmetry:
-                continue
-            ctx.set_option(_lib.OPT_DIST_OWNER, o)
+        for b in (1, 2, 4, 8):
             ctx.set_option(_lib.OPT_DIST_BATCH, b)
             ctx.solve(root)
             barrier()
@@ -302,13 +400,11 @@ def main():
             torch.cuda.synchronize()
             dt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3], dtype=torch.float64, device="cuda")
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            autotune["owner%d_batch%d" % (o, b)] = (round(float(dt.item()), 4), o, b)
-        _, args.dist_owner, args.dist_batch = min(autotune.values())
+            autotune["batch%d" % b] = (round(float(dt.item()), 4), b)
+        _, args.dist_batch = min(autotune.values())
         autotune = {k: v[0] for k, v in autotune.items()}
-        ctx.set_option(_lib.OPT_DIST_OWNER, args.dist_owner)
         ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch)
     args.dist_batch = args.dist_batch or 4
-    args.dist_owner = args.dist_owner or 0
     for _ in range(args.warmup):
         n, rec = ctx.solve(root)
     barrier()
@@ -338,11 +434,21 @@ def main():
         dist.all_gather(allr, mine)
         per_rank = [[round(float(x), 4) for x in a.tolist()] for a in allr]
 
-    # closed-form check of the root: LOSS iff xor over heaps of (h mod 3) == 0
+    # parity of the last timed solve: the whole table's digest (summed over ranks)
+    # against the C oracle's digest of the same table
+    digest, ndig = summed_digest(ctx, world, dist, torch)
+    watchdog.cancel()
     g = 0
     for i in range(args.heaps):
         g ^= ((root >> (4 * i)) & 15) % 3
-    assert (rec >> 14) == (1 if g == 0 else 0), "root record %#x contradicts the closed form" % rec
+    closed_form_ok = (rec >> 14) == (1 if g == 0 else 0)   # LOSS iff xor over heaps of (h mod 3) == 0
+    ref = committed_digest("subtract_%d" % args.heaps) if root == (1 << (4 * args.heaps)) - 1 else None
+    parity = {"digest": "%#018x" % digest, "positions_in_digest": ndig, "root_record": rec,
+              "root_closed_form_ok": closed_form_ok,
+              "matches_committed_oracle_digest": (None if ref is None else
+                                                  (digest, ndig, rec) == (ref["digest"], ref["positions"],
+                                                                          ref["root_record"])),
+              "matches_live_oracle_digest": None}
 
     positions = n
     value = positions * args.steps / elapsed
@@ -351,12 +457,12 @@ def main():
     traffic_launch, traffic_solve = pmc_traffic(args.heaps)
     copy_gbs = copy_bandwidth(torch) if world == 1 else None
     kernel_s_per_solve = kernel_ms / 1e3 / max(1, args.steps)
-    compulsory_gbs = (COMPULSORY_BYTES_PER_POSITION * positions / kernel_s_per_solve / 1e9
-                      if kernel_s_per_solve > 0 else None)
-    # bytes this rank's tier launches move, per the SURVEY §8d model
-    algo_per_launch = st["algo_bytes"] / launches_per_solve
     avg_launch_s = (kernel_ms / 1e3) / max(1, launches)
-    achieved = algo_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
+    # algorithmic (compulsory) bytes per launch: 3 B x the positions this rank's launches solve
+    own_positions = positions if world == 1 else positions / world
+    compulsory_per_launch = COMPULSORY_BYTES_PER_POSITION * own_positions / launches_per_solve
+    achieved = compulsory_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
+    traffic_gbs = (traffic_launch / avg_launch_s / 1e9) if (traffic_launch and avg_launch_s > 0) else None
     out = {
         "metric": METRIC,
         "value": value,
@@ -372,25 +478,29 @@ def main():
         "data": "synthetic (the game itself: every position of the 2^32-state subtraction game)",
         "config": {"workload": "subtraction game, %d heaps x 4 bits, root %#x (config 5)" % (args.heaps, root),
                    "positions": positions, "parallelism": "1 GPU" if world == 1 else "block-sharded x%d" % world},
+        "parity": parity,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic_launch,
+                     "traffic_gbs": traffic_gbs,
+                     "traffic_frac": (traffic_gbs / HBM_PEAK_GBS) if traffic_gbs else None,
                      "kernel": "sub_tier_kernel_b4<%d>" % (args.heaps - 3),
+                     "algo_bytes_per_position": COMPULSORY_BYTES_PER_POSITION,
+                     "algo_bytes_model": "compulsory: 1 B code written + 2 B producer-tier reads per position",
                      "launches_per_solve": launches_per_solve,
                      "avg_launch_us": avg_launch_s * 1e6,
                      "kernel_ms_per_solve": kernel_ms / max(1, args.steps),
-                     "algo_bytes_per_position": ALGO_BYTES_PER_POSITION,
-                     "survey_u16_model_bytes_per_position": 31.0,
                      "traffic_bytes_per_position": (traffic_solve / positions) if traffic_solve else None,
-                     "traffic_gbs": (traffic_solve / kernel_s_per_solve / 1e9) if traffic_solve else None,
-                     "compulsory_bytes_per_position": COMPULSORY_BYTES_PER_POSITION,
-                     "compulsory_gbs": compulsory_gbs,
-                     "compulsory_frac": (compulsory_gbs / HBM_PEAK_GBS) if compulsory_gbs else None,
+                     "traffic_source": "profiles/traffic_subtract%d.json (rocprofv3 --pmc FETCH_SIZE x2 + "
+                                       "WRITE_SIZE, per launch)" % args.heaps,
+                     "diag_edge_model_bytes_per_position": EDGE_MODEL_BYTES_PER_POSITION,
+                     "diag_edge_model_gbs": (EDGE_MODEL_BYTES_PER_POSITION * own_positions / kernel_s_per_solve / 1e9
+                                             if kernel_s_per_solve > 0 else None),
                      "measured_copy_gbs": copy_gbs,
                      "timing": ("HIP events bracketing each solve's tier-launch graph replay on the launch "
                                 "stream; avg launch = span / launches (includes in-graph gaps)"
                                 if world == 1 else
-                                "HIP events around rank 0's whole sharded solve (includes halo waits)")},
+                                "HIP events around this rank's whole sharded solve (includes halo waits)")},
         "exchanged_bytes_per_step_rank0": st["exchanged_bytes"],
         "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
             "halo_batch_tiers": args.dist_batch, "halo_batch_autotune_ms": autotune, "halo_slots": args.dist_slots,
@@ -401,7 +511,11 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_heaps)
+        out["cpu_baseline"], live = cpu_baseline(args.cpu_heaps)
+        if live is not None and args.heaps == args.cpu_heaps == 8 and root == 0xFFFFFFFF:
+            parity["matches_live_oracle_digest"] = live == digest
+    parity["ok"] = bool(closed_form_ok and parity["matches_committed_oracle_digest"] is not False
+                        and parity["matches_live_oracle_digest"] is not False)
     ctx.close()
     if args.virtual_ranks == 1 and not args.no_toot:
         del table
@@ -417,6 +531,9 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not parity["ok"]:
+        sys.stderr.write("bench.py: PARITY FAILURE of the headline table: %s\n" % json.dumps(parity))
+        sys.exit(2)
 
 
 if __name__ == "__main__":

@@ -61,6 +61,8 @@
 // cross-rank wait is enqueued after the record it waits for.
 #include "gm_internal.hpp"
 
+#include <mutex>
+
 #include <algorithm>
 
 namespace gm {
@@ -277,7 +279,17 @@ static int plan_lists(const Ctx *c, const DistSub *d, int rank, Plan &P) {
                                   (unsigned long long)H, a);
                         return GM_E_STATE;
                     }
-                    if (q == rank) { fill[t].push_back((uint32_t)H); fill[t].push_back((uint32_t)src); }
+                    if (q == rank) {
+                        // same guard as the upward branch: the fill source must be an own
+                        // block of the same tier, computed by this rank's tier-t launch
+                        if (owner_of(d, src) != rank || tsum(src) != t) {
+                            set_error("symmetric fill source of block %llx is not an own block of its tier",
+                                      (unsigned long long)H);
+                            return GM_E_STATE;
+                        }
+                        fill[t].push_back((uint32_t)H);
+                        fill[t].push_back((uint32_t)src);
+                    }
                     continue;
                 }
             }
@@ -848,9 +860,12 @@ int dist_sub_plan(int heaps, int world, int rank, const int32_t *opts, int what,
              (uint32_t)d.nslots, (uint32_t)d.g};
         for (int j = 0; j < d.nbatch; j++) { O.push_back((uint32_t)d.lo[j]); O.push_back((uint32_t)d.hi[j]); }
     } else {
-        // the last plan is kept: a caller reads one rank's lists with several calls
+        // the last plan is kept (a caller reads one rank's lists with several calls),
+        // behind a lock: this context-free entry point may be called from any thread
+        static std::mutex mu;
         static std::vector<int> last_key;
         static Plan last;
+        std::lock_guard<std::mutex> lock(mu);
         const std::vector<int> key = {heaps, world, rank, d.batch, d.nslots, c.dist_symmetry, c.dist_owner};
         if (key != last_key) {
             last_key.clear();

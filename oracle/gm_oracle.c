@@ -665,3 +665,282 @@ int oracle_threads(void) {
     return 1;
 #endif
 }
+
+static uint64_t digest_term(uint64_t key, uint16_t rec) {
+    return mix(key * 0x9E3779B97F4A7C15ull + rec);   /* the gm_digest formula, include/gmsolve.h */
+}
+
+/* Digest of a dense table rec[0..n) (key = index), OpenMP.  With the dense
+ * solvers above it pins the device's full 2^32 table: gm_digest of the GPU
+ * solve must equal oracle_dense_digest(oracle_subtract_dense_mt(8)). */
+int oracle_dense_digest(const uint16_t *rec, uint64_t n, int threads, uint64_t *digest) {
+    uint64_t sum = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+#pragma omp parallel for reduction(+ : sum) schedule(static)
+    for (long long k = 0; k < (long long)n; k++) sum += digest_term((uint64_t)k, rec[k]);
+    *digest = sum;
+    return 0;
+}
+
+/* ------------------------------------------------ layered solver (OpenMP) */
+/* The same Appendix-A fixed point as oracle_solve, on a different data
+ * structure so the two check each other: per tier a SORTED array of distinct
+ * keys (parallel LSD radix sort + unique) instead of one hash map, children
+ * found by binary search in their tier's array.  Memory ~ 10 B per position plus
+ * the duplicate child keys of one tier, so Toot-and-Otto 6x4 (1.19 G positions,
+ * SURVEY App. D) fits a 64 GB host: it is the full-size oracle of config 3.
+ * Also the host-core CPU baseline of configs 3 and 4 in bench.py. */
+#define LAYER_MAXSKIP 16
+
+static int nthreads_now(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+static int thread_id(void) {
+#ifdef _OPENMP
+    return omp_get_thread_num();
+#else
+    return 0;
+#endif
+}
+
+/* stable parallel LSD radix sort of a[0..n) on its varying bits, 11-bit digits;
+ * returns the array holding the result (a or tmp) */
+static uint64_t *radix_sort(uint64_t *a, uint64_t *tmp, uint64_t n) {
+    if (n < 2) return a;
+    uint64_t vary = 0;
+    for (uint64_t i = 1; i < n; i++) vary |= a[i] ^ a[0];
+    if (!vary) return a;
+    int lo = __builtin_ctzll(vary), hi = 63 - __builtin_clzll(vary);
+    const int T = nthreads_now(), DB = 11, NB = 1 << DB;
+    uint64_t *hist = (uint64_t *)malloc((size_t)T * NB * sizeof(uint64_t));
+    if (!hist) return NULL;
+    for (int shift = lo; shift <= hi; shift += DB) {
+        memset(hist, 0, (size_t)T * NB * sizeof(uint64_t));
+#pragma omp parallel num_threads(T)
+        {
+            const int t = thread_id();
+            const uint64_t b0 = n * (uint64_t)t / T, b1 = n * (uint64_t)(t + 1) / T;
+            uint64_t *h = hist + (size_t)t * NB;
+            for (uint64_t i = b0; i < b1; i++) h[(a[i] >> shift) & (NB - 1)]++;
+#pragma omp barrier
+#pragma omp single
+            {
+                uint64_t run = 0;
+                for (int d = 0; d < NB; d++)
+                    for (int u = 0; u < T; u++) {
+                        uint64_t c = hist[(size_t)u * NB + d];
+                        hist[(size_t)u * NB + d] = run;
+                        run += c;
+                    }
+            }
+            for (uint64_t i = b0; i < b1; i++) tmp[h[(a[i] >> shift) & (NB - 1)]++] = a[i];
+        }
+        uint64_t *s = a; a = tmp; tmp = s;
+    }
+    free(hist);
+    return a;
+}
+
+typedef struct {
+    uint64_t *keys;     /* sorted distinct keys of the tier */
+    uint16_t *rec;
+    uint64_t n;
+    uint64_t *idx;      /* idx[p] = first key whose top bits (key - kmin) >> ishift >= p */
+    int ishift;
+    uint64_t kmin, np;
+} layer_t;
+
+static void layer_index(layer_t *L) {
+    L->idx = NULL;
+    if (L->n < 64) return;
+    uint64_t span = L->keys[L->n - 1] - L->keys[0];
+    int bits = 1;
+    while (((uint64_t)1 << bits) < L->n / 4 && bits < 26) bits++;
+    int top = 64 - __builtin_clzll(span | 1);
+    L->ishift = top > bits ? top - bits : 0;
+    L->kmin = L->keys[0];
+    uint64_t np = (span >> L->ishift) + 2;
+    L->np = np;
+    L->idx = (uint64_t *)malloc(np * sizeof(uint64_t));
+    if (!L->idx) return;
+    uint64_t j = 0;
+    for (uint64_t p = 0; p < np; p++) {
+        while (j < L->n && ((L->keys[j] - L->kmin) >> L->ishift) < p) j++;
+        L->idx[p] = j;
+    }
+}
+
+static int64_t layer_find(const layer_t *L, uint64_t k) {
+    uint64_t lo = 0, hi = L->n;
+    if (L->idx) {
+        if (k < L->kmin) return -1;
+        uint64_t p = (k - L->kmin) >> L->ishift;
+        if (p + 1 >= L->np) return -1;
+        lo = L->idx[p];
+        hi = L->idx[p + 1];
+    }
+    while (lo < hi) {
+        uint64_t m = (lo + hi) >> 1;
+        if (L->keys[m] < k) lo = m + 1; else hi = m;
+    }
+    return (lo < L->n && L->keys[lo] == k) ? (int64_t)lo : -1;
+}
+
+/* Strong solve from root on `threads` OpenMP threads (<= 0: all).  Outputs the
+ * number of positions, the digest of the full table, the root's record and the
+ * positions per tier (tier = descriptor potential - root's; for Toot the ply).
+ * Returns 0, or -1 with oracle_last_error(). */
+int oracle_solve_layered(int game, const int32_t *params, int nparams, uint64_t root, int threads,
+                         uint64_t *n_positions, uint64_t *digest, uint16_t *root_record,
+                         uint64_t *per_tier, int per_tier_cap, int *n_tiers) {
+    game_t g;
+    if (g_make(&g, game, params, nparams)) return -1;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+    const int T = nthreads_now();
+    const int64_t t0 = g_tier(&g, root);
+    int64_t cap = 64, maxt = 0;
+    layer_t *lay = (layer_t *)calloc(cap, sizeof(layer_t));
+    vec_t *pend = (vec_t *)calloc(cap, sizeof(vec_t));   /* children (with duplicates) waiting per tier */
+    vec_t *loc = (vec_t *)calloc((size_t)T * (LAYER_MAXSKIP + 1), sizeof(vec_t));
+    int err = 0;
+    if (!lay || !pend || !loc) { err = 1; goto done; }
+    if (vec_push(&pend[0], root)) { err = 1; goto done; }
+    /* forward: tier t's pending children -> sorted distinct keys -> their children */
+    for (int64_t t = 0; t <= maxt && !err; t++) {
+        vec_t *pv = &pend[t];
+        uint64_t *tmp = (uint64_t *)malloc((pv->n ? pv->n : 1) * sizeof(uint64_t));
+        if (!tmp) { err = 1; break; }
+        uint64_t *s = pv->n ? radix_sort(pv->v, tmp, pv->n) : tmp;
+        if (!s) { free(tmp); err = 1; break; }
+        uint64_t m = 0;
+        for (uint64_t i = 0; i < pv->n; i++)
+            if (i == 0 || s[i] != s[i - 1]) s[m++] = s[i];
+        /* keep the sorted buffer, free the other */
+        if (s == pv->v) free(tmp); else free(pv->v);
+        lay[t].keys = (uint64_t *)realloc(s, (m ? m : 1) * sizeof(uint64_t));
+        lay[t].n = m;
+        pv->v = NULL; pv->n = pv->cap = 0;
+        lay[t].rec = (uint16_t *)malloc((m ? m : 1) * sizeof(uint16_t));
+        if (!lay[t].keys || !lay[t].rec) { err = 1; break; }
+        int64_t dmax = 0;
+#pragma omp parallel num_threads(T) reduction(max : dmax)
+        {
+            const int th = thread_id();
+            uint64_t kids[MAXKIDS];
+            vec_t *mine = loc + (size_t)th * (LAYER_MAXSKIP + 1);
+#pragma omp for schedule(dynamic, 4096)
+            for (long long i = 0; i < (long long)m; i++) {
+                const uint64_t k = lay[t].keys[i];
+                const int p = g_prim(&g, k);
+                if (p == DRAW) { dmax = 1000000; continue; }
+                if (p != UNDECIDED) continue;
+                const int nk = g_kids(&g, k, kids);
+                if (nk <= 0) { dmax = 2000000; continue; }
+                for (int c = 0; c < nk; c++) {
+                    const int64_t d = g_tier(&g, kids[c]) - t0 - t;
+                    if (d < 1 || d > LAYER_MAXSKIP) { dmax = 3000000; continue; }
+                    if (d > dmax) dmax = d;
+                    if (vec_push(&mine[d], kids[c])) dmax = 4000000;
+                }
+            }
+        }
+        if (dmax >= 1000000) {
+            snprintf(g_err, sizeof g_err, "%s", dmax == 1000000 ? "DRAW primitive" : dmax == 2000000 ?
+                     "non-primitive position without moves" : dmax == 3000000 ?
+                     "tier not increasing along a move (or skip > 16)" : "out of memory");
+            err = 2;
+            break;
+        }
+        if (t + dmax >= cap) {
+            int64_t nc = cap;
+            while (t + dmax >= nc) nc *= 2;
+            layer_t *nl = (layer_t *)realloc(lay, nc * sizeof(layer_t));
+            if (nl) lay = nl;
+            vec_t *np = (vec_t *)realloc(pend, nc * sizeof(vec_t));
+            if (np) pend = np;
+            if (!nl || !np) { err = 1; break; }
+            memset(lay + cap, 0, (nc - cap) * sizeof(layer_t));
+            memset(pend + cap, 0, (nc - cap) * sizeof(vec_t));
+            cap = nc;
+        }
+        for (int64_t d = 1; d <= dmax; d++) {
+            uint64_t add = 0;
+            for (int th = 0; th < T; th++) add += loc[(size_t)th * (LAYER_MAXSKIP + 1) + d].n;
+            if (!add) continue;
+            vec_t *q = &pend[t + d];
+            uint64_t *nv = (uint64_t *)realloc(q->v, (q->n + add) * sizeof(uint64_t));
+            if (!nv) { err = 1; break; }
+            q->v = nv;
+            q->cap = q->n + add;
+            for (int th = 0; th < T; th++) {
+                vec_t *src = &loc[(size_t)th * (LAYER_MAXSKIP + 1) + d];
+                memcpy(q->v + q->n, src->v, src->n * sizeof(uint64_t));
+                q->n += src->n;
+                src->n = 0;
+            }
+            if (t + d > maxt) maxt = t + d;
+        }
+    }
+    if (err) goto done;
+    for (int64_t t = 0; t <= maxt; t++) layer_index(&lay[t]);
+    /* backward: deepest tier first */
+    for (int64_t t = maxt; t >= 0 && !err; t--) {
+        int bad = 0;
+#pragma omp parallel for num_threads(T) schedule(dynamic, 4096) reduction(| : bad)
+        for (long long i = 0; i < (long long)lay[t].n; i++) {
+            uint64_t kids[MAXKIDS];
+            const uint64_t k = lay[t].keys[i];
+            const int p = g_prim(&g, k);
+            if (p != UNDECIDED) { lay[t].rec[i] = (uint16_t)(p << 14); continue; }
+            const int nk = g_kids(&g, k, kids);
+            uint32_t best = 0;
+            for (int c = 0; c < nk; c++) {
+                const int64_t tc = g_tier(&g, kids[c]) - t0;
+                const int64_t j = layer_find(&lay[tc], kids[c]);
+                if (j < 0) { bad = 1; continue; }
+                const uint32_t sc = pref(lay[tc].rec[j]);
+                if (sc > best) best = sc;
+            }
+            lay[t].rec[i] = from_pref(best);
+        }
+        if (bad) { snprintf(g_err, sizeof g_err, "child missing from its tier"); err = 2; }
+    }
+    if (err) goto done;
+    {
+        uint64_t n = 0, dsum = 0;
+        for (int64_t t = 0; t <= maxt; t++) {
+            uint64_t s = 0;
+#pragma omp parallel for num_threads(T) reduction(+ : s) schedule(static)
+            for (long long i = 0; i < (long long)lay[t].n; i++) s += digest_term(lay[t].keys[i], lay[t].rec[i]);
+            dsum += s;
+            n += lay[t].n;
+            if (per_tier && t < per_tier_cap) per_tier[t] = lay[t].n;
+        }
+        *n_positions = n;
+        *digest = dsum;
+        *root_record = lay[0].rec[0];
+        if (n_tiers) *n_tiers = (int)(maxt + 1);
+    }
+done:
+    if (err == 1) snprintf(g_err, sizeof g_err, "out of memory");
+    if (lay)
+        for (int64_t t = 0; t < cap; t++) { free(lay[t].keys); free(lay[t].rec); free(lay[t].idx); }
+    if (pend)
+        for (int64_t t = 0; t < cap; t++) free(pend[t].v);
+    if (loc)
+        for (int i = 0; i < T * (LAYER_MAXSKIP + 1); i++) free(loc[i].v);
+    free(lay); free(pend); free(loc);
+    return err ? -1 : 0;
+}

@@ -55,6 +55,10 @@ class Oracle:
                                     P(ctypes.c_uint64), P(ctypes.c_int), P(ctypes.c_int), P(ctypes.c_int64)]
         L.oracle_subtract_dense.argtypes = [ctypes.c_int, ctypes.c_void_p]
         L.oracle_subtract_dense_mt.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_dense_digest.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, P(ctypes.c_uint64)]
+        L.oracle_solve_layered.argtypes = [ctypes.c_int, P(ctypes.c_int32), ctypes.c_int, ctypes.c_uint64,
+                                           ctypes.c_int, P(ctypes.c_uint64), P(ctypes.c_uint64),
+                                           P(ctypes.c_uint16), P(ctypes.c_uint64), ctypes.c_int, P(ctypes.c_int)]
         L.oracle_last_error.restype = ctypes.c_char_p
         L.oracle_free.argtypes = [ctypes.c_void_p]
         self.L = L
@@ -100,6 +104,26 @@ class Oracle:
         out = np.empty(1 << (4 * heaps), dtype=np.uint16)
         assert self.L.oracle_subtract_dense_mt(heaps, out.ctypes.data, threads) == 0
         return out
+
+    def dense_digest(self, recs, threads=0):
+        """gm_digest of a dense table (key = index), computed by the oracle library."""
+        d = ctypes.c_uint64()
+        recs = np.ascontiguousarray(recs, dtype=np.uint16)
+        assert self.L.oracle_dense_digest(recs.ctypes.data, ctypes.c_uint64(len(recs)), threads,
+                                          ctypes.byref(d)) == 0
+        return d.value
+
+    def solve_layered(self, game, params=(), root=None, threads=0):
+        """Sorted-layer OpenMP solver: (positions, digest, root record, per-tier counts)."""
+        p, n = self._params(params)
+        if root is None:
+            root = self.initial(game, params)
+        npos, dg, rr, nt = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint16(), ctypes.c_int()
+        tiers = (ctypes.c_uint64 * 4096)()
+        if self.L.oracle_solve_layered(game, p, n, ctypes.c_uint64(root), threads, ctypes.byref(npos),
+                                       ctypes.byref(dg), ctypes.byref(rr), tiers, 4096, ctypes.byref(nt)) != 0:
+            raise RuntimeError(self.L.oracle_last_error().decode())
+        return npos.value, dg.value, rr.value, [int(x) for x in tiers[:nt.value]]
 
 
 @pytest.fixture(scope="session")

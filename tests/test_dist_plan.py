@@ -214,3 +214,47 @@ def test_gloo_ranks_exchange_halos(world, batch, slots, symmetry, owner):
     assert all(r["own_ok"] and r["held_ok"] for r in res), res
     assert sum(r["own_blocks"] for r in res) == 1 << 12
     assert any(r["halo_blocks"] > 0 for r in res)
+
+
+OP_TIER, OP_SEND, OP_RECORD, OP_WAIT = 0, 3, 5, 6
+EV_XCH = 1
+
+
+@pytest.mark.parametrize("owner,heaps,world", [(0, 6, 2), (0, 7, 4), (0, 8, 8), (1, 6, 2), (1, 7, 4), (1, 8, 8)])
+def test_ring_slot_waits_name_the_last_nonempty_message(owner, heaps, world):
+    """GM_PLAN_OPS at ONE ring slot: before the tier that starts writing halo message jj
+    into its slot, the compute stream waits for the exchange of the slot's previous
+    NON-EMPTY message (empty messages record nothing), and every such wait names a
+    message whose exchange was recorded earlier.  Covers owner 0 and 1."""
+    for batch in (1, 3):
+        shape_off, shape = _lib.dist_plan(heaps, world, 0, _lib.PLAN_SHAPE, batch=batch, slots=1, owner=owner)
+        g, nslots = int(shape[6]), int(shape[5])
+        assert nslots == 1
+        lo = shape_off[0::2].astype(int)
+        for r in range(world):
+            _, ops = _lib.dist_plan(heaps, world, r, _lib.PLAN_OPS, batch=batch, slots=1, owner=owner)
+            ops = ops.reshape(-1, 6).astype(int)
+            for a in range(g):
+                if (r >> a) & 1:
+                    continue   # upper side of axis a: receives only
+                soff, _ = _lib.dist_plan(heaps, world, r, _lib.PLAN_SEND, axis=a, batch=batch, slots=1, owner=owner)
+                nonempty = [j for j in range(len(soff) - 1) if soff[j + 1] > soff[j]]
+                recorded = {}
+                waits = []
+                first_tier = {}
+                for i, (kind, ax, ev, onx, arg, peer) in enumerate(ops):
+                    if kind == OP_RECORD and ev == EV_XCH and ax == a and onx == 1:
+                        recorded[arg] = i
+                    if kind == OP_WAIT and ev == EV_XCH and ax == a and onx == 0:
+                        waits.append((i, arg))
+                    if kind == OP_TIER and arg not in first_tier:
+                        first_tier[arg] = i
+                for i, jp in waits:
+                    assert jp in nonempty, "wait on an empty message %d" % jp
+                    assert jp in recorded and recorded[jp] < i, "wait on message %d before its exchange" % jp
+                # every non-empty message after the first must wait for its predecessor
+                for prev, jj in zip(nonempty, nonempty[1:]):
+                    t0 = lo[jj]
+                    assert any(jp == prev and i < first_tier[t0] for i, jp in waits), \
+                        "rank %d axis %d: message %d does not wait for %d" % (r, a, jj, prev)
+                assert len(waits) == max(0, len(nonempty) - 1)

@@ -171,6 +171,23 @@ def test_subtract_full_2_32_properties():
     assert rec >> 14 == 1               # all heaps 15: xor of (15 mod 3) = 0 -> LOSS
 
 
+def test_subtract_8_heaps_full_table_vs_oracle(oracle):
+    """Config 5 at FULL size: the 2^32 table of the headline kernel instance
+    (sub_tier_kernel_b4<5>) equals the C oracle's, through the order-independent
+    digest of every (key, record) -- against the committed oracle digest
+    (tests/golden/make_oracle_digests.py) and a live oracle solve on the host.
+    Semantics: reference src/new_process.py:189-198, 249-250."""
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["subtract_8"]
+    ctx, n, rec = _solve(SUB, (8,))
+    got = ctx.digest()
+    assert (n, rec) == (ref["positions"], ref["root_record"])
+    assert got == (ref["digest"], ref["positions"])
+    ctx.close()
+    live = oracle.subtract_dense_mt(8)
+    assert oracle.dense_digest(live) == got[0]
+    assert int(live[-1]) == rec
+
+
 def test_subtract_7_heaps_vs_oracle_digest(oracle):
     ref = oracle.subtract_dense(7)
     ctx, n, rec = _solve(SUB, (7,))
@@ -205,11 +222,13 @@ def test_toot_6x4_known_per_ply_counts():
     assert [int(x) for x in ctx.tier_counts()] == app_d
 
 
-@pytest.mark.parametrize("board", ["toot_4x4", "toot_5x4"])
+@pytest.mark.parametrize("board", ["toot_4x4", "toot_5x4", "toot_6x4"])
 @pytest.mark.parametrize("ranks", [1, 8])
 def test_toot_large_boards_vs_oracle_digest(board, ranks):
-    """Toot 4x4 / 5x4 (3.5 M / 70 M positions): per-ply counts, root record and the
-    full-table digest equal the C oracle's (tests/golden/make_oracle_digests.py)."""
+    """Toot 4x4 / 5x4 / 6x4 (3.5 M / 70 M / 1.19 G positions; 6x4 is config 3):
+    per-ply counts, root record and the full-table digest equal the C oracle's
+    (tests/golden/make_oracle_digests.py), on one GPU and hash-sharded over 8
+    loopback ranks.  Rules: reference test_games/toot_and_otto_bitstring.py:46-115."""
     ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))[board]
     L, H = (int(v) for v in board.split("_")[1].split("x"))
     ctx = Context(TOOT, (L, H), device=0)

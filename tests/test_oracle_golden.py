@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import canonical
-from conftest import GOLDEN, golden, load_plugin
+from conftest import GOLDEN, digest, golden, load_plugin
 
 F2O, TTT, TOOT, OTH, SUB = 1, 2, 3, 4, 5
 
@@ -158,3 +158,54 @@ def test_toot_4x4_oracle_totals(oracle):
     k, r = oracle.solve(TOOT, (4, 4))
     assert len(k) == 3468773
     assert (r != 0xFFFF).all()
+
+
+# ---- the sorted-layer OpenMP oracle (oracle_solve_layered): the full-size checker
+# of configs 3 and 4 and the bench's CPU baseline for them.  Pinned here to the
+# same golden tables (digest equality) and to the hash-map oracle.
+
+@pytest.mark.parametrize("name,game,params,root", CASES)
+def test_layered_oracle_matches_golden(oracle, name, game, params, root):
+    keys, recs = golden(name)
+    n, dg, rr, tiers = oracle.solve_layered(game, params, root)
+    assert n == len(keys) and sum(tiers) == n
+    assert dg == digest(keys, recs)
+    root_key = oracle.initial(game, params) if root is None else root
+    assert rr == int(recs[np.searchsorted(keys, np.uint64(root_key & (2 ** 64 - 1)))])
+
+
+@pytest.mark.parametrize("threads", [1, 3, 0])
+def test_layered_oracle_toot_4x4_equals_hash_oracle(oracle, threads):
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["toot_4x4"]
+    n, dg, rr, tiers = oracle.solve_layered(TOOT, (4, 4), threads=threads)
+    assert (n, dg, rr, tiers) == (ref["positions"], ref["digest"], ref["root_record"], ref["per_ply"])
+
+
+def test_layered_oracle_subtract_equals_dense(oracle):
+    for heaps in (2, 3, 4):
+        n, dg, rr, tiers = oracle.solve_layered(SUB, (heaps,))
+        dense = oracle.subtract_dense(heaps)
+        assert n == 16 ** heaps and dg == oracle.dense_digest(dense)
+        assert dg == digest(np.arange(16 ** heaps, dtype=np.uint64), dense)
+        assert rr == int(dense[-1])
+
+
+def test_full_size_oracle_digests_committed():
+    """tests/golden/oracle_digests.json holds the full-size oracle tables of configs 3-5
+    (tests/golden/make_oracle_digests.py); its Toot 6x4 per-ply counts are SURVEY App. D."""
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))
+    app_d = [1, 12, 114, 748, 4266, 19692, 81140, 285708, 928196, 2665424, 7098172, 17010952,
+             37792450, 64636776, 100084356, 136321692, 169785424, 180777508, 172831136,
+             135153280, 91440950, 45953432, 19196602, 4537828, 606968]
+    assert ref["toot_6x4"]["per_ply"] == app_d and ref["toot_6x4"]["positions"] == sum(app_d) == 1187212827
+    assert ref["subtract_8"]["positions"] == 1 << 32
+    assert ref["subtract_8"]["root_record"] == (1 << 14) | 80        # LOSS in 80 (all heaps 15)
+    keys, recs = golden("othello_4x4")
+    assert ref["othello_4x4"]["digest"] == digest(keys, recs)
+    assert ref["othello_4x4"]["root_record"] == (1 << 14) | 12       # LOSS in 12
+
+
+def test_dense_digest_matches_python_formula(oracle):
+    rng = np.random.default_rng(3)
+    recs = rng.integers(0, 1 << 16, size=100003, dtype=np.uint16)
+    assert oracle.dense_digest(recs) == digest(np.arange(len(recs), dtype=np.uint64), recs)
