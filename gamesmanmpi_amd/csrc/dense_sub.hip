@@ -363,6 +363,10 @@ __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ 
     __amdgpu_buffer_rsrc_t wr[K];
 #pragma unroll
     for (int k = 0; k < K; k++) wr[k] = block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0);
+#if defined(GM_EXP) && (GM_EXP & 4)
+#pragma unroll
+    for (int k = 0; k < K; k++) wr[k] = block_rsrc(table, 0);   // experiment: stores dropped (out of range)
+#endif
     {
         const uint32_t c = tid;
         u32x4v out[K];   // 16 codes of chunk c per block
@@ -396,12 +400,21 @@ __global__ __launch_bounds__(256) void sub_tier_kernel_x4(uint8_t *__restrict__ 
 __device__ __forceinline__ uint32_t code_x4(uint32_t b) {   // parent_code on four bytes
     return ~b + ((b >> 6) & 0x02020202u);
 }
+// parent codes of split halves: E holds codes in the low byte of each u16, O in the high byte
+__device__ __forceinline__ uint32_t code_lo2(uint32_t e) { return (0x00FF00FFu - e) + ((e >> 6) & 0x00020002u); }
+__device__ __forceinline__ uint32_t code_hi2(uint32_t o) { return (0xFF00FF00u - o) + ((o >> 6) & 0x02000200u); }
 
+#ifndef GM_PASSB_PRIO
+#define GM_PASSB_PRIO 0   // s_setprio of pass B (0 = off)
+#endif
 #ifndef GM_PASSB_REG
 #define GM_PASSB_REG 1   // pass B children (a0-1, a0-2) by DPP and (c-1, c-2) from registers
 #endif
 #ifndef GM_B4_WAVES
 #define GM_B4_WAVES 1
+#endif
+#ifndef GM_B4_STORE_CPOL
+#define GM_B4_STORE_CPOL 0   // 16 = sc1: write-through, the stored block does not stay in L2
 #endif
 // One workgroup solves the four blocks hp[0..3] (valid[k] false: slot unused).
 // CPOL = cache policy of the child loads and the stores (0 plain; CPOL_SC1 in the
@@ -453,6 +466,9 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
     __syncthreads();
 
     // ---- pass B (see sub_tier_kernel_x4): thread (a0, a1), position c = tau - a0 - a1
+#if GM_PASSB_PRIO
+    __builtin_amdgcn_s_setprio(GM_PASSB_PRIO);   // the barrier chain before other workgroups' folds
+#endif
     const int a0 = tid & 15, a1 = tid >> 4, s0 = a0 + a1;
     const uint32_t d01 = a0 >= 1 ? 1u : 0u, d02 = a0 >= 2 ? 2u : 0u;
     const uint32_t d11 = a1 >= 1 ? 16u : 0u, d12 = a1 >= 2 ? 32u : 0u;
@@ -461,6 +477,44 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
 #else
     constexpr int TAU_END = 45;
 #endif
+#if GM_PASSB_REG == 2
+    // As below, with the codes split while they live in registers (w1_solve): E =
+    // bytes 0, 2 in the low byte of each u16 half, O = bytes 1, 3 in the high byte;
+    // an inactive lane records 0, so (c-1, c-2) need no validity select.
+    uint32_t pe1 = 0, po1 = 0, pe2 = 0, po2 = 0;
+    if (tid == 0) {
+        const uint32_t v = s[0];
+        uint32_t re = code_lo2(v & 0x00FF00FFu), ro = code_hi2(v & 0xFF00FF00u);
+        if (valid[0] && hp[0] == 0) re = (re & 0xFFFFFF00u) | 255u;   // all heaps empty: LOSS in 0
+        s[0] = re | ro;
+        pe1 = re;
+        po1 = ro;
+    }
+    __syncthreads();
+    for (int tau = 1; tau <= TAU_END; tau++) {
+        const uint32_t n1e = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pe1, 0x111, 0xF, 0xF, true);
+        const uint32_t n1o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)po1, 0x111, 0xF, 0xF, true);
+        const uint32_t n2e = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pe2, 0x112, 0xF, 0xF, true);
+        const uint32_t n2o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)po2, 0x112, 0xF, 0xF, true);
+        const int c = tau - s0;
+        uint32_t re = 0, ro = 0;
+        if (c >= 0 && c <= 15) {
+            const uint32_t o = (uint32_t)(tid + 256 * c);
+            const uint32_t v0 = s[o], v3 = s[o - d11], v4 = s[o - d12];
+            const uint32_t me = pk_max(pk_max(pk_max(v0 & 0x00FF00FFu, v3 & 0x00FF00FFu), pk_max(v4 & 0x00FF00FFu, n1e)),
+                                       pk_max(pk_max(n2e, pe1), pe2));
+            const uint32_t mo = pk_max(pk_max(pk_max(v0, v3), pk_max(v4, n1o)), pk_max(pk_max(n2o, po1), po2));
+            re = code_lo2(me);
+            ro = code_hi2(mo & 0xFF00FF00u);
+            s[o] = re | ro;
+        }
+        pe2 = pe1;
+        po2 = po1;
+        pe1 = re;
+        po1 = ro;
+        __syncthreads();
+    }
+#else
     uint32_t p1 = 0, p2 = 0;   // this thread's codes of the last two steps: (a0, a1, c-1), (a0, a1, c-2)
     if (tid == 0) {
         uint32_t r = code_x4(s[0]);
@@ -469,7 +523,9 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
         p1 = r;
     }
     __syncthreads();
-#if GM_PASSB_REG
+#endif
+#if GM_PASSB_REG == 2
+#elif GM_PASSB_REG
     // Children inside the block, by where they live: (a0-1 | a0-2, a1, c) are the codes
     // lanes tid-1 / tid-2 (same 16-lane DPP row) produced one / two steps ago, moved
     // with row_shr (an invalid child reads 0, which max ignores: every position but
@@ -515,9 +571,16 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
 #endif
 
     // ---- pass C: back to four 16-byte rows per chunk
+#if GM_PASSB_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     __amdgpu_buffer_rsrc_t wr[K];
 #pragma unroll
     for (int k = 0; k < K; k++) wr[k] = block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0);
+#if defined(GM_EXP) && (GM_EXP & 4)
+#pragma unroll
+    for (int k = 0; k < K; k++) wr[k] = block_rsrc(table, 0);   // experiment: stores dropped (out of range)
+#endif
     {
         const uint32_t c = tid;
         u32x4v out[K];
@@ -562,7 +625,7 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *
         valid[k] = idx < nblk;
         hp[k] = valid[k] ? blocks[idx] : 0u;
     }
-    b4_solve<HIGH, 0>(table, zero, hp, valid, s);
+    b4_solve<HIGH, GM_B4_STORE_CPOL, 0>(table, zero, hp, valid, s);
 }
 
 // The sharded solve's tier kernel (csrc/dist_sub.hip): as above, plus each block's
@@ -585,6 +648,247 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
         hp[k] = valid[k] ? blocks[idx] : 0u;
     }
     b4_solve<HIGH, 0, 0, true>(table, zero, hp, valid, s, xoff, xdst, grp * K);
+}
+
+// ---------------------------------------------------------------------------
+// One-wave variant (GM_OPT_SUB_INTERLEAVE 8): a 64-lane workgroup solves four
+// blocks in the byte image of the b4 kernel (16 KiB of LDS) with NO workgroup
+// barrier.  Measured on the b4 kernel (tools/gpu_call_ablation.sh): its pass B
+// alone took 3.2 ms of the 5.4 ms solve, a chain of 46 barrier-separated steps
+// in which the four waves wait for the slowest; pass A + C alone took 4.2 ms.
+// Here one wave owns the whole 4-block group:
+//   * pass A: lane l folds chunks l, l+64, l+128, l+192 (16 positions each) of
+//     the four blocks' <= 2*HIGH child blocks -- one buffer descriptor over the
+//     whole table, each child a scalar offset;
+//   * pass B: the 16 x 16 (a0, a1) columns are four "slots" of four 16-lane DPP
+//     rows (a1 = 4j .. 4j+3); at low tier tau slot j works iff tau in
+//     [4j, 4j+33], every slot's children are from tiers tau-1 and tau-2, so the
+//     slots of one step are independent and the step needs no barrier: LDS ops
+//     of one wave execute in order (a wavefront-scope fence keeps the compiler
+//     from reordering them across steps);
+//   * codes stay split while they live in registers: E = bytes 0 and 2 (blocks
+//     0, 2) in the low byte of each u16 half, O = bytes 1 and 3 in the high
+//     byte, so a bytewise max is one v_pk_max_u16 per half-set and the packed
+//     code for LDS is E | O.  An inactive lane records 0, so a column's
+//     (c-1, c-2) children and the DPP neighbours need no validity select.
+// 10 workgroups per CU (LDS-bound), each independent.
+#ifndef GM_W1_WAVES
+#define GM_W1_WAVES 3
+#endif
+#ifndef GM_W1_STORE_CPOL
+#define GM_W1_STORE_CPOL 0
+#endif
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int HIGH, bool XD>
+__device__ __forceinline__ void w1_solve(uint8_t *__restrict__ table, const uint32_t (&hp)[4], const bool (&valid)[4],
+                                         uint32_t *s, const uint32_t *__restrict__ xoff,
+                                         const uint64_t *__restrict__ xdst, uint32_t idx0) {
+    constexpr int NPOS = 4096, K = 4;
+    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
+    const uint32_t lane = threadIdx.x;
+
+    // ---- pass A
+    {
+        // whole-table descriptor (offsets < 2^32; the last table byte is never a
+        // child), and a zero-size one for a block without high children (reads 0)
+        const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(table, 0, 0xFFFFFFFFu, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(table, 0, 0, 0x00020000);
+        uint32_t soff[K][NMAX];
+        bool has[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            uint32_t first = 0;
+            bool any = false;
+#pragma unroll
+            for (int j = HIGH - 1; j >= 0; j--)
+                if (valid[k] && ((hp[k] >> (4 * j)) & 15u) >= 1) { first = (hp[k] - (1u << (4 * j))) << 12; any = true; }
+#pragma unroll
+            for (int j = 0; j < HIGH; j++) {
+                const uint32_t h = (hp[k] >> (4 * j)) & 15u;
+                soff[k][2 * j] = (valid[k] && h >= 1) ? (hp[k] - (1u << (4 * j))) << 12 : first;
+                soff[k][2 * j + 1] = (valid[k] && h >= 2) ? (hp[k] - (2u << (4 * j))) << 12 : first;
+            }
+            if constexpr (HIGH == 0) soff[k][0] = 0;
+            has[k] = any;
+        }
+        // 16 rounds (chunk i, block k) of NMAX loads; round n+1's loads are issued
+        // before round n is folded, so two rounds are in flight per lane
+        u32x4v vb[2][NMAX];
+        auto issue = [&](int n, u32x4v (&v)[NMAX]) {
+            const int i = n >> 2, k = n & 3;
+            const __amdgpu_buffer_rsrc_t r = has[k] ? rt : rz;
+#pragma unroll
+            for (int m = 0; m < NMAX; m++)
+                v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * (lane + 64u * i),
+                                                                                         soff[k][m], 0));
+        };
+        issue(0, vb[0]);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t c = lane + 64u * i;   // chunk: positions 16c .. 16c+15
+            uint32_t e[K][4], o[K][4];
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int n = 4 * i + k;
+                if (n + 1 < 16) issue(n + 1, vb[(n + 1) & 1]);
+                const u32x4v(&v)[NMAX] = vb[n & 1];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    uint32_t ev = v[0][j] & 0x00FF00FFu, ov = v[0][j];   // ov: odd bytes valid in the high byte
+#pragma unroll
+                    for (int m = 1; m < NMAX; m++) {
+                        ev = pk_max(ev, v[m][j] & 0x00FF00FFu);
+                        ov = pk_max(ov, v[m][j]);
+                    }
+                    e[k][j] = ev;
+                    o[k][j] = ov;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {   // positions 4j .. 4j+3 -> one dword each (bytes = blocks 0..3)
+                const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);
+                const uint32_t ye = __builtin_amdgcn_perm(e[3][j], e[2][j], 0x06020400u);
+                const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);
+                const uint32_t yo = __builtin_amdgcn_perm(o[3][j], o[2][j], 0x07030501u);
+                u32x4v q;
+                q[0] = __builtin_amdgcn_perm(ye, xe, 0x05040100u);   // 4j
+                q[1] = __builtin_amdgcn_perm(yo, xo, 0x05040100u);   // 4j+1
+                q[2] = __builtin_amdgcn_perm(ye, xe, 0x07060302u);   // 4j+2
+                q[3] = __builtin_amdgcn_perm(yo, xo, 0x07060302u);   // 4j+3
+                *(u32x4v *)(s + 16 * c + 4 * j) = q;
+            }
+        }
+    }
+    wave_fence();
+
+    // ---- pass B: lane = a0 + 16 r; slot j holds a1 = 4j + r
+    const int a0 = (int)(lane & 15u), r0 = (int)(lane >> 4);
+#if defined(GM_EXP) && (GM_EXP & 1)
+    constexpr int TAU_END = 0;
+#else
+    constexpr int TAU_END = 45;
+#endif
+    uint32_t pe1[4] = {0, 0, 0, 0}, po1[4] = {0, 0, 0, 0}, pe2[4] = {0, 0, 0, 0}, po2[4] = {0, 0, 0, 0};
+    if (lane == 0) {   // position 0 (tau 0) of slot 0
+        const uint32_t v = s[0];
+        uint32_t re = code_lo2(v & 0x00FF00FFu), ro = code_hi2(v & 0xFF00FF00u);
+        if (valid[0] && hp[0] == 0) re = (re & 0xFFFFFF00u) | 255u;   // all heaps empty: LOSS in 0
+        s[0] = re | ro;
+        pe1[0] = re;
+        po1[0] = ro;
+    }
+    wave_fence();
+    for (int tau = 1; tau <= TAU_END; tau++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (tau < 4 * j || tau > 4 * j + 33) continue;   // wave-uniform: no column of the slot is on this tier
+            const int a1 = 4 * j + r0, cc = tau - a0 - a1;
+            // (a0-1 | a0-2, a1, c): lanes -1 / -2 of the row one / two steps ago (0 past the row start)
+            const uint32_t n1e = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pe1[j], 0x111, 0xF, 0xF, true);
+            const uint32_t n1o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)po1[j], 0x111, 0xF, 0xF, true);
+            const uint32_t n2e = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pe2[j], 0x112, 0xF, 0xF, true);
+            const uint32_t n2o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)po2[j], 0x112, 0xF, 0xF, true);
+            uint32_t re = 0, ro = 0;
+            if (cc >= 0 && cc <= 15) {
+                const uint32_t o = lane + 64u * (uint32_t)j + 256u * (uint32_t)cc;   // = a0 + 16 a1 + 256 c
+                const uint32_t d1 = a1 >= 1 ? 16u : 0u, d2 = a1 >= 2 ? 32u : 0u;
+                const uint32_t v0 = s[o], v3 = s[o - d1], v4 = s[o - d2];
+                const uint32_t me = pk_max(pk_max(pk_max(v0 & 0x00FF00FFu, v3 & 0x00FF00FFu),
+                                                  pk_max(v4 & 0x00FF00FFu, n1e)),
+                                           pk_max(pk_max(n2e, pe1[j]), pe2[j]));
+                const uint32_t mo = pk_max(pk_max(pk_max(v0, v3), pk_max(v4, n1o)), pk_max(pk_max(n2o, po1[j]), po2[j]));
+                re = code_lo2(me);
+                ro = code_hi2(mo & 0xFF00FF00u);
+                s[o] = re | ro;
+            }
+            pe2[j] = pe1[j];
+            po2[j] = po1[j];
+            pe1[j] = re;
+            po1[j] = ro;
+        }
+        wave_fence();
+    }
+
+    // ---- pass C
+    __amdgpu_buffer_rsrc_t wr[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) wr[k] = block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0);
+#if defined(GM_EXP) && (GM_EXP & 4)
+#pragma unroll
+    for (int k = 0; k < K; k++) wr[k] = block_rsrc(table, 0);   // experiment: stores dropped (out of range)
+#endif
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t c = lane + 64u * i;
+        u32x4v out[K];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const u32x4v q = *(const u32x4v *)(s + 16 * c + 4 * j);
+            const uint32_t t01 = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u);
+            const uint32_t t23 = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u);
+            const uint32_t u01 = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);
+            const uint32_t u23 = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
+            out[0][j] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+            out[1][j] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+            out[2][j] = __builtin_amdgcn_perm(u23, u01, 0x05040100u);
+            out[3][j] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++)
+            __builtin_amdgcn_raw_buffer_store_b128(out[k], wr[k], 16u * c, 0, GM_W1_STORE_CPOL);
+        if constexpr (XD) {
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                if (!valid[k]) continue;
+                const uint32_t m1 = xoff[idx0 + k + 1];
+                for (uint32_t m = xoff[idx0 + k]; m < m1; m++)
+                    __builtin_amdgcn_raw_buffer_store_b128(out[k], block_rsrc((uint8_t *)xdst[m], NPOS), 16u * c, 0, 0);
+            }
+        }
+    }
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(64, GM_W1_WAVES) void sub_tier_kernel_w1(uint8_t *__restrict__ table,
+                                                        const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                        const uint8_t *__restrict__ zero) {
+    constexpr int K = 4;
+    __shared__ __attribute__((aligned(16))) uint32_t s[4096];   // 16 KiB
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
+    uint32_t hp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = grp * K + k;
+        valid[k] = idx < nblk;
+        hp[k] = valid[k] ? __builtin_amdgcn_readfirstlane(blocks[idx]) : 0u;
+    }
+    w1_solve<HIGH, false>(table, hp, valid, s, nullptr, nullptr, 0);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(64, GM_W1_WAVES) void sub_tier_kernel_w1x(uint8_t *__restrict__ table,
+                                                         const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                         const uint8_t *__restrict__ zero,
+                                                         const uint32_t *__restrict__ xoff,
+                                                         const uint64_t *__restrict__ xdst) {
+    constexpr int K = 4;
+    __shared__ __attribute__((aligned(16))) uint32_t s[4096];   // 16 KiB
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
+    uint32_t hp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = grp * K + k;
+        valid[k] = idx < nblk;
+        hp[k] = valid[k] ? __builtin_amdgcn_readfirstlane(blocks[idx]) : 0u;
+    }
+    w1_solve<HIGH, true>(table, hp, valid, s, xoff, xdst, grp * K);
 }
 
 // ---------------------------------------------------------------------------
@@ -717,6 +1021,18 @@ static tier_kernel_t pick_b4(int high) {
     return nullptr;
 }
 
+static tier_kernel_t pick_w1(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel_w1<0>;
+    case 1: return sub_tier_kernel_w1<1>;
+    case 2: return sub_tier_kernel_w1<2>;
+    case 3: return sub_tier_kernel_w1<3>;
+    case 4: return sub_tier_kernel_w1<4>;
+    case 5: return sub_tier_kernel_w1<5>;
+    }
+    return nullptr;
+}
+
 static tier_kernel_t pick_x4(int high, bool diag) {
     switch (high) {
     case 0: return diag ? sub_tier_kernel_x4<0, true> : sub_tier_kernel_x4<0, false>;
@@ -764,8 +1080,10 @@ static tier_kernel_t pick_kernel(int low, int high, int nt) {
 }
 
 // nt == 0 / -1 / -2 select the 4-block interleaved kernels (LOW = 3, 256 threads):
-// u16 image with row-major / anti-diagonal pass B, byte image.
+// u16 image with row-major / anti-diagonal pass B, byte image; nt == -4 the
+// one-wave byte-image kernel (64 threads).
 static tier_kernel_t pick_interleaved(int high, int nt) {
+    if (nt == -4) return pick_w1(high);
     return nt == -2 ? pick_b4(high) : pick_x4(high, nt == -1);
 }
 
@@ -778,8 +1096,8 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
                      const uint8_t *zero, hipStream_t s) {
     if (!nblocks) return;
     if (nt <= 0)
-        hipLaunchKernelGGL(pick_interleaved(high, nt), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks,
-                           zero);
+        hipLaunchKernelGGL(pick_interleaved(high, nt), dim3((nblocks + 3) / 4), dim3(nt == -4 ? 64 : 256), 0, s, table,
+                           list, nblocks, zero);
     else
         hipLaunchKernelGGL(pick_kernel(low, high, nt), dim3(nblocks), dim3(nt), 0, s, table, list, nblocks, zero);
 }
@@ -797,13 +1115,24 @@ static tier_kernel_x_t pick_b4x(int high) {
     return nullptr;
 }
 
-bool sub_kernel_x_exists(int high) { return pick_b4x(high) != nullptr; }
+static tier_kernel_x_t pick_w1x(int high) {
+    switch (high) {
+    case 1: return sub_tier_kernel_w1x<1>;
+    case 2: return sub_tier_kernel_w1x<2>;
+    case 3: return sub_tier_kernel_w1x<3>;
+    case 4: return sub_tier_kernel_w1x<4>;
+    case 5: return sub_tier_kernel_w1x<5>;
+    }
+    return nullptr;
+}
+
+bool sub_kernel_x_exists(int high) { return pick_b4x(high) != nullptr && pick_w1x(high) != nullptr; }
 
 void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
-                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s) {
+                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, bool wave) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(pick_b4x(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero, xoff,
-                       xdst);
+    hipLaunchKernelGGL(wave ? pick_w1x(high) : pick_b4x(high), dim3((nblocks + 3) / 4), dim3(wave ? 64 : 256), 0, s,
+                       table, list, nblocks, zero, xoff, xdst);
 }
 
 int sub_kernel_threads(const Ctx *c, int low) {
@@ -811,6 +1140,7 @@ int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 5) return -1;
     if (low == 3 && c->sub_interleave == 6) return -2;
     if (low == 3 && c->sub_interleave == 7) return -3;
+    if (low == 3 && c->sub_interleave == 8) return -4;
     return c->sub_threads;
 }
 
@@ -854,10 +1184,39 @@ static uint32_t morton_of(uint32_t v, int high) {
     return m;
 }
 
-void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &off, int high) {
-    for (size_t t = 0; t + 1 < off.size(); t++)
-        std::sort(order.begin() + off[t], order.begin() + off[t + 1],
-                  [high](uint32_t a, uint32_t b) { return morton_of(a, high) < morton_of(b, high); });
+// Hilbert index (Skilling's transpose form) of the first n = high - 1 nibbles: a
+// tier's blocks have high - 1 free coordinates (the last nibble is fixed by the
+// sum), and a Hilbert walk of them keeps consecutive blocks adjacent (order 2).
+static uint64_t hilbert_of(uint32_t v, int high) {
+    const int n = std::max(1, high - 1);
+    uint32_t x[8];
+    for (int i = 0; i < n; i++) x[i] = (v >> (4 * i)) & 15u;
+    for (uint32_t q = 8; q > 1; q >>= 1) {
+        const uint32_t p = q - 1;
+        for (int i = 0; i < n; i++) {
+            if (x[i] & q) x[0] ^= p;
+            else { const uint32_t t = (x[0] ^ x[i]) & p; x[0] ^= t; x[i] ^= t; }
+        }
+    }
+    for (int i = 1; i < n; i++) x[i] ^= x[i - 1];
+    uint32_t t = 0;
+    for (uint32_t q = 8; q > 1; q >>= 1) if (x[n - 1] & q) t ^= q - 1;
+    for (int i = 0; i < n; i++) x[i] ^= t;
+    uint64_t h = 0;
+    for (int b = 3; b >= 0; b--)
+        for (int i = 0; i < n; i++) h = (h << 1) | ((x[i] >> b) & 1u);
+    return h;
+}
+
+void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &off, int high, int mode) {
+    for (size_t t = 0; t + 1 < off.size(); t++) {
+        if (mode == 2)
+            std::sort(order.begin() + off[t], order.begin() + off[t + 1],
+                      [high](uint32_t a, uint32_t b) { return hilbert_of(a, high) < hilbert_of(b, high); });
+        else
+            std::sort(order.begin() + off[t], order.begin() + off[t + 1],
+                      [high](uint32_t a, uint32_t b) { return morton_of(a, high) < morton_of(b, high); });
+    }
 }
 
 static int prepare(Ctx *c, DenseSub *d) {
@@ -883,7 +1242,7 @@ static int prepare(Ctx *c, DenseSub *d) {
     d->tier_off.assign(cnt.begin(), cnt.end());
     std::vector<uint32_t> pos(cnt.begin(), cnt.end() - 1);
     for (uint64_t v = 0; v < nhigh; v++) order[pos[tsum(v)]++] = (uint32_t)v;
-    if (c->sub_order == 1) sort_tiers_morton(order, d->tier_off, high);
+    if (c->sub_order >= 1) sort_tiers_morton(order, d->tier_off, high, c->sub_order);
     GM_HIP(hipMalloc(&d->d_blocks, nhigh * sizeof(uint32_t)));
     GM_HIP(hipMemcpy(d->d_blocks, order.data(), nhigh * sizeof(uint32_t), hipMemcpyHostToDevice));
     size_t zbytes = std::max<size_t>(16, (size_t)1 << (4 * low));

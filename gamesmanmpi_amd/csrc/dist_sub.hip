@@ -323,7 +323,7 @@ static int plan_lists(const Ctx *c, const DistSub *d, int rank, Plan &P) {
         off[L.size()] = (uint32_t)flat.size();
     };
     flatten(own, P.off, P.own);
-    if (c->sub_order == 1) sort_tiers_morton(P.own, P.off, d->high);
+    if (c->sub_order >= 1) sort_tiers_morton(P.own, P.off, d->high, c->sub_order);
     flatten(fill, P.fill_off, P.fill);
     for (int a = 0; a < d->g; a++) {
         flatten(Sd[a], P.send_off[a], P.send[a]);
@@ -567,7 +567,7 @@ static int exec_op(DistSub *d, SubRank &R, const Op &o) {
     switch (o.kind) {
     case OP_TIER:
         launch_sub_tier_x(d->high, cnt(R.off, j), R.table, R.dlist + R.off[j], d->zero, R.dxoff + R.off[j], R.dxdst,
-                          st);
+                          st, d->want_x4 == 8);
         break;
     case OP_FILL:
     case OP_PACK:   // folded into OP_TIER (extra destinations); not in the lists

@@ -214,11 +214,11 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sub_threads = (int)v;
         return GM_OK;
     case GM_OPT_SUB_INTERLEAVE:
-        if (v != 1 && (v < 4 || v > 7)) { set_error("sub_interleave must be 1, 4, 5, 6 or 7"); return GM_E_ARG; }
+        if (v != 1 && (v < 4 || v > 8)) { set_error("sub_interleave must be 1, 4, 5, 6, 7 or 8"); return GM_E_ARG; }
         c->sub_interleave = (int)v;
         return GM_OK;
     case GM_OPT_SUB_ORDER:
-        if (v != 0 && v != 1) { set_error("sub_order must be 0 or 1"); return GM_E_ARG; }
+        if (v < 0 || v > 2) { set_error("sub_order must be 0, 1 or 2"); return GM_E_ARG; }
         c->sub_order = (int)v;
         return GM_OK;
     case GM_OPT_DIST_BATCH:

@@ -130,9 +130,9 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
 // the sharded solve's byte-image tier kernel with per-block extra destinations (LOW = 3)
 bool sub_kernel_x_exists(int high);
 void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
-                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s);
+                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, bool wave);
 int sub_kernel_threads(const Ctx *c, int low);   // 0 = the 4-block interleaved kernel
-void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &tier_off, int high);
+void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &tier_off, int high, int mode);
 
 // partitioned dense solve: `world` ranks, real (RCCL, one per process) or virtual (loopback)
 int dist_sub_solve(Ctx *c, uint64_t root);
