@@ -408,13 +408,13 @@ __device__ __forceinline__ uint32_t code_hi2(uint32_t o) { return (0xFF00FF00u -
 #define GM_PASSB_PRIO 0   // s_setprio of pass B (0 = off)
 #endif
 #ifndef GM_PASSB_REG
-#define GM_PASSB_REG 1   // pass B children (a0-1, a0-2) by DPP and (c-1, c-2) from registers
+#define GM_PASSB_REG 2   // pass B children (a0-1, a0-2) by DPP and (c-1, c-2) from registers, codes split (2)
 #endif
 #ifndef GM_B4_WAVES
 #define GM_B4_WAVES 1
 #endif
 #ifndef GM_B4_STORE_CPOL
-#define GM_B4_STORE_CPOL 0   // 16 = sc1: write-through, the stored block does not stay in L2
+#define GM_B4_STORE_CPOL 16   // sc1: write-through, the stored block does not stay in L2 (0 = plain)
 #endif
 // One workgroup solves the four blocks hp[0..3] (valid[k] false: slot unused).
 // CPOL = cache policy of the child loads and the stores (0 plain; CPOL_SC1 in the
@@ -648,6 +648,245 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
         hp[k] = valid[k] ? blocks[idx] : 0u;
     }
     b4_solve<HIGH, 0, 0, true>(table, zero, hp, valid, s, xoff, xdst, grp * K);
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined persistent variant (GM_OPT_SUB_INTERLEAVE 9).  Measured on the b4
+// kernel: its loads and stores alone (pass B skipped) take 4.0 ms of the 5.1 ms
+// solve, and while a workgroup walks pass B's barrier chain it has no load in
+// flight.  Here a workgroup keeps two byte images (32 KiB) and works through a
+// run of 4-block groups: while pass B walks group g's 46 low tiers in image
+// g & 1, the child blocks of group g+1 are loaded and folded into the other image
+// -- one block's 2*HIGH loads issued every 11 pass-B steps and folded 11 steps
+// later -- so the memory pipe stays busy during the chain.  The grid is 4
+// workgroups per CU (118 VGPRs; 5 would fit the LDS); XCD x works through a contiguous run of
+// the tier's groups (the runs of xcd_order), its workgroups striding by their
+// count, so at any time an XCD covers a window of neighbouring groups.
+#ifndef GM_P4_WAVES
+#define GM_P4_WAVES 4   // waves per SIMD = workgroups of 4 waves per CU (5 fit the LDS but spill at 96 VGPRs)
+#endif
+constexpr int P4_PER_CU = GM_P4_WAVES;
+
+template <int NMAX>
+__device__ __forceinline__ void p4_fold(const u32x4v (&v)[NMAX], uint32_t (&e)[4], uint32_t (&o)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint32_t ev = v[0][j] & 0x00FF00FFu, ov = v[0][j];   // ov: odd bytes valid in the high byte of each u16
+#pragma unroll
+        for (int m = 1; m < NMAX; m++) {
+            ev = pk_max(ev, v[m][j] & 0x00FF00FFu);
+            ov = pk_max(ov, v[m][j]);
+        }
+        e[j] = ev;
+        o[j] = ov;
+    }
+}
+// four blocks' folds of chunk c -> the byte image (position p: byte k = block k)
+__device__ __forceinline__ void p4_write_image(uint32_t *s, uint32_t c, const uint32_t (&e)[4][4],
+                                               const uint32_t (&o)[4][4]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);
+        const uint32_t ye = __builtin_amdgcn_perm(e[3][j], e[2][j], 0x06020400u);
+        const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);
+        const uint32_t yo = __builtin_amdgcn_perm(o[3][j], o[2][j], 0x07030501u);
+        u32x4v q;
+        q[0] = __builtin_amdgcn_perm(ye, xe, 0x05040100u);   // 4j
+        q[1] = __builtin_amdgcn_perm(yo, xo, 0x05040100u);   // 4j+1
+        q[2] = __builtin_amdgcn_perm(ye, xe, 0x07060302u);   // 4j+2
+        q[3] = __builtin_amdgcn_perm(yo, xo, 0x07060302u);   // 4j+3
+        *(u32x4v *)(s + 16 * c + 4 * j) = q;
+    }
+}
+// the 2*HIGH child blocks of block hp: one whole-table descriptor, each child a
+// scalar offset (a missing child re-reads the first existing one; a block with
+// none, only high part 0, reads through a zero-size descriptor: all 0)
+// the folds of blocks 2 pr and 2 pr + 1 -> bytes 2 pr, 2 pr + 1 of the image's dwords (u16 stores)
+__device__ __forceinline__ void p4_write_pair(uint32_t *s, uint32_t c, int pr, const uint32_t (&e)[2][4],
+                                              const uint32_t (&o)[2][4]) {
+    char *const b = (char *)s;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);   // positions 4j | 4j+2
+        const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);   // positions 4j+1 | 4j+3
+        const uint32_t a = 4u * (16u * c + 4u * j) + 2u * (uint32_t)pr;
+        *(uint16_t *)(b + a) = (uint16_t)xe;
+        *(uint16_t *)(b + a + 4) = (uint16_t)xo;
+        *(uint16_t *)(b + a + 8) = (uint16_t)(xe >> 16);
+        *(uint16_t *)(b + a + 12) = (uint16_t)(xo >> 16);
+    }
+}
+template <int HIGH>
+__device__ __forceinline__ void p4_issue(uint8_t *table, uint32_t hp, bool valid, uint32_t c,
+                                         u32x4v (&v)[2 * HIGH > 0 ? 2 * HIGH : 1]) {
+    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
+    uint32_t soff[NMAX];
+    uint32_t first = 0;
+    bool any = false;
+#pragma unroll
+    for (int j = HIGH - 1; j >= 0; j--)
+        if (valid && ((hp >> (4 * j)) & 15u) >= 1) { first = (hp - (1u << (4 * j))) << 12; any = true; }
+#pragma unroll
+    for (int j = 0; j < HIGH; j++) {
+        const uint32_t h = (hp >> (4 * j)) & 15u;
+        soff[2 * j] = (valid && h >= 1) ? (hp - (1u << (4 * j))) << 12 : first;
+        soff[2 * j + 1] = (valid && h >= 2) ? (hp - (2u << (4 * j))) << 12 : first;
+    }
+    if constexpr (HIGH == 0) soff[0] = 0;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(table, 0, any ? 0xFFFFFFFFu : 0u, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < NMAX; m++)
+        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * c, soff[m], 0));
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_P4_WAVES) void sub_tier_kernel_p4(uint8_t *__restrict__ table,
+                                                         const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                         const uint8_t *__restrict__ zero) {
+    constexpr int K = 4, NPOS = 4096;
+    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
+    __shared__ __attribute__((aligned(16))) uint32_t img[2][4096];   // 2 x 16 KiB
+    const int tid = threadIdx.x;
+    const uint32_t c = tid;   // pass A / C chunk: positions 16c .. 16c+15
+    const uint32_t ng = (nblk + K - 1) / K;
+    uint32_t g, stride, gend;
+    if (ng <= gridDim.x) {   // one group per workgroup
+        g = xcd_order(blockIdx.x, ng);
+        stride = 1;
+        gend = g + 1;
+    } else {                 // gridDim.x = 8 W: XCD x's W workgroups stride through its run
+        const uint32_t x = blockIdx.x & 7u, i = blockIdx.x >> 3, W = gridDim.x >> 3;
+        const uint32_t q = ng >> 3, r = ng & 7u;
+        const uint32_t start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, len = x < r ? q + 1 : q;
+        g = start + i;
+        stride = W;
+        gend = start + len;
+    }
+    if (g >= gend) return;
+    auto group = [&](uint32_t grp, uint32_t (&hp)[K], bool (&valid)[K]) {
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint32_t idx = grp * K + k;
+            valid[k] = idx < nblk;
+            hp[k] = valid[k] ? blocks[idx] : 0u;
+        }
+    };
+    uint32_t hp[K];
+    bool valid[K];
+    group(g, hp, valid);
+
+    // pass A of the first group, on its own
+#pragma unroll
+    for (int k = 0; k < K; k += 2) {
+        uint32_t e[2][4], o[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            u32x4v v[NMAX];
+            p4_issue<HIGH>(table, hp[k + h], valid[k + h], c, v);
+            p4_fold<NMAX>(v, e[h], o[h]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        p4_write_pair(img[0], c, k >> 1, e, o);
+    }
+    __syncthreads();
+
+    const int a0 = tid & 15, a1 = tid >> 4, s0 = a0 + a1;
+    const uint32_t d11 = a1 >= 1 ? 16u : 0u, d12 = a1 >= 2 ? 32u : 0u;
+    int cur = 0;
+    for (;;) {
+        const uint32_t gn = g + stride;
+        const bool more = gn < gend;
+        uint32_t hq[K];
+        bool vq[K];
+        group(more ? gn : g, hq, vq);
+        if (!more)
+#pragma unroll
+            for (int k = 0; k < K; k++) vq[k] = false;
+        uint32_t *s = img[cur];
+
+        // ---- pass B on image cur (split registers, as GM_PASSB_REG 2), with pass A
+        //      of group gn into image cur ^ 1 between its steps
+        uint32_t pe1 = 0, po1 = 0, pe2 = 0, po2 = 0;
+        if (tid == 0) {
+            const uint32_t v = s[0];
+            uint32_t re = code_lo2(v & 0x00FF00FFu), ro = code_hi2(v & 0xFF00FF00u);
+            if (valid[0] && hp[0] == 0) re = (re & 0xFFFFFF00u) | 255u;   // all heaps empty: LOSS in 0
+            s[0] = re | ro;
+            pe1 = re;
+            po1 = ro;
+        }
+        __syncthreads();
+        auto step = [&](int tau) {
+            const uint32_t n1e = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pe1, 0x111, 0xF, 0xF, true);
+            const uint32_t n1o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)po1, 0x111, 0xF, 0xF, true);
+            const uint32_t n2e = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pe2, 0x112, 0xF, 0xF, true);
+            const uint32_t n2o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)po2, 0x112, 0xF, 0xF, true);
+            const int cc = tau - s0;
+            uint32_t re = 0, ro = 0;
+            if (cc >= 0 && cc <= 15) {
+                const uint32_t o = (uint32_t)(tid + 256 * cc);
+                const uint32_t v0 = s[o], v3 = s[o - d11], v4 = s[o - d12];
+                const uint32_t me = pk_max(pk_max(pk_max(v0 & 0x00FF00FFu, v3 & 0x00FF00FFu),
+                                                  pk_max(v4 & 0x00FF00FFu, n1e)),
+                                           pk_max(pk_max(n2e, pe1), pe2));
+                const uint32_t mo = pk_max(pk_max(pk_max(v0, v3), pk_max(v4, n1o)), pk_max(pk_max(n2o, po1), po2));
+                re = code_lo2(me);
+                ro = code_hi2(mo & 0xFF00FF00u);
+                s[o] = re | ro;
+            }
+            pe2 = pe1;
+            po2 = po1;
+            pe1 = re;
+            po1 = ro;
+            __syncthreads();
+        };
+        // block k's fold is held until block k ^ 1's is done, then the pair goes to
+        // the other image as u16 halves (bytes k & 2, (k & 2) + 1 of each dword)
+        uint32_t e[2][4], o[2][4];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            u32x4v v[NMAX];
+            if (more) p4_issue<HIGH>(table, hq[k], vq[k], c, v);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 1
+            for (int t = 1; t <= 11; t++) step(11 * k + t);   // kept rolled: unrolled, the compiler hoists
+                                                              // every step's addresses out of the group loop
+            __builtin_amdgcn_sched_barrier(0);
+            if (more) {
+                p4_fold<NMAX>(v, e[k & 1], o[k & 1]);
+                if (k & 1) p4_write_pair(img[cur ^ 1], c, k >> 1, e, o);
+            }
+        }
+        step(45);
+
+        // ---- pass C of group g
+        __amdgpu_buffer_rsrc_t wr[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) wr[k] = block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0);
+        {
+            u32x4v out[K];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const u32x4v q = *(const u32x4v *)(s + 16 * c + 4 * j);
+                const uint32_t t01 = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u);
+                const uint32_t t23 = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u);
+                const uint32_t u01 = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);
+                const uint32_t u23 = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
+                out[0][j] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+                out[1][j] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+                out[2][j] = __builtin_amdgcn_perm(u23, u01, 0x05040100u);
+                out[3][j] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);
+            }
+#pragma unroll
+            for (int k = 0; k < K; k++) __builtin_amdgcn_raw_buffer_store_b128(out[k], wr[k], 16u * c, 0, GM_B4_STORE_CPOL);
+        }
+        if (!more) break;
+        __syncthreads();   // image cur is read by pass C above and written by the next pass A
+        cur ^= 1;
+        g = gn;
+#pragma unroll
+        for (int k = 0; k < K; k++) { hp[k] = hq[k]; valid[k] = vq[k]; }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1033,6 +1272,18 @@ static tier_kernel_t pick_w1(int high) {
     return nullptr;
 }
 
+static tier_kernel_t pick_p4(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel_p4<0>;
+    case 1: return sub_tier_kernel_p4<1>;
+    case 2: return sub_tier_kernel_p4<2>;
+    case 3: return sub_tier_kernel_p4<3>;
+    case 4: return sub_tier_kernel_p4<4>;
+    case 5: return sub_tier_kernel_p4<5>;
+    }
+    return nullptr;
+}
+
 static tier_kernel_t pick_x4(int high, bool diag) {
     switch (high) {
     case 0: return diag ? sub_tier_kernel_x4<0, true> : sub_tier_kernel_x4<0, false>;
@@ -1084,6 +1335,7 @@ static tier_kernel_t pick_kernel(int low, int high, int nt) {
 // one-wave byte-image kernel (64 threads).
 static tier_kernel_t pick_interleaved(int high, int nt) {
     if (nt == -4) return pick_w1(high);
+    if (nt == -5) return pick_p4(high);
     return nt == -2 ? pick_b4(high) : pick_x4(high, nt == -1);
 }
 
@@ -1095,7 +1347,16 @@ bool sub_kernel_exists(int low, int high, int nt) {
 void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table, const uint32_t *list,
                      const uint8_t *zero, hipStream_t s) {
     if (!nblocks) return;
-    if (nt <= 0)
+    if (nt == -5) {   // persistent: at most P4_PER_CU workgroups per CU (a multiple of 8)
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+        }
+        const uint32_t ng = (nblocks + 3) / 4, cap = (uint32_t)(P4_PER_CU * cus) & ~7u;
+        hipLaunchKernelGGL(pick_p4(high), dim3(ng <= cap ? ng : cap), dim3(256), 0, s, table, list, nblocks, zero);
+    } else if (nt <= 0)
         hipLaunchKernelGGL(pick_interleaved(high, nt), dim3((nblocks + 3) / 4), dim3(nt == -4 ? 64 : 256), 0, s, table,
                            list, nblocks, zero);
     else
@@ -1141,6 +1402,7 @@ int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 6) return -2;
     if (low == 3 && c->sub_interleave == 7) return -3;
     if (low == 3 && c->sub_interleave == 8) return -4;
+    if (low == 3 && c->sub_interleave == 9) return -5;
     return c->sub_threads;
 }
 

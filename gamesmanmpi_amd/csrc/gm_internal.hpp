@@ -76,7 +76,7 @@ struct Ctx {
     int sub_low = 3;
     int sub_threads = 128;
     int sub_interleave = 6;      // 4 u16 image, 5 u16 + diagonal pass B, 6 byte image (default), 1 one block
-    int sub_order = 1;
+    int sub_order = 2;   // block order inside a tier: 0 key, 1 Morton, 2 Hilbert (default)
     bool use_graph = true;
     bool timing = false;
 

@@ -33,6 +33,13 @@ struct Sparse {
     uint32_t *d_err = nullptr;
     int64_t t_root = 0;
     uint64_t edges = 0;
+    // replay (GM_SPARSE_REPLAY, default on): a solve of the same game, parameters and
+    // root as the synced solve that built these tables re-runs them with no host
+    // round trip -- every table size and list length is known -- as one hipGraph
+    bool plan_ok = false;
+    int64_t plan_key[6] = {0, 0, 0, 0, 0, 0};   // game, params[0..3], root
+    unsigned long long *d_tscr = nullptr;       // per-tier classify counters, 16 per tier
+    hipGraphExec_t graph = nullptr;
 };
 
 // ----------------------------------------------------------------- kernels
@@ -135,9 +142,108 @@ static int read_err(Ctx *c, Sparse *sp) {
     return e ? dev_error_to_gm(e) : GM_OK;
 }
 
+static bool replay_enabled() {
+    const char *e = getenv("GM_SPARSE_REPLAY");
+    return !e || atoi(e) != 0;
+}
+
+static bool plan_matches(const Ctx *c, const Sparse *sp, uint64_t root) {
+    const int64_t key[6] = {c->game, c->params[0], c->params[1], c->params[2], c->params[3], (int64_t)root};
+    return sp && sp->plan_ok && std::equal(key, key + 6, sp->plan_key);
+}
+
+// Re-run the previous solve's tier sequence on its own tables (see Sparse::graph):
+// refill, re-insert the root, classify + expand every tier, retrograde, all
+// enqueued (and captured once) with the recorded sizes; one read-back at the end
+// checks every tier's insert count, positions seen and interior count against
+// the record.  Any difference (or device error) drops the record: the caller
+// then runs the synced solve.
+template <class D>
+static int replay_with(Ctx *c, const D &d, uint64_t root) {
+    constexpr int S = D::MAX_SKIP;
+    Sparse *sp = c->sp;
+    const size_t T = sp->tiers.size();
+    const double t0 = now_ms();
+    if (!sp->graph) {
+        GM_TRY(ensure_counts(sp, T + S + 1));
+        if (!sp->d_tscr) GM_HIP(hipMalloc(&sp->d_tscr, 16 * T * sizeof(unsigned long long)));
+        hipGraph_t g;
+        GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        GM_HIP(hipMemsetAsync(sp->d_err, 0, 4, c->stream));
+        GM_HIP(hipMemsetAsync(sp->d_counts, 0, sp->counts_cap * sizeof(unsigned long long), c->stream));
+        GM_HIP(hipMemsetAsync(sp->d_tscr, 0, 16 * T * sizeof(unsigned long long), c->stream));
+        for (size_t t = 0; t < T; t++)
+            if (sp->tiers[t].cap)
+                hipLaunchKernelGGL(slot_fill_kernel, dim3(grid_for(sp->tiers[t].cap)), dim3(256), 0, c->stream,
+                                   sp->tiers[t].slots, sp->tiers[t].cap);
+        hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, front_ref(sp, 0), root,
+                           sp->d_err);
+        for (size_t t = 0; t < T; t++) {
+            SpTier &Tt = sp->tiers[t];
+            if (!Tt.count) continue;
+            unsigned long long *scr = sp->d_tscr + 16 * t;
+            hipLaunchKernelGGL(classify_kernel<D>, dim3(grid_for(Tt.cap / CROWS + 1)), dim3(256), 0, c->stream, d,
+                               Tt.slots, Tt.cap, Tt.ikeys, Tt.islot, scr + 9, scr, scr + 10, sp->d_err);
+            if (!Tt.ni) continue;
+            Fronts<S> nx;
+            for (int s = 0; s < S; s++) {
+                const size_t u = t + 1 + s;   // a tier past the last one received nothing: no table
+                nx.t[s] = u < T ? front_ref(sp, u) : FrontRef{nullptr, 0, sp->d_counts + u};
+            }
+            hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(Tt.ni)), dim3(256), 0, c->stream, d, Tt.ikeys, Tt.ni,
+                               nx, Tt.iwon, sp->d_err);
+        }
+        for (size_t tt = T; tt-- > 0;) {
+            SpTier &Tt = sp->tiers[tt];
+            if (!Tt.ni) continue;
+            Ress<S> nx;
+            for (int s = 0; s < S; s++) {
+                const size_t u = tt + 1 + s;
+                nx.t[s] = u < T ? res_ref(sp, u) : ResRef{nullptr, 0};
+            }
+            hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(Tt.ni)), dim3(256), 0, c->stream, d, Tt.ikeys, Tt.islot,
+                               Tt.iwon, Tt.ni, res_ref(sp, tt), nx, sp->d_err);
+        }
+        const hipError_t e = hipStreamEndCapture(c->stream, &g);
+        if (e != hipSuccess) { set_error("sparse replay capture failed: %s", hipGetErrorString(e)); return GM_E_HIP; }
+        GM_HIP(hipGraphInstantiate(&sp->graph, g, nullptr, nullptr, 0));
+        GM_HIP(hipGraphDestroy(g));
+    }
+    GM_HIP(hipGraphLaunch(sp->graph, c->stream));
+    std::vector<unsigned long long> cnt(T), scr(16 * T);
+    uint32_t err = 0;
+    GM_HIP(hipMemcpyAsync(cnt.data(), sp->d_counts, T * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipMemcpyAsync(scr.data(), sp->d_tscr, 16 * T * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                          c->stream));
+    GM_HIP(hipMemcpyAsync(&err, sp->d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipStreamSynchronize(c->stream));
+    bool ok = !err;
+    for (size_t t = 0; t < T && ok; t++) {
+        const SpTier &Tt = sp->tiers[t];
+        ok = cnt[t] == Tt.count && (!Tt.count || (scr[16 * t + 10] == Tt.count && scr[16 * t + 9] == Tt.ni));
+    }
+    if (!ok) {
+        if (trace_on()) fprintf(stderr, "[gm] sparse replay differs from its record (err %#x): full solve\n", err);
+        sp->plan_ok = false;
+        return GM_E_STATE;
+    }
+    const double t1 = now_ms();
+    {
+        uint64_t rk[1] = {root};
+        uint16_t rr[1];
+        GM_TRY(sparse_query(c, rk, rr, 1));
+        c->root_record = rr[0];
+    }
+    c->stats.forward_ms = 0;
+    c->stats.backward_ms = t1 - t0;
+    c->stats.solve_ms = t1 - t0;
+    return GM_OK;   // positions, tiers, edges, bytes: unchanged from the recorded solve
+}
+
 template <class D>
 static int solve_with(Ctx *c, const D &d, uint64_t root) {
     constexpr int S = D::MAX_SKIP;
+    if (replay_enabled() && plan_matches(c, c->sp, root) && replay_with(c, d, root) == GM_OK) return GM_OK;
     sparse_free(c);
     Sparse *sp = c->sp = new Sparse();
     sp->t_root = d.tier(root);
@@ -261,6 +367,10 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     // SURVEY §8d sparse model: 8 (parent key) + 8 d (child keys) + 8 d (dedup) + 2 (1 + d) per position
     c->stats.algo_bytes = 10 * n + 18 * sp->edges;
     c->stats.table_bytes = tb;
+    // record for replay: the tables, lists and counts above belong to (game, params, root)
+    const int64_t key[6] = {c->game, c->params[0], c->params[1], c->params[2], c->params[3], (int64_t)root};
+    std::copy(key, key + 6, sp->plan_key);
+    sp->plan_ok = true;
     return GM_OK;
 }
 
@@ -370,7 +480,8 @@ void sparse_free(Ctx *c) {
     if (!sp) return;
     for (auto &T : sp->tiers) free_tier(c, T);
     (void)hipStreamSynchronize(c->stream);
-    for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err})
+    if (sp->graph) (void)hipGraphExecDestroy(sp->graph);
+    for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err, (void *)sp->d_tscr})
         if (p) (void)hipFree(p);
     delete sp;
     c->sp = nullptr;

@@ -84,8 +84,11 @@ enum {
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
     GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path, 4 blocks per workgroup: 6 = byte LDS image (default),
                                   7 = byte image, whole solve as one dataflow launch (per-block child flags),
+                                  8 = byte image, one 64-lane wave per workgroup (no barriers),
+                                  9 = byte image, persistent, next group's loads pipelined into pass B,
                                   4 = u16 image, 5 = u16 image + anti-diagonal pass B; 1 = one block */
-    GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton (default) */
+    GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton,
+                               2 = Hilbert walk of the tier's free high nibbles (default) */
     GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
     GM_OPT_DIST_SLOTS = 10, /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
     GM_OPT_DIST_SOLO = 12,  /* diagnostic, loopback sharded SUBTRACT path: r + 1 = enqueue only rank r's

@@ -66,6 +66,41 @@ def test_othello_4x4():
     assert rec == (1 << 14) | 12         # LOSS in 12
 
 
+@pytest.mark.parametrize("game,params,name", [(OTH, (4, 4), "othello_4x4"), (TOOT, (4, 3), "toot_4x3"),
+                                              (F2O, (), "four_to_one_six")])
+def test_sparse_replay_is_identical(game, params, name):
+    """A repeated solve of the same (game, parameters, root) replays the recorded tier
+    sequence as one graph with no host round trip (csrc/sparse.hip replay_with); every
+    replay must give the golden table, and a different root must not reuse the record."""
+    keys, recs = golden(name)
+    ctx = Context(game, params, device=0)
+    root = 6 if game == F2O else ctx.initial()
+    for i in range(4):
+        n, rec = ctx.solve(root)
+        k, r = ctx.export()
+        assert n == len(keys) and np.array_equal(k, keys) and np.array_equal(r, recs), i
+        assert ctx.digest() == (digest(keys, recs), len(keys))
+    if game == F2O:   # another root: a fresh synced solve, then its own replays
+        k4, r4 = golden("four_to_one_four")
+        for i in range(2):
+            ctx.solve(4)
+            k, r = ctx.export()
+            assert np.array_equal(k, k4) and np.array_equal(r, r4), i
+        ctx.solve(6)
+        k, r = ctx.export()
+        assert np.array_equal(k, keys) and np.array_equal(r, recs)
+
+
+def test_sparse_replay_is_faster():
+    """Othello 4x4 (54,089 positions): the replay has no per-tier host round trip."""
+    ctx = Context(OTH, (4, 4), device=0)
+    root = ctx.initial()
+    ctx.solve(root)
+    first = ctx.stats()["solve_ms"]
+    best = min((ctx.solve(root), ctx.stats()["solve_ms"])[1] for _ in range(5))
+    assert best < first
+
+
 @pytest.mark.parametrize("dims", [(3, 3), (4, 3)])
 def test_toot_small_boards(dims):
     keys, recs = golden("toot_%dx%d" % dims)
@@ -95,7 +130,7 @@ def test_subtract_dense_vs_oracle(oracle, heaps, low):
     assert np.array_equal(r, ref)
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("heaps", [3, 4, 5, 6])
 def test_subtract_kernel_variants_vs_oracle(oracle, heaps, variant):
     """Interleaved kernel variants (GM_OPT_SUB_INTERLEAVE 4 / 5 / 6, 7 = dataflow, 8 = one wave) against the oracle."""
@@ -104,7 +139,7 @@ def test_subtract_kernel_variants_vs_oracle(oracle, heaps, variant):
     assert np.array_equal(ctx.export()[1], ref)
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [5, 6, 7, 8, 9])
 def test_subtract_kernel_variants_full_2_32_match(variant):
     a, n1, r1 = _solve(SUB, (8,), sub_interleave=4)
     d1 = a.digest()
