@@ -21,6 +21,7 @@ OPT_DIST_SLOTS = 10
 OPT_DIST_SYMMETRY = 11
 OPT_DIST_SOLO = 12
 OPT_DIST_OWNER = 13
+OPT_SYMMETRY = 14
 BUF_DENSE_TABLE = 1
 PLAN_SHAPE, PLAN_OWN, PLAN_FILL, PLAN_SEND, PLAN_RECV, PLAN_OPS, PLAN_XDEST = 0, 1, 2, 3, 4, 5, 6
 REC_UNSOLVED = 0xFFFF

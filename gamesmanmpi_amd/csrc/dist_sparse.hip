@@ -331,7 +331,7 @@ static int classify_tier(Ctx *c, DistSparse *d, const D &desc, size_t t) {
         const uint64_t n = T.fcount;
         if (!n) continue;
         GM_TRY(classify_tier_table(c, desc, T, R.d_scr, R.d_err));
-        unsigned long long sc[11];
+        unsigned long long sc[12];
         GM_HIP(hipMemcpyAsync(sc, R.d_scr, sizeof sc, hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
         if (sc[10] != n) {
@@ -339,6 +339,7 @@ static int classify_tier(Ctx *c, DistSparse *d, const D &desc, size_t t) {
             return GM_E_STATE;
         }
         T.count = n;
+        T.count_all = sc[11];
         T.ni = sc[9];
     }
     return GM_OK;
@@ -548,12 +549,27 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     GM_HIP(hipMemcpyAsync(&rs, d->d_root, 4, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     c->root_record = record_of_score((uint16_t)rs);
+    // positions per tier: the stored representatives' orbits (games.hpp), summed over ranks
+    std::vector<uint64_t> gall(d->gcount.size(), 0);
+    for (auto &R : d->ranks)
+        for (size_t t = 0; t < gall.size() && t < R.tiers.size(); t++) gall[t] += R.tiers[t].count_all;
+    if (!d->loopback && !gall.empty()) {
+        if (gall.size() > d->tot_cap) {
+            if (d->d_tot) dev_free(c, d->d_tot);
+            d->tot_cap = std::max<size_t>(64, 2 * gall.size());
+            GM_TRY(dev_alloc(c, (void **)&d->d_tot, d->tot_cap * 8));
+        }
+        GM_HIP(hipMemcpyAsync(d->d_tot, gall.data(), gall.size() * 8, hipMemcpyHostToDevice, c->stream));
+        GM_NCCL(ncclAllReduce(d->d_tot, d->d_tot, gall.size(), ncclUint64, ncclSum, c->comm, c->stream));
+        GM_HIP(hipMemcpyAsync(gall.data(), d->d_tot, gall.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        GM_HIP(hipStreamSynchronize(c->stream));
+    }
     uint64_t n = 0, tb = 0;
-    for (auto v : d->gcount) n += v;
+    for (auto v : gall) n += v;
     for (auto &R : d->ranks)
         for (auto &T : R.tiers) tb += T.cap * sizeof(RSlot) + T.ni * 13;
     c->n_positions = n;
-    c->tier_counts = d->gcount;
+    c->tier_counts = gall;
     c->stats.n_positions = n;
     c->stats.n_tiers = (int32_t)d->gcount.size();
     c->stats.world = G;
@@ -564,6 +580,19 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     c->stats.n_edges = d->edges;
     c->stats.table_bytes = tb;
     return GM_OK;
+}
+
+template <class F>
+static int with_game(Ctx *c, F &&f) {
+    switch (c->game) {
+    case GM_GAME_FOUR_TO_ONE: return f(c->f2o);
+    case GM_GAME_TTT: return f(c->ttt);
+    case GM_GAME_TOOT: return f(c->toot);
+    case GM_GAME_OTHELLO: return f(c->oth);
+    case GM_GAME_SUBTRACT: return f(c->sub);
+    }
+    set_error("unknown game");
+    return GM_E_GAME;
 }
 
 int dist_sparse_solve(Ctx *c, uint64_t root) {
@@ -582,7 +611,7 @@ int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uin
     DistSparse *d = c->dist_sp;
     uint64_t total = 0;
     for (auto &R : d->ranks)
-        for (auto &T : R.tiers) total += T.count;
+        for (auto &T : R.tiers) total += T.count_all;
     *n = total;
     if (!keys) return GM_OK;
     if (cap < total) { set_error("export buffer too small"); return GM_E_CAP; }
@@ -593,11 +622,14 @@ int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uin
     GM_HIP(hipMalloc(&dr, std::max<uint64_t>(1, total) * 2));
     GM_HIP(hipMalloc(&cur, 8));
     GM_HIP(hipMemsetAsync(cur, 0, 8, c->stream));
-    for (auto &R : d->ranks)
-        for (auto &T : R.tiers)
-            if (T.count)
-                hipLaunchKernelGGL(res_gather_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap,
-                                   dk, dr, cur);
+    GM_TRY(with_game(c, [&](const auto &desc) {
+        for (auto &R : d->ranks)
+            for (auto &T : R.tiers)
+                if (T.count)
+                    hipLaunchKernelGGL(res_gather_kernel<std::decay_t<decltype(desc)>>, dim3(grid_for(T.cap)),
+                                       dim3(256), 0, c->stream, desc, T.slots, T.cap, dk, dr, cur);
+        return GM_OK;
+    }));
     std::vector<uint64_t> hk(total);
     std::vector<uint16_t> hr(total);
     GM_HIP(hipMemcpyAsync(hk.data(), dk, total * 8, hipMemcpyDeviceToHost, c->stream));
@@ -620,12 +652,15 @@ int dist_sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     GM_HIP(hipMemsetAsync(acc, 0, 8, c->stream));
     uint64_t total = 0;
     for (auto &R : d->ranks)
-        for (auto &T : R.tiers) {
-            total += T.count;
-            if (T.count)
-                hipLaunchKernelGGL(res_digest_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap,
-                                   acc);
-        }
+        for (auto &T : R.tiers) total += T.count_all;
+    GM_TRY(with_game(c, [&](const auto &desc) {
+        for (auto &R : d->ranks)
+            for (auto &T : R.tiers)
+                if (T.count)
+                    hipLaunchKernelGGL(res_digest_kernel<std::decay_t<decltype(desc)>>, dim3(grid_for(T.cap)),
+                                       dim3(256), 0, c->stream, desc, T.slots, T.cap, acc);
+        return GM_OK;
+    }));
     unsigned long long h;
     GM_HIP(hipMemcpyAsync(&h, acc, 8, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));

@@ -33,10 +33,22 @@ GM_HD int collect(const D &d, uint64_t k, uint64_t *out) {
     return n;
 }
 
+// Symmetry hooks (the reference's own hook is othello_bit_new.py:224-235,
+// symmetry_functions, unused by its engines).  canon(k) is the representative the
+// tables store; orbit(k, f) calls f once per distinct position the representative
+// stands for.  A descriptor whose visit() returns canonical children solves one
+// representative per orbit; counts, digests and exports expand every orbit, so the
+// results are those of the unreduced game.  Games without a symmetry in use:
+struct NoSym {
+    GM_HD uint64_t canon(uint64_t k) const { return k; }
+    template <class F>
+    GM_HD void orbit(uint64_t k, F &&f) const { f(k); }
+};
+
 // ---------------------------------------------------------------- Four-To-One
 // reference test_games/four_to_one.py:8-31 (moves are always -1, -2: the
 // `x == 1` test at :15 compares a str with an int and never fires).
-struct DescF2O {
+struct DescF2O : NoSym {
     static constexpr int MAX_SKIP = 2;
     static constexpr int MAXC = 2;
     GM_HD int primitive(uint64_t k) const { return (int64_t)k <= 0 ? LOSS : UNDECIDED; }
@@ -55,7 +67,7 @@ struct DescF2O {
 // ---------------------------------------------------------------- Tic-tac-toe
 // reference test_games/mttt.py:11-127 and tic_tac_toe_np.py:7-61.
 // key = sum c_i 3^i, i = x + 3y, c: 0 blank, 1 X (player 1), 2 O (player 2).
-struct DescTTT {
+struct DescTTT : NoSym {
     static constexpr int MAX_SKIP = 1;
     static constexpr int MAXC = 9;
     static constexpr uint32_t SLOTS = 19683;
@@ -115,6 +127,37 @@ struct DescToot {
     uint32_t amask;
     uint32_t start_h, start_v, start_d, start_a;   // segment starts per direction
     uint32_t colmask;                              // cells of column x' = 0
+    // left-right mirror symmetry (set per solve, gm_api.hip: only when the root is its
+    // own mirror image): the rules are mirror-invariant -- TOOT and OTTO are
+    // palindromes, and the mirror swaps the two diagonal directions -- so a position
+    // and its mirror image share value and remoteness, and with sym set visit()
+    // returns min(child, mirror(child)).  Hands (bits 0..15) are unchanged.
+    uint32_t sym = 0;
+    GM_HD uint32_t mirror_plane(uint32_t p) const {
+        uint32_t m = 0;
+        for (int y = 0; y < H; y++) {
+            const uint32_t row = (p >> (L * y)) & ((1u << L) - 1u);
+            m |= (__builtin_bitreverse32(row) >> (32 - L)) << (L * y);
+        }
+        return m;
+    }
+    GM_HD uint64_t mirror(uint64_t k) const {
+        return (k & 0xFFFFull) | ((uint64_t)mirror_plane(oplane(k)) << 16) |
+               ((uint64_t)mirror_plane(tplane(k)) << (A + 16));
+    }
+    GM_HD uint64_t canon(uint64_t k) const {
+        if (!sym) return k;
+        const uint64_t m = mirror(k);
+        return m < k ? m : k;
+    }
+    template <class F>
+    GM_HD void orbit(uint64_t k, F &&f) const {
+        f(k);
+        if (sym) {
+            const uint64_t m = mirror(k);
+            if (m != k) f(m);
+        }
+    }
 
     static bool make(int L_, int H_, DescToot *d) {
         if (L_ < 1 || H_ < 1 || L_ > 8 || 2 * L_ * H_ + 16 > 64) return false;
@@ -163,8 +206,8 @@ struct DescToot {
             if (occ & (1u << xr)) continue;           // top cell (x, H-1) taken
             int filled = popc64(occ & (colmask << xr));
             int bit = L * (H - 1 - filled) + xr;      // lowest empty y (:112-115)
-            if (have_t && !f(k - (1ull << tsh) + (1ull << (A + 16 + bit)))) return;
-            if (have_o && !f(k - (1ull << osh) + (1ull << (16 + bit)))) return;
+            if (have_t && !f(canon(k - (1ull << tsh) + (1ull << (A + 16 + bit))))) return;
+            if (have_o && !f(canon(k - (1ull << osh) + (1ull << (16 + bit))))) return;
         }
     }
     GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
@@ -189,7 +232,7 @@ struct DescToot {
 // reference test_games/othello_bit_new.py (square boards).  Key = all 2A+16
 // string bits: WHITE plane at [A+16, 2A+16), BLACK plane at [16, A+16), the
 // signed turn byte (1 BLACK, 2 WHITE) at bits 8..15, the pass byte at 0..7.
-struct DescOthello {
+struct DescOthello : NoSym {
     static constexpr int MAX_SKIP = 3;
     static constexpr int MAXC = 24;
     int L, A;
@@ -266,7 +309,7 @@ struct DescOthello {
 // The build's synthetic game: `heaps` heaps of 4 bits; a move
 // takes 1 or 2 from one non-empty heap, floor 0 (duplicate children dropped);
 // all heaps empty is a LOSS.  One heap = Four-To-One for piles >= 0.
-struct DescSub {
+struct DescSub : NoSym {
     static constexpr int MAX_SKIP = 2;
     static constexpr int MAXC = 16;
     int heaps;

@@ -241,6 +241,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         if (v < 0 || v > 64) { set_error("dist_solo must be 0..64"); return GM_E_ARG; }
         c->dist_solo = (int)v;
         return GM_OK;
+    case GM_OPT_SYMMETRY:
+        if (v < 0 || v > 1) { set_error("symmetry must be 0 or 1"); return GM_E_ARG; }
+        c->symmetry = (int)v;
+        return GM_OK;
     case GM_OPT_VIRTUAL_RANKS:
         if (v < 1 || v > 64) { set_error("virtual ranks must be 1..64"); return GM_E_ARG; }
         c->virtual_ranks = (int)v;
@@ -281,7 +285,12 @@ int gm_expand_host(gm_ctx *h, uint64_t key, uint64_t *children, int cap, int *n,
     switch (c->game) {
     case GM_GAME_FOUR_TO_ONE: p = c->f2o.primitive(key); t = c->f2o.tier(key); if (p == UNDECIDED) k = c->f2o.children(key, kids); break;
     case GM_GAME_TTT: p = c->ttt.primitive(key); t = c->ttt.tier(key); if (p == UNDECIDED) k = c->ttt.children(key, kids); break;
-    case GM_GAME_TOOT: p = c->toot.primitive(key); t = c->toot.tier(key); if (p == UNDECIDED) k = c->toot.children(key, kids); break;
+    case GM_GAME_TOOT: {   // the plugin's own moves: no symmetry reduction
+        DescToot d = c->toot;
+        d.sym = 0;
+        p = d.primitive(key); t = d.tier(key); if (p == UNDECIDED) k = d.children(key, kids);
+        break;
+    }
     case GM_GAME_OTHELLO: p = c->oth.primitive(key); t = c->oth.tier(key); if (p == UNDECIDED) k = c->oth.children(key, kids); break;
     case GM_GAME_SUBTRACT: p = c->sub.primitive(key); t = c->sub.tier(key); if (p == UNDECIDED) k = c->sub.children(key, kids); break;
     default: return GM_E_GAME;
@@ -332,6 +341,8 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     c->stats.kernel_launches = c->timing ? launches : 0;
     c->stats.world = c->world;
     c->root = root;
+    // symmetry reduction (games.hpp): Toot-and-Otto's mirror, when the root is its own mirror image
+    if (c->game == GM_GAME_TOOT) c->toot.sym = (c->symmetry && c->toot.mirror(root) == root) ? 1u : 0u;
     int eng = engine_for(c);
     // GM_ENGINE_DIST_SPARSE forces the hash-sharded engine, e.g. over a one-rank communicator
     const bool force_dist_sparse = c->engine_opt == GM_ENGINE_DIST_SPARSE;

@@ -37,8 +37,10 @@ struct Sparse {
     // root as the synced solve that built these tables re-runs them with no host
     // round trip -- every table size and list length is known -- as one hipGraph
     bool plan_ok = false;
-    int64_t plan_key[6] = {0, 0, 0, 0, 0, 0};   // game, params[0..3], root
-    unsigned long long *d_tscr = nullptr;       // per-tier classify counters, 16 per tier
+    int64_t plan_key[7] = {0, 0, 0, 0, 0, 0, 0};   // game, params[0..3], root, symmetry
+    unsigned long long *d_replay = nullptr;     // replay results: counts | 16 classify counters per tier | err | root
+    unsigned long long *h_replay = nullptr;     // pinned host copy
+    uint64_t replay_words = 0;
     hipGraphExec_t graph = nullptr;
 };
 
@@ -147,9 +149,16 @@ static bool replay_enabled() {
     return !e || atoi(e) != 0;
 }
 
+static void plan_key_of(const Ctx *c, uint64_t root, int64_t (&key)[7]) {
+    const int64_t k[7] = {c->game, c->params[0], c->params[1], c->params[2], c->params[3], (int64_t)root,
+                          c->game == GM_GAME_TOOT ? (int64_t)c->toot.sym : 0};
+    std::copy(k, k + 7, key);
+}
+
 static bool plan_matches(const Ctx *c, const Sparse *sp, uint64_t root) {
-    const int64_t key[6] = {c->game, c->params[0], c->params[1], c->params[2], c->params[3], (int64_t)root};
-    return sp && sp->plan_ok && std::equal(key, key + 6, sp->plan_key);
+    int64_t key[7];
+    plan_key_of(c, root, key);
+    return sp && sp->plan_ok && std::equal(key, key + 7, sp->plan_key);
 }
 
 // Re-run the previous solve's tier sequence on its own tables (see Sparse::graph):
@@ -162,36 +171,36 @@ template <class D>
 static int replay_with(Ctx *c, const D &d, uint64_t root) {
     constexpr int S = D::MAX_SKIP;
     Sparse *sp = c->sp;
-    const size_t T = sp->tiers.size();
+    const size_t T = sp->tiers.size(), NC = T + S + 1;
     const double t0 = now_ms();
     if (!sp->graph) {
-        GM_TRY(ensure_counts(sp, T + S + 1));
-        if (!sp->d_tscr) GM_HIP(hipMalloc(&sp->d_tscr, 16 * T * sizeof(unsigned long long)));
+        // one buffer for everything read back: insert counts [0, NC), classify counters
+        // [NC, NC + 16 T), the device error word, the root record
+        sp->replay_words = NC + 16 * T + 2;
+        GM_HIP(hipMalloc(&sp->d_replay, sp->replay_words * 8));
+        GM_HIP(hipHostMalloc(&sp->h_replay, sp->replay_words * 8, hipHostMallocDefault));
+        unsigned long long *cnt = sp->d_replay, *tscr = sp->d_replay + NC, *rootw = sp->d_replay + NC + 16 * T + 1;
+        uint32_t *err = (uint32_t *)(sp->d_replay + NC + 16 * T);
+        auto fref = [&](size_t u) { return FrontRef{u < T ? sp->tiers[u].slots : nullptr, u < T ? sp->tiers[u].cap : 0,
+                                                    cnt + u}; };
         hipGraph_t g;
         GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        GM_HIP(hipMemsetAsync(sp->d_err, 0, 4, c->stream));
-        GM_HIP(hipMemsetAsync(sp->d_counts, 0, sp->counts_cap * sizeof(unsigned long long), c->stream));
-        GM_HIP(hipMemsetAsync(sp->d_tscr, 0, 16 * T * sizeof(unsigned long long), c->stream));
+        GM_HIP(hipMemsetAsync(sp->d_replay, 0, sp->replay_words * 8, c->stream));
         for (size_t t = 0; t < T; t++)
             if (sp->tiers[t].cap)
                 hipLaunchKernelGGL(slot_fill_kernel, dim3(grid_for(sp->tiers[t].cap)), dim3(256), 0, c->stream,
                                    sp->tiers[t].slots, sp->tiers[t].cap);
-        hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, front_ref(sp, 0), root,
-                           sp->d_err);
+        hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, fref(0), root, err);
         for (size_t t = 0; t < T; t++) {
             SpTier &Tt = sp->tiers[t];
             if (!Tt.count) continue;
-            unsigned long long *scr = sp->d_tscr + 16 * t;
-            hipLaunchKernelGGL(classify_kernel<D>, dim3(grid_for(Tt.cap / CROWS + 1)), dim3(256), 0, c->stream, d,
-                               Tt.slots, Tt.cap, Tt.ikeys, Tt.islot, scr + 9, scr, scr + 10, sp->d_err);
+            unsigned long long *scr = tscr + 16 * t;
+            launch_classify(c->stream, d, Tt.slots, Tt.cap, Tt.ikeys, Tt.islot, scr, err);
             if (!Tt.ni) continue;
-            Fronts<S> nx;
-            for (int s = 0; s < S; s++) {
-                const size_t u = t + 1 + s;   // a tier past the last one received nothing: no table
-                nx.t[s] = u < T ? front_ref(sp, u) : FrontRef{nullptr, 0, sp->d_counts + u};
-            }
+            Fronts<S> nx;   // a tier past the last one received nothing: no table (cap 0)
+            for (int s = 0; s < S; s++) nx.t[s] = fref(t + 1 + s);
             hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(Tt.ni)), dim3(256), 0, c->stream, d, Tt.ikeys, Tt.ni,
-                               nx, Tt.iwon, sp->d_err);
+                               nx, Tt.iwon, err);
         }
         for (size_t tt = T; tt-- > 0;) {
             SpTier &Tt = sp->tiers[tt];
@@ -202,25 +211,26 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
                 nx.t[s] = u < T ? res_ref(sp, u) : ResRef{nullptr, 0};
             }
             hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(Tt.ni)), dim3(256), 0, c->stream, d, Tt.ikeys, Tt.islot,
-                               Tt.iwon, Tt.ni, res_ref(sp, tt), nx, sp->d_err);
+                               Tt.iwon, Tt.ni, res_ref(sp, tt), nx, err);
         }
+        hipLaunchKernelGGL(res_lookup_one_kernel, dim3(1), dim3(64), 0, c->stream, res_ref(sp, 0), d.canon(root),
+                           rootw);
+        GM_HIP(hipMemcpyAsync(sp->h_replay, sp->d_replay, sp->replay_words * 8, hipMemcpyDeviceToHost, c->stream));
         const hipError_t e = hipStreamEndCapture(c->stream, &g);
         if (e != hipSuccess) { set_error("sparse replay capture failed: %s", hipGetErrorString(e)); return GM_E_HIP; }
         GM_HIP(hipGraphInstantiate(&sp->graph, g, nullptr, nullptr, 0));
         GM_HIP(hipGraphDestroy(g));
     }
     GM_HIP(hipGraphLaunch(sp->graph, c->stream));
-    std::vector<unsigned long long> cnt(T), scr(16 * T);
-    uint32_t err = 0;
-    GM_HIP(hipMemcpyAsync(cnt.data(), sp->d_counts, T * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-    GM_HIP(hipMemcpyAsync(scr.data(), sp->d_tscr, 16 * T * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                          c->stream));
-    GM_HIP(hipMemcpyAsync(&err, sp->d_err, 4, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
-    bool ok = !err;
+    const unsigned long long *h = sp->h_replay, *scr = h + NC;
+    const uint32_t err = (uint32_t)h[NC + 16 * T];
+    const unsigned long long rootw = h[NC + 16 * T + 1];
+    bool ok = !err && (rootw >> 32);
     for (size_t t = 0; t < T && ok; t++) {
         const SpTier &Tt = sp->tiers[t];
-        ok = cnt[t] == Tt.count && (!Tt.count || (scr[16 * t + 10] == Tt.count && scr[16 * t + 9] == Tt.ni));
+        ok = h[t] == Tt.count && (!Tt.count || (scr[16 * t + 10] == Tt.count && scr[16 * t + 9] == Tt.ni &&
+                                                scr[16 * t + 11] == Tt.count_all));
     }
     if (!ok) {
         if (trace_on()) fprintf(stderr, "[gm] sparse replay differs from its record (err %#x): full solve\n", err);
@@ -228,12 +238,7 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
         return GM_E_STATE;
     }
     const double t1 = now_ms();
-    {
-        uint64_t rk[1] = {root};
-        uint16_t rr[1];
-        GM_TRY(sparse_query(c, rk, rr, 1));
-        c->root_record = rr[0];
-    }
+    c->root_record = (uint16_t)(rootw & 0xFFFF);
     c->stats.forward_ms = 0;
     c->stats.backward_ms = t1 - t0;
     c->stats.solve_ms = t1 - t0;
@@ -266,7 +271,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         if (!n) continue;
         // 1. the tier is complete: score it in place, list its undecided positions
         GM_TRY(classify_tier_table(c, d, sp->tiers[t], sp->d_scratch, sp->d_err));
-        unsigned long long sc[11];
+        unsigned long long sc[12];
         GM_HIP(hipMemcpyAsync(sc, sp->d_scratch, sizeof sc, hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
         GM_TRY(read_err(c, sp));
@@ -275,6 +280,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
             return GM_E_STATE;
         }
         sp->tiers[t].count = n;
+        sp->tiers[t].count_all = sc[11];
         sp->tiers[t].ni = sc[9];
         if (!sp->tiers[t].ni) continue;
         // 2. size the tables of the tiers the children land in: load <= 0.7 for the
@@ -353,8 +359,8 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     uint64_t n = 0, tb = 0;
     c->tier_counts.clear();
     for (auto &T : sp->tiers) {
-        n += T.count;
-        c->tier_counts.push_back(T.count);
+        n += T.count_all;
+        c->tier_counts.push_back(T.count_all);
         tb += T.cap * sizeof(RSlot) + T.ni * 13;
     }
     c->n_positions = n;
@@ -368,10 +374,23 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     c->stats.algo_bytes = 10 * n + 18 * sp->edges;
     c->stats.table_bytes = tb;
     // record for replay: the tables, lists and counts above belong to (game, params, root)
-    const int64_t key[6] = {c->game, c->params[0], c->params[1], c->params[2], c->params[3], (int64_t)root};
-    std::copy(key, key + 6, sp->plan_key);
+    plan_key_of(c, root, sp->plan_key);
     sp->plan_ok = true;
     return GM_OK;
+}
+
+// call f with the context's game descriptor
+template <class F>
+static int with_desc(Ctx *c, F &&f) {
+    switch (c->game) {
+    case GM_GAME_FOUR_TO_ONE: return f(c->f2o);
+    case GM_GAME_TTT: return f(c->ttt);
+    case GM_GAME_TOOT: return f(c->toot);
+    case GM_GAME_OTHELLO: return f(c->oth);
+    case GM_GAME_SUBTRACT: return f(c->sub);
+    }
+    set_error("sparse engine: unknown game");
+    return GM_E_GAME;
 }
 
 int sparse_solve(Ctx *c, uint64_t root) {
@@ -424,7 +443,7 @@ int sparse_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
 int sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
     Sparse *sp = c->sp;
     uint64_t total = 0;
-    for (auto &T : sp->tiers) total += T.count;
+    for (auto &T : sp->tiers) total += T.count_all;
     *n = total;
     if (!keys) return GM_OK;
     if (cap < total) {
@@ -436,10 +455,13 @@ int sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t
     GM_HIP(hipMalloc(&dk, std::max<uint64_t>(1, total) * 8));
     GM_HIP(hipMalloc(&dr, std::max<uint64_t>(1, total) * 2));
     GM_HIP(hipMemsetAsync(sp->d_scratch + 12, 0, 8, c->stream));
-    for (auto &T : sp->tiers)
-        if (T.count)
-            hipLaunchKernelGGL(res_gather_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap, dk,
-                               dr, sp->d_scratch + 12);
+    GM_TRY(with_desc(c, [&](const auto &d) {
+        for (auto &T : sp->tiers)
+            if (T.count)
+                hipLaunchKernelGGL(res_gather_kernel<std::decay_t<decltype(d)>>, dim3(grid_for(T.cap)), dim3(256), 0,
+                                   c->stream, d, T.slots, T.cap, dk, dr, sp->d_scratch + 12);
+        return GM_OK;
+    }));
     std::vector<uint64_t> hk(total);
     std::vector<uint16_t> hr(total);
     GM_HIP(hipMemcpyAsync(hk.data(), dk, total * 8, hipMemcpyDeviceToHost, c->stream));
@@ -461,12 +483,14 @@ int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     Sparse *sp = c->sp;
     GM_HIP(hipMemsetAsync(sp->d_scratch + 12, 0, 8, c->stream));
     uint64_t total = 0;
-    for (auto &T : sp->tiers) {
-        total += T.count;
-        if (T.count)
-            hipLaunchKernelGGL(res_digest_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap,
-                               sp->d_scratch + 12);
-    }
+    for (auto &T : sp->tiers) total += T.count_all;
+    GM_TRY(with_desc(c, [&](const auto &d) {
+        for (auto &T : sp->tiers)
+            if (T.count)
+                hipLaunchKernelGGL(res_digest_kernel<std::decay_t<decltype(d)>>, dim3(grid_for(T.cap)), dim3(256), 0,
+                                   c->stream, d, T.slots, T.cap, sp->d_scratch + 12);
+        return GM_OK;
+    }));
     unsigned long long h;
     GM_HIP(hipMemcpyAsync(&h, sp->d_scratch + 12, 8, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
@@ -481,8 +505,9 @@ void sparse_free(Ctx *c) {
     for (auto &T : sp->tiers) free_tier(c, T);
     (void)hipStreamSynchronize(c->stream);
     if (sp->graph) (void)hipGraphExecDestroy(sp->graph);
-    for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err, (void *)sp->d_tscr})
+    for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err, (void *)sp->d_replay})
         if (p) (void)hipFree(p);
+    if (sp->h_replay) (void)hipHostFree(sp->h_replay);
     delete sp;
     c->sp = nullptr;
 }

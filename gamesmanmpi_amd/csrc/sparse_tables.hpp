@@ -51,7 +51,8 @@ struct SpTier {
     RSlot *slots = nullptr;
     uint64_t cap = 0;
     uint64_t fcount = 0;         // keys inserted so far (host mirror of the device counter)
-    uint64_t count = 0;          // positions of the tier once classified
+    uint64_t count = 0;          // positions of the tier once classified (stored representatives)
+    uint64_t count_all = 0;      // positions they stand for (orbits expanded, games.hpp NoSym)
     uint64_t *ikeys = nullptr;   // interior (undecided) positions and their slots
     uint32_t *islot = nullptr;
     uint8_t *iwon = nullptr;     // per interior position: 1 = has a LOSS-in-0 child (set by expand)
@@ -111,6 +112,14 @@ __global__ void front_rehash_kernel(const RSlot *__restrict__ old, uint64_t ocap
     }
 }
 
+// the record of one key of a resolved table (0 = not found) -> *out
+__global__ void res_lookup_one_kernel(ResRef t, uint64_t key, unsigned long long *out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        const int s = res_find(t, key);
+        *out = s < 0 ? 0ull : (unsigned long long)record_of_score((uint16_t)s) | (1ull << 32);
+    }
+}
+
 __global__ void front_insert_one_kernel(FrontRef t, uint64_t key, uint32_t *err) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && front_insert(t, key, err)) atomicAdd(t.count, 1ull);
 }
@@ -120,34 +129,40 @@ __global__ void front_insert_one_kernel(FrontRef t, uint64_t key, uint32_t *err)
 // appended to the interior list with their edge counts per tier step.  A
 // workgroup takes CROWS rows of 256 slots and reserves its part of the interior
 // list with ONE atomic (a per-wave atomic on one counter serialises at ~90 per
-// microsecond).  seen = positions found (a check against the insert count).
+// microsecond).  seen = positions found (a check against the insert count);
+// seen[1] = the positions they stand for (each representative's orbit, games.hpp).
+// Tables below CLASSIFY_ROWS_MIN slots take one row per workgroup: with CROWS rows a
+// small tier ran on one or two workgroups whose threads each walked 16 positions in
+// turn (Othello 4x4: classify 0.1-0.4 ms per tier, most of the solve).
 constexpr int CROWS = 16;
-template <class D>
+constexpr uint64_t CLASSIFY_ROWS_MIN = 1ull << 22;
+template <class D, int ROWS>
 __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ slots, uint64_t cap,
                                                        uint64_t *__restrict__ ikeys, uint32_t *__restrict__ islot,
                                                        unsigned long long *icount, unsigned long long *edges,
                                                        unsigned long long *seen, uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
-    __shared__ uint32_t woff[CROWS * 4];
+    __shared__ uint32_t woff[ROWS * 4];
     __shared__ unsigned long long sbase;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t below = (1ull << lane) - 1ull;
     uint64_t cnt[S];
 #pragma unroll
     for (int s = 0; s < S; s++) cnt[s] = 0;
-    uint64_t nseen = 0;
-    for (uint64_t chunk = blockIdx.x * (256ull * CROWS); chunk < cap; chunk += (uint64_t)gridDim.x * 256ull * CROWS) {
-        uint64_t k[CROWS], m[CROWS];
+    uint64_t nseen = 0, nall = 0;
+    for (uint64_t chunk = blockIdx.x * (256ull * ROWS); chunk < cap; chunk += (uint64_t)gridDim.x * 256ull * ROWS) {
+        uint64_t k[ROWS], m[ROWS];
 #pragma unroll
-        for (int r = 0; r < CROWS; r++) {
+        for (int r = 0; r < ROWS; r++) {
             const uint64_t i = chunk + 256ull * r + threadIdx.x;
             k[r] = i < cap ? slots[i].key : EMPTY_KEY;
         }
 #pragma unroll
-        for (int r = 0; r < CROWS; r++) {
+        for (int r = 0; r < ROWS; r++) {
             bool interior = false;
             if (k[r] != EMPTY_KEY) {
                 nseen++;
+                d.orbit(k[r], [&](uint64_t) { nall++; });
                 const uint64_t i = chunk + 256ull * r + threadIdx.x;
                 const int p = d.primitive(k[r]);
                 if (p == DRAW) atomicOr(err, DEV_ERR_DRAW);
@@ -174,7 +189,7 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ 
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t acc = 0;
-            for (int j = 0; j < CROWS * 4; j++) {
+            for (int j = 0; j < ROWS * 4; j++) {
                 const uint32_t c = woff[j];
                 woff[j] = acc;
                 acc += c;
@@ -183,7 +198,7 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ 
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < CROWS; r++)
+        for (int r = 0; r < ROWS; r++)
             if ((m[r] >> lane) & 1ull) {
                 const uint64_t at = sbase + woff[r * 4 + w] + __popcll(m[r] & below);
                 ikeys[at] = k[r];
@@ -194,6 +209,7 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ 
 #pragma unroll
     for (int s = 0; s < S; s++) wave_add(edges + s, cnt[s]);
     wave_add(seen, nseen);
+    wave_add(seen + 1, nall);
 }
 
 template <class D>
@@ -205,31 +221,40 @@ __global__ void query_kernel(D d, int64_t t_root, const ResRef *tabs, int ntabs,
     int64_t t = d.valid(k) ? d.tier(k) - t_root : -1;
     uint16_t r = REC_UNSOLVED;
     if (t >= 0 && t < ntabs) {
-        int s = res_find(tabs[t], k);
+        int s = res_find(tabs[t], d.canon(k));
         if (s >= 0) r = record_of_score((uint16_t)s);
     }
     out[i] = r;
 }
 
-__global__ void res_digest_kernel(const RSlot *__restrict__ s, uint64_t cap, unsigned long long *acc) {
+// digest and export expand every stored representative's orbit (games.hpp)
+template <class D>
+__global__ void res_digest_kernel(D d, const RSlot *__restrict__ s, uint64_t cap, unsigned long long *acc) {
     uint64_t sum = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const u64x2 v = *(const u64x2 *)&s[i];
-        if (v[0] != EMPTY_KEY) sum += digest_term(v[0], record_of_score((uint16_t)v[1]));
+        if (v[0] != EMPTY_KEY) {
+            const uint16_t rec = record_of_score((uint16_t)v[1]);
+            d.orbit(v[0], [&](uint64_t k) { sum += digest_term(k, rec); });
+        }
     }
     wave_add(acc, sum);
 }
 
-__global__ void res_gather_kernel(const RSlot *__restrict__ s, uint64_t cap, uint64_t *okeys, uint16_t *orec,
+template <class D>
+__global__ void res_gather_kernel(D d, const RSlot *__restrict__ s, uint64_t cap, uint64_t *okeys, uint16_t *orec,
                                   unsigned long long *cursor) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const u64x2 v = *(const u64x2 *)&s[i];
         if (v[0] == EMPTY_KEY) continue;
-        unsigned long long at = atomicAdd(cursor, 1ull);
-        okeys[at] = v[0];
-        orec[at] = record_of_score((uint16_t)v[1]);
+        const uint16_t rec = record_of_score((uint16_t)v[1]);
+        d.orbit(v[0], [&](uint64_t k) {
+            const unsigned long long at = atomicAdd(cursor, 1ull);
+            okeys[at] = k;
+            orec[at] = rec;
+        });
     }
 }
 
@@ -289,6 +314,18 @@ struct DedupEstimate {
 
 // classify a finished tier table: scores in place, interior list, edge counts
 // (scr[0, S) edges by step, scr[9] interior count, scr[10] positions seen)
+// scr: [0, S) edges per tier step, [9] interior count, [10] positions, [11] positions with orbits
+template <class D>
+inline void launch_classify(hipStream_t st, const D &d, RSlot *slots, uint64_t cap, uint64_t *ikeys, uint32_t *islot,
+                            unsigned long long *scr, uint32_t *err) {
+    if (cap >= CLASSIFY_ROWS_MIN)
+        hipLaunchKernelGGL((classify_kernel<D, CROWS>), dim3(grid_for(cap / CROWS + 1)), dim3(256), 0, st, d, slots,
+                           cap, ikeys, islot, scr + 9, scr, scr + 10, err);
+    else
+        hipLaunchKernelGGL((classify_kernel<D, 1>), dim3(grid_for(cap)), dim3(256), 0, st, d, slots, cap, ikeys,
+                           islot, scr + 9, scr, scr + 10, err);
+}
+
 template <class D>
 inline int classify_tier_table(Ctx *c, const D &d, SpTier &T, unsigned long long *scr, uint32_t *d_err) {
     const uint64_t n = T.fcount;
@@ -296,8 +333,7 @@ inline int classify_tier_table(Ctx *c, const D &d, SpTier &T, unsigned long long
     GM_TRY(dev_alloc(c, (void **)&T.islot, std::max<uint64_t>(n, 1) * 4));
     GM_TRY(dev_alloc(c, (void **)&T.iwon, std::max<uint64_t>(n, 1)));
     GM_HIP(hipMemsetAsync(scr, 0, 16 * sizeof(unsigned long long), c->stream));
-    hipLaunchKernelGGL(classify_kernel<D>, dim3(grid_for(T.cap / CROWS + 1)), dim3(256), 0, c->stream, d, T.slots,
-                       T.cap, T.ikeys, T.islot, scr + 9, scr, scr + 10, d_err);
+    launch_classify(c->stream, d, T.slots, T.cap, T.ikeys, T.islot, scr, d_err);
     GM_HIP(hipGetLastError());
     return GM_OK;
 }

@@ -96,10 +96,14 @@ enum {
                                critical path; the results are NOT valid.  0 (default) = off. */
     GM_OPT_DIST_SYMMETRY = 11, /* sharded SUBTRACT path: 1 (default) = fill halo blocks that are a heap
                                  permutation of an own block locally, 0 = receive every halo block */
-    GM_OPT_DIST_OWNER = 13  /* sharded SUBTRACT path, block owner: 0 = split the top heaps in halves
+    GM_OPT_DIST_OWNER = 13, /* sharded SUBTRACT path, block owner: 0 = split the top heaps in halves
                                (rank bit a = [heap >= 8]); 1 = tier-balanced: rank bits compare two
                                heaps ([h_x < h_y]) while enough heaps remain, [heap >= 8] after, so
                                every rank holds a share of every tier (needs GM_OPT_DIST_SYMMETRY 1) */
+    GM_OPT_SYMMETRY = 14    /* sparse engines, symmetry reduction (the reference's unused
+                               hook othello_bit_new.py:224-235): 1 (default) = TOOT stores one position
+                               per left-right mirror pair when the root is its own mirror image; every
+                               count, export, query and digest still covers both positions.  0 = off */
 };
 
 /* Buffer roles for gm_adopt_buffer. */

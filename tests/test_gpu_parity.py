@@ -275,6 +275,65 @@ def test_toot_large_boards_vs_oracle_digest(board, ranks):
     assert ctx.digest() == (ref["digest"], ref["positions"])
 
 
+def _toot_mirror(k, L, H):
+    """Left-right mirror of a Toot key (planes at bits 16 and 16 + L*H, cell L*y + x)."""
+    A = L * H
+
+    def plane(p):
+        return sum(((p >> (L * y + x)) & 1) << (L * y + L - 1 - x) for y in range(H) for x in range(L))
+
+    return (k & 0xFFFF) | (plane((k >> 16) & ((1 << A) - 1)) << 16) | (plane((k >> (A + 16)) & ((1 << A) - 1)) << (A + 16))
+
+
+@pytest.mark.parametrize("board", ["toot_4x4", "toot_5x4"])
+@pytest.mark.parametrize("ranks", [1, 8])
+def test_toot_symmetry_off_matches_oracle_and_halves_tables(board, ranks):
+    """GM_OPT_SYMMETRY: with the mirror reduction off the solve gives the
+    same oracle digest; on (the default) it stores about half the positions (the tables
+    are sized from predicted insert counts, so their bytes shrink a little less)."""
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))[board]
+    L, H = (int(v) for v in board.split("_")[1].split("x"))
+    bytes_ = {}
+    for sym in (0, 1):
+        ctx = Context(TOOT, (L, H), device=0)
+        ctx.set_option(_lib.OPT_SYMMETRY, sym)
+        if ranks > 1:
+            ctx.set_option(_lib.OPT_VIRTUAL_RANKS, ranks)
+        n, rec = ctx.solve(ctx.initial())
+        assert n == ref["positions"] and rec == ref["root_record"]
+        assert [int(x) for x in ctx.tier_counts()] == ref["per_ply"]
+        assert ctx.digest() == (ref["digest"], ref["positions"])
+        bytes_[sym] = ctx.stats()["table_bytes"]
+        ctx.close()
+    assert bytes_[1] < 0.8 * bytes_[0]
+
+
+@pytest.mark.parametrize("ranks", [1, 3])
+def test_toot_symmetry_custom_roots_vs_oracle(oracle, ranks):
+    """Roots other than the empty board (Toot 4x3): a mirror-symmetric grandchild keeps the
+    reduction on, an asymmetric child turns it off; both tables equal the C oracle's,
+    mirror images included, and queries of mirror images agree."""
+    hd = games.HostDescriptor(games.TootCodec(4, 3))
+    root = hd.initial()
+    _, kids, _ = hd.expand(root)
+    grand = [g for k in kids for g in hd.expand(k)[1]]
+    sym_root = next(g for g in grand if _toot_mirror(g, 4, 3) == g)
+    asym_root = next(k for k in kids if _toot_mirror(k, 4, 3) != k)
+    hd.close()
+    for r in (sym_root, asym_root):
+        ok, orec = oracle.solve(TOOT, (4, 3), root=r)
+        ctx = Context(TOOT, (4, 3), device=0)
+        if ranks > 1:
+            ctx.set_option(_lib.OPT_VIRTUAL_RANKS, ranks)
+        n, rec = ctx.solve(r)
+        k, rr = ctx.export()
+        assert n == len(ok) and np.array_equal(k, ok) and np.array_equal(rr, orec)
+        mk = np.array([_toot_mirror(int(x), 4, 3) for x in ok[:2000]], dtype=np.uint64)
+        if r == sym_root:
+            assert np.array_equal(ctx.query(mk), ctx.query(ok[:2000]))
+        ctx.close()
+
+
 @pytest.mark.parametrize("ranks", [1, 8])
 def test_toot_full_table_rerun(monkeypatch, ranks):
     """A pinned, far too small distinct-child prediction fills every large tier
