@@ -100,3 +100,32 @@ def test_launcher_solves_a_descriptorless_plugin(tmp_path):
     from gamesmanmpi_amd.persist import read_reference_tables
     back = read_reference_tables(str(tmp_path))
     assert back[str((5, 6, 7))] == table[(5, 6, 7)]
+
+
+@pytest.mark.parametrize("rel", ["test_games/mttt.py", "test_games/tic_tac_toe_np.py", "tests/plugins/nim3.py"])
+def test_parallel_enumeration_equals_serial(monkeypatch, rel):
+    """Levels expanded by the spawned worker pool (forced on with PAR_MIN = 8) give the
+    serial walk's numbering, primitives and CSR exactly."""
+    from gamesmanmpi_amd import graph
+    mod = load_plugin(rel)
+    root = mod.initial_position()
+    serial = enumerate_graph(mod, root, workers=1)
+    monkeypatch.setattr(graph, "PAR_MIN", 8)
+    monkeypatch.setattr(graph, "BATCH", 64)
+    par = enumerate_graph(mod, root, workers=2)
+    assert [position_key(p) for p in par[0]] == [position_key(p) for p in serial[0]]
+    for a, b in zip(par[1:], serial[1:]):
+        assert np.array_equal(a, b)
+
+
+def test_enumeration_fails_fast_with_a_projection():
+    """Othello at its 8x8 default has no device descriptor: the walk stops with the level
+    sizes and the projected next level once the projection passes the limit."""
+    import time
+    from gamesmanmpi_amd.graph import TooLarge
+    mod = load_plugin("test_games/othello_bit_new.py")
+    assert games.identify(mod) is None
+    t = time.perf_counter()
+    with pytest.raises(TooLarge, match="projected"):
+        enumerate_graph(mod, mod.initial_position(), limit=20_000, workers=1)
+    assert time.perf_counter() - t < 60
