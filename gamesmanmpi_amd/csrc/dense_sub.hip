@@ -416,6 +416,78 @@ __device__ __forceinline__ uint32_t code_hi2(uint32_t o) { return (0xFF00FF00u -
 #ifndef GM_B4_STORE_CPOL
 #define GM_B4_STORE_CPOL 16   // sc1: write-through, the stored block does not stay in L2 (0 = plain)
 #endif
+template <int NMAX>
+__device__ __forceinline__ void p4_fold(const u32x4v (&v)[NMAX], uint32_t (&e)[4], uint32_t (&o)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint32_t ev = v[0][j] & 0x00FF00FFu, ov = v[0][j];   // ov: odd bytes valid in the high byte of each u16
+#pragma unroll
+        for (int m = 1; m < NMAX; m++) {
+            ev = pk_max(ev, v[m][j] & 0x00FF00FFu);
+            ov = pk_max(ov, v[m][j]);
+        }
+        e[j] = ev;
+        o[j] = ov;
+    }
+}
+// four blocks' folds of chunk c -> the byte image (position p: byte k = block k)
+__device__ __forceinline__ void p4_write_image(uint32_t *s, uint32_t c, const uint32_t (&e)[4][4],
+                                               const uint32_t (&o)[4][4]) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);
+        const uint32_t ye = __builtin_amdgcn_perm(e[3][j], e[2][j], 0x06020400u);
+        const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);
+        const uint32_t yo = __builtin_amdgcn_perm(o[3][j], o[2][j], 0x07030501u);
+        u32x4v q;
+        q[0] = __builtin_amdgcn_perm(ye, xe, 0x05040100u);   // 4j
+        q[1] = __builtin_amdgcn_perm(yo, xo, 0x05040100u);   // 4j+1
+        q[2] = __builtin_amdgcn_perm(ye, xe, 0x07060302u);   // 4j+2
+        q[3] = __builtin_amdgcn_perm(yo, xo, 0x07060302u);   // 4j+3
+        *(u32x4v *)(s + 16 * c + 4 * j) = q;
+    }
+}
+// the 2*HIGH child blocks of block hp: one whole-table descriptor, each child a
+// scalar offset (a missing child re-reads the first existing one; a block with
+// none, only high part 0, reads through a zero-size descriptor: all 0)
+// the folds of blocks 2 pr and 2 pr + 1 -> bytes 2 pr, 2 pr + 1 of the image's dwords (u16 stores)
+__device__ __forceinline__ void p4_write_pair(uint32_t *s, uint32_t c, int pr, const uint32_t (&e)[2][4],
+                                              const uint32_t (&o)[2][4]) {
+    char *const b = (char *)s;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);   // positions 4j | 4j+2
+        const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);   // positions 4j+1 | 4j+3
+        const uint32_t a = 4u * (16u * c + 4u * j) + 2u * (uint32_t)pr;
+        *(uint16_t *)(b + a) = (uint16_t)xe;
+        *(uint16_t *)(b + a + 4) = (uint16_t)xo;
+        *(uint16_t *)(b + a + 8) = (uint16_t)(xe >> 16);
+        *(uint16_t *)(b + a + 12) = (uint16_t)(xo >> 16);
+    }
+}
+template <int HIGH>
+__device__ __forceinline__ void p4_issue(uint8_t *table, uint32_t hp, bool valid, uint32_t c,
+                                         u32x4v (&v)[2 * HIGH > 0 ? 2 * HIGH : 1]) {
+    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
+    uint32_t soff[NMAX];
+    uint32_t first = 0;
+    bool any = false;
+#pragma unroll
+    for (int j = HIGH - 1; j >= 0; j--)
+        if (valid && ((hp >> (4 * j)) & 15u) >= 1) { first = (hp - (1u << (4 * j))) << 12; any = true; }
+#pragma unroll
+    for (int j = 0; j < HIGH; j++) {
+        const uint32_t h = (hp >> (4 * j)) & 15u;
+        soff[2 * j] = (valid && h >= 1) ? (hp - (1u << (4 * j))) << 12 : first;
+        soff[2 * j + 1] = (valid && h >= 2) ? (hp - (2u << (4 * j))) << 12 : first;
+    }
+    if constexpr (HIGH == 0) soff[0] = 0;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(table, 0, any ? 0xFFFFFFFFu : 0u, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < NMAX; m++)
+        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * c, soff[m], 0));
+}
+
 // One workgroup solves the four blocks hp[0..3] (valid[k] false: slot unused).
 // CPOL = cache policy of the child loads and the stores (0 plain; CPOL_SC1 in the
 // dataflow kernel, whose consumers may sit on another XCD: write-through stores,
@@ -666,78 +738,6 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
 #define GM_P4_WAVES 4   // waves per SIMD = workgroups of 4 waves per CU (5 fit the LDS but spill at 96 VGPRs)
 #endif
 constexpr int P4_PER_CU = GM_P4_WAVES;
-
-template <int NMAX>
-__device__ __forceinline__ void p4_fold(const u32x4v (&v)[NMAX], uint32_t (&e)[4], uint32_t (&o)[4]) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        uint32_t ev = v[0][j] & 0x00FF00FFu, ov = v[0][j];   // ov: odd bytes valid in the high byte of each u16
-#pragma unroll
-        for (int m = 1; m < NMAX; m++) {
-            ev = pk_max(ev, v[m][j] & 0x00FF00FFu);
-            ov = pk_max(ov, v[m][j]);
-        }
-        e[j] = ev;
-        o[j] = ov;
-    }
-}
-// four blocks' folds of chunk c -> the byte image (position p: byte k = block k)
-__device__ __forceinline__ void p4_write_image(uint32_t *s, uint32_t c, const uint32_t (&e)[4][4],
-                                               const uint32_t (&o)[4][4]) {
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);
-        const uint32_t ye = __builtin_amdgcn_perm(e[3][j], e[2][j], 0x06020400u);
-        const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);
-        const uint32_t yo = __builtin_amdgcn_perm(o[3][j], o[2][j], 0x07030501u);
-        u32x4v q;
-        q[0] = __builtin_amdgcn_perm(ye, xe, 0x05040100u);   // 4j
-        q[1] = __builtin_amdgcn_perm(yo, xo, 0x05040100u);   // 4j+1
-        q[2] = __builtin_amdgcn_perm(ye, xe, 0x07060302u);   // 4j+2
-        q[3] = __builtin_amdgcn_perm(yo, xo, 0x07060302u);   // 4j+3
-        *(u32x4v *)(s + 16 * c + 4 * j) = q;
-    }
-}
-// the 2*HIGH child blocks of block hp: one whole-table descriptor, each child a
-// scalar offset (a missing child re-reads the first existing one; a block with
-// none, only high part 0, reads through a zero-size descriptor: all 0)
-// the folds of blocks 2 pr and 2 pr + 1 -> bytes 2 pr, 2 pr + 1 of the image's dwords (u16 stores)
-__device__ __forceinline__ void p4_write_pair(uint32_t *s, uint32_t c, int pr, const uint32_t (&e)[2][4],
-                                              const uint32_t (&o)[2][4]) {
-    char *const b = (char *)s;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);   // positions 4j | 4j+2
-        const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);   // positions 4j+1 | 4j+3
-        const uint32_t a = 4u * (16u * c + 4u * j) + 2u * (uint32_t)pr;
-        *(uint16_t *)(b + a) = (uint16_t)xe;
-        *(uint16_t *)(b + a + 4) = (uint16_t)xo;
-        *(uint16_t *)(b + a + 8) = (uint16_t)(xe >> 16);
-        *(uint16_t *)(b + a + 12) = (uint16_t)(xo >> 16);
-    }
-}
-template <int HIGH>
-__device__ __forceinline__ void p4_issue(uint8_t *table, uint32_t hp, bool valid, uint32_t c,
-                                         u32x4v (&v)[2 * HIGH > 0 ? 2 * HIGH : 1]) {
-    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
-    uint32_t soff[NMAX];
-    uint32_t first = 0;
-    bool any = false;
-#pragma unroll
-    for (int j = HIGH - 1; j >= 0; j--)
-        if (valid && ((hp >> (4 * j)) & 15u) >= 1) { first = (hp - (1u << (4 * j))) << 12; any = true; }
-#pragma unroll
-    for (int j = 0; j < HIGH; j++) {
-        const uint32_t h = (hp >> (4 * j)) & 15u;
-        soff[2 * j] = (valid && h >= 1) ? (hp - (1u << (4 * j))) << 12 : first;
-        soff[2 * j + 1] = (valid && h >= 2) ? (hp - (2u << (4 * j))) << 12 : first;
-    }
-    if constexpr (HIGH == 0) soff[0] = 0;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(table, 0, any ? 0xFFFFFFFFu : 0u, 0x00020000);
-#pragma unroll
-    for (int m = 0; m < NMAX; m++)
-        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * c, soff[m], 0));
-}
 
 template <int HIGH>
 __global__ __launch_bounds__(256, GM_P4_WAVES) void sub_tier_kernel_p4(uint8_t *__restrict__ table,

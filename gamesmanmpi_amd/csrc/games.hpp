@@ -228,6 +228,16 @@ struct DescToot {
     }
 };
 
+// the descriptor with its symmetry reduction off: where only a child's tier matters
+// (classify's edge counts), canonicalising every child is wasted work
+template <class D>
+GM_HD D unreduced(const D &d) { return d; }
+GM_HD DescToot unreduced(const DescToot &d) {
+    DescToot r = d;
+    r.sym = 0;
+    return r;
+}
+
 // ---------------------------------------------------------------- Othello
 // reference test_games/othello_bit_new.py (square boards).  Key = all 2A+16
 // string bits: WHITE plane at [A+16, 2A+16), BLACK plane at [16, A+16), the

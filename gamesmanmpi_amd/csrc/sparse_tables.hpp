@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ 
                 } else {
                     const int64_t tk = d.tier(k[r]);
                     int nk = 0;
-                    d.visit(k[r], [&](uint64_t c) {
+                    unreduced(d).visit(k[r], [&](uint64_t c) {   // tiers only: no canonical children
                         const int64_t dt = d.tier(c) - tk;
                         nk++;
                         if (dt < 1 || dt > S) atomicOr(err, DEV_ERR_TIER);
