@@ -40,6 +40,7 @@ struct Sparse {
     int64_t plan_key[7] = {0, 0, 0, 0, 0, 0, 0};   // game, params[0..3], root, symmetry
     unsigned long long *d_replay = nullptr;     // replay results: counts | 16 classify counters per tier | err | root
     unsigned long long *h_replay = nullptr;     // pinned host copy
+    ResRef *d_tabs = nullptr;                   // the tier tables, for the one-launch refill
     uint64_t replay_words = 0;
     hipGraphExec_t graph = nullptr;
 };
@@ -110,6 +111,113 @@ __global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restr
         if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
         self.s[islot[i]].score = parent_score(best);
     }
+}
+
+// Small tiers (fewer than SPLIT_MAX interior positions): latency, not throughput,
+// bounds a tier, and with one lane per parent a lane walks its children's inserts
+// (or lookups) one after the other.  The split kernels give each parent G = 16
+// lanes of one DPP row; lane j handles the parent's children j, j + G, ...  (every
+// lane runs the descriptor's move generator, which is arithmetic only), so the
+// memory round trips of one parent overlap.  The won flag (expand) is a ballot over
+// the row, the best child score (retro) a max over the row.
+constexpr uint64_t SPLIT_MAX = 1ull << 16;
+constexpr int SPLIT_G = 16;
+
+template <class D>
+__global__ __launch_bounds__(256) void expand_split_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n,
+                                                           Fronts<D::MAX_SKIP> next, uint8_t *__restrict__ iwon,
+                                                           uint32_t *err) {
+    constexpr int S = D::MAX_SKIP, G = SPLIT_G;
+    uint64_t fresh[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) fresh[s] = 0;
+    const int sub = threadIdx.x % G, row = (threadIdx.x & 63) & ~(G - 1);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x / G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G; i < n; i += stride) {
+        const uint64_t k = ikeys[i];
+        const int64_t tk = d.tier(k);
+        bool won = false;
+        int idx = 0;
+        d.visit(k, [&](uint64_t c) {
+            if (idx++ % G != sub) return true;
+            const int64_t dt = d.tier(c) - tk;
+#pragma unroll
+            for (int s = 0; s < S; s++)
+                if (dt == s + 1 && front_insert(next.t[s], c, err)) fresh[s]++;
+            if (!won) won = d.primitive(c) == LOSS;
+            return true;
+        });
+        const uint64_t m = (__ballot(won) >> row) & ((1ull << G) - 1);
+        if (sub == 0) iwon[i] = m ? 1 : 0;
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
+}
+
+template <class D>
+__global__ __launch_bounds__(256) void retro_split_kernel(D d, const uint64_t *__restrict__ ikeys,
+                                                          const uint32_t *__restrict__ islot,
+                                                          const uint8_t *__restrict__ iwon, uint64_t n, ResRef self,
+                                                          Ress<D::MAX_SKIP> next, uint32_t *err) {
+    constexpr int S = D::MAX_SKIP, G = SPLIT_G;
+    const int sub = threadIdx.x % G;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x / G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G; i < n; i += stride) {
+        uint32_t best = 0;
+        if (iwon[i]) {   // a LOSS-in-0 child: nothing beats it, no lookup needed
+            best = 0xFFFFu;
+        } else {
+            const uint64_t k = ikeys[i];
+            const int64_t tk = d.tier(k);
+            int idx = 0;
+            d.visit(k, [&](uint64_t c) {
+                if (idx++ % G != sub) return true;
+                const int p = d.primitive(c);
+                uint32_t sc;
+                if (p != UNDECIDED) {
+                    sc = score_of_primitive(p);
+                } else {
+                    const int64_t dt = d.tier(c) - tk;
+                    int f = -1;
+#pragma unroll
+                    for (int s = 0; s < S; s++)
+                        if (dt == s + 1) f = res_find(next.t[s], c);
+                    if (f < 0) { atomicOr(err, DEV_ERR_MISSING_CHILD); f = 0; }
+                    sc = (uint32_t)f;
+                }
+                best = max(best, sc);
+                return best != 0xFFFFu;
+            });
+        }
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, o, G));
+        if (sub == 0) {
+            if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
+            self.s[islot[i]].score = parent_score(best);
+        }
+    }
+}
+
+// expand / retro of one tier: the split kernels below SPLIT_MAX interior positions
+template <class D>
+static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fronts<D::MAX_SKIP> &nx, uint32_t *err) {
+    if (T.ni < SPLIT_MAX)
+        hipLaunchKernelGGL(expand_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys, T.ni,
+                           nx, T.iwon, err);
+    else
+        hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.ikeys, T.ni, nx, T.iwon,
+                           err);
+}
+
+template <class D>
+static void launch_retro(hipStream_t st, const D &d, const SpTier &T, const ResRef &self,
+                         const Ress<D::MAX_SKIP> &nx, uint32_t *err) {
+    if (T.ni < SPLIT_MAX)
+        hipLaunchKernelGGL(retro_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys,
+                           T.islot, T.iwon, T.ni, self, nx, err);
+    else
+        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.ikeys, T.islot, T.iwon,
+                           T.ni, self, nx, err);
 }
 
 // ----------------------------------------------------------------- host side
@@ -183,13 +291,19 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
         uint32_t *err = (uint32_t *)(sp->d_replay + NC + 16 * T);
         auto fref = [&](size_t u) { return FrontRef{u < T ? sp->tiers[u].slots : nullptr, u < T ? sp->tiers[u].cap : 0,
                                                     cnt + u}; };
+        std::vector<ResRef> tabs(T);
+        uint64_t maxcap = 1;
+        for (size_t t = 0; t < T; t++) {
+            tabs[t] = res_ref(sp, t);
+            maxcap = std::max(maxcap, sp->tiers[t].cap);
+        }
+        GM_HIP(hipMalloc(&sp->d_tabs, T * sizeof(ResRef)));
+        GM_HIP(hipMemcpy(sp->d_tabs, tabs.data(), T * sizeof(ResRef), hipMemcpyHostToDevice));
         hipGraph_t g;
         GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         GM_HIP(hipMemsetAsync(sp->d_replay, 0, sp->replay_words * 8, c->stream));
-        for (size_t t = 0; t < T; t++)
-            if (sp->tiers[t].cap)
-                hipLaunchKernelGGL(slot_fill_kernel, dim3(grid_for(sp->tiers[t].cap)), dim3(256), 0, c->stream,
-                                   sp->tiers[t].slots, sp->tiers[t].cap);
+        hipLaunchKernelGGL(slot_fill_many_kernel, dim3(grid_for(maxcap), (unsigned)T), dim3(256), 0, c->stream,
+                           sp->d_tabs);   // refill every tier table with one launch
         hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, fref(0), root, err);
         for (size_t t = 0; t < T; t++) {
             SpTier &Tt = sp->tiers[t];
@@ -199,8 +313,7 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
             if (!Tt.ni) continue;
             Fronts<S> nx;   // a tier past the last one received nothing: no table (cap 0)
             for (int s = 0; s < S; s++) nx.t[s] = fref(t + 1 + s);
-            hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(Tt.ni)), dim3(256), 0, c->stream, d, Tt.ikeys, Tt.ni,
-                               nx, Tt.iwon, err);
+            launch_expand(c->stream, d, Tt, nx, err);
         }
         for (size_t tt = T; tt-- > 0;) {
             SpTier &Tt = sp->tiers[tt];
@@ -210,8 +323,7 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
                 const size_t u = tt + 1 + s;
                 nx.t[s] = u < T ? res_ref(sp, u) : ResRef{nullptr, 0};
             }
-            hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(Tt.ni)), dim3(256), 0, c->stream, d, Tt.ikeys, Tt.islot,
-                               Tt.iwon, Tt.ni, res_ref(sp, tt), nx, err);
+            launch_retro(c->stream, d, Tt, res_ref(sp, tt), nx, err);
         }
         hipLaunchKernelGGL(res_lookup_one_kernel, dim3(1), dim3(64), 0, c->stream, res_ref(sp, 0), d.canon(root),
                            rootw);
@@ -300,8 +412,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         for (int attempt = 0;; attempt++) {
             Fronts<S> nx;
             for (int s = 0; s < S; s++) nx.t[s] = front_ref(sp, t + 1 + s);
-            hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(sp->tiers[t].ni)), dim3(256), 0, c->stream, d,
-                               sp->tiers[t].ikeys, sp->tiers[t].ni, nx, sp->tiers[t].iwon, sp->d_err);
+            launch_expand(c->stream, d, sp->tiers[t], nx, sp->d_err);
             GM_HIP(hipGetLastError());
             uint32_t e;
             GM_HIP(hipMemcpyAsync(&e, sp->d_err, 4, hipMemcpyDeviceToHost, c->stream));
@@ -343,8 +454,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
             const size_t u = tt + 1 + s;
             nx.t[s] = u < sp->tiers.size() ? res_ref(sp, u) : ResRef{nullptr, 0};
         }
-        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, d, T.ikeys, T.islot,
-                           T.iwon, T.ni, res_ref(sp, tt), nx, sp->d_err);
+        launch_retro(c->stream, d, T, res_ref(sp, tt), nx, sp->d_err);
     }
     GM_HIP(hipGetLastError());
     GM_TRY(read_err(c, sp));
@@ -505,7 +615,8 @@ void sparse_free(Ctx *c) {
     for (auto &T : sp->tiers) free_tier(c, T);
     (void)hipStreamSynchronize(c->stream);
     if (sp->graph) (void)hipGraphExecDestroy(sp->graph);
-    for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err, (void *)sp->d_replay})
+    for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err, (void *)sp->d_replay,
+                    (void *)sp->d_tabs})
         if (p) (void)hipFree(p);
     if (sp->h_replay) (void)hipHostFree(sp->h_replay);
     delete sp;

@@ -104,6 +104,13 @@ __global__ void slot_fill_kernel(RSlot *s, uint64_t n) {
         *(u64x2 *)&s[i] = u64x2{EMPTY_KEY, 0};
 }
 
+// every table of a replay in one launch: blockIdx.y = table, x strides inside it
+__global__ void slot_fill_many_kernel(const ResRef *__restrict__ t) {
+    const ResRef r = t[blockIdx.y];
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < r.cap; i += (uint64_t)gridDim.x * blockDim.x)
+        *(u64x2 *)&r.s[i] = u64x2{EMPTY_KEY, 0};
+}
+
 __global__ void front_rehash_kernel(const RSlot *__restrict__ old, uint64_t ocap, FrontRef dst, uint32_t *err) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ocap;
          i += (uint64_t)gridDim.x * blockDim.x) {
