@@ -537,4 +537,13 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException as e:   # one error line on rank 0 instead of a bare traceback
+        import traceback
+        traceback.print_exc()
+        if int(os.environ.get("RANK", 0)) == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "error": "%s: %s" % (type(e).__name__, e)}), flush=True)
+        sys.exit(1)
