@@ -496,7 +496,10 @@ constexpr int CPOL_SC1 = 16;
 // XD (sharded solve): block k also goes to the extra destinations xdst[xoff[idx0 + k] ..
 // xoff[idx0 + k + 1]) -- symmetric-fill images in the table and halo ring slots --
 // from the same registers, so no separate fill / pack launch follows the tier.
-template <int HIGH, int CPOL, int LCPOL = CPOL, bool XD = false>
+// LAT (small tiers, latency-bound): all four blocks' child loads are issued before
+// any is folded -- one memory round trip instead of four -- at the price of the
+// VGPRs that limit the default kernel to 7 workgroups per CU.
+template <int HIGH, int CPOL, int LCPOL = CPOL, bool XD = false, bool LAT = false>
 __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint8_t *__restrict__ zero,
                                          const uint32_t (&hp)[4], const bool (&valid)[4], uint32_t *s,
                                          const uint32_t *__restrict__ xoff = nullptr,
@@ -507,7 +510,22 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
     static_assert(NCH == NT, "one chunk per thread");
 
     // ---- pass A: chunk tid = positions 16 tid .. 16 tid + 15
-    {
+    if constexpr (LAT && LCPOL == 0) {
+        const uint32_t c = tid;
+        u32x4v v[K][NMAX];
+#pragma unroll
+        for (int k = 0; k < K; k++) p4_issue<HIGH>(table, hp[k], valid[k], c, v[k]);
+#if GM_B4_LAT_BARRIER
+        __builtin_amdgcn_sched_barrier(0);   // keep every load ahead of the first fold
+#endif
+        uint32_t e[2][4], o[2][4];
+#pragma unroll
+        for (int k = 0; k < K; k += 2) {
+            p4_fold<NMAX>(v[k], e[0], o[0]);
+            p4_fold<NMAX>(v[k + 1], e[1], o[1]);
+            p4_write_pair(s, c, k >> 1, e, o);
+        }
+    } else {
         const uint32_t c = tid;
         Fold16 f[K];
 #pragma unroll
@@ -682,7 +700,7 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
     }
 }
 
-template <int HIGH>
+template <int HIGH, bool LAT = false>
 __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *__restrict__ table,
                                                           const uint32_t *__restrict__ blocks, uint32_t nblk,
                                                           const uint8_t *__restrict__ zero) {
@@ -697,12 +715,12 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *
         valid[k] = idx < nblk;
         hp[k] = valid[k] ? blocks[idx] : 0u;
     }
-    b4_solve<HIGH, GM_B4_STORE_CPOL, 0>(table, zero, hp, valid, s);
+    b4_solve<HIGH, GM_B4_STORE_CPOL, 0, false, LAT>(table, zero, hp, valid, s);
 }
 
 // The sharded solve's tier kernel (csrc/dist_sub.hip): as above, plus each block's
 // extra destinations (xoff / xdst indexed like `blocks`).
-template <int HIGH>
+template <int HIGH, bool LAT = false>
 __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t *__restrict__ table,
                                                            const uint32_t *__restrict__ blocks, uint32_t nblk,
                                                            const uint8_t *__restrict__ zero,
@@ -719,7 +737,7 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
         valid[k] = idx < nblk;
         hp[k] = valid[k] ? blocks[idx] : 0u;
     }
-    b4_solve<HIGH, 0, 0, true>(table, zero, hp, valid, s, xoff, xdst, grp * K);
+    b4_solve<HIGH, 0, 0, true, LAT>(table, zero, hp, valid, s, xoff, xdst, grp * K);
 }
 
 // ---------------------------------------------------------------------------
@@ -738,6 +756,10 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
 #define GM_P4_WAVES 4   // waves per SIMD = workgroups of 4 waves per CU (5 fit the LDS but spill at 96 VGPRs)
 #endif
 constexpr int P4_PER_CU = GM_P4_WAVES;
+constexpr uint32_t B4_LAT_MAX_BLOCKS = 0xFFFFFFFFu;   // every tier (measured: faster at all sizes)
+#ifndef GM_B4_LAT_BARRIER
+#define GM_B4_LAT_BARRIER 0
+#endif
 
 template <int HIGH>
 __global__ __launch_bounds__(256, GM_P4_WAVES) void sub_tier_kernel_p4(uint8_t *__restrict__ table,
@@ -1248,16 +1270,25 @@ static flow_kernel_t pick_flow(int high) {
     return nullptr;
 }
 
+template <bool LAT>
 static tier_kernel_t pick_b4(int high) {
     switch (high) {
-    case 0: return sub_tier_kernel_b4<0>;
-    case 1: return sub_tier_kernel_b4<1>;
-    case 2: return sub_tier_kernel_b4<2>;
-    case 3: return sub_tier_kernel_b4<3>;
-    case 4: return sub_tier_kernel_b4<4>;
-    case 5: return sub_tier_kernel_b4<5>;
+    case 0: return sub_tier_kernel_b4<0, LAT>;
+    case 1: return sub_tier_kernel_b4<1, LAT>;
+    case 2: return sub_tier_kernel_b4<2, LAT>;
+    case 3: return sub_tier_kernel_b4<3, LAT>;
+    case 4: return sub_tier_kernel_b4<4, LAT>;
+    case 5: return sub_tier_kernel_b4<5, LAT>;
     }
     return nullptr;
+}
+static tier_kernel_t pick_b4(int high) { return pick_b4<false>(high); }
+
+// Tiers of at most this many blocks (GM_B4_LAT overrides, development aid) run the
+// latency variant of the b4 kernel: every child load issued up front.
+static uint32_t b4_lat_max() {
+    static const uint32_t v = getenv("GM_B4_LAT") ? (uint32_t)atoi(getenv("GM_B4_LAT")) : B4_LAT_MAX_BLOCKS;
+    return v;
 }
 
 static tier_kernel_t pick_w1(int high) {
@@ -1356,6 +1387,8 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
         }
         const uint32_t ng = (nblocks + 3) / 4, cap = (uint32_t)(P4_PER_CU * cus) & ~7u;
         hipLaunchKernelGGL(pick_p4(high), dim3(ng <= cap ? ng : cap), dim3(256), 0, s, table, list, nblocks, zero);
+    } else if (nt == -2 && nblocks <= b4_lat_max()) {
+        hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
     } else if (nt <= 0)
         hipLaunchKernelGGL(pick_interleaved(high, nt), dim3((nblocks + 3) / 4), dim3(nt == -4 ? 64 : 256), 0, s, table,
                            list, nblocks, zero);
@@ -1365,16 +1398,18 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
 
 typedef void (*tier_kernel_x_t)(uint8_t *, const uint32_t *, uint32_t, const uint8_t *, const uint32_t *,
                                 const uint64_t *);
+template <bool LAT>
 static tier_kernel_x_t pick_b4x(int high) {
     switch (high) {
-    case 1: return sub_tier_kernel_b4x<1>;
-    case 2: return sub_tier_kernel_b4x<2>;
-    case 3: return sub_tier_kernel_b4x<3>;
-    case 4: return sub_tier_kernel_b4x<4>;
-    case 5: return sub_tier_kernel_b4x<5>;
+    case 1: return sub_tier_kernel_b4x<1, LAT>;
+    case 2: return sub_tier_kernel_b4x<2, LAT>;
+    case 3: return sub_tier_kernel_b4x<3, LAT>;
+    case 4: return sub_tier_kernel_b4x<4, LAT>;
+    case 5: return sub_tier_kernel_b4x<5, LAT>;
     }
     return nullptr;
 }
+static tier_kernel_x_t pick_b4x(int high) { return pick_b4x<false>(high); }
 
 static tier_kernel_x_t pick_w1x(int high) {
     switch (high) {
@@ -1392,7 +1427,8 @@ bool sub_kernel_x_exists(int high) { return pick_b4x(high) != nullptr && pick_w1
 void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
                        const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, bool wave) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(wave ? pick_w1x(high) : pick_b4x(high), dim3((nblocks + 3) / 4), dim3(wave ? 64 : 256), 0, s,
+    hipLaunchKernelGGL(wave ? pick_w1x(high) : nblocks <= b4_lat_max() ? pick_b4x<true>(high) : pick_b4x<false>(high),
+                       dim3((nblocks + 3) / 4), dim3(wave ? 64 : 256), 0, s,
                        table, list, nblocks, zero, xoff, xdst);
 }
 
