@@ -701,7 +701,7 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
 }
 
 template <int HIGH, bool LAT = false>
-__global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *__restrict__ table,
+__global__ __launch_bounds__(256, LAT ? GM_B4_LAT_WAVES : GM_B4_WAVES) void sub_tier_kernel_b4(uint8_t *__restrict__ table,
                                                           const uint32_t *__restrict__ blocks, uint32_t nblk,
                                                           const uint8_t *__restrict__ zero) {
     constexpr int K = 4;
@@ -757,6 +757,9 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
 #endif
 constexpr int P4_PER_CU = GM_P4_WAVES;
 constexpr uint32_t B4_LAT_MAX_BLOCKS = 0xFFFFFFFFu;   // every tier (measured: faster at all sizes)
+#ifndef GM_B4_LAT_WAVES
+#define GM_B4_LAT_WAVES 1   // min waves per SIMD for the latency form (1: the compiler's choice, 126 VGPRs)
+#endif
 #ifndef GM_B4_LAT_BARRIER
 #define GM_B4_LAT_BARRIER 0
 #endif
