@@ -413,6 +413,9 @@ __device__ __forceinline__ uint32_t code_hi2(uint32_t o) { return (0xFF00FF00u -
 #ifndef GM_B4_WAVES
 #define GM_B4_WAVES 1
 #endif
+#ifndef GM_B4_LAT_WAVES
+#define GM_B4_LAT_WAVES 1   // min waves per SIMD for the latency form (1: the compiler's choice, 126 VGPRs)
+#endif
 #ifndef GM_B4_STORE_CPOL
 #define GM_B4_STORE_CPOL 16   // sc1: write-through, the stored block does not stay in L2 (0 = plain)
 #endif
@@ -757,9 +760,6 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
 #endif
 constexpr int P4_PER_CU = GM_P4_WAVES;
 constexpr uint32_t B4_LAT_MAX_BLOCKS = 0xFFFFFFFFu;   // every tier (measured: faster at all sizes)
-#ifndef GM_B4_LAT_WAVES
-#define GM_B4_LAT_WAVES 1   // min waves per SIMD for the latency form (1: the compiler's choice, 126 VGPRs)
-#endif
 #ifndef GM_B4_LAT_BARRIER
 #define GM_B4_LAT_BARRIER 0
 #endif
