@@ -66,6 +66,27 @@ def test_othello_4x4():
     assert rec == (1 << 14) | 12         # LOSS in 12
 
 
+@pytest.mark.parametrize("ranks", [1, 4])
+def test_othello_custom_roots_vs_oracle(oracle, ranks):
+    """Othello 4x4 from positions two and four plies in (the launcher's --custom path),
+    one GPU and hash-sharded, against the C oracle."""
+    hd = games.HostDescriptor(games.OthelloCodec(4, 4))
+    level = [hd.initial()]
+    for ply in range(1, 5):
+        level = sorted({c for k in level for c in hd.expand(k)[1]})
+        if ply in (2, 4):
+            r = level[len(level) // 2]
+            ok, orec = oracle.solve(OTH, (4, 4), root=r)
+            ctx = Context(OTH, (4, 4), device=0)
+            if ranks > 1:
+                ctx.set_option(_lib.OPT_VIRTUAL_RANKS, ranks)
+            n, rec = ctx.solve(r)
+            k, rr = ctx.export()
+            assert n == len(ok) and np.array_equal(k, ok) and np.array_equal(rr, orec)
+            ctx.close()
+    hd.close()
+
+
 @pytest.mark.parametrize("game,params,name", [(OTH, (4, 4), "othello_4x4"), (TOOT, (4, 3), "toot_4x3"),
                                               (F2O, (), "four_to_one_six")])
 def test_sparse_replay_is_identical(game, params, name):
