@@ -309,7 +309,7 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
             SpTier &Tt = sp->tiers[t];
             if (!Tt.count) continue;
             unsigned long long *scr = tscr + 16 * t;
-            launch_classify(c->stream, d, Tt.slots, Tt.cap, Tt.ikeys, Tt.islot, scr, err);
+            launch_classify<D, false>(c->stream, d, Tt.slots, Tt.cap, Tt.ikeys, Tt.islot, scr, err);
             if (!Tt.ni) continue;
             Fronts<S> nx;   // a tier past the last one received nothing: no table (cap 0)
             for (int s = 0; s < S; s++) nx.t[s] = fref(t + 1 + s);

@@ -143,7 +143,7 @@ __global__ void front_insert_one_kernel(FrontRef t, uint64_t key, uint32_t *err)
 // turn (Othello 4x4: classify 0.1-0.4 ms per tier, most of the solve).
 constexpr int CROWS = 16;
 constexpr uint64_t CLASSIFY_ROWS_MIN = 1ull << 22;
-template <class D, int ROWS>
+template <class D, int ROWS, bool COUNT = true>
 __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ slots, uint64_t cap,
                                                        uint64_t *__restrict__ ikeys, uint32_t *__restrict__ islot,
                                                        unsigned long long *icount, unsigned long long *edges,
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ 
                 interior = p == UNDECIDED;
                 if (!interior) {
                     *(u64x2 *)&slots[i] = u64x2{k[r], (uint64_t)score_of_primitive(p)};
-                } else {
+                } else if (COUNT) {   // a replay knows its sizes: no edge counts
                     const int64_t tk = d.tier(k[r]);
                     int nk = 0;
                     unreduced(d).visit(k[r], [&](uint64_t c) {   // tiers only: no canonical children
@@ -322,14 +322,14 @@ struct DedupEstimate {
 // classify a finished tier table: scores in place, interior list, edge counts
 // (scr[0, S) edges by step, scr[9] interior count, scr[10] positions seen)
 // scr: [0, S) edges per tier step, [9] interior count, [10] positions, [11] positions with orbits
-template <class D>
+template <class D, bool COUNT = true>
 inline void launch_classify(hipStream_t st, const D &d, RSlot *slots, uint64_t cap, uint64_t *ikeys, uint32_t *islot,
                             unsigned long long *scr, uint32_t *err) {
     if (cap >= CLASSIFY_ROWS_MIN)
-        hipLaunchKernelGGL((classify_kernel<D, CROWS>), dim3(grid_for(cap / CROWS + 1)), dim3(256), 0, st, d, slots,
-                           cap, ikeys, islot, scr + 9, scr, scr + 10, err);
+        hipLaunchKernelGGL((classify_kernel<D, CROWS, COUNT>), dim3(grid_for(cap / CROWS + 1)), dim3(256), 0, st, d,
+                           slots, cap, ikeys, islot, scr + 9, scr, scr + 10, err);
     else
-        hipLaunchKernelGGL((classify_kernel<D, 1>), dim3(grid_for(cap)), dim3(256), 0, st, d, slots, cap, ikeys,
+        hipLaunchKernelGGL((classify_kernel<D, 1, COUNT>), dim3(grid_for(cap)), dim3(256), 0, st, d, slots, cap, ikeys,
                            islot, scr + 9, scr, scr + 10, err);
 }
 
