@@ -43,6 +43,12 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# The sharded solve drives a compute stream and one exchange stream per split heap
+# (3 at 8 GPUs) beside torch's streams; with HIP's default of 4 hardware queues some
+# share a queue, and a blocked RCCL receive then holds back the kernels queued behind
+# it.  Read by HIP at initialisation, so set before torch is imported.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 EDGE_MODEL_BYTES_PER_POSITION = 15.5  # SURVEY §8d edge model, 1-B records: 1 write + 14.5 child reads (diagnostic)
 COMPULSORY_BYTES_PER_POSITION = 3.0  # SURVEY §8d compulsory bound with 1-B records: 1 write + 2 producer-tier reads

@@ -30,6 +30,7 @@ def _devices():
 
 
 def _rank_main(rank, world, game, params, opts, uidq, out):
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")   # as bench.py: a queue per stream
     try:
         import ctypes
         from gamesmanmpi_amd import Context, _lib
