@@ -475,6 +475,9 @@ __device__ __forceinline__ void p4_issue(uint8_t *table, uint32_t hp, bool valid
     uint32_t soff[NMAX];
     uint32_t first = 0;
     bool any = false;
+#if defined(GM_EXP) && (GM_EXP & 2)
+    valid = false;   // experiment: no child-block traffic (out-of-range loads return 0)
+#endif
 #pragma unroll
     for (int j = HIGH - 1; j >= 0; j--)
         if (valid && ((hp >> (4 * j)) & 15u) >= 1) { first = (hp - (1u << (4 * j))) << 12; any = true; }
@@ -741,6 +744,230 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
         hp[k] = valid[k] ? blocks[idx] : 0u;
     }
     b4_solve<HIGH, 0, 0, true, LAT>(table, zero, hp, valid, s, xoff, xdst, grp * K);
+}
+
+// ---------------------------------------------------------------------------
+// Walker form of the 4-block kernel (GM_OPT_SUB_INTERLEAVE 10, the default).
+//
+// Pass B of b4_solve maps thread (a0, a1) to the column c = tau - a0 - a1: 256
+// threads walk the block's 46 low tiers with one barrier each, and a thread has a
+// position in only 16 of them, so two thirds of pass B's issue slots -- measured:
+// pass B alone 2.4 ms of the 4.9 ms 2^32 solve -- are spent on idle lanes and
+// barriers.  Here ONE wave walks the whole block after pass A: lane (z = c,
+// yb) of the 64 takes the rows y = 4 yb .. 4 yb + 3 (y = a1) of column z and walks
+// p = 4 x + (y - 4 yb) (x = a0) in order, lane (z, yb) p steps after its start
+// z + 4 yb.  Every child of a position was made at least one step earlier:
+//   (z-1 | z-2)  lanes z-1 / z-2 of the same 16-lane row, one / two steps ago:
+//                DPP row_shr of their last two codes (z = 0, 1: bound_ctrl zero);
+//   (x-1 | x-2)  this lane, 4 / 8 steps ago: a ring of the last 8 codes in
+//                registers (x = 0, 1: the ring's initial zeros);
+//   (y-1 | y-2)  the image in LDS, where every code is stored as it is made:
+//                this lane one / two steps ago, or the row below (lane - 16) one
+//                or two steps ago -- one wave's LDS operations complete in
+//                order, so no barrier is needed; y = 0, 1 read two zero rows
+//                in front of every z slice.
+// 91 steps with 64 of 64 lanes busy in most of them, against 4 waves x 46 steps:
+// about half the VALU issue of pass B and no barrier.  The other three waves leave
+// after pass A (their registers go back to the CU for the next workgroup), the
+// walking wave writes the four blocks (pass C) itself.
+#ifndef GM_WK_ROT
+#define GM_WK_ROT 1   // the walking wave is wave (blockIdx & 3) of the workgroup
+#endif
+#ifndef GM_WK_WAVES
+#define GM_WK_WAVES 4   // waves per SIMD the register budget must allow (128 VGPRs)
+#endif
+constexpr int WK_ZS = 292;   // dwords per z slice of the image: 18 rows of 16 + 4 (bank spread for the walk)
+__device__ __forceinline__ uint32_t wk_chunk(uint32_t c) {   // image dword of position (0, c & 15, c >> 4)
+    return 16u * (c & 15u) + 32u + WK_ZS * (c >> 4);
+}
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t dpp_shr2(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+}
+// parent codes of the split halves (gm_common.hpp parent_code: (255 - b) + 2 (b >> 7)),
+// E: codes in the low byte of each u16 (high bytes zero); O: codes in the high byte
+__device__ __forceinline__ uint32_t wk_code_e(uint32_t e) { return (e ^ 0x00FF00FFu) + ((e >> 6) & 0x00020002u); }
+__device__ __forceinline__ uint32_t wk_code_o(uint32_t o) { return (~o & 0xFF00FF00u) + ((o >> 6) & 0x02000200u); }
+
+template <int HIGH, int CPOL, bool XD>
+__device__ __forceinline__ void wk_solve(uint8_t *__restrict__ table, const uint32_t (&hp)[4], const bool (&valid)[4],
+                                         uint32_t *s, const uint32_t *__restrict__ xoff = nullptr,
+                                         const uint64_t *__restrict__ xdst = nullptr, uint32_t idx0 = 0) {
+    constexpr int NPOS = 4096, K = 4;
+    constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
+    const int tid = threadIdx.x;
+
+    // ---- pass A (every child load of the four blocks in flight at once), into the padded image
+    {
+        const uint32_t c = tid;
+        // the zero rows y = -2, -1 of every z slice: 16 x 32 dwords
+        *(u32x2v *)(s + WK_ZS * (uint32_t)(tid >> 4) + 2u * (uint32_t)(tid & 15)) = u32x2v{0u, 0u};
+        u32x4v v[K][NMAX];
+#pragma unroll
+        for (int k = 0; k < K; k++) p4_issue<HIGH>(table, hp[k], valid[k], c, v[k]);
+        char *const b = (char *)s;
+        const uint32_t base = wk_chunk(c);
+#pragma unroll
+        for (int k = 0; k < K; k += 2) {
+            uint32_t e[2][4], o[2][4];
+            p4_fold<NMAX>(v[k], e[0], o[0]);
+            p4_fold<NMAX>(v[k + 1], e[1], o[1]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {   // bytes k, k+1 of positions 4j .. 4j+3 (see p4_write_pair)
+                const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);
+                const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);
+                const uint32_t a = 4u * (base + 4u * j) + 2u * (uint32_t)(k >> 1);
+                *(uint16_t *)(b + a) = (uint16_t)xe;
+                *(uint16_t *)(b + a + 4) = (uint16_t)xo;
+                *(uint16_t *)(b + a + 8) = (uint16_t)(xe >> 16);
+                *(uint16_t *)(b + a + 12) = (uint16_t)(xo >> 16);
+            }
+        }
+    }
+    __syncthreads();
+    // one wave walks and stores; which one rotates with the workgroup, so the walkers of
+    // the workgroups on a CU spread over its four SIMDs
+#if GM_WK_ROT
+    if ((uint32_t)(tid >> 6) != (blockIdx.x & 3u)) return;
+#else
+    if (tid >= 64) return;
+#endif
+    const int lane = tid & 63;
+
+    // ---- pass B: the walk
+    {
+        const uint32_t z = lane & 15, yb = lane >> 4;
+        const int s0 = (int)(z + 4u * yb);
+        const uint32_t lbase = 16u * (4u * yb + 2u) + WK_ZS * z;   // image dword of (0, 4 yb, z)
+        uint32_t re[8], ro[8];   // this lane's codes of the last 8 steps (split halves), ring by step
+#pragma unroll
+        for (int j = 0; j < 8; j++) re[j] = ro[j] = 0;
+#if defined(GM_EXP) && (GM_EXP & 1)
+        constexpr int TAU_END = 0;   // experiment: no pass B
+#else
+        constexpr int TAU_END = 91;  // p = tau - s0 in [0, 64), s0 <= 15 + 12
+#endif
+        // Only (y-1) -- the code this wave stored one step ago -- is on the step-to-step
+        // chain; the fold F and (y-2) of the next step are read a step ahead (any lane's
+        // address is clamped into its own column, an idle lane's values are unused).
+        // Addresses: p = t0 + j - s0 with t0 a multiple of 8, so (p >> 2, p & 3) =
+        // (t0 / 4 + ((j - s0) >> 2), (j - s0) & 3) and the image dword is
+        // lbase + t0 / 4 + cj[j]: one add per step.  An idle lane (p outside [0, 64))
+        // reads some dword of the image (unused), writes a dword of its own in the
+        // slice's spare tail, and records 0.
+        int cj[9];
+#pragma unroll
+        for (int j = 0; j < 9; j++) cj[j] = ((j - s0) >> 2) + 16 * ((j - s0) & 3);
+        const uint32_t dummy = WK_ZS * z + 288u + yb;
+        uint32_t Fv, Y2v;
+        {
+            const uint32_t o = lbase + cj[0];
+            Fv = s[o];
+            Y2v = s[o - 32];
+        }
+        for (int t0 = 0; t0 < TAU_END; t0 += 8) {
+            const uint32_t b0 = lbase + (uint32_t)(t0 >> 2);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t o = b0 + cj[j];
+                const uint32_t Y1 = s[o - 16];   // stored one step ago (this lane or the row below)
+                const uint32_t on = b0 + cj[j + 1];   // cj[8] = cj[0] + 2: the next t0's first step
+                const uint32_t Fn = s[on], Y2n = s[on - 32];
+                const uint32_t n1e = dpp_shr1(re[(j + 7) & 7]), n1o = dpp_shr1(ro[(j + 7) & 7]);
+                const uint32_t n2e = dpp_shr2(re[(j + 6) & 7]), n2o = dpp_shr2(ro[(j + 6) & 7]);
+                // all-ones on an active lane; opaque, so the compiler keeps this straight-line
+                // (a branch would sink the (y-1) read behind the prefetch)
+                uint32_t act = (uint32_t)(t0 + j - s0) < 64u ? ~0u : 0u;
+                asm volatile("" : "+v"(act));
+                const uint32_t pe = pk_max(pk_max(Fv & 0x00FF00FFu, Y2v & 0x00FF00FFu),
+                                           pk_max(pk_max(n2e, re[(j + 4) & 7]), re[j]));
+                const uint32_t po = pk_max(pk_max(Fv, Y2v), pk_max(pk_max(n2o, ro[(j + 4) & 7]), ro[j]));
+                const uint32_t me = pk_max(pk_max(pe, n1e), Y1 & 0x00FF00FFu);
+                const uint32_t mo = pk_max(pk_max(po, n1o), Y1);
+                re[j] = wk_code_e(me) & act;
+                ro[j] = wk_code_o(mo) & act;
+                s[dummy + ((o - dummy) & act)] = re[j] | ro[j];
+                Fv = Fn;
+                Y2v = Y2n;
+            }
+        }
+    }
+
+    // ---- pass C: the walking wave writes the four blocks (chunks lane + 64 i)
+    __amdgpu_buffer_rsrc_t wr[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) wr[k] = block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0);
+#if defined(GM_EXP) && (GM_EXP & 4)
+#pragma unroll
+    for (int k = 0; k < K; k++) wr[k] = block_rsrc(table, 0);   // experiment: stores dropped (out of range)
+#endif
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t c = (uint32_t)lane + 64u * i;
+        const uint32_t base = wk_chunk(c);
+        u32x4v out[K];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const u32x4v q = *(const u32x4v *)(s + base + 4 * j);
+            const uint32_t t01 = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u);
+            const uint32_t t23 = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u);
+            const uint32_t u01 = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);
+            const uint32_t u23 = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
+            out[0][j] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+            out[1][j] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+            out[2][j] = __builtin_amdgcn_perm(u23, u01, 0x05040100u);
+            out[3][j] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) __builtin_amdgcn_raw_buffer_store_b128(out[k], wr[k], 16u * c, 0, CPOL);
+        if constexpr (XD) {
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                if (!valid[k]) continue;
+                const uint32_t m1 = xoff[idx0 + k + 1];
+                for (uint32_t m = xoff[idx0 + k]; m < m1; m++)
+                    __builtin_amdgcn_raw_buffer_store_b128(out[k], block_rsrc((uint8_t *)xdst[m], NPOS), 16u * c, 0, 0);
+            }
+        }
+    }
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                                          uint32_t nblk, const uint8_t *__restrict__ zero) {
+    constexpr int K = 4;
+    __shared__ __attribute__((aligned(16))) uint32_t s[WK_ZS * 16];   // 18.25 KiB
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
+    uint32_t hp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = grp * K + k;
+        valid[k] = idx < nblk;
+        hp[k] = valid[k] ? blocks[idx] : 0u;
+    }
+    wk_solve<HIGH, GM_B4_STORE_CPOL, false>(table, hp, valid, s);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wkx(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                                           uint32_t nblk, const uint8_t *__restrict__ zero,
+                                                           const uint32_t *__restrict__ xoff,
+                                                           const uint64_t *__restrict__ xdst) {
+    constexpr int K = 4;
+    __shared__ __attribute__((aligned(16))) uint32_t s[WK_ZS * 16];
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
+    uint32_t hp[K];
+    bool valid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = grp * K + k;
+        valid[k] = idx < nblk;
+        hp[k] = valid[k] ? blocks[idx] : 0u;
+    }
+    wk_solve<HIGH, 0, true>(table, hp, valid, s, xoff, xdst, grp * K);
 }
 
 // ---------------------------------------------------------------------------
@@ -1294,6 +1521,12 @@ static uint32_t b4_lat_max() {
     return v;
 }
 
+// development aid: GM_PAD_LDS=<bytes> of unused dynamic LDS per workgroup (fewer workgroups per CU)
+static unsigned pad_lds() {
+    static const unsigned v = getenv("GM_PAD_LDS") ? (unsigned)atoi(getenv("GM_PAD_LDS")) : 0u;
+    return v;
+}
+
 static tier_kernel_t pick_w1(int high) {
     switch (high) {
     case 0: return sub_tier_kernel_w1<0>;
@@ -1302,6 +1535,18 @@ static tier_kernel_t pick_w1(int high) {
     case 3: return sub_tier_kernel_w1<3>;
     case 4: return sub_tier_kernel_w1<4>;
     case 5: return sub_tier_kernel_w1<5>;
+    }
+    return nullptr;
+}
+
+static tier_kernel_t pick_wk(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel_wk<0>;
+    case 1: return sub_tier_kernel_wk<1>;
+    case 2: return sub_tier_kernel_wk<2>;
+    case 3: return sub_tier_kernel_wk<3>;
+    case 4: return sub_tier_kernel_wk<4>;
+    case 5: return sub_tier_kernel_wk<5>;
     }
     return nullptr;
 }
@@ -1370,6 +1615,7 @@ static tier_kernel_t pick_kernel(int low, int high, int nt) {
 static tier_kernel_t pick_interleaved(int high, int nt) {
     if (nt == -4) return pick_w1(high);
     if (nt == -5) return pick_p4(high);
+    if (nt == -6) return pick_wk(high);
     return nt == -2 ? pick_b4(high) : pick_x4(high, nt == -1);
 }
 
@@ -1391,7 +1637,10 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
         const uint32_t ng = (nblocks + 3) / 4, cap = (uint32_t)(P4_PER_CU * cus) & ~7u;
         hipLaunchKernelGGL(pick_p4(high), dim3(ng <= cap ? ng : cap), dim3(256), 0, s, table, list, nblocks, zero);
     } else if (nt == -2 && nblocks <= b4_lat_max()) {
-        hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
+        hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), pad_lds(), s, table, list, nblocks,
+                           zero);
+    } else if (nt == -6) {
+        hipLaunchKernelGGL(pick_wk(high), dim3((nblocks + 3) / 4), dim3(256), pad_lds(), s, table, list, nblocks, zero);
     } else if (nt <= 0)
         hipLaunchKernelGGL(pick_interleaved(high, nt), dim3((nblocks + 3) / 4), dim3(nt == -4 ? 64 : 256), 0, s, table,
                            list, nblocks, zero);
@@ -1414,6 +1663,17 @@ static tier_kernel_x_t pick_b4x(int high) {
 }
 static tier_kernel_x_t pick_b4x(int high) { return pick_b4x<false>(high); }
 
+static tier_kernel_x_t pick_wkx(int high) {
+    switch (high) {
+    case 1: return sub_tier_kernel_wkx<1>;
+    case 2: return sub_tier_kernel_wkx<2>;
+    case 3: return sub_tier_kernel_wkx<3>;
+    case 4: return sub_tier_kernel_wkx<4>;
+    case 5: return sub_tier_kernel_wkx<5>;
+    }
+    return nullptr;
+}
+
 static tier_kernel_x_t pick_w1x(int high) {
     switch (high) {
     case 1: return sub_tier_kernel_w1x<1>;
@@ -1425,12 +1685,17 @@ static tier_kernel_x_t pick_w1x(int high) {
     return nullptr;
 }
 
-bool sub_kernel_x_exists(int high) { return pick_b4x(high) != nullptr && pick_w1x(high) != nullptr; }
+bool sub_kernel_x_exists(int high) {
+    return pick_b4x(high) != nullptr && pick_w1x(high) != nullptr && pick_wkx(high) != nullptr;
+}
 
+// kind: the sub_interleave option (8 one-wave kernel, 10 walker, otherwise the b4 kernel)
 void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
-                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, bool wave) {
+                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, int kind) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(wave ? pick_w1x(high) : nblocks <= b4_lat_max() ? pick_b4x<true>(high) : pick_b4x<false>(high),
+    const bool wave = kind == 8;
+    hipLaunchKernelGGL(wave ? pick_w1x(high) : kind == 10 ? pick_wkx(high)
+                       : nblocks <= b4_lat_max() ? pick_b4x<true>(high) : pick_b4x<false>(high),
                        dim3((nblocks + 3) / 4), dim3(wave ? 64 : 256), 0, s,
                        table, list, nblocks, zero, xoff, xdst);
 }
@@ -1442,6 +1707,7 @@ int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 7) return -3;
     if (low == 3 && c->sub_interleave == 8) return -4;
     if (low == 3 && c->sub_interleave == 9) return -5;
+    if (low == 3 && c->sub_interleave == 10) return -6;
     return c->sub_threads;
 }
 

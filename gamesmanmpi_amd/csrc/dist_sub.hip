@@ -567,7 +567,7 @@ static int exec_op(DistSub *d, SubRank &R, const Op &o) {
     switch (o.kind) {
     case OP_TIER:
         launch_sub_tier_x(d->high, cnt(R.off, j), R.table, R.dlist + R.off[j], d->zero, R.dxoff + R.off[j], R.dxdst,
-                          st, d->want_x4 == 8);
+                          st, d->want_x4);
         break;
     case OP_FILL:
     case OP_PACK:   // folded into OP_TIER (extra destinations); not in the lists

@@ -75,7 +75,7 @@ struct Ctx {
     int engine_opt = GM_ENGINE_AUTO;
     int sub_low = 3;
     int sub_threads = 128;
-    int sub_interleave = 6;      // 4 u16 image, 5 u16 + diagonal pass B, 6 byte image (default), 1 one block
+    int sub_interleave = 10;     // 4 u16 image, 5 u16 + diagonal pass B, 6 byte image, 10 walker (default), 1 one block
     int sub_order = 2;   // block order inside a tier: 0 key, 1 Morton, 2 Hilbert (default)
     bool use_graph = true;
     bool timing = false;
@@ -131,7 +131,7 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
 // the sharded solve's byte-image tier kernel with per-block extra destinations (LOW = 3)
 bool sub_kernel_x_exists(int high);
 void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
-                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, bool wave);
+                       const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, int kind);
 int sub_kernel_threads(const Ctx *c, int low);   // 0 = the 4-block interleaved kernel
 void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &tier_off, int high, int mode);
 

@@ -2,7 +2,7 @@
 """Summarise rocprofv3 kernel-trace / PMC CSVs of a bench run into profiles/.
 
     python tools/pmc_summary.py --kt gpurun_out/prof_kt --fetch gpurun_out/prof_fetch \
-        --write gpurun_out/prof_write --kernel sub_tier_kernel_b4 --launches-per-solve 76 \
+        --write gpurun_out/prof_write --kernel sub_tier_kernel_wk --launches-per-solve 76 \
         --tag r01_subtract8 [--traffic-json profiles/traffic_subtract8.json]
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in KiB,
