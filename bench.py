@@ -490,7 +490,7 @@ def main():
                      "traffic": traffic_launch,
                      "traffic_gbs": traffic_gbs,
                      "traffic_frac": (traffic_gbs / HBM_PEAK_GBS) if traffic_gbs else None,
-                     "kernel": "sub_tier_kernel_wk<%d>" % (args.heaps - 3),
+                     "kernel": "sub_tier_kernel_wk<%d> (tiers of >= 4096 blocks), sub_tier_kernel_b4<%d> (smaller)" % (args.heaps - 3, args.heaps - 3),
                      "algo_bytes_per_position": COMPULSORY_BYTES_PER_POSITION,
                      "algo_bytes_model": "compulsory: 1 B code written + 2 B producer-tier reads per position",
                      "launches_per_solve": launches_per_solve,

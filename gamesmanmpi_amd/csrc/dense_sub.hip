@@ -747,7 +747,7 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
 }
 
 // ---------------------------------------------------------------------------
-// Walker form of the 4-block kernel (GM_OPT_SUB_INTERLEAVE 10, the default).
+// Walker form of the 4-block kernel (GM_OPT_SUB_INTERLEAVE 10 and 11).
 //
 // Pass B of b4_solve maps thread (a0, a1) to the column c = tau - a0 - a1: 256
 // threads walk the block's 46 low tiers with one barrier each, and a thread has a
@@ -767,16 +767,30 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
 //                order, so no barrier is needed; y = 0, 1 read two zero rows
 //                in front of every z slice.
 // 91 steps with 64 of 64 lanes busy in most of them, against 4 waves x 46 steps:
-// about half the VALU issue of pass B and no barrier.  The other three waves leave
-// after pass A (their registers go back to the CU for the next workgroup), the
-// walking wave writes the four blocks (pass C) itself.
+// about half the VALU issue of pass B and no barrier.
+//
+// Option 10 (sub_tier_kernel_wk): 256 threads load (pass A), then one wave walks and
+// writes the blocks (pass C); the other three leave.  A per-workgroup trace
+// (GM_WK_TRACE build, tools/wk_trace.py) showed what that buys: an exited wave's
+// slot is not reused while its workgroup lives, so a CU holds 4 such workgroups
+// (128 VGPRs) and at any time ~2 of them walk while ~2 load -- the walk (9.9 us per
+// group) and the loads (9 us) alternate instead of overlapping.
+//
+// Option 11 (sub_tier_kernel_wkp, the default): persistent workgroups of 5 waves and two
+// images.  Four waves load and fold group i+1 into one image while the fifth walks
+// and writes group i from the other; one barrier per group.  A CU holds 3 of them
+// (15 waves of 128 VGPRs), each walking all the time while its loads are in flight.
 #ifndef GM_WK_ROT
-#define GM_WK_ROT 1   // the walking wave is wave (blockIdx & 3) of the workgroup
+#define GM_WK_ROT 1   // the walking wave rotates with the workgroup index (spread over the SIMDs)
 #endif
 #ifndef GM_WK_WAVES
 #define GM_WK_WAVES 4   // waves per SIMD the register budget must allow (128 VGPRs)
 #endif
+#ifndef GM_WKP_PER_CU
+#define GM_WKP_PER_CU 3   // persistent 320-thread workgroups per CU (5 waves x 128 VGPRs: 15 of 16 slots)
+#endif
 constexpr int WK_ZS = 292;   // dwords per z slice of the image: 18 rows of 16 + 4 (bank spread for the walk)
+constexpr int WK_IMG = WK_ZS * 16;   // dwords per image (18.25 KiB)
 __device__ __forceinline__ uint32_t wk_chunk(uint32_t c) {   // image dword of position (0, c & 15, c >> 4)
     return 16u * (c & 15u) + 32u + WK_ZS * (c >> 4);
 }
@@ -791,111 +805,130 @@ __device__ __forceinline__ uint32_t dpp_shr2(uint32_t v) {
 __device__ __forceinline__ uint32_t wk_code_e(uint32_t e) { return (e ^ 0x00FF00FFu) + ((e >> 6) & 0x00020002u); }
 __device__ __forceinline__ uint32_t wk_code_o(uint32_t o) { return (~o & 0xFF00FF00u) + ((o >> 6) & 0x02000200u); }
 
-template <int HIGH, int CPOL, bool XD>
-__device__ __forceinline__ void wk_solve(uint8_t *__restrict__ table, const uint32_t (&hp)[4], const bool (&valid)[4],
-                                         uint32_t *s, const uint32_t *__restrict__ xoff = nullptr,
-                                         const uint64_t *__restrict__ xdst = nullptr, uint32_t idx0 = 0) {
-    constexpr int NPOS = 4096, K = 4;
+#ifdef GM_WK_TRACE
+// diagnostic build only (-DGM_WK_TRACE): per-workgroup phase timestamps (s_memrealtime,
+// 100 MHz) and hardware ids, written by the walking wave's lane 0 with vector stores
+__device__ uint64_t *gm_trace_buf;
+__device__ uint32_t *gm_trace_cnt;
+__device__ __forceinline__ void wk_trace(uint64_t t0, uint64_t t1, uint64_t t2, uint32_t hp0, uint64_t tl, uint64_t tf) {
+    if (gm_trace_buf) {
+        const uint64_t t3 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t slot = atomicAdd(gm_trace_cnt, 1u);
+        if (slot < (1u << 20)) {
+            uint64_t *e = gm_trace_buf + 8ull * slot;
+            e[0] = t0; e[1] = t1; e[2] = t2; e[3] = t3;
+            e[4] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                   ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);   // HW_ID, XCC_ID
+            e[5] = (uint64_t)blockIdx.x | ((uint64_t)hp0 << 32);
+            e[6] = tl;   // the walking wave's loads all back
+            e[7] = tf;   // its folds written
+        }
+    }
+}
+#endif
+
+// pass A by 256 loader threads (lt = 0..255: chunk lt of all four blocks, every child
+// load in flight at once): the folds into image s; zero = also clear its zero rows
+template <int HIGH>
+__device__ __forceinline__ void wk_load(uint8_t *__restrict__ table, const uint32_t (&hp)[4], const bool (&valid)[4],
+                                        uint32_t *s, uint32_t lt, bool zero, uint64_t *tl = nullptr) {
+    constexpr int K = 4;
     constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
-    const int tid = threadIdx.x;
-
-    // ---- pass A (every child load of the four blocks in flight at once), into the padded image
-    {
-        const uint32_t c = tid;
-        // the zero rows y = -2, -1 of every z slice: 16 x 32 dwords
-        *(u32x2v *)(s + WK_ZS * (uint32_t)(tid >> 4) + 2u * (uint32_t)(tid & 15)) = u32x2v{0u, 0u};
-        u32x4v v[K][NMAX];
+    const uint32_t c = lt;
+    // the zero rows y = -2, -1 of every z slice: 16 x 32 dwords
+    if (zero) *(u32x2v *)(s + WK_ZS * (lt >> 4) + 2u * (lt & 15u)) = u32x2v{0u, 0u};
+    u32x4v v[K][NMAX];
 #pragma unroll
-        for (int k = 0; k < K; k++) p4_issue<HIGH>(table, hp[k], valid[k], c, v[k]);
-        char *const b = (char *)s;
-        const uint32_t base = wk_chunk(c);
+    for (int k = 0; k < K; k++) p4_issue<HIGH>(table, hp[k], valid[k], c, v[k]);
+#ifdef GM_WK_TRACE
+    __builtin_amdgcn_s_waitcnt(0);   // diagnostic: every load back before the first fold
+    if (tl) *tl = __builtin_amdgcn_s_memrealtime();
+#endif
+    char *const b = (char *)s;
+    const uint32_t base = wk_chunk(c);
 #pragma unroll
-        for (int k = 0; k < K; k += 2) {
-            uint32_t e[2][4], o[2][4];
-            p4_fold<NMAX>(v[k], e[0], o[0]);
-            p4_fold<NMAX>(v[k + 1], e[1], o[1]);
+    for (int k = 0; k < K; k += 2) {
+        uint32_t e[2][4], o[2][4];
+        p4_fold<NMAX>(v[k], e[0], o[0]);
+        p4_fold<NMAX>(v[k + 1], e[1], o[1]);
 #pragma unroll
-            for (int j = 0; j < 4; j++) {   // bytes k, k+1 of positions 4j .. 4j+3 (see p4_write_pair)
-                const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);
-                const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);
-                const uint32_t a = 4u * (base + 4u * j) + 2u * (uint32_t)(k >> 1);
-                *(uint16_t *)(b + a) = (uint16_t)xe;
-                *(uint16_t *)(b + a + 4) = (uint16_t)xo;
-                *(uint16_t *)(b + a + 8) = (uint16_t)(xe >> 16);
-                *(uint16_t *)(b + a + 12) = (uint16_t)(xo >> 16);
-            }
+        for (int j = 0; j < 4; j++) {   // bytes k, k+1 of positions 4j .. 4j+3 (see p4_write_pair)
+            const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);
+            const uint32_t xo = __builtin_amdgcn_perm(o[1][j], o[0][j], 0x07030501u);
+            const uint32_t a = 4u * (base + 4u * j) + 2u * (uint32_t)(k >> 1);
+            *(uint16_t *)(b + a) = (uint16_t)xe;
+            *(uint16_t *)(b + a + 4) = (uint16_t)xo;
+            *(uint16_t *)(b + a + 8) = (uint16_t)(xe >> 16);
+            *(uint16_t *)(b + a + 12) = (uint16_t)(xo >> 16);
         }
     }
-    __syncthreads();
-    // one wave walks and stores; which one rotates with the workgroup, so the walkers of
-    // the workgroups on a CU spread over its four SIMDs
-#if GM_WK_ROT
-    if ((uint32_t)(tid >> 6) != (blockIdx.x & 3u)) return;
-#else
-    if (tid >= 64) return;
-#endif
-    const int lane = tid & 63;
+}
 
-    // ---- pass B: the walk
-    {
-        const uint32_t z = lane & 15, yb = lane >> 4;
-        const int s0 = (int)(z + 4u * yb);
-        const uint32_t lbase = 16u * (4u * yb + 2u) + WK_ZS * z;   // image dword of (0, 4 yb, z)
-        uint32_t re[8], ro[8];   // this lane's codes of the last 8 steps (split halves), ring by step
+// pass B: one wave (lane 0..63) walks image s in place (folds in, codes out)
+__device__ __forceinline__ void wk_walk(uint32_t *s, uint32_t lane) {
+    const uint32_t z = lane & 15, yb = lane >> 4;
+    const int s0 = (int)(z + 4u * yb);
+    const uint32_t lbase = 16u * (4u * yb + 2u) + WK_ZS * z;   // image dword of (0, 4 yb, z)
+    uint32_t re[8], ro[8];   // this lane's codes of the last 8 steps (split halves), ring by step
 #pragma unroll
-        for (int j = 0; j < 8; j++) re[j] = ro[j] = 0;
+    for (int j = 0; j < 8; j++) re[j] = ro[j] = 0;
 #if defined(GM_EXP) && (GM_EXP & 1)
-        constexpr int TAU_END = 0;   // experiment: no pass B
+    constexpr int TAU_END = 0;   // experiment: no pass B
 #else
-        constexpr int TAU_END = 91;  // p = tau - s0 in [0, 64), s0 <= 15 + 12
+    constexpr int TAU_END = 91;  // p = tau - s0 in [0, 64), s0 <= 15 + 12
 #endif
-        // Only (y-1) -- the code this wave stored one step ago -- is on the step-to-step
-        // chain; the fold F and (y-2) of the next step are read a step ahead (any lane's
-        // address is clamped into its own column, an idle lane's values are unused).
-        // Addresses: p = t0 + j - s0 with t0 a multiple of 8, so (p >> 2, p & 3) =
-        // (t0 / 4 + ((j - s0) >> 2), (j - s0) & 3) and the image dword is
-        // lbase + t0 / 4 + cj[j]: one add per step.  An idle lane (p outside [0, 64))
-        // reads some dword of the image (unused), writes a dword of its own in the
-        // slice's spare tail, and records 0.
-        int cj[9];
+    // Only (y-1) -- the code this wave stored one step ago -- is on the step-to-step
+    // chain; the fold F and (y-2) of the next step are read a step ahead.
+    // Addresses: p = t0 + j - s0 with t0 a multiple of 8, so (p >> 2, p & 3) =
+    // (t0 / 4 + ((j - s0) >> 2), (j - s0) & 3) and the image dword is
+    // lbase + t0 / 4 + cj[j]: one add per step.  An idle lane (p outside [0, 64))
+    // reads some dword of the image (unused), writes a dword of its own in the
+    // slice's spare tail, and records 0.
+    int cj[9];
 #pragma unroll
-        for (int j = 0; j < 9; j++) cj[j] = ((j - s0) >> 2) + 16 * ((j - s0) & 3);
-        const uint32_t dummy = WK_ZS * z + 288u + yb;
-        uint32_t Fv, Y2v;
-        {
-            const uint32_t o = lbase + cj[0];
-            Fv = s[o];
-            Y2v = s[o - 32];
-        }
-        for (int t0 = 0; t0 < TAU_END; t0 += 8) {
-            const uint32_t b0 = lbase + (uint32_t)(t0 >> 2);
+    for (int j = 0; j < 9; j++) cj[j] = ((j - s0) >> 2) + 16 * ((j - s0) & 3);
+    const uint32_t dummy = WK_ZS * z + 288u + yb;
+    uint32_t Fv, Y2v;
+    {
+        const uint32_t o = lbase + cj[0];
+        Fv = s[o];
+        Y2v = s[o - 32];
+    }
+    for (int t0 = 0; t0 < TAU_END; t0 += 8) {
+        const uint32_t b0 = lbase + (uint32_t)(t0 >> 2);
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const uint32_t o = b0 + cj[j];
-                const uint32_t Y1 = s[o - 16];   // stored one step ago (this lane or the row below)
-                const uint32_t on = b0 + cj[j + 1];   // cj[8] = cj[0] + 2: the next t0's first step
-                const uint32_t Fn = s[on], Y2n = s[on - 32];
-                const uint32_t n1e = dpp_shr1(re[(j + 7) & 7]), n1o = dpp_shr1(ro[(j + 7) & 7]);
-                const uint32_t n2e = dpp_shr2(re[(j + 6) & 7]), n2o = dpp_shr2(ro[(j + 6) & 7]);
-                // all-ones on an active lane; opaque, so the compiler keeps this straight-line
-                // (a branch would sink the (y-1) read behind the prefetch)
-                uint32_t act = (uint32_t)(t0 + j - s0) < 64u ? ~0u : 0u;
-                asm volatile("" : "+v"(act));
-                const uint32_t pe = pk_max(pk_max(Fv & 0x00FF00FFu, Y2v & 0x00FF00FFu),
-                                           pk_max(pk_max(n2e, re[(j + 4) & 7]), re[j]));
-                const uint32_t po = pk_max(pk_max(Fv, Y2v), pk_max(pk_max(n2o, ro[(j + 4) & 7]), ro[j]));
-                const uint32_t me = pk_max(pk_max(pe, n1e), Y1 & 0x00FF00FFu);
-                const uint32_t mo = pk_max(pk_max(po, n1o), Y1);
-                re[j] = wk_code_e(me) & act;
-                ro[j] = wk_code_o(mo) & act;
-                s[dummy + ((o - dummy) & act)] = re[j] | ro[j];
-                Fv = Fn;
-                Y2v = Y2n;
-            }
+        for (int j = 0; j < 8; j++) {
+            const uint32_t o = b0 + cj[j];
+            const uint32_t Y1 = s[o - 16];   // stored one step ago (this lane or the row below)
+            const uint32_t on = b0 + cj[j + 1];   // cj[8] = cj[0] + 2: the next t0's first step
+            const uint32_t Fn = s[on], Y2n = s[on - 32];
+            const uint32_t n1e = dpp_shr1(re[(j + 7) & 7]), n1o = dpp_shr1(ro[(j + 7) & 7]);
+            const uint32_t n2e = dpp_shr2(re[(j + 6) & 7]), n2o = dpp_shr2(ro[(j + 6) & 7]);
+            // all-ones on an active lane; opaque, so the compiler keeps this straight-line
+            // (a branch would sink the (y-1) read behind the prefetch)
+            uint32_t act = (uint32_t)(t0 + j - s0) < 64u ? ~0u : 0u;
+            asm volatile("" : "+v"(act));
+            const uint32_t pe = pk_max(pk_max(Fv & 0x00FF00FFu, Y2v & 0x00FF00FFu),
+                                       pk_max(pk_max(n2e, re[(j + 4) & 7]), re[j]));
+            const uint32_t po = pk_max(pk_max(Fv, Y2v), pk_max(pk_max(n2o, ro[(j + 4) & 7]), ro[j]));
+            const uint32_t me = pk_max(pk_max(pe, n1e), Y1 & 0x00FF00FFu);
+            const uint32_t mo = pk_max(pk_max(po, n1o), Y1);
+            re[j] = wk_code_e(me) & act;
+            ro[j] = wk_code_o(mo) & act;
+            s[dummy + ((o - dummy) & act)] = re[j] | ro[j];
+            Fv = Fn;
+            Y2v = Y2n;
         }
     }
+}
 
-    // ---- pass C: the walking wave writes the four blocks (chunks lane + 64 i)
+// pass C: one wave writes the four blocks from image s (chunks lane + 64 i), and in the
+// sharded solve (XD) each block also to its extra destinations
+template <int CPOL, bool XD>
+__device__ __forceinline__ void wk_store(uint8_t *__restrict__ table, const uint32_t (&hp)[4], const bool (&valid)[4],
+                                         const uint32_t *s, uint32_t lane, const uint32_t *__restrict__ xoff,
+                                         const uint64_t *__restrict__ xdst, uint32_t idx0) {
+    constexpr int NPOS = 4096, K = 4;
     __amdgpu_buffer_rsrc_t wr[K];
 #pragma unroll
     for (int k = 0; k < K; k++) wr[k] = block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0);
@@ -905,7 +938,7 @@ __device__ __forceinline__ void wk_solve(uint8_t *__restrict__ table, const uint
 #endif
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        const uint32_t c = (uint32_t)lane + 64u * i;
+        const uint32_t c = lane + 64u * i;
         const uint32_t base = wk_chunk(c);
         u32x4v out[K];
 #pragma unroll
@@ -934,21 +967,59 @@ __device__ __forceinline__ void wk_solve(uint8_t *__restrict__ table, const uint
     }
 }
 
-template <int HIGH>
-__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
-                                                          uint32_t nblk, const uint8_t *__restrict__ zero) {
-    constexpr int K = 4;
-    __shared__ __attribute__((aligned(16))) uint32_t s[WK_ZS * 16];   // 18.25 KiB
-    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
-    uint32_t hp[K];
-    bool valid[K];
+__device__ __forceinline__ void wk_group(const uint32_t *__restrict__ blocks, uint32_t nblk, uint32_t g, uint32_t (&hp)[4],
+                                         bool (&valid)[4]) {
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint32_t idx = grp * K + k;
+    for (int k = 0; k < 4; k++) {
+        const uint32_t idx = g * 4 + k;
         valid[k] = idx < nblk;
         hp[k] = valid[k] ? blocks[idx] : 0u;
     }
-    wk_solve<HIGH, GM_B4_STORE_CPOL, false>(table, hp, valid, s);
+}
+
+// option 10: one group per workgroup of 256 threads
+template <int HIGH, int CPOL, bool XD>
+__device__ __forceinline__ void wk_solve(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                         uint32_t *s, const uint32_t *__restrict__ xoff = nullptr,
+                                         const uint64_t *__restrict__ xdst = nullptr) {
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + 3) / 4);
+    uint32_t hp[4];
+    bool valid[4];
+    wk_group(blocks, nblk, grp, hp, valid);
+    const uint32_t tid = threadIdx.x;
+#ifdef GM_WK_TRACE
+    const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t trl = 0;
+    wk_load<HIGH>(table, hp, valid, s, tid, true, &trl);
+    const uint64_t trf = __builtin_amdgcn_s_memrealtime();
+#else
+    wk_load<HIGH>(table, hp, valid, s, tid, true);
+#endif
+    __syncthreads();
+#if GM_WK_ROT
+    if ((tid >> 6) != (blockIdx.x & 3u)) return;   // one wave walks and stores
+#else
+    if (tid >= 64) return;
+#endif
+    const uint32_t lane = tid & 63;
+#ifdef GM_WK_TRACE
+    const uint64_t tr1 = __builtin_amdgcn_s_memrealtime();
+#endif
+    wk_walk(s, lane);
+#ifdef GM_WK_TRACE
+    const uint64_t tr2 = __builtin_amdgcn_s_memrealtime();
+#endif
+    wk_store<CPOL, XD>(table, hp, valid, s, lane, xoff, xdst, grp * 4);
+#ifdef GM_WK_TRACE
+    if (lane == 0) wk_trace(tr0, tr1, tr2, hp[0], trl, trf);
+#endif
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                                          uint32_t nblk, const uint8_t *__restrict__ zero) {
+    __shared__ __attribute__((aligned(16))) uint32_t s[WK_IMG];   // 18.25 KiB
+    wk_solve<HIGH, GM_B4_STORE_CPOL, false>(table, blocks, nblk, s);
 }
 
 template <int HIGH>
@@ -956,18 +1027,139 @@ __global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wkx(uint8_t 
                                                            uint32_t nblk, const uint8_t *__restrict__ zero,
                                                            const uint32_t *__restrict__ xoff,
                                                            const uint64_t *__restrict__ xdst) {
-    constexpr int K = 4;
-    __shared__ __attribute__((aligned(16))) uint32_t s[WK_ZS * 16];
-    const uint32_t grp = xcd_order(blockIdx.x, (nblk + K - 1) / K);
-    uint32_t hp[K];
-    bool valid[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        const uint32_t idx = grp * K + k;
-        valid[k] = idx < nblk;
-        hp[k] = valid[k] ? blocks[idx] : 0u;
+    __shared__ __attribute__((aligned(16))) uint32_t s[WK_IMG];
+    wk_solve<HIGH, 0, true>(table, blocks, nblk, s, xoff, xdst);
+}
+
+// option 12: two groups per workgroup of 256 threads, two images.  Pass A loads and
+// folds them one after the other (the same registers), then two waves walk them at
+// once, one group each.  Per group a CU's wave slots are held for ~13 us instead of
+// ~21 us (option 10: the three waves that leave after pass A keep their slots until
+// the walker is done).
+template <int HIGH, int CPOL, bool XD>
+__device__ __forceinline__ void wk2_solve(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                          uint32_t *img, const uint32_t *__restrict__ xoff = nullptr,
+                                          const uint64_t *__restrict__ xdst = nullptr) {
+    const uint32_t ng = (nblk + 3) / 4;
+    const uint32_t pair = xcd_order(blockIdx.x, (ng + 1) / 2);
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    uint32_t hp[4];
+    bool valid[4];
+    const bool two = 2 * pair + 1 < ng;   // uniform
+    wk_group(blocks, nblk, 2 * pair, hp, valid);
+    wk_load<HIGH>(table, hp, valid, img, tid, true);
+    __builtin_amdgcn_sched_barrier(0);   // the second group's loads reuse the first's registers
+    if (two) {
+        wk_group(blocks, nblk, 2 * pair + 1, hp, valid);
+        wk_load<HIGH>(table, hp, valid, img + WK_IMG, tid, true);
     }
-    wk_solve<HIGH, 0, true>(table, hp, valid, s, xoff, xdst, grp * K);
+    __syncthreads();
+#if GM_WK_ROT
+    const uint32_t w0 = (blockIdx.x & 1u) * 2u;   // waves (0, 1) or (2, 3): two different SIMDs either way
+#else
+    const uint32_t w0 = 0;
+#endif
+    if (wave != w0 && !(two && wave == w0 + 1)) return;
+    const uint32_t g = 2 * pair + (wave - w0);
+    uint32_t *s = img + (wave - w0) * WK_IMG;
+    wk_group(blocks, nblk, g, hp, valid);
+    wk_walk(s, lane);
+    wk_store<CPOL, XD>(table, hp, valid, s, lane, xoff, xdst, g * 4);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk2(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                                           uint32_t nblk, const uint8_t *__restrict__ zero) {
+    __shared__ __attribute__((aligned(16))) uint32_t img[2 * WK_IMG];   // 36.5 KiB
+    wk2_solve<HIGH, GM_B4_STORE_CPOL, false>(table, blocks, nblk, img);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk2x(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                                            uint32_t nblk, const uint8_t *__restrict__ zero,
+                                                            const uint32_t *__restrict__ xoff,
+                                                            const uint64_t *__restrict__ xdst) {
+    __shared__ __attribute__((aligned(16))) uint32_t img[2 * WK_IMG];
+    wk2_solve<HIGH, 0, true>(table, blocks, nblk, img, xoff, xdst);
+}
+
+// option 11: persistent, 320 threads, two images.  XCD x (= blockIdx & 7 under the
+// round-robin dispatch) owns the contiguous run of the tier's groups that xcd_order
+// gives it; its workgroups take the run's groups in turn (i0, i0 + nx, ...).
+template <int HIGH, int CPOL, bool XD>
+__device__ __forceinline__ void wkp_run(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                        uint32_t *img, const uint32_t *__restrict__ xoff = nullptr,
+                                        const uint64_t *__restrict__ xdst = nullptr) {
+    const uint32_t ng = (nblk + 3) / 4, G = gridDim.x, x = blockIdx.x & 7u, i0 = blockIdx.x >> 3;
+    const uint32_t q = ng >> 3, r = ng & 7u;
+    const uint32_t start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, len = q + (x < r ? 1u : 0u);
+    const uint32_t nx = (G + 7u - x) >> 3;   // workgroups on XCD x
+    if (i0 >= len) return;   // the whole workgroup
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+#if GM_WK_ROT
+    const uint32_t walker = (blockIdx.x >> 3) % 5u;   // spread the walkers of a CU's workgroups over its SIMDs
+#else
+    const uint32_t walker = 0;
+#endif
+    const uint32_t end = start + len;
+    uint32_t hp[4];
+    bool valid[4];
+    // the two roles run separate loops with the same barrier count (one per group)
+    if (wave == walker) {
+        __syncthreads();
+        for (uint32_t g = start + i0, it = 0;; g += nx, it++) {
+            uint32_t *cur = img + (it & 1u) * WK_IMG;
+            wk_group(blocks, nblk, g, hp, valid);
+            wk_walk(cur, lane);
+            wk_store<CPOL, XD>(table, hp, valid, cur, lane, xoff, xdst, g * 4);
+            __syncthreads();
+            if (g + nx >= end) break;
+        }
+    } else {
+        const uint32_t lt = ((wave + 4u - walker) % 5u) * 64u + lane;   // loader thread 0..255
+        wk_group(blocks, nblk, start + i0, hp, valid);
+        wk_load<HIGH>(table, hp, valid, img, lt, true);
+        *(u32x2v *)(img + WK_IMG + WK_ZS * (lt >> 4) + 2u * (lt & 15u)) = u32x2v{0u, 0u};   // image 1's zero rows
+        __syncthreads();
+        for (uint32_t g = start + i0, it = 0;; g += nx, it++) {
+            const uint32_t gn = g + nx;
+            if (gn < end) {
+                wk_group(blocks, nblk, gn, hp, valid);
+                wk_load<HIGH>(table, hp, valid, img + ((it + 1u) & 1u) * WK_IMG, lt, false);
+            }
+            __syncthreads();
+            if (gn >= end) break;
+        }
+    }
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(320, GM_WK_WAVES) void sub_tier_kernel_wkp(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                                           uint32_t nblk, const uint8_t *__restrict__ zero) {
+    __shared__ __attribute__((aligned(16))) uint32_t img[2 * WK_IMG];   // 36.5 KiB
+    wkp_run<HIGH, GM_B4_STORE_CPOL, false>(table, blocks, nblk, img);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(320, GM_WK_WAVES) void sub_tier_kernel_wkpx(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                                            uint32_t nblk, const uint8_t *__restrict__ zero,
+                                                            const uint32_t *__restrict__ xoff,
+                                                            const uint64_t *__restrict__ xdst) {
+    __shared__ __attribute__((aligned(16))) uint32_t img[2 * WK_IMG];
+    wkp_run<HIGH, 0, true>(table, blocks, nblk, img, xoff, xdst);
+}
+
+// grid of the persistent walker kernel: at most GM_WKP_PER_CU workgroups per CU
+static uint32_t wkp_grid(uint32_t nblocks) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    }
+    static const int per = getenv("GM_WKP_PER_CU") ? atoi(getenv("GM_WKP_PER_CU")) : GM_WKP_PER_CU;   // dev aid
+    const uint32_t ng = (nblocks + 3) / 4, cap = (uint32_t)(per * cus);
+    return ng < cap ? ng : cap;
 }
 
 // ---------------------------------------------------------------------------
@@ -1521,6 +1713,18 @@ static uint32_t b4_lat_max() {
     return v;
 }
 
+// Tiers of fewer blocks than this run the b4 kernel instead of the walker: a lone
+// workgroup's walk (91 dependent steps, ~8 us) is longer than b4's 46-step barrier
+// chain, so below a few rounds of workgroups per CU the b4 kernel's latency wins
+// (GM_WK_MIN overrides, development aid).
+#ifndef GM_WK_MIN_BLOCKS
+#define GM_WK_MIN_BLOCKS 4096
+#endif
+static uint32_t wk_min_blocks() {
+    static const uint32_t v = getenv("GM_WK_MIN") ? (uint32_t)atoi(getenv("GM_WK_MIN")) : GM_WK_MIN_BLOCKS;
+    return v;
+}
+
 // development aid: GM_PAD_LDS=<bytes> of unused dynamic LDS per workgroup (fewer workgroups per CU)
 static unsigned pad_lds() {
     static const unsigned v = getenv("GM_PAD_LDS") ? (unsigned)atoi(getenv("GM_PAD_LDS")) : 0u;
@@ -1535,6 +1739,30 @@ static tier_kernel_t pick_w1(int high) {
     case 3: return sub_tier_kernel_w1<3>;
     case 4: return sub_tier_kernel_w1<4>;
     case 5: return sub_tier_kernel_w1<5>;
+    }
+    return nullptr;
+}
+
+static tier_kernel_t pick_wkp(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel_wkp<0>;
+    case 1: return sub_tier_kernel_wkp<1>;
+    case 2: return sub_tier_kernel_wkp<2>;
+    case 3: return sub_tier_kernel_wkp<3>;
+    case 4: return sub_tier_kernel_wkp<4>;
+    case 5: return sub_tier_kernel_wkp<5>;
+    }
+    return nullptr;
+}
+
+static tier_kernel_t pick_wk2(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel_wk2<0>;
+    case 1: return sub_tier_kernel_wk2<1>;
+    case 2: return sub_tier_kernel_wk2<2>;
+    case 3: return sub_tier_kernel_wk2<3>;
+    case 4: return sub_tier_kernel_wk2<4>;
+    case 5: return sub_tier_kernel_wk2<5>;
     }
     return nullptr;
 }
@@ -1616,6 +1844,8 @@ static tier_kernel_t pick_interleaved(int high, int nt) {
     if (nt == -4) return pick_w1(high);
     if (nt == -5) return pick_p4(high);
     if (nt == -6) return pick_wk(high);
+    if (nt == -7) return pick_wkp(high);
+    if (nt == -8) return pick_wk2(high);
     return nt == -2 ? pick_b4(high) : pick_x4(high, nt == -1);
 }
 
@@ -1639,8 +1869,15 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
     } else if (nt == -2 && nblocks <= b4_lat_max()) {
         hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), pad_lds(), s, table, list, nblocks,
                            zero);
+    } else if (nt == -6 && nblocks < wk_min_blocks()) {   // small tier: one workgroup's latency decides
+        hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
     } else if (nt == -6) {
         hipLaunchKernelGGL(pick_wk(high), dim3((nblocks + 3) / 4), dim3(256), pad_lds(), s, table, list, nblocks, zero);
+    } else if (nt == -8) {
+        hipLaunchKernelGGL(pick_wk2(high), dim3(((nblocks + 3) / 4 + 1) / 2), dim3(256), pad_lds(), s, table, list,
+                           nblocks, zero);
+    } else if (nt == -7) {
+        hipLaunchKernelGGL(pick_wkp(high), dim3(wkp_grid(nblocks)), dim3(320), pad_lds(), s, table, list, nblocks, zero);
     } else if (nt <= 0)
         hipLaunchKernelGGL(pick_interleaved(high, nt), dim3((nblocks + 3) / 4), dim3(nt == -4 ? 64 : 256), 0, s, table,
                            list, nblocks, zero);
@@ -1662,6 +1899,28 @@ static tier_kernel_x_t pick_b4x(int high) {
     return nullptr;
 }
 static tier_kernel_x_t pick_b4x(int high) { return pick_b4x<false>(high); }
+
+static tier_kernel_x_t pick_wkpx(int high) {
+    switch (high) {
+    case 1: return sub_tier_kernel_wkpx<1>;
+    case 2: return sub_tier_kernel_wkpx<2>;
+    case 3: return sub_tier_kernel_wkpx<3>;
+    case 4: return sub_tier_kernel_wkpx<4>;
+    case 5: return sub_tier_kernel_wkpx<5>;
+    }
+    return nullptr;
+}
+
+static tier_kernel_x_t pick_wk2x(int high) {
+    switch (high) {
+    case 1: return sub_tier_kernel_wk2x<1>;
+    case 2: return sub_tier_kernel_wk2x<2>;
+    case 3: return sub_tier_kernel_wk2x<3>;
+    case 4: return sub_tier_kernel_wk2x<4>;
+    case 5: return sub_tier_kernel_wk2x<5>;
+    }
+    return nullptr;
+}
 
 static tier_kernel_x_t pick_wkx(int high) {
     switch (high) {
@@ -1686,15 +1945,26 @@ static tier_kernel_x_t pick_w1x(int high) {
 }
 
 bool sub_kernel_x_exists(int high) {
-    return pick_b4x(high) != nullptr && pick_w1x(high) != nullptr && pick_wkx(high) != nullptr;
+    return pick_b4x(high) != nullptr && pick_w1x(high) != nullptr && pick_wkx(high) != nullptr &&
+           pick_wkpx(high) != nullptr && pick_wk2x(high) != nullptr;
 }
 
 // kind: the sub_interleave option (8 one-wave kernel, 10 walker, otherwise the b4 kernel)
 void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
                        const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, int kind) {
     if (!nblocks) return;
+    if (kind == 12) {
+        hipLaunchKernelGGL(pick_wk2x(high), dim3(((nblocks + 3) / 4 + 1) / 2), dim3(256), 0, s, table, list, nblocks,
+                           zero, xoff, xdst);
+        return;
+    }
+    if (kind == 11) {
+        hipLaunchKernelGGL(pick_wkpx(high), dim3(wkp_grid(nblocks)), dim3(320), 0, s, table, list, nblocks, zero, xoff,
+                           xdst);
+        return;
+    }
     const bool wave = kind == 8;
-    hipLaunchKernelGGL(wave ? pick_w1x(high) : kind == 10 ? pick_wkx(high)
+    hipLaunchKernelGGL(wave ? pick_w1x(high) : kind == 10 && nblocks >= wk_min_blocks() ? pick_wkx(high)
                        : nblocks <= b4_lat_max() ? pick_b4x<true>(high) : pick_b4x<false>(high),
                        dim3((nblocks + 3) / 4), dim3(wave ? 64 : 256), 0, s,
                        table, list, nblocks, zero, xoff, xdst);
@@ -1708,6 +1978,8 @@ int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 8) return -4;
     if (low == 3 && c->sub_interleave == 9) return -5;
     if (low == 3 && c->sub_interleave == 10) return -6;
+    if (low == 3 && c->sub_interleave == 11) return -7;
+    if (low == 3 && c->sub_interleave == 12) return -8;
     return c->sub_threads;
 }
 
@@ -1915,6 +2187,19 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
         d = c->dsub = new DenseSub();
         GM_TRY(prepare(c, d));
     }
+#ifdef GM_WK_TRACE
+    static uint64_t *tbuf = nullptr;
+    static uint32_t *tcnt = nullptr;
+    const char *tpath = getenv("GM_TRACE_OUT");
+    if (tpath && !tbuf) {
+        GM_HIP(hipMalloc(&tbuf, 64ull << 20));
+        GM_HIP(hipMalloc(&tcnt, 4));
+        GM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(gm_trace_buf), &tbuf, sizeof(tbuf)));
+        GM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(gm_trace_cnt), &tcnt, sizeof(tcnt)));
+        GM_HIP(hipMemset(tcnt, 0, 4));
+        GM_HIP(hipDeviceSynchronize());
+    }
+#endif
     double t0 = now_ms();
     bool timed = c->timing;
     if (timed) GM_TRY(ensure_events(d));
@@ -1952,6 +2237,17 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
         return GM_E_STATE;
     }
 
+#ifdef GM_WK_TRACE
+    if (tpath && tbuf) {   // the entries of this solve, then reset for the next
+        uint32_t cnt = 0;
+        GM_HIP(hipMemcpy(&cnt, tcnt, 4, hipMemcpyDeviceToHost));
+        cnt = std::min(cnt, 1u << 20);
+        std::vector<uint64_t> h(8ull * cnt);
+        GM_HIP(hipMemcpy(h.data(), tbuf, h.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE *f = fopen(tpath, "wb")) { fwrite(h.data(), 8, h.size(), f); fclose(f); }
+        GM_HIP(hipMemset(tcnt, 0, 4));
+    }
+#endif
     c->root_record = record_of_code(rs);
     uint64_t n = 1;
     for (int j = 0; j < d->heaps; j++) n *= ((root >> (4 * j)) & 15u) + 1;

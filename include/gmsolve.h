@@ -82,8 +82,10 @@ enum {
                                 context on one GPU (loopback transport instead of RCCL); for testing
                                 the multi-GPU partition on a single device */
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
-    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path, 4 blocks per workgroup: 10 = byte LDS image walked by
-                                  one wave, no barriers (default), 6 = byte LDS image, 256-thread barrier walk,
+    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path, 4 blocks per workgroup: 11 = persistent workgroups, one
+                                  wave walks a byte LDS image with no barrier while four load the next (default),
+                                  10 = the same walk, one group per workgroup,
+                                  6 = byte LDS image, 256-thread barrier walk,
                                   7 = byte image, whole solve as one dataflow launch (per-block child flags),
                                   8 = byte image, one 64-lane wave per workgroup (no barriers),
                                   9 = byte image, persistent, next group's loads pipelined into pass B,

@@ -151,22 +151,54 @@ def test_subtract_dense_vs_oracle(oracle, heaps, low):
     assert np.array_equal(r, ref)
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("heaps", [3, 4, 5, 6])
 def test_subtract_kernel_variants_vs_oracle(oracle, heaps, variant):
-    """Interleaved kernel variants (GM_OPT_SUB_INTERLEAVE 4 / 5 / 6, 7 = dataflow, 8 = one wave, 10 = walker) against the oracle."""
+    """Interleaved kernel variants (GM_OPT_SUB_INTERLEAVE 4 / 5 / 6, 7 = dataflow, 8 = one wave, 10 = walker, 11 = pipelined walker, 12 = two walkers) against the oracle."""
     ref = oracle.subtract_dense(heaps)
     ctx, n, rec = _solve(SUB, (heaps,), sub_interleave=variant)
     assert np.array_equal(ctx.export()[1], ref)
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [5, 6, 7, 8, 9, 10, 11, 12])
 def test_subtract_kernel_variants_full_2_32_match(variant):
     a, n1, r1 = _solve(SUB, (8,), sub_interleave=4)
     d1 = a.digest()
     a.close()
     b, n2, r2 = _solve(SUB, (8,), sub_interleave=variant)
     assert (n2, r2) == (n1, r1) and b.digest() == d1
+
+
+_WALKER_EVERYWHERE = r'''
+import ctypes, os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from gamesmanmpi_amd import Context, _lib
+ol = ctypes.CDLL(os.path.join(sys.argv[1], "oracle", "_build", "liboracle.so"))
+ol.oracle_subtract_dense.argtypes = [ctypes.c_int, ctypes.c_void_p]
+for heaps in (3, 4, 5, 6):
+    ctx = Context(_lib.GAME_SUBTRACT, (heaps,), device=0)
+    ctx.set_option(_lib.OPT_SUB_INTERLEAVE, 10)
+    ctx.solve(ctx.initial())
+    ref = np.empty(16 ** heaps, dtype=np.uint16)
+    assert ol.oracle_subtract_dense(heaps, ref.ctypes.data) == 0
+    assert np.array_equal(ctx.export()[1], ref), heaps
+    ctx.close()
+print("ok")
+'''
+
+
+def test_walker_kernel_on_every_tier_vs_oracle():
+    """The walker kernel runs only tiers of >= GM_WK_MIN blocks (smaller ones take the b4
+    kernel); with GM_WK_MIN=0 it solves every tier of the 3..6-heap games (fresh process:
+    the threshold is read once)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GM_WK_MIN="0")
+    r = subprocess.run([sys.executable, "-c", _WALKER_EVERYWHERE, repo], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
 def test_subtract_graph_replay_is_identical(oracle):
