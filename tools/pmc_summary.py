@@ -2,7 +2,7 @@
 """Summarise rocprofv3 kernel-trace / PMC CSVs of a bench run into profiles/.
 
     python tools/pmc_summary.py --kt gpurun_out/prof_kt --fetch gpurun_out/prof_fetch \
-        --write gpurun_out/prof_write --kernel sub_tier_kernel_wk --launches-per-solve 76 \
+        --write gpurun_out/prof_write --kernel sub_tier_kernel_ --launches-per-solve 76 \
         --tag r01_subtract8 [--traffic-json profiles/traffic_subtract8.json]
 
 HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE and WRITE_SIZE are in KiB,
@@ -38,11 +38,12 @@ def main():
     shutil.copy(os.path.join(a.kt, "run_kernel_stats.csv"), "profiles/%s_kernel_stats.csv" % a.tag)
     kt = [r for r in rows(os.path.join(a.kt, "run_kernel_trace.csv")) if a.kernel in r["Kernel_Name"]]
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in kt]
-    out = {"kernel": kt[0]["Kernel_Name"] if kt else a.kernel, "dispatches": len(durs),
+    names = sorted(set(r["Kernel_Name"] for r in kt))
+    out = {"kernel": names[0] if len(names) == 1 else names or a.kernel, "dispatches": len(durs),
            "avg_duration_us": sum(durs) / len(durs) / 1e3 if durs else None,
            "solve_kernel_ms": sum(durs) / (len(durs) / a.launches_per_solve) / 1e6 if durs else None,
            "launches_per_solve": a.launches_per_solve,
-           "vgpr": kt[0].get("VGPR_Count") if kt else None, "lds_bytes": kt[0].get("LDS_Block_Size") if kt else None}
+           "vgpr": sorted(set(r.get("VGPR_Count") for r in kt)), "lds_bytes": sorted(set(r.get("LDS_Block_Size") for r in kt))}
     pmc = {}
     for name, d in (("FETCH_SIZE", a.fetch), ("WRITE_SIZE", a.write)):
         if not d:
