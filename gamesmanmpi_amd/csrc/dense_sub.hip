@@ -137,6 +137,13 @@ __device__ __forceinline__ uint32_t xcd_order(uint32_t b, uint32_t n) {
     const uint32_t q = n >> 3, r = n & 7u, x = b & 7u, i = b >> 3;
     return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
+// the same runs, each walked from its end (serpentine order on alternate tiers: the
+// groups an XCD starts a tier with are next to the ones it ended the previous tier with)
+__device__ __forceinline__ uint32_t xcd_order_rev(uint32_t b, uint32_t n) {
+    const uint32_t q = n >> 3, r = n & 7u, x = b & 7u, i = b >> 3;
+    const uint32_t len = q + (x < r ? 1u : 0u);
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (len - 1u - i);
+}
 
 // ---------------------------------------------------------------------------
 // One block per workgroup of NT threads (any LOW).
@@ -799,8 +806,14 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
 #ifndef GM_WK_ROT
 #define GM_WK_ROT 1   // the walking wave rotates with the workgroup index (spread over the SIMDs)
 #endif
+#ifndef GM_WK_SERP
+#define GM_WK_SERP 0   // serpentine XCD runs (alternate tiers walked backwards)
+#endif
+#ifndef GM_WK_PAIRS
+#define GM_WK_PAIRS 0   // pass A in two rounds of two blocks' loads (development option)
+#endif
 #ifndef GM_WK_WAVES
-#define GM_WK_WAVES 4   // waves per SIMD the register budget must allow (128 VGPRs)
+#define GM_WK_WAVES (GM_WK_PAIRS ? 5 : 4)   // waves per SIMD the register budget must allow
 #endif
 #ifndef GM_WKP_PER_CU
 #define GM_WKP_PER_CU 3   // persistent 320-thread workgroups per CU (5 waves x 128 VGPRs: 15 of 16 slots)
@@ -853,6 +866,19 @@ __device__ __forceinline__ void wk_load(uint8_t *__restrict__ table, const uint3
     const uint32_t c = lt;
     // the zero rows y = -2, -1 of every z slice: 16 x 32 dwords
     if (zero) *(u32x2v *)(s + WK_ZS * (lt >> 4) + 2u * (lt & 15u)) = u32x2v{0u, 0u};
+#if GM_WK_PAIRS
+    // two rounds of 2 blocks' loads (fewer registers, more workgroups per CU)
+    char *const b = (char *)s;
+    const uint32_t base = wk_chunk(c);
+#pragma unroll
+    for (int k = 0; k < K; k += 2) {
+        u32x4v v[2][NMAX];
+        p4_issue<HIGH>(table, hp[k], valid[k], c, v[0]);
+        p4_issue<HIGH>(table, hp[k + 1], valid[k + 1], c, v[1]);
+        uint32_t e[2][4], o[2][4];
+        p4_fold<NMAX>(v[0], e[0], o[0]);
+        p4_fold<NMAX>(v[1], e[1], o[1]);
+#else
     u32x4v v[K][NMAX];
 #pragma unroll
     for (int k = 0; k < K; k++) p4_issue<HIGH>(table, hp[k], valid[k], c, v[k]);
@@ -867,6 +893,7 @@ __device__ __forceinline__ void wk_load(uint8_t *__restrict__ table, const uint3
         uint32_t e[2][4], o[2][4];
         p4_fold<NMAX>(v[k], e[0], o[0]);
         p4_fold<NMAX>(v[k + 1], e[1], o[1]);
+#endif
 #pragma unroll
         for (int j = 0; j < 4; j++) {   // bytes k, k+1 of positions 4j .. 4j+3 (see p4_write_pair)
             const uint32_t xe = __builtin_amdgcn_perm(e[1][j], e[0][j], 0x06020400u);
@@ -1000,7 +1027,17 @@ template <int HIGH, int CPOL, bool XD>
 __device__ __forceinline__ void wk_solve(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks, uint32_t nblk,
                                          uint32_t *s, const uint32_t *__restrict__ xoff = nullptr,
                                          const uint64_t *__restrict__ xdst = nullptr) {
+#if GM_WK_SERP
+    uint32_t t0 = 0;   // the tier's parity from its first block's high-nibble sum
+    {
+        const uint32_t h = blocks[0];
+#pragma unroll
+        for (int j = 0; j < 8; j++) t0 += (h >> (4 * j)) & 15u;
+    }
+    const uint32_t grp = (t0 & 1u) ? xcd_order_rev(blockIdx.x, (nblk + 3) / 4) : xcd_order(blockIdx.x, (nblk + 3) / 4);
+#else
     const uint32_t grp = xcd_order(blockIdx.x, (nblk + 3) / 4);
+#endif
     uint32_t hp[4];
     bool valid[4];
     wk_group(blocks, nblk, grp, hp, valid);
