@@ -39,6 +39,16 @@ GM_HD int collect(const D &d, uint64_t k, uint64_t *out) {
 // stands for.  A descriptor whose visit() returns canonical children solves one
 // representative per orbit; counts, digests and exports expand every orbit, so the
 // results are those of the unreduced game.  Games without a symmetry in use:
+// descriptors with a visit_part() (the split kernels' per-lane share of visit())
+template <class D, class = void>
+struct part_visit_t {
+    static constexpr bool value = false;
+};
+template <class D>
+struct part_visit_t<D, std::void_t<decltype(D::PART_VISIT)>> {
+    static constexpr bool value = D::PART_VISIT;
+};
+
 struct NoSym {
     GM_HD uint64_t canon(uint64_t k) const { return k; }
     template <class F>
@@ -304,6 +314,32 @@ struct DescOthello : NoSym {
         if (!n) fn(k + 1);                                        // [None]: pass + 1 (:122-124)
     }
     GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
+    // The split kernels' per-lane share of visit(): the children from the empty squares
+    // part, part + nparts, ... only (a 16-lane row of the 4x4 board: one square per
+    // lane instead of every lane scanning all 16).  Returns how many legal moves they
+    // gave; the caller emits pass_child(k) when no lane of the row found one.
+    static constexpr bool PART_VISIT = true;
+    template <class F>
+    GM_HD int visit_part(uint64_t k, int part, int nparts, F &&fn) const {
+        uint32_t w = wplane(k), b = bplane(k);
+        int turn = sbyte(k, 8);
+        bool black = turn == 1;
+        uint32_t me = black ? b : w, opp = black ? w : b;
+        uint64_t low = ((uint64_t)(uint8_t)(3 - turn)) << 8;
+        int n = 0;
+        for (int sq = part; sq < A; sq += nparts) {
+            uint32_t cell = 1u << sq;
+            if ((w | b) & cell) continue;
+            uint32_t f = flips(me, opp, sq % L, sq / L);
+            if (!f) continue;
+            uint32_t nme = me | cell | f, nopp = opp & ~f;
+            uint32_t nw = black ? nopp : nme, nb = black ? nme : nopp;
+            n++;
+            if (!fn(((uint64_t)nw << (A + 16)) | ((uint64_t)nb << 16) | low)) return n;
+        }
+        return n;
+    }
+    GM_HD uint64_t pass_child(uint64_t k) const { return k + 1; }
     GM_HD int64_t tier(uint64_t k) const {
         return 3 * popc64(wplane(k) | bplane(k)) + sbyte(k, 0);
     }

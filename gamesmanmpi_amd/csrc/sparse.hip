@@ -137,16 +137,21 @@ __global__ __launch_bounds__(256) void expand_split_kernel(D d, const uint64_t *
         const uint64_t k = ikeys[i];
         const int64_t tk = d.tier(k);
         bool won = false;
-        int idx = 0;
-        d.visit(k, [&](uint64_t c) {
-            if (idx++ % G != sub) return true;
+        auto child = [&](uint64_t c) {
             const int64_t dt = d.tier(c) - tk;
 #pragma unroll
             for (int s = 0; s < S; s++)
                 if (dt == s + 1 && front_insert(next.t[s], c, err)) fresh[s]++;
             if (!won) won = d.primitive(c) == LOSS;
             return true;
-        });
+        };
+        if constexpr (part_visit_t<D>::value) {
+            const int nm = d.visit_part(k, sub, G, child);
+            if (!((__ballot(nm > 0) >> row) & ((1ull << G) - 1)) && sub == 0) child(d.pass_child(k));
+        } else {
+            int idx = 0;
+            d.visit(k, [&](uint64_t c) { return idx++ % G != sub ? true : child(c); });
+        }
         const uint64_t m = (__ballot(won) >> row) & ((1ull << G) - 1);
         if (sub == 0) iwon[i] = m ? 1 : 0;
     }
@@ -160,18 +165,15 @@ __global__ __launch_bounds__(256) void retro_split_kernel(D d, const uint64_t *_
                                                           const uint8_t *__restrict__ iwon, uint64_t n, ResRef self,
                                                           Ress<D::MAX_SKIP> next, uint32_t *err) {
     constexpr int S = D::MAX_SKIP, G = SPLIT_G;
-    const int sub = threadIdx.x % G;
+    const int sub = threadIdx.x % G, row = (threadIdx.x & 63) & ~(G - 1);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x / G;
     for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G; i < n; i += stride) {
         uint32_t best = 0;
-        if (iwon[i]) {   // a LOSS-in-0 child: nothing beats it, no lookup needed
-            best = 0xFFFFu;
-        } else {
-            const uint64_t k = ikeys[i];
-            const int64_t tk = d.tier(k);
-            int idx = 0;
-            d.visit(k, [&](uint64_t c) {
-                if (idx++ % G != sub) return true;
+        const bool won = iwon[i];   // a LOSS-in-0 child: nothing beats it, no lookup needed
+        if (won) best = 0xFFFFu;
+        const uint64_t k = ikeys[i];
+        const int64_t tk = d.tier(k);
+        auto child = [&](uint64_t c) {
                 const int p = d.primitive(c);
                 uint32_t sc;
                 if (p != UNDECIDED) {
@@ -187,7 +189,14 @@ __global__ __launch_bounds__(256) void retro_split_kernel(D d, const uint64_t *_
                 }
                 best = max(best, sc);
                 return best != 0xFFFFu;
-            });
+        };
+        if constexpr (part_visit_t<D>::value) {
+            // every lane of the row takes part in the ballot, won or not
+            const int nm = won ? 1 : d.visit_part(k, sub, G, child);
+            if (!((__ballot(nm > 0) >> row) & ((1ull << G) - 1)) && sub == 0) child(d.pass_child(k));
+        } else if (!won) {
+            int idx = 0;
+            d.visit(k, [&](uint64_t c) { return idx++ % G != sub ? true : child(c); });
         }
 #pragma unroll
         for (int o = G / 2; o > 0; o >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, o, G));
