@@ -25,7 +25,7 @@ def timed(ctx, root, reps=4):
 def main():
     heaps = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     for G in (2, 4, 8):
-        for variant in (6,):
+        for variant in [int(v) for v in os.environ.get("GM_SOLO_VARIANTS", "6").split(",")]:
             ctx = Context(_lib.GAME_SUBTRACT, (heaps,), device=0)
             ctx.set_option(_lib.OPT_VIRTUAL_RANKS, G)
             ctx.set_option(_lib.OPT_SUB_INTERLEAVE, variant)
