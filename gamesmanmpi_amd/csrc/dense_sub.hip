@@ -32,6 +32,7 @@
 #include "gm_internal.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <chrono>
 
 namespace gm {
@@ -939,31 +940,46 @@ __device__ __forceinline__ void wk_walk(uint32_t *s, uint32_t lane) {
         Fv = s[o];
         Y2v = s[o - 32];
     }
-    for (int t0 = 0; t0 < TAU_END; t0 += 8) {
+    auto step = [&](int t0, auto J) {
+        constexpr int j = decltype(J)::value;
         const uint32_t b0 = lbase + (uint32_t)(t0 >> 2);
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t o = b0 + cj[j];
-            const uint32_t Y1 = s[o - 16];   // stored one step ago (this lane or the row below)
-            const uint32_t on = b0 + cj[j + 1];   // cj[8] = cj[0] + 2: the next t0's first step
-            const uint32_t Fn = s[on], Y2n = s[on - 32];
-            const uint32_t n1e = dpp_shr1(re[(j + 7) & 7]), n1o = dpp_shr1(ro[(j + 7) & 7]);
-            const uint32_t n2e = dpp_shr2(re[(j + 6) & 7]), n2o = dpp_shr2(ro[(j + 6) & 7]);
-            // all-ones on an active lane; opaque, so the compiler keeps this straight-line
-            // (a branch would sink the (y-1) read behind the prefetch)
-            uint32_t act = (uint32_t)(t0 + j - s0) < 64u ? ~0u : 0u;
-            asm volatile("" : "+v"(act));
-            const uint32_t pe = pk_max(pk_max(Fv & 0x00FF00FFu, Y2v & 0x00FF00FFu),
-                                       pk_max(pk_max(n2e, re[(j + 4) & 7]), re[j]));
-            const uint32_t po = pk_max(pk_max(Fv, Y2v), pk_max(pk_max(n2o, ro[(j + 4) & 7]), ro[j]));
-            const uint32_t me = pk_max(pk_max(pe, n1e), Y1 & 0x00FF00FFu);
-            const uint32_t mo = pk_max(pk_max(po, n1o), Y1);
-            re[j] = wk_code_e(me) & act;
-            ro[j] = wk_code_o(mo) & act;
-            s[dummy + ((o - dummy) & act)] = re[j] | ro[j];
-            Fv = Fn;
-            Y2v = Y2n;
-        }
+        const uint32_t o = b0 + cj[j];
+        const uint32_t Y1 = s[o - 16];   // stored one step ago (this lane or the row below)
+        const uint32_t on = b0 + cj[j + 1];   // cj[8] = cj[0] + 2: the next t0's first step
+        const uint32_t Fn = s[on], Y2n = s[on - 32];
+        const uint32_t n1e = dpp_shr1(re[(j + 7) & 7]), n1o = dpp_shr1(ro[(j + 7) & 7]);
+        const uint32_t n2e = dpp_shr2(re[(j + 6) & 7]), n2o = dpp_shr2(ro[(j + 6) & 7]);
+        // all-ones on an active lane; opaque, so the compiler keeps this straight-line
+        // (a branch would sink the (y-1) read behind the prefetch)
+        uint32_t act = (uint32_t)(t0 + j - s0) < 64u ? ~0u : 0u;
+        asm volatile("" : "+v"(act));
+        const uint32_t pe = pk_max(pk_max(Fv & 0x00FF00FFu, Y2v & 0x00FF00FFu),
+                                   pk_max(pk_max(n2e, re[(j + 4) & 7]), re[j]));
+        const uint32_t po = pk_max(pk_max(Fv, Y2v), pk_max(pk_max(n2o, ro[(j + 4) & 7]), ro[j]));
+        const uint32_t me = pk_max(pk_max(pe, n1e), Y1 & 0x00FF00FFu);
+        const uint32_t mo = pk_max(pk_max(po, n1o), Y1);
+        re[j] = wk_code_e(me) & act;
+        ro[j] = wk_code_o(mo) & act;
+        s[dummy + ((o - dummy) & act)] = re[j] | ro[j];
+        Fv = Fn;
+        Y2v = Y2n;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using I5 = std::integral_constant<int, 5>;
+    using I6 = std::integral_constant<int, 6>;
+    using I7 = std::integral_constant<int, 7>;
+    // 88 steps in blocks of 8 (the ring's period), then the last three (tau 88..90)
+    constexpr int MAIN = TAU_END >= 88 ? 88 : TAU_END;
+    for (int t0 = 0; t0 < MAIN; t0 += 8) {
+        step(t0, I0{}); step(t0, I1{}); step(t0, I2{}); step(t0, I3{});
+        step(t0, I4{}); step(t0, I5{}); step(t0, I6{}); step(t0, I7{});
+    }
+    if constexpr (TAU_END > 88) {
+        step(88, I0{}); step(88, I1{}); step(88, I2{});
     }
 }
 
