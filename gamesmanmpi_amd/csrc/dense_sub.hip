@@ -807,6 +807,9 @@ __global__ __launch_bounds__(256, GM_B4_WAVES) void sub_tier_kernel_b4x(uint8_t 
 #ifndef GM_WK_ROT
 #define GM_WK_ROT 1   // the walking wave rotates with the workgroup index (spread over the SIMDs)
 #endif
+#ifndef GM_WK_UNMASK
+#define GM_WK_UNMASK 1   // no activity masking in the walk's all-active middle steps
+#endif
 #ifndef GM_WK_SERP
 #define GM_WK_SERP 0   // serpentine XCD runs (alternate tiers walked backwards)
 #endif
@@ -940,8 +943,9 @@ __device__ __forceinline__ void wk_walk(uint32_t *s, uint32_t lane) {
         Fv = s[o];
         Y2v = s[o - 32];
     }
-    auto step = [&](int t0, auto J) {
+    auto step = [&](int t0, auto J, auto MASK) {
         constexpr int j = decltype(J)::value;
+        constexpr bool masked = decltype(MASK)::value;
         const uint32_t b0 = lbase + (uint32_t)(t0 >> 2);
         const uint32_t o = b0 + cj[j];
         const uint32_t Y1 = s[o - 16];   // stored one step ago (this lane or the row below)
@@ -951,16 +955,25 @@ __device__ __forceinline__ void wk_walk(uint32_t *s, uint32_t lane) {
         const uint32_t n2e = dpp_shr2(re[(j + 6) & 7]), n2o = dpp_shr2(ro[(j + 6) & 7]);
         // all-ones on an active lane; opaque, so the compiler keeps this straight-line
         // (a branch would sink the (y-1) read behind the prefetch)
-        uint32_t act = (uint32_t)(t0 + j - s0) < 64u ? ~0u : 0u;
-        asm volatile("" : "+v"(act));
+        uint32_t act = ~0u;
+        if constexpr (masked) {
+            act = (uint32_t)(t0 + j - s0) < 64u ? ~0u : 0u;
+            asm volatile("" : "+v"(act));
+        }
         const uint32_t pe = pk_max(pk_max(Fv & 0x00FF00FFu, Y2v & 0x00FF00FFu),
                                    pk_max(pk_max(n2e, re[(j + 4) & 7]), re[j]));
         const uint32_t po = pk_max(pk_max(Fv, Y2v), pk_max(pk_max(n2o, ro[(j + 4) & 7]), ro[j]));
         const uint32_t me = pk_max(pk_max(pe, n1e), Y1 & 0x00FF00FFu);
         const uint32_t mo = pk_max(pk_max(po, n1o), Y1);
-        re[j] = wk_code_e(me) & act;
-        ro[j] = wk_code_o(mo) & act;
-        s[dummy + ((o - dummy) & act)] = re[j] | ro[j];
+        if constexpr (masked) {
+            re[j] = wk_code_e(me) & act;
+            ro[j] = wk_code_o(mo) & act;
+            s[dummy + ((o - dummy) & act)] = re[j] | ro[j];
+        } else {
+            re[j] = wk_code_e(me);
+            ro[j] = wk_code_o(mo);
+            s[o] = re[j] | ro[j];
+        }
         Fv = Fn;
         Y2v = Y2n;
     };
@@ -972,14 +985,22 @@ __device__ __forceinline__ void wk_walk(uint32_t *s, uint32_t lane) {
     using I5 = std::integral_constant<int, 5>;
     using I6 = std::integral_constant<int, 6>;
     using I7 = std::integral_constant<int, 7>;
-    // 88 steps in blocks of 8 (the ring's period), then the last three (tau 88..90)
+    // 88 steps in blocks of 8 (the ring's period), then the last three (tau 88..90);
+    // in tau 32..63 every lane has a position (s0 <= 27, p < 64): no masking there
+    using M1 = std::true_type;
+    using M0 = std::false_type;
     constexpr int MAIN = TAU_END >= 88 ? 88 : TAU_END;
     for (int t0 = 0; t0 < MAIN; t0 += 8) {
-        step(t0, I0{}); step(t0, I1{}); step(t0, I2{}); step(t0, I3{});
-        step(t0, I4{}); step(t0, I5{}); step(t0, I6{}); step(t0, I7{});
+        if (GM_WK_UNMASK && t0 >= 32 && t0 < 64) {
+            step(t0, I0{}, M0{}); step(t0, I1{}, M0{}); step(t0, I2{}, M0{}); step(t0, I3{}, M0{});
+            step(t0, I4{}, M0{}); step(t0, I5{}, M0{}); step(t0, I6{}, M0{}); step(t0, I7{}, M0{});
+        } else {
+            step(t0, I0{}, M1{}); step(t0, I1{}, M1{}); step(t0, I2{}, M1{}); step(t0, I3{}, M1{});
+            step(t0, I4{}, M1{}); step(t0, I5{}, M1{}); step(t0, I6{}, M1{}); step(t0, I7{}, M1{});
+        }
     }
     if constexpr (TAU_END > 88) {
-        step(88, I0{}); step(88, I1{}); step(88, I2{});
+        step(88, I0{}, M1{}); step(88, I1{}, M1{}); step(88, I2{}, M1{});
     }
 }
 
