@@ -479,7 +479,7 @@ __device__ __forceinline__ void p4_write_pair(uint32_t *s, uint32_t c, int pr, c
 #ifndef GM_SKIP_MISSING
 #define GM_SKIP_MISSING 1
 #endif
-template <int HIGH>
+template <int HIGH, int LCPOL = 0>
 __device__ __forceinline__ void p4_issue(uint8_t *table, uint32_t hp, bool valid, uint32_t c,
                                          u32x4v (&v)[2 * HIGH > 0 ? 2 * HIGH : 1]) {
     constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
@@ -509,12 +509,12 @@ __device__ __forceinline__ void p4_issue(uint8_t *table, uint32_t hp, bool valid
     for (int m = 0; m < NMAX; m++) {
         const uint32_t h = HIGH > 0 ? (hp >> (4 * (m >> 1))) & 15u : 0u;
         const bool ok = HIGH > 0 && valid && h >= (uint32_t)(m & 1) + 1u;
-        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ok ? r : rz, 16u * c, soff[m], 0));
+        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ok ? r : rz, 16u * c, soff[m], LCPOL));
     }
 #else
 #pragma unroll
     for (int m = 0; m < NMAX; m++)
-        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * c, soff[m], 0));
+        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * c, soff[m], LCPOL));
 #endif
 }
 
@@ -540,11 +540,11 @@ __device__ __forceinline__ void b4_solve(uint8_t *__restrict__ table, const uint
     static_assert(NCH == NT, "one chunk per thread");
 
     // ---- pass A: chunk tid = positions 16 tid .. 16 tid + 15
-    if constexpr (LAT && LCPOL == 0) {
+    if constexpr (LAT) {
         const uint32_t c = tid;
         u32x4v v[K][NMAX];
 #pragma unroll
-        for (int k = 0; k < K; k++) p4_issue<HIGH>(table, hp[k], valid[k], c, v[k]);
+        for (int k = 0; k < K; k++) p4_issue<HIGH, LCPOL>(table, hp[k], valid[k], c, v[k]);
 #if GM_B4_LAT_BARRIER
         __builtin_amdgcn_sched_barrier(0);   // keep every load ahead of the first fold
 #endif
@@ -1695,6 +1695,9 @@ __device__ __forceinline__ uint32_t xcc_id() {
     return x & 7u;
 }
 
+#ifndef GM_FLOW_LAT
+#define GM_FLOW_LAT 0   // 1: the latency form of pass A (measured 7.5 ms against 5.4)
+#endif
 #ifndef GM_FLOW_WAVES
 #define GM_FLOW_WAVES 1
 #endif
@@ -1761,7 +1764,7 @@ __global__ __launch_bounds__(256, GM_FLOW_WAVES) void sub_flow_kernel_b4(uint8_t
             }
         }
         __syncthreads();
-        b4_solve<HIGH, CPOL_SC1, GM_FLOW_LOAD_CPOL>(table, zero, hp, valid, s);
+        b4_solve<HIGH, CPOL_SC1, GM_FLOW_LOAD_CPOL, false, GM_FLOW_LAT>(table, zero, hp, valid, s);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid < K && valid[tid]) __hip_atomic_store(&flags[hp[tid]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
