@@ -946,11 +946,13 @@ __device__ __forceinline__ void wk_walk(uint32_t *s, uint32_t lane) {
     auto step = [&](int t0, auto J, auto MASK) {
         constexpr int j = decltype(J)::value;
         constexpr bool masked = decltype(MASK)::value;
-        const uint32_t b0 = lbase + (uint32_t)(t0 >> 2);
-        const uint32_t o = b0 + cj[j];
-        const uint32_t Y1 = s[o - 16];   // stored one step ago (this lane or the row below)
-        const uint32_t on = b0 + cj[j + 1];   // cj[8] = cj[0] + 2: the next t0's first step
-        const uint32_t Fn = s[on], Y2n = s[on - 32];
+        // one base per position (its (y-2) dword): (y-1) and the position itself are at
+        // +16 and +32 dwords, immediate offsets of the same LDS address
+        const uint32_t b0 = lbase - 32u + (uint32_t)(t0 >> 2);
+        const uint32_t o2 = b0 + cj[j], o = o2 + 32u;
+        const uint32_t Y1 = s[o2 + 16];   // stored one step ago (this lane or the row below)
+        const uint32_t on2 = b0 + cj[j + 1];   // cj[8] = cj[0] + 2: the next t0's first step
+        const uint32_t Fn = s[on2 + 32], Y2n = s[on2];
         const uint32_t n1e = dpp_shr1(re[(j + 7) & 7]), n1o = dpp_shr1(ro[(j + 7) & 7]);
         const uint32_t n2e = dpp_shr2(re[(j + 6) & 7]), n2o = dpp_shr2(ro[(j + 6) & 7]);
         // all-ones on an active lane; opaque, so the compiler keeps this straight-line
