@@ -1008,7 +1008,7 @@ __device__ __forceinline__ void wk_walk(uint32_t *s, uint32_t lane) {
 
 // pass C: one wave writes the four blocks from image s (chunks lane + 64 i), and in the
 // sharded solve (XD) each block also to its extra destinations
-template <int CPOL, bool XD>
+template <int CPOL, bool XD, int NW = 1>
 __device__ __forceinline__ void wk_store(uint8_t *__restrict__ table, const uint32_t (&hp)[4], const bool (&valid)[4],
                                          const uint32_t *s, uint32_t lane, const uint32_t *__restrict__ xoff,
                                          const uint64_t *__restrict__ xdst, uint32_t idx0) {
@@ -1021,8 +1021,8 @@ __device__ __forceinline__ void wk_store(uint8_t *__restrict__ table, const uint
     for (int k = 0; k < K; k++) wr[k] = block_rsrc(table, 0);   // experiment: stores dropped (out of range)
 #endif
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t c = lane + 64u * i;
+    for (int i = 0; i < 4 / NW; i++) {   // lane = 0 .. 64 NW - 1 over the NW storing waves
+        const uint32_t c = lane + 64u * NW * i;
         const uint32_t base = wk_chunk(c);
         u32x4v out[K];
 #pragma unroll
@@ -1123,6 +1123,106 @@ __global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wkx(uint8_t 
                                                            const uint64_t *__restrict__ xdst) {
     __shared__ __attribute__((aligned(16))) uint32_t s[WK_IMG];
     wk_solve<HIGH, 0, true>(table, blocks, nblk, s, xoff, xdst);
+}
+
+// pass B by TWO waves (option 14): wave h walks the rows y = 8h .. 8h + 7, lane (z, yb) the
+// rows y = 8h + 2 yb + {0, 1} of column z in the order p = 2x + (y - 8h - 2 yb), starting
+// z + 2 yb + 16 h steps late: 69 steps instead of 91.  Every dependency is as in wk_walk
+// ((x-1 | x-2) now 2 / 4 steps back in the ring), except rows y = 8, 9 of wave 1, whose
+// (y-1 | y-2) wave 0 made 9-10 steps earlier: both waves pass a barrier every 8 steps, so
+// those LDS writes are visible.  An idle lane writes out of the LDS allocation (dropped).
+__device__ __forceinline__ void wk_walk2(uint32_t *s, uint32_t lane, uint32_t h) {
+    const uint32_t z = lane & 15, yb = lane >> 4;
+    const int s0 = (int)(z + 2u * yb + 16u * h);
+    const uint32_t lbase = 16u * (8u * h + 2u * yb + 2u) + WK_ZS * z;   // image dword of (0, 8h + 2yb, z)
+    uint32_t re[8], ro[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) re[j] = ro[j] = 0;
+    int cj[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) cj[j] = ((j - s0) >> 1) + 16 * ((j - s0) & 1);
+    constexpr uint32_t DUMMY = 0x3FFFFFC0u;   // an idle lane's write: beyond the allocation, dropped
+    uint32_t Fv, Y2v;
+    {
+        const uint32_t o2 = lbase - 32u + cj[0];
+        Fv = s[o2 + 32];
+        Y2v = s[o2];
+    }
+    auto step = [&](int t0, auto J) {
+        constexpr int j = decltype(J)::value;
+        const uint32_t b0 = lbase - 32u + (uint32_t)(t0 >> 1);
+        const uint32_t o2 = b0 + cj[j], o = o2 + 32u;
+        const uint32_t Y1 = s[o2 + 16];
+        const uint32_t on2 = b0 + cj[j + 1];   // cj[8] = cj[0] + 4
+        const uint32_t Fn = s[on2 + 32], Y2n = s[on2];
+        const uint32_t n1e = dpp_shr1(re[(j + 7) & 7]), n1o = dpp_shr1(ro[(j + 7) & 7]);
+        const uint32_t n2e = dpp_shr2(re[(j + 6) & 7]), n2o = dpp_shr2(ro[(j + 6) & 7]);
+        uint32_t act = (uint32_t)(t0 + j - s0) < 32u ? ~0u : 0u;
+        asm volatile("" : "+v"(act));
+        const uint32_t pe = pk_max(pk_max(Fv & 0x00FF00FFu, Y2v & 0x00FF00FFu),
+                                   pk_max(pk_max(n2e, re[(j + 6) & 7]), re[(j + 4) & 7]));
+        const uint32_t po = pk_max(pk_max(Fv, Y2v), pk_max(pk_max(n2o, ro[(j + 6) & 7]), ro[(j + 4) & 7]));
+        const uint32_t me = pk_max(pk_max(pe, n1e), Y1 & 0x00FF00FFu);
+        const uint32_t mo = pk_max(pk_max(po, n1o), Y1);
+        re[j] = wk_code_e(me) & act;
+        ro[j] = wk_code_o(mo) & act;
+        s[DUMMY + ((o - DUMMY) & act)] = re[j] | ro[j];
+        Fv = Fn;
+        Y2v = Y2n;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using I5 = std::integral_constant<int, 5>;
+    using I6 = std::integral_constant<int, 6>;
+    using I7 = std::integral_constant<int, 7>;
+    // steps 0 .. 71 (69 needed: the last three are idle for both waves), a barrier
+    // after every 8 (the other wave's (y-1 | y-2) writes of >= 9 steps ago are visible)
+    for (int t0 = 0; t0 < 72; t0 += 8) {
+        step(t0, I0{}); step(t0, I1{}); step(t0, I2{}); step(t0, I3{});
+        step(t0, I4{}); step(t0, I5{}); step(t0, I6{}); step(t0, I7{});
+        __syncthreads();
+    }
+}
+
+// option 14: pass A by 256 threads, pass B by two waves, pass C by each wave for its half
+// of the rows (chunks with y in its range)
+template <int HIGH, int CPOL, bool XD>
+__device__ __forceinline__ void wk2w_solve(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                           uint32_t nblk, uint32_t *s, const uint32_t *__restrict__ xoff = nullptr,
+                                           const uint64_t *__restrict__ xdst = nullptr) {
+    const uint32_t grp = xcd_order(blockIdx.x, (nblk + 3) / 4);
+    uint32_t hp[4];
+    bool valid[4];
+    wk_group(blocks, nblk, grp, hp, valid);
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    wk_load<HIGH>(table, hp, valid, s, tid, true);
+    __syncthreads();
+    const uint32_t w0 = (blockIdx.x & 1u) * 2u;   // waves (0, 1) or (2, 3): two SIMDs either way
+    if (wave != w0 && wave != w0 + 1) return;
+    wk_walk2(s, lane, wave - w0);
+    __syncthreads();   // both halves walked
+    wk_store<CPOL, XD, 2>(table, hp, valid, s, lane + 64u * (wave - w0), xoff, xdst, grp * 4);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk2w(uint8_t *__restrict__ table,
+                                                            const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                            const uint8_t *__restrict__ zero) {
+    __shared__ __attribute__((aligned(16))) uint32_t s[WK_IMG];
+    wk2w_solve<HIGH, GM_B4_STORE_CPOL, false>(table, blocks, nblk, s);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk2wx(uint8_t *__restrict__ table,
+                                                             const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                             const uint8_t *__restrict__ zero,
+                                                             const uint32_t *__restrict__ xoff,
+                                                             const uint64_t *__restrict__ xdst) {
+    __shared__ __attribute__((aligned(16))) uint32_t s[WK_IMG];
+    wk2w_solve<HIGH, 0, true>(table, blocks, nblk, s, xoff, xdst);
 }
 
 // option 12: two groups per workgroup of 256 threads, two images.  Pass A loads and
@@ -2042,6 +2142,18 @@ static tier_kernel_t pick_wkp(int high) {
     return nullptr;
 }
 
+static tier_kernel_t pick_wk2w(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel_wk2w<0>;
+    case 1: return sub_tier_kernel_wk2w<1>;
+    case 2: return sub_tier_kernel_wk2w<2>;
+    case 3: return sub_tier_kernel_wk2w<3>;
+    case 4: return sub_tier_kernel_wk2w<4>;
+    case 5: return sub_tier_kernel_wk2w<5>;
+    }
+    return nullptr;
+}
+
 static tier_kernel_t pick_wk2(int high) {
     switch (high) {
     case 0: return sub_tier_kernel_wk2<0>;
@@ -2133,6 +2245,7 @@ static tier_kernel_t pick_interleaved(int high, int nt) {
     if (nt == -6) return pick_wk(high);
     if (nt == -7) return pick_wkp(high);
     if (nt == -8) return pick_wk2(high);
+    if (nt == -10) return pick_wk2w(high);
     return nt == -2 ? pick_b4(high) : pick_x4(high, nt == -1);
 }
 
@@ -2157,7 +2270,9 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
     } else if (nt == -2 && nblocks <= b4_lat_max()) {
         hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), pad_lds(), s, table, list, nblocks,
                            zero);
-    } else if (nt == -6 && nblocks < wk_min_blocks()) {   // small tier: one workgroup's latency decides
+    } else if (nt == -10 && nblocks >= wk_min_blocks()) {
+        hipLaunchKernelGGL(pick_wk2w(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
+    } else if ((nt == -6 || nt == -10) && nblocks < wk_min_blocks()) {   // small tier: one workgroup's latency decides
         hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
     } else if (nt == -6) {
         hipLaunchKernelGGL(pick_wk(high), dim3((nblocks + 3) / 4), dim3(256), pad_lds(), s, table, list, nblocks, zero);
@@ -2199,6 +2314,17 @@ static tier_kernel_x_t pick_wkpx(int high) {
     return nullptr;
 }
 
+static tier_kernel_x_t pick_wk2wx(int high) {
+    switch (high) {
+    case 1: return sub_tier_kernel_wk2wx<1>;
+    case 2: return sub_tier_kernel_wk2wx<2>;
+    case 3: return sub_tier_kernel_wk2wx<3>;
+    case 4: return sub_tier_kernel_wk2wx<4>;
+    case 5: return sub_tier_kernel_wk2wx<5>;
+    }
+    return nullptr;
+}
+
 static tier_kernel_x_t pick_wk2x(int high) {
     switch (high) {
     case 1: return sub_tier_kernel_wk2x<1>;
@@ -2234,7 +2360,7 @@ static tier_kernel_x_t pick_w1x(int high) {
 
 bool sub_kernel_x_exists(int high) {
     return pick_b4x(high) != nullptr && pick_w1x(high) != nullptr && pick_wkx(high) != nullptr &&
-           pick_wkpx(high) != nullptr && pick_wk2x(high) != nullptr;
+           pick_wkpx(high) != nullptr && pick_wk2x(high) != nullptr && pick_wk2wx(high) != nullptr;
 }
 
 // kind: the sub_interleave option (8 one-wave kernel, 10 walker, otherwise the b4 kernel)
@@ -2253,6 +2379,7 @@ void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_
     }
     const bool wave = kind == 8;
     hipLaunchKernelGGL(wave ? pick_w1x(high) : kind == 10 && nblocks >= wk_min_blocks() ? pick_wkx(high)
+                       : kind == 14 && nblocks >= wk_min_blocks() ? pick_wk2wx(high)
                        : nblocks <= b4_lat_max() ? pick_b4x<true>(high) : pick_b4x<false>(high),
                        dim3((nblocks + 3) / 4), dim3(wave ? 64 : 256), 0, s,
                        table, list, nblocks, zero, xoff, xdst);
@@ -2269,6 +2396,7 @@ int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 11) return -7;
     if (low == 3 && c->sub_interleave == 12) return -8;
     if (low == 3 && c->sub_interleave == 13) return -9;
+    if (low == 3 && c->sub_interleave == 14) return -10;
     return c->sub_threads;
 }
 
