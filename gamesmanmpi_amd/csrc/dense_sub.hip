@@ -1225,6 +1225,69 @@ __global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk2wx(uint8_
     wk2w_solve<HIGH, 0, true>(table, blocks, nblk, s, xoff, xdst);
 }
 
+// option 15: two groups per workgroup, the second one's loads overlapped with the first's
+// walk.  The per-workgroup trace of option 10 showed the walk as the limiter: a CU keeps
+// ~2 walkers busy (the rest of its slots are loading), each walk 10 us.  Here pass A of
+// group A runs on all four waves; then the walking wave walks and writes A while the
+// other three load and fold group B into the second image (192 loader threads: chunks
+// 0-191 in one round, 192-255 by the first loader wave in a second); then the walker
+// walks and writes B.  The walker is busy for ~2/3 of the workgroup's life instead of
+// ~1/2.
+template <int HIGH, int CPOL, bool XD>
+__device__ __forceinline__ void wk2p_solve(uint8_t *__restrict__ table, const uint32_t *__restrict__ blocks,
+                                           uint32_t nblk, uint32_t *img, const uint32_t *__restrict__ xoff = nullptr,
+                                           const uint64_t *__restrict__ xdst = nullptr) {
+    const uint32_t ng = (nblk + 3) / 4;
+    const uint32_t pair = xcd_order(blockIdx.x, (ng + 1) / 2);
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const bool two = 2 * pair + 1 < ng;   // uniform
+    uint32_t hp[4];
+    bool valid[4];
+    wk_group(blocks, nblk, 2 * pair, hp, valid);
+    *(u32x2v *)(img + WK_IMG + WK_ZS * (tid >> 4) + 2u * (tid & 15u)) = u32x2v{0u, 0u};   // image 1's zero rows
+    wk_load<HIGH>(table, hp, valid, img, tid, true);
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+#if GM_WK_ROT
+    const uint32_t w0 = blockIdx.x & 3u;
+#else
+    const uint32_t w0 = 0;
+#endif
+    if (wave == w0) {
+        wk_walk(img, lane);
+        wk_store<CPOL, XD>(table, hp, valid, img, lane, xoff, xdst, 2 * pair * 4);
+    } else if (two) {
+        const uint32_t li = (wave + 3u - w0) & 3u, lt = li * 64u + lane;   // loader thread 0 .. 191
+        wk_group(blocks, nblk, 2 * pair + 1, hp, valid);
+        wk_load<HIGH>(table, hp, valid, img + WK_IMG, lt, false);
+        __builtin_amdgcn_sched_barrier(0);   // the second round reuses the first's registers
+        if (li == 0) wk_load<HIGH>(table, hp, valid, img + WK_IMG, 192u + lt, false);
+    }
+    __syncthreads();
+    if (wave != w0 || !two) return;
+    wk_group(blocks, nblk, 2 * pair + 1, hp, valid);
+    wk_walk(img + WK_IMG, lane);
+    wk_store<CPOL, XD>(table, hp, valid, img + WK_IMG, lane, xoff, xdst, (2 * pair + 1) * 4);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk2p(uint8_t *__restrict__ table,
+                                                            const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                            const uint8_t *__restrict__ zero) {
+    __shared__ __attribute__((aligned(16))) uint32_t img[2 * WK_IMG];   // 36.5 KiB
+    wk2p_solve<HIGH, GM_B4_STORE_CPOL, false>(table, blocks, nblk, img);
+}
+
+template <int HIGH>
+__global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wk2px(uint8_t *__restrict__ table,
+                                                             const uint32_t *__restrict__ blocks, uint32_t nblk,
+                                                             const uint8_t *__restrict__ zero,
+                                                             const uint32_t *__restrict__ xoff,
+                                                             const uint64_t *__restrict__ xdst) {
+    __shared__ __attribute__((aligned(16))) uint32_t img[2 * WK_IMG];
+    wk2p_solve<HIGH, 0, true>(table, blocks, nblk, img, xoff, xdst);
+}
+
 // option 12: two groups per workgroup of 256 threads, two images.  Pass A loads and
 // folds them one after the other (the same registers), then two waves walk them at
 // once, one group each.  Per group a CU's wave slots are held for ~13 us instead of
@@ -2154,6 +2217,18 @@ static tier_kernel_t pick_wk2w(int high) {
     return nullptr;
 }
 
+static tier_kernel_t pick_wk2p(int high) {
+    switch (high) {
+    case 0: return sub_tier_kernel_wk2p<0>;
+    case 1: return sub_tier_kernel_wk2p<1>;
+    case 2: return sub_tier_kernel_wk2p<2>;
+    case 3: return sub_tier_kernel_wk2p<3>;
+    case 4: return sub_tier_kernel_wk2p<4>;
+    case 5: return sub_tier_kernel_wk2p<5>;
+    }
+    return nullptr;
+}
+
 static tier_kernel_t pick_wk2(int high) {
     switch (high) {
     case 0: return sub_tier_kernel_wk2<0>;
@@ -2246,6 +2321,7 @@ static tier_kernel_t pick_interleaved(int high, int nt) {
     if (nt == -7) return pick_wkp(high);
     if (nt == -8) return pick_wk2(high);
     if (nt == -10) return pick_wk2w(high);
+    if (nt == -11) return pick_wk2p(high);
     return nt == -2 ? pick_b4(high) : pick_x4(high, nt == -1);
 }
 
@@ -2270,9 +2346,12 @@ void launch_sub_tier(int low, int high, int nt, uint32_t nblocks, uint8_t *table
     } else if (nt == -2 && nblocks <= b4_lat_max()) {
         hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), pad_lds(), s, table, list, nblocks,
                            zero);
+    } else if (nt == -11 && nblocks >= wk_min_blocks()) {
+        hipLaunchKernelGGL(pick_wk2p(high), dim3(((nblocks + 3) / 4 + 1) / 2), dim3(256), 0, s, table, list, nblocks,
+                           zero);
     } else if (nt == -10 && nblocks >= wk_min_blocks()) {
         hipLaunchKernelGGL(pick_wk2w(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
-    } else if ((nt == -6 || nt == -10) && nblocks < wk_min_blocks()) {   // small tier: one workgroup's latency decides
+    } else if ((nt == -6 || nt == -10 || nt == -11) && nblocks < wk_min_blocks()) {   // small tier: one workgroup's latency decides
         hipLaunchKernelGGL(pick_b4<true>(high), dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero);
     } else if (nt == -6) {
         hipLaunchKernelGGL(pick_wk(high), dim3((nblocks + 3) / 4), dim3(256), pad_lds(), s, table, list, nblocks, zero);
@@ -2325,6 +2404,17 @@ static tier_kernel_x_t pick_wk2wx(int high) {
     return nullptr;
 }
 
+static tier_kernel_x_t pick_wk2px(int high) {
+    switch (high) {
+    case 1: return sub_tier_kernel_wk2px<1>;
+    case 2: return sub_tier_kernel_wk2px<2>;
+    case 3: return sub_tier_kernel_wk2px<3>;
+    case 4: return sub_tier_kernel_wk2px<4>;
+    case 5: return sub_tier_kernel_wk2px<5>;
+    }
+    return nullptr;
+}
+
 static tier_kernel_x_t pick_wk2x(int high) {
     switch (high) {
     case 1: return sub_tier_kernel_wk2x<1>;
@@ -2360,13 +2450,19 @@ static tier_kernel_x_t pick_w1x(int high) {
 
 bool sub_kernel_x_exists(int high) {
     return pick_b4x(high) != nullptr && pick_w1x(high) != nullptr && pick_wkx(high) != nullptr &&
-           pick_wkpx(high) != nullptr && pick_wk2x(high) != nullptr && pick_wk2wx(high) != nullptr;
+           pick_wkpx(high) != nullptr && pick_wk2x(high) != nullptr && pick_wk2wx(high) != nullptr &&
+           pick_wk2px(high) != nullptr;
 }
 
 // kind: the sub_interleave option (8 one-wave kernel, 10 walker, otherwise the b4 kernel)
 void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
                        const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, int kind) {
     if (!nblocks) return;
+    if (kind == 15 && nblocks >= wk_min_blocks()) {
+        hipLaunchKernelGGL(pick_wk2px(high), dim3(((nblocks + 3) / 4 + 1) / 2), dim3(256), 0, s, table, list, nblocks,
+                           zero, xoff, xdst);
+        return;
+    }
     if (kind == 12) {
         hipLaunchKernelGGL(pick_wk2x(high), dim3(((nblocks + 3) / 4 + 1) / 2), dim3(256), 0, s, table, list, nblocks,
                            zero, xoff, xdst);
@@ -2397,6 +2493,7 @@ int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 12) return -8;
     if (low == 3 && c->sub_interleave == 13) return -9;
     if (low == 3 && c->sub_interleave == 14) return -10;
+    if (low == 3 && c->sub_interleave == 15) return -11;
     return c->sub_threads;
 }
 

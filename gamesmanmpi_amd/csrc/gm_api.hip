@@ -214,7 +214,7 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sub_threads = (int)v;
         return GM_OK;
     case GM_OPT_SUB_INTERLEAVE:
-        if (v != 1 && (v < 4 || v > 14)) { set_error("sub_interleave must be 1 or 4..14"); return GM_E_ARG; }
+        if (v != 1 && (v < 4 || v > 15)) { set_error("sub_interleave must be 1 or 4..15"); return GM_E_ARG; }
         c->sub_interleave = (int)v;
         return GM_OK;
     case GM_OPT_SUB_ORDER:

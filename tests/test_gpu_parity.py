@@ -151,16 +151,16 @@ def test_subtract_dense_vs_oracle(oracle, heaps, low):
     assert np.array_equal(r, ref)
 
 
-@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("variant", [4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("heaps", [3, 4, 5, 6])
 def test_subtract_kernel_variants_vs_oracle(oracle, heaps, variant):
-    """Interleaved kernel variants (GM_OPT_SUB_INTERLEAVE 4 / 5 / 6, 7 = dataflow, 8 = one wave, 10 = walker, 11 = pipelined walker, 12 = two walkers, 13 = row-granular dataflow, 14 = two-wave walker) against the oracle."""
+    """Interleaved kernel variants (GM_OPT_SUB_INTERLEAVE 4 / 5 / 6, 7 = dataflow, 8 = one wave, 10 = walker, 11 = pipelined walker, 12 = two walkers, 13 = row-granular dataflow, 14 = two-wave walker, 15 = two groups, second loaded during the first walk) against the oracle."""
     ref = oracle.subtract_dense(heaps)
     ctx, n, rec = _solve(SUB, (heaps,), sub_interleave=variant)
     assert np.array_equal(ctx.export()[1], ref)
 
 
-@pytest.mark.parametrize("variant", [5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("variant", [5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 def test_subtract_kernel_variants_full_2_32_match(variant):
     a, n1, r1 = _solve(SUB, (8,), sub_interleave=4)
     d1 = a.digest()
@@ -176,7 +176,7 @@ sys.path.insert(0, sys.argv[1])
 from gamesmanmpi_amd import Context, _lib
 ol = ctypes.CDLL(os.path.join(sys.argv[1], "oracle", "_build", "liboracle.so"))
 ol.oracle_subtract_dense.argtypes = [ctypes.c_int, ctypes.c_void_p]
-for heaps, variant in [(h, v) for h in (3, 4, 5, 6) for v in (10, 14)]:
+for heaps, variant in [(h, v) for h in (3, 4, 5, 6) for v in (10, 14, 15)]:
     ctx = Context(_lib.GAME_SUBTRACT, (heaps,), device=0)
     ctx.set_option(_lib.OPT_SUB_INTERLEAVE, variant)
     ctx.solve(ctx.initial())
