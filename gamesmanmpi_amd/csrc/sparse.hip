@@ -43,6 +43,7 @@ struct Sparse {
     ResRef *d_tabs = nullptr;                   // the tier tables, for the one-launch refill
     uint64_t replay_words = 0;
     hipGraphExec_t graph = nullptr;
+    gm_stats_t rec_stats{};                     // the recorded solve's counts, restored by a replay
 };
 
 // ----------------------------------------------------------------- kernels
@@ -360,6 +361,10 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
     }
     const double t1 = now_ms();
     c->root_record = (uint16_t)(rootw & 0xFFFF);
+    const gm_stats_t keep = c->stats;
+    c->stats = sp->rec_stats;
+    c->stats.kernel_launches = keep.kernel_launches;
+    c->stats.world = keep.world;
     c->stats.forward_ms = 0;
     c->stats.backward_ms = t1 - t0;
     c->stats.solve_ms = t1 - t0;
@@ -494,6 +499,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     c->stats.table_bytes = tb;
     // record for replay: the tables, lists and counts above belong to (game, params, root)
     plan_key_of(c, root, sp->plan_key);
+    sp->rec_stats = c->stats;
     sp->plan_ok = true;
     return GM_OK;
 }

@@ -96,11 +96,16 @@ def test_sparse_replay_is_identical(game, params, name):
     keys, recs = golden(name)
     ctx = Context(game, params, device=0)
     root = 6 if game == F2O else ctx.initial()
+    first = None
     for i in range(4):
         n, rec = ctx.solve(root)
         k, r = ctx.export()
         assert n == len(keys) and np.array_equal(k, keys) and np.array_equal(r, recs), i
         assert ctx.digest() == (digest(keys, recs), len(keys))
+        st = ctx.stats()   # a replay reports the recorded solve's counts, not zeros
+        counts = (st["n_positions"], st["n_tiers"], st["n_edges"], st["algo_bytes"], st["table_bytes"])
+        first = first or counts
+        assert counts == first and st["n_edges"] > 0, i
     if game == F2O:   # another root: a fresh synced solve, then its own replays
         k4, r4 = golden("four_to_one_four")
         for i in range(2):
