@@ -2561,9 +2561,44 @@ static uint64_t hilbert_of(uint32_t v, int high) {
     return h;
 }
 
+// Order 3: the Hilbert order's eight XCD runs (xcd_order) keep their blocks, but
+// each run is walked layer by layer in one high nibble (GM_ORDER_LAYER, default 3),
+// a 3-D Hilbert walk of the other free nibbles inside a layer, alternate layers
+// reversed: a child block's same-tier parents (+1 in one nibble) are then at most
+// about one layer apart in the run, inside the window the XCD's L2 still holds,
+// where the 4-D walk puts some of them half a run away.
+static int order_layer_nibble(int high) {
+    const char *s = getenv("GM_ORDER_LAYER");
+    const int j = s ? atoi(s) : 3;
+    return j >= 0 && j < high ? j : high - 1;
+}
+
+static void layer_runs(std::vector<uint32_t> &order, uint32_t b0, uint32_t b1, int high) {
+    if (high < 3) return;
+    const int L = order_layer_nibble(high);
+    auto key = [&](uint32_t v) {
+        uint32_t rest = 0;
+        for (int j = 0, k = 0; j < high - 1 && k < 3; j++)
+            if (j != L) rest |= ((v >> (4 * j)) & 15u) << (4 * k++);
+        const uint32_t layer = (v >> (4 * L)) & 15u;
+        const uint64_t h = hilbert_of(rest, std::min(high, 4));
+        return ((uint64_t)layer << 32) | (layer & 1u ? ~h & 0xFFFFFFFFull : h);
+    };
+    std::stable_sort(order.begin() + b0, order.begin() + b1,
+                     [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+}
+
 void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &off, int high, int mode) {
     for (size_t t = 0; t + 1 < off.size(); t++) {
-        if (mode == 2)
+        if (mode == 3) {
+            std::sort(order.begin() + off[t], order.begin() + off[t + 1],
+                      [high](uint32_t a, uint32_t b) { return hilbert_of(a, high) < hilbert_of(b, high); });
+            const uint32_t nb = off[t + 1] - off[t], ng = (nb + 3) / 4, q = ng >> 3, r = ng & 7;
+            for (uint32_t x = 0; x < 8; x++) {
+                const uint32_t g0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, len = x < r ? q + 1 : q;
+                if (len) layer_runs(order, off[t] + 4 * g0, off[t] + std::min(nb, 4 * (g0 + len)), high);
+            }
+        } else if (mode == 2)
             std::sort(order.begin() + off[t], order.begin() + off[t + 1],
                       [high](uint32_t a, uint32_t b) { return hilbert_of(a, high) < hilbert_of(b, high); });
         else

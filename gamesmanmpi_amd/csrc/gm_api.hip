@@ -218,7 +218,7 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sub_interleave = (int)v;
         return GM_OK;
     case GM_OPT_SUB_ORDER:
-        if (v < 0 || v > 2) { set_error("sub_order must be 0, 1 or 2"); return GM_E_ARG; }
+        if (v < 0 || v > 3) { set_error("sub_order must be 0, 1, 2 or 3"); return GM_E_ARG; }
         c->sub_order = (int)v;
         return GM_OK;
     case GM_OPT_DIST_BATCH:

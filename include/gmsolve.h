@@ -91,7 +91,9 @@ enum {
                                   9 = byte image, persistent, next group's loads pipelined into pass B,
                                   4 = u16 image, 5 = u16 image + anti-diagonal pass B; 1 = one block */
     GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton,
-                               2 = Hilbert walk of the tier's free high nibbles (default) */
+                               2 = Hilbert walk of the tier's free high nibbles (default), 3 = the
+                               Hilbert runs of the eight XCDs each walked layer by layer in one
+                               nibble (env GM_ORDER_LAYER; measured: more L2 misses) */
     GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
     GM_OPT_DIST_SLOTS = 10, /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
     GM_OPT_DIST_SOLO = 12,  /* diagnostic, loopback sharded SUBTRACT path: r + 1 = enqueue only rank r's

@@ -165,6 +165,17 @@ def test_subtract_kernel_variants_vs_oracle(oracle, heaps, variant):
     assert np.array_equal(ctx.export()[1], ref)
 
 
+@pytest.mark.parametrize("order", [0, 1, 2, 3])
+@pytest.mark.parametrize("heaps", [5, 6])
+def test_subtract_block_orders_vs_oracle(oracle, heaps, order):
+    """Block order inside a tier (GM_OPT_SUB_ORDER 0 key, 1 Morton, 2 Hilbert, 3 Hilbert
+    runs walked by layers, csrc/dense_sub.hip sort_tiers_morton) changes only which
+    workgroup solves which block: the table must not change."""
+    ref = oracle.subtract_dense(heaps)
+    ctx, n, rec = _solve(SUB, (heaps,), sub_order=order)
+    assert np.array_equal(ctx.export()[1], ref)
+
+
 @pytest.mark.parametrize("variant", [5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 def test_subtract_kernel_variants_full_2_32_match(variant):
     a, n1, r1 = _solve(SUB, (8,), sub_interleave=4)

@@ -57,6 +57,15 @@ struct Result { double l2_miss, mall_miss; };
 // order: sort key per block within a tier; groups of K blocks; xcd: whether runs per XCD
 static bool g_write_alloc = true;
 static bool g_flush = false;   // empty every L2 at each launch boundary
+static int g_layer = -1;       // >= 0: each XCD run re-walked layer by layer in this nibble (order 3)
+static uint64_t hilbert(const uint32_t *xin, int n, int b);
+static uint64_t layer_key(uint32_t v) {
+    uint32_t x[3];
+    for (int j = 0, k = 0; j < 4 && k < 3; j++) if (j != g_layer) x[k++] = nib(v, j);
+    const uint32_t layer = nib(v, g_layer);
+    const uint64_t h = hilbert(x, 3, 4);
+    return ((uint64_t)layer << 32) | (layer & 1u ? ~h & 0xFFFFFFFFull : h);
+}
 // Skilling's transpose form of the n-dimensional Hilbert index (b bits per axis)
 static uint64_t hilbert(const uint32_t *xin, int n, int b) {
     uint32_t x[8];
@@ -91,6 +100,15 @@ static Result run(std::function<uint64_t(uint32_t)> key, size_t l2cap, size_t ma
             for (auto &l : l2) { l.q.clear(); l.m.clear(); }
         std::stable_sort(t.begin(), t.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
         const uint32_t ng = (t.size() + K - 1) / K;
+        if (g_layer >= 0) {
+            const uint32_t q = ng >> 3, r = ng & 7;
+            for (uint32_t x = 0; x < 8; x++) {
+                const uint32_t g0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, len = x < r ? q + 1 : q;
+                if (!len) continue;
+                const size_t b0 = (size_t)K * g0, b1 = std::min(t.size(), (size_t)K * (g0 + len));
+                std::stable_sort(t.begin() + b0, t.begin() + b1, [](uint32_t a, uint32_t b) { return layer_key(a) < layer_key(b); });
+            }
+        }
         // per XCD, the groups in dispatch order
         std::vector<std::vector<uint32_t>> per(8);
         for (uint32_t b = 0; b < ng; b++) {
@@ -183,6 +201,16 @@ int main(int argc, char **argv) {
         fflush(stdout);
     };
     double imb = 0;
+    if (argc > 3 && argv[3][0] == 'L') {   // the order-3 comparison only
+        auto hil4 = [&](uint32_t v) { uint32_t x[4] = {(uint32_t)nib(v, 0), (uint32_t)nib(v, 1), (uint32_t)nib(v, 2), (uint32_t)nib(v, 3)}; return hilbert(x, 4, 4); };
+        show("hilbert 4D (h0..h3)", run(hil4, l2cap, mallcap));
+        for (g_layer = 0; g_layer < 5; g_layer++) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "hilbert 4D runs, layered in h%d", g_layer);
+            show(nm, run(hil4, l2cap, mallcap));
+        }
+        return 0;
+    }
     auto lt = [](uint32_t v, int a, int b) { return nib(v, a) < nib(v, b) || (nib(v, a) == nib(v, b) && (nib(v, 0) + nib(v, 1) + nib(v, 2) + nib(v, 3) + nib(v, 4)) % 2); };
     auto reg_cmp = [&](uint32_t v) {
         int s12 = nib(v, 0) + nib(v, 1), s34 = nib(v, 2) + nib(v, 3);
@@ -197,6 +225,12 @@ int main(int argc, char **argv) {
         show("morton (current)", run([&](uint32_t v) { return (uint64_t)morton(v, all5, 5); }, l2cap, mallcap));
         auto hil4 = [&](uint32_t v) { uint32_t x[4] = {(uint32_t)nib(v, 0), (uint32_t)nib(v, 1), (uint32_t)nib(v, 2), (uint32_t)nib(v, 3)}; return hilbert(x, 4, 4); };
         show("hilbert 4D (h0..h3)", run(hil4, l2cap, mallcap));
+        for (g_layer = 0; g_layer < 5; g_layer++) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "hilbert 4D runs, layered in h%d", g_layer);
+            show(nm, run(hil4, l2cap, mallcap));
+        }
+        g_layer = -1;
         auto hil5 = [&](uint32_t v) { uint32_t x[5]; for (int j = 0; j < 5; j++) x[j] = nib(v, j); return hilbert(x, 5, 4); };
         show("hilbert 5D", run(hil5, l2cap, mallcap));
         auto mor4 = [&](uint32_t v) { const int d4[4] = {0, 1, 2, 3}; return (uint64_t)morton(v, d4, 4); };
