@@ -2573,37 +2573,40 @@ static int order_layer_nibble(int high) {
     return j >= 0 && j < high ? j : high - 1;
 }
 
+// sorts order[b0, b1) by key(v); every key is unique inside a tier (its free nibbles
+// name the block), so the keys are computed once and the pairs sorted
+template <class K>
+static void sort_by_key(std::vector<uint32_t> &order, size_t b0, size_t b1, K key) {
+    std::vector<std::pair<uint64_t, uint32_t>> kv(b1 - b0);
+    for (size_t i = b0; i < b1; i++) kv[i - b0] = {key(order[i]), order[i]};
+    std::sort(kv.begin(), kv.end());
+    for (size_t i = b0; i < b1; i++) order[i] = kv[i - b0].second;
+}
+
 static void layer_runs(std::vector<uint32_t> &order, uint32_t b0, uint32_t b1, int high) {
     if (high < 3) return;
     const int L = order_layer_nibble(high);
-    auto key = [&](uint32_t v) {
+    sort_by_key(order, b0, b1, [&](uint32_t v) {
         uint32_t rest = 0;
         for (int j = 0, k = 0; j < high - 1 && k < 3; j++)
             if (j != L) rest |= ((v >> (4 * j)) & 15u) << (4 * k++);
         const uint32_t layer = (v >> (4 * L)) & 15u;
         const uint64_t h = hilbert_of(rest, std::min(high, 4));
         return ((uint64_t)layer << 32) | (layer & 1u ? ~h & 0xFFFFFFFFull : h);
-    };
-    std::stable_sort(order.begin() + b0, order.begin() + b1,
-                     [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+    });
 }
 
 void sort_tiers_morton(std::vector<uint32_t> &order, const std::vector<uint32_t> &off, int high, int mode) {
     for (size_t t = 0; t + 1 < off.size(); t++) {
+        if (mode >= 2) sort_by_key(order, off[t], off[t + 1], [high](uint32_t v) { return hilbert_of(v, high); });
+        else sort_by_key(order, off[t], off[t + 1], [high](uint32_t v) { return (uint64_t)morton_of(v, high); });
         if (mode == 3) {
-            std::sort(order.begin() + off[t], order.begin() + off[t + 1],
-                      [high](uint32_t a, uint32_t b) { return hilbert_of(a, high) < hilbert_of(b, high); });
             const uint32_t nb = off[t + 1] - off[t], ng = (nb + 3) / 4, q = ng >> 3, r = ng & 7;
             for (uint32_t x = 0; x < 8; x++) {
                 const uint32_t g0 = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q, len = x < r ? q + 1 : q;
                 if (len) layer_runs(order, off[t] + 4 * g0, off[t] + std::min(nb, 4 * (g0 + len)), high);
             }
-        } else if (mode == 2)
-            std::sort(order.begin() + off[t], order.begin() + off[t + 1],
-                      [high](uint32_t a, uint32_t b) { return hilbert_of(a, high) < hilbert_of(b, high); });
-        else
-            std::sort(order.begin() + off[t], order.begin() + off[t + 1],
-                      [high](uint32_t a, uint32_t b) { return morton_of(a, high) < morton_of(b, high); });
+        }
     }
 }
 
