@@ -201,6 +201,15 @@ int main(int argc, char **argv) {
         fflush(stdout);
     };
     double imb = 0;
+    if (argc > 3 && argv[3][0] == 'K') {   // blocks per workgroup sharing child loads
+        auto hil4 = [&](uint32_t v) { uint32_t x[4] = {(uint32_t)nib(v, 0), (uint32_t)nib(v, 1), (uint32_t)nib(v, 2), (uint32_t)nib(v, 3)}; return hilbert(x, 4, 4); };
+        for (int K : {4, 8, 16, 32}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "hilbert 4D, %d blocks per workgroup", K);
+            show(nm, run(hil4, l2cap, mallcap, K));
+        }
+        return 0;
+    }
     if (argc > 3 && argv[3][0] == 'L') {   // the order-3 comparison only
         auto hil4 = [&](uint32_t v) { uint32_t x[4] = {(uint32_t)nib(v, 0), (uint32_t)nib(v, 1), (uint32_t)nib(v, 2), (uint32_t)nib(v, 3)}; return hilbert(x, 4, 4); };
         show("hilbert 4D (h0..h3)", run(hil4, l2cap, mallcap));
