@@ -258,7 +258,8 @@ def other_configs(rank, world, dist, torch, budget_s=240.0, emit=None):
     timer.start()
     for name, game, params in (("othello_4x4", _lib.GAME_OTHELLO, (4, 4)), ("toot_6x4", _lib.GAME_TOOT, (6, 4))):
         try:
-            res[name] = sparse_config(name, game, params, rank, world, dist, torch)
+            res[name] = sparse_config(name, game, params, rank, world, dist, torch,
+                                      repeats=5 if name == "othello_4x4" else 2)
         except Exception as e:  # reported in the line; a rank that fails here leaves the others to the watchdog
             res[name] = {"error": "%s: %s" % (type(e).__name__, e)}
             if world > 1:
