@@ -277,7 +277,8 @@ def test_subtract_full_2_32_properties():
 
 def test_subtract_8_heaps_full_table_vs_oracle(oracle):
     """Config 5 at FULL size: the 2^32 table of the headline kernel instance
-    (sub_tier_kernel_b4<5>) equals the C oracle's, through the order-independent
+    (sub_tier_kernel_wk<5> on tiers of >= 4096 blocks, sub_tier_kernel_b4<5> below)
+    equals the C oracle's, through the order-independent
     digest of every (key, record) -- against the committed oracle digest
     (tests/golden/make_oracle_digests.py) and a live oracle solve on the host.
     Semantics: reference src/new_process.py:189-198, 249-250."""
