@@ -214,11 +214,15 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sub_threads = (int)v;
         return GM_OK;
     case GM_OPT_SUB_INTERLEAVE:
-        if (v != 1 && (v < 4 || v > 15)) { set_error("sub_interleave must be 1 or 4..15"); return GM_E_ARG; }
+        if (v != 1 && v != 6 && v != 10 && v != 13) {
+            set_error("sub_interleave must be 1 (one block per workgroup), 6 (four-block kernel), 10 (walker, "
+                      "default) or 13 (row-granular dataflow)");
+            return GM_E_ARG;
+        }
         c->sub_interleave = (int)v;
         return GM_OK;
     case GM_OPT_SUB_ORDER:
-        if (v < 0 || v > 3) { set_error("sub_order must be 0, 1, 2 or 3"); return GM_E_ARG; }
+        if (v < 0 || v > 2) { set_error("sub_order must be 0, 1 or 2"); return GM_E_ARG; }
         c->sub_order = (int)v;
         return GM_OK;
     case GM_OPT_DIST_BATCH:

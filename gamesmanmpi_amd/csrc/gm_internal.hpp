@@ -75,8 +75,8 @@ struct Ctx {
     int engine_opt = GM_ENGINE_AUTO;
     int sub_low = 3;
     int sub_threads = 128;
-    int sub_interleave = 10;     // 4 u16 image, 5 u16 + diagonal pass B, 6 byte image, 10 walker (default), 11 pipelined walker, 1 one block
-    int sub_order = 2;   // block order inside a tier: 0 key, 1 Morton, 2 Hilbert (default), 3 Hilbert runs walked by layers
+    int sub_interleave = 10;     // 10 walker (default), 6 four-block kernel, 13 row dataflow, 1 one block
+    int sub_order = 2;   // block order inside a tier: 0 key, 1 Morton, 2 Hilbert (default)
     bool use_graph = true;
     bool timing = false;
 

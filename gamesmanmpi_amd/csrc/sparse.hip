@@ -44,7 +44,19 @@ struct Sparse {
     uint64_t replay_words = 0;
     hipGraphExec_t graph = nullptr;
     gm_stats_t rec_stats{};                     // the recorded solve's counts, restored by a replay
+    uint64_t rec_n_positions = 0;               // ... and its position count and per-tier counts: another
+    std::vector<uint64_t> rec_tier_counts;      // engine may have solved on this context in between
 };
+
+// Abandon a capture that failed half-way: the stream must leave capture mode (the
+// caller falls back to a synced solve on it) and the partial graph is dropped.
+static int abort_capture(Ctx *c, int rc) {
+    hipGraph_t partial = nullptr;
+    (void)hipStreamEndCapture(c->stream, &partial);
+    if (partial) (void)hipGraphDestroy(partial);
+    (void)hipGetLastError();
+    return rc;
+}
 
 // ----------------------------------------------------------------- kernels
 // Also marks the parents with a LOSS-in-0 child (a move that wins at once): their
@@ -293,10 +305,11 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
     const double t0 = now_ms();
     if (!sp->graph) {
         // one buffer for everything read back: insert counts [0, NC), classify counters
-        // [NC, NC + 16 T), the device error word, the root record
+        // [NC, NC + 16 T), the device error word, the root record (kept from an
+        // earlier attempt whose capture failed)
         sp->replay_words = NC + 16 * T + 2;
-        GM_HIP(hipMalloc(&sp->d_replay, sp->replay_words * 8));
-        GM_HIP(hipHostMalloc(&sp->h_replay, sp->replay_words * 8, hipHostMallocDefault));
+        if (!sp->d_replay) GM_HIP(hipMalloc(&sp->d_replay, sp->replay_words * 8));
+        if (!sp->h_replay) GM_HIP(hipHostMalloc(&sp->h_replay, sp->replay_words * 8, hipHostMallocDefault));
         unsigned long long *cnt = sp->d_replay, *tscr = sp->d_replay + NC, *rootw = sp->d_replay + NC + 16 * T + 1;
         uint32_t *err = (uint32_t *)(sp->d_replay + NC + 16 * T);
         auto fref = [&](size_t u) { return FrontRef{u < T ? sp->tiers[u].slots : nullptr, u < T ? sp->tiers[u].cap : 0,
@@ -307,11 +320,12 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
             tabs[t] = res_ref(sp, t);
             maxcap = std::max(maxcap, sp->tiers[t].cap);
         }
-        GM_HIP(hipMalloc(&sp->d_tabs, T * sizeof(ResRef)));
+        if (!sp->d_tabs) GM_HIP(hipMalloc(&sp->d_tabs, T * sizeof(ResRef)));
         GM_HIP(hipMemcpy(sp->d_tabs, tabs.data(), T * sizeof(ResRef), hipMemcpyHostToDevice));
         hipGraph_t g;
         GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        GM_HIP(hipMemsetAsync(sp->d_replay, 0, sp->replay_words * 8, c->stream));
+        if (hipMemsetAsync(sp->d_replay, 0, sp->replay_words * 8, c->stream) != hipSuccess)
+            return abort_capture(c, GM_E_HIP);
         hipLaunchKernelGGL(slot_fill_many_kernel, dim3(grid_for(maxcap), (unsigned)T), dim3(256), 0, c->stream,
                            sp->d_tabs);   // refill every tier table with one launch
         hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, fref(0), root, err);
@@ -337,11 +351,23 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
         }
         hipLaunchKernelGGL(res_lookup_one_kernel, dim3(1), dim3(64), 0, c->stream, res_ref(sp, 0), d.canon(root),
                            rootw);
-        GM_HIP(hipMemcpyAsync(sp->h_replay, sp->d_replay, sp->replay_words * 8, hipMemcpyDeviceToHost, c->stream));
+        if (hipMemcpyAsync(sp->h_replay, sp->d_replay, sp->replay_words * 8, hipMemcpyDeviceToHost, c->stream) !=
+            hipSuccess)
+            return abort_capture(c, GM_E_HIP);
+        g = nullptr;
         const hipError_t e = hipStreamEndCapture(c->stream, &g);
-        if (e != hipSuccess) { set_error("sparse replay capture failed: %s", hipGetErrorString(e)); return GM_E_HIP; }
-        GM_HIP(hipGraphInstantiate(&sp->graph, g, nullptr, nullptr, 0));
-        GM_HIP(hipGraphDestroy(g));
+        if (e != hipSuccess) {
+            if (g) (void)hipGraphDestroy(g);
+            set_error("sparse replay capture failed: %s", hipGetErrorString(e));
+            return GM_E_HIP;
+        }
+        const hipError_t ie = hipGraphInstantiate(&sp->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ie != hipSuccess) {
+            sp->graph = nullptr;
+            set_error("sparse replay instantiate failed: %s", hipGetErrorString(ie));
+            return GM_E_HIP;
+        }
     }
     GM_HIP(hipGraphLaunch(sp->graph, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
@@ -361,6 +387,8 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
     }
     const double t1 = now_ms();
     c->root_record = (uint16_t)(rootw & 0xFFFF);
+    c->n_positions = sp->rec_n_positions;
+    c->tier_counts = sp->rec_tier_counts;
     const gm_stats_t keep = c->stats;
     c->stats = sp->rec_stats;
     c->stats.kernel_launches = keep.kernel_launches;
@@ -500,6 +528,8 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     // record for replay: the tables, lists and counts above belong to (game, params, root)
     plan_key_of(c, root, sp->plan_key);
     sp->rec_stats = c->stats;
+    sp->rec_n_positions = c->n_positions;
+    sp->rec_tier_counts = c->tier_counts;
     sp->plan_ok = true;
     return GM_OK;
 }

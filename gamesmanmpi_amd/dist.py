@@ -18,13 +18,30 @@ def unique_id():
     return buf.raw
 
 
-def share_unique_id(rank, backend="gloo"):
+def init_group(backend="gloo"):
+    """The launcher's process group (host side only: gloo touches no GPU); the
+    rendezvous comes from torch.distributed.run's MASTER_ADDR / MASTER_PORT."""
     import torch.distributed as tdist
     if not tdist.is_initialized():
         tdist.init_process_group(backend)
-    uid = [unique_id() if rank == 0 else None]
-    tdist.broadcast_object_list(uid, src=0)
-    return uid[0]
+    return tdist
+
+
+def broadcast(obj, src=0):
+    """`obj` of rank `src` on every rank (reference: comm.bcast)."""
+    box = [obj]
+    init_group().broadcast_object_list(box, src=src)
+    return box[0]
+
+
+def barrier():
+    """All ranks (reference solver_launcher.py:60,114,166 comm.Barrier)."""
+    init_group().barrier()
+
+
+def share_unique_id(rank, backend="gloo"):
+    init_group(backend)
+    return broadcast(unique_id() if rank == 0 else None)
 
 
 def join(ctx, rank, world, backend="gloo"):

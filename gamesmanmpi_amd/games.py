@@ -4,10 +4,12 @@ A GamesmanMPI plugin (``initial_position / gen_moves / do_move / primitive``,
 reference README.md:28-88) is solved on the GPU when one of the device
 descriptors (gamesmanmpi_amd/csrc/games.hpp) reproduces it.  ``identify()``
 finds that descriptor: each codec below converts the plugin's positions to u64
-keys, and the match is confirmed by replaying the plugin
-against the descriptor's host twin (``gm_expand_host``) on a sample of
-positions -- primitive values and child sets must agree exactly.
+keys, and a match must be certain: a known plugin file
+(code fingerprint, gamesmanmpi_amd/fingerprint.py) or an exhaustive replay of the
+plugin against the descriptor's host twin (``gm_expand_host``) -- primitive values
+and child sets must agree exactly on every reachable position.
 """
+import os
 import random
 
 import numpy as np
@@ -279,15 +281,78 @@ def verify(module, codec, root, samples=48, max_positions=600, seed=0):
         hd.close()
 
 
-def identify(module, root=None):
-    """Return the codec whose device descriptor reproduces ``module`` (or None)."""
+EXHAUSTIVE_MAX = int(os.environ.get("GM_BIND_EXHAUSTIVE_MAX", 1_000_000))
+
+
+def verify_exhaustive(module, codec, root, max_positions=None):
+    """Every position reachable from ``root`` checked against the descriptor: the
+    primitive value and the set of child keys.  True iff they all agree; False at
+    the first difference or once more than ``max_positions`` positions are reached
+    (then the match is not certain)."""
+    max_positions = EXHAUSTIVE_MAX if max_positions is None else max_positions
+    try:
+        hd = HostDescriptor(codec)
+    except _lib.GMError:
+        return False
+    try:
+        k0 = codec.key(root)
+        seen = {k0}
+        frontier = [root]
+        while frontier:
+            nxt = []
+            for pos in frontier:
+                prim, kids, _ = hd.expand(codec.key(pos))
+                if module.primitive(pos) != prim:
+                    return False
+                if prim != 4:
+                    continue
+                children = [module.do_move(pos, m) for m in module.gen_moves(pos)]
+                ck = [codec.key(c) for c in children]
+                if sorted(ck) != sorted(kids):
+                    return False
+                for c, k in zip(children, ck):
+                    if k not in seen:
+                        seen.add(k)
+                        nxt.append(c)
+                if len(seen) > max_positions:
+                    return False
+            frontier = nxt
+        return True
+    except (ValueError, TypeError, KeyError, IndexError, AttributeError, _lib.GMError):
+        return False
+    finally:
+        hd.close()
+
+
+def identify(module, root=None, exhaustive_max=None):
+    """Return the codec whose device descriptor reproduces ``module`` (or None).
+
+    Binding must be certain (a plugin that differs from a descriptor only in deep
+    or rare positions would otherwise be solved with the descriptor's rules, a
+    wrong answer with no error), so a codec is returned only when
+      * the plugin's code fingerprint (gamesmanmpi_amd/fingerprint.py) is one of the
+        plugin files that descriptor was written from -- the reference's own
+        test_games files or this repo's rewrites -- and a sample of positions
+        agrees (the board dimensions and heap count are module parameters); or
+      * every position reachable from ``root``, at most ``exhaustive_max``
+        (GM_BIND_EXHAUSTIVE_MAX, default 10^6), agrees with the descriptor.
+    Otherwise the plugin goes to the explicit-graph engine (gamesmanmpi_amd/graph.py).
+    Reference: the launcher's plugin check, solver_launcher.py:70-81."""
+    from . import fingerprint as fp
     if root is None:
         root = module.initial_position()
+    cands = []
     for codec in _candidates(module):
         try:
             codec.key(root)
         except (ValueError, TypeError, OverflowError):
             continue
-        if verify(module, codec, root):
+        cands.append(codec)
+    mine = fp.known().get(fp.fingerprint(module))
+    for codec in cands:
+        if mine and mine["codec"] == codec.name and verify(module, codec, root):
+            return codec
+    for codec in cands:
+        if verify(module, codec, root) and verify_exhaustive(module, codec, root, exhaustive_max):
             return codec
     return None

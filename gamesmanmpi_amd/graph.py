@@ -9,9 +9,12 @@ hands the graph to ``gm_solve_graph``, whose kernels run the retrograde.
 
 Host enumeration is level-synchronous.  A level of at least ``PAR_MIN``
 positions is expanded in batches by a pool of worker processes (the plugin's
-Python runs in parallel; ``GM_HOST_WORKERS``, default min(8, cpus)); the parent
-deduplicates the returned children in level order, so the numbering is the
-serial walk's.  Before each level the walk projects the next one from the
+Python runs in parallel; ``GM_HOST_WORKERS``, default the process's CPU share,
+at most 16); the pool is started while the first levels run serially, and the
+parent deduplicates each batch's children as it arrives, in level order, so the
+numbering is the serial walk's.  Workers rebuild the plugin from its file; when
+the caller's module differs from a fresh import in anything that cannot be
+passed along (a replaced function, a changed table), the walk stays serial.  Before each level the walk projects the next one from the
 growth so far and stops at once -- with the level sizes and the projection in
 the message -- when the reachable set would pass ``limit`` positions or the
 walk would pass ``budget_s`` seconds: a plugin far too large for host
@@ -29,8 +32,8 @@ import numpy as np
 from . import _lib
 
 UNDECIDED = 4
-PAR_MIN = 4096        # positions in a level before it is expanded by the worker pool
-BATCH = 2048          # positions per worker task
+PAR_MIN = 1024        # positions in a level before it is expanded by the worker pool
+BATCH = 1024          # positions per worker task
 
 
 class TooLarge(RuntimeError):
@@ -63,21 +66,76 @@ def _simple(v):
     return isinstance(v, tuple) and all(_simple(x) for x in v)
 
 
+def _load_fresh(path, name="gm_graph_plugin"):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _same(a, b):
+    """True when b (a fresh import's attribute) behaves as a (the caller's)."""
+    import types
+    if a is b:
+        return True
+    if isinstance(a, types.FunctionType) and isinstance(b, types.FunctionType):
+        ca, cb = a.__code__, b.__code__
+        if not (ca.co_code == cb.co_code and ca.co_consts == cb.co_consts and ca.co_names == cb.co_names
+                and a.__defaults__ == b.__defaults__ and len(a.__closure__ or ()) == len(b.__closure__ or ())):
+            return False
+        try:   # decorated functions (src.utils encode_int / decode_int): compare what they wrap
+            return all(_same(x.cell_contents, y.cell_contents) for x, y in zip(a.__closure__ or (), b.__closure__ or ()))
+        except ValueError:   # an empty cell
+            return False
+    if isinstance(a, types.ModuleType) or isinstance(a, type):
+        return a is b or getattr(a, "__name__", 0) == getattr(b, "__name__", 1)
+    try:
+        if isinstance(a, np.ndarray) or isinstance(b, np.ndarray):
+            return isinstance(a, np.ndarray) and isinstance(b, np.ndarray) and a.dtype == b.dtype and \
+                np.array_equal(a, b)
+        return type(a) is type(b) and bool(a == b)
+    except Exception:
+        return False
+
+
 def _module_spec(module):
-    """(file, simple module-level values) that rebuild the plugin in a worker, or None."""
+    """(file, module-level values) that rebuild the caller's plugin in a worker, or None
+    when that cannot be done faithfully.  A value the caller changed is passed along
+    if it pickles (ints, tuples, lists, dicts, arrays, ...); a replaced function or
+    anything else that differs from the file's own value makes the walk serial --
+    a worker would otherwise expand a different game with no error."""
+    import pickle
     path = getattr(module, "__file__", None)
     if not path or not os.path.exists(path):
         return None
-    attrs = {k: v for k, v in vars(module).items() if not k.startswith("__") and _simple(v)}
+    try:
+        fresh = _load_fresh(path, "gm_graph_plugin_check")
+    except Exception:
+        return None
+    attrs = {}
+    for k, v in vars(module).items():
+        if k.startswith("__"):
+            continue
+        if _simple(v):
+            attrs[k] = v
+        elif hasattr(fresh, k) and _same(v, getattr(fresh, k)):
+            continue
+        else:
+            import types
+            if isinstance(v, (types.FunctionType, types.ModuleType, type)):
+                return None
+            try:
+                pickle.dumps(v)
+            except Exception:
+                return None
+            attrs[k] = v
     return path, attrs
 
 
 def _worker_init(path, attrs):
     global _WORKER_MODULE
-    spec = importlib.util.spec_from_file_location("gm_graph_plugin", path)
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    for k, v in attrs.items():   # parameters the caller set on its module (board size, ...)
+    mod = _load_fresh(path)
+    for k, v in attrs.items():   # values the caller set on its module (board size, ...)
         setattr(mod, k, v)
     _WORKER_MODULE = mod
 
@@ -87,10 +145,20 @@ def _worker_expand(batch):
 
 
 def _default_workers():
+    """GM_HOST_WORKERS, else the CPUs this process may use (the GPU box grants each GPU a
+    share of a large machine and says so in OMP_NUM_THREADS), at most 16."""
     env = os.environ.get("GM_HOST_WORKERS")
     if env:
         return max(1, int(env))
-    return max(1, min(8, os.cpu_count() or 1))
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(16, n))
+
+
+def _noop():
+    return 0
 
 
 def _main_importable():
@@ -102,33 +170,48 @@ def _main_importable():
 
 
 class _Expander:
-    """Expands a level serially or, when large, in batches on a spawned worker pool.
-    Any pool failure (a worker that cannot start or dies) falls back to the serial walk."""
+    """Expands a level serially or, when large, in batches on a spawned worker pool,
+    yielding (primitive, children) per position in level order as batches complete.
+    The pool starts at construction (its processes import while the small first
+    levels run serially).  A pool failure (a worker that cannot start or dies)
+    before any result of a level was yielded falls back to the serial walk."""
 
     def __init__(self, module, workers):
         self.module = module
         self.workers = workers
         self.pool = None
         self.spec = _module_spec(module) if workers > 1 and _main_importable() else None
+        if self.spec is not None:
+            from concurrent.futures import ProcessPoolExecutor
+            try:
+                self.pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("spawn"),
+                                                initializer=_worker_init, initargs=self.spec)
+                for _ in range(self.workers):   # start every worker now
+                    self.pool.submit(_noop)
+            except (OSError, ImportError):
+                self.close()
+                self.spec = None
 
     def __call__(self, level):
         if self.spec is None or len(level) < PAR_MIN:
-            return [_expand_one(self.module, pos) for pos in level]
-        from concurrent.futures import ProcessPoolExecutor
+            for pos in level:
+                yield _expand_one(self.module, pos)
+            return
         from concurrent.futures.process import BrokenProcessPool
+        batches = [level[i:i + BATCH] for i in range(0, len(level), BATCH)]
+        done = 0
         try:
-            if self.pool is None:
-                self.pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("spawn"),
-                                                initializer=_worker_init, initargs=self.spec)
-            batches = [level[i:i + BATCH] for i in range(0, len(level), BATCH)]
-            out = []
             for res in self.pool.map(_worker_expand, batches):
-                out.extend(res)
-            return out
+                for r in res:
+                    yield r
+                done += 1
         except (BrokenProcessPool, OSError, ImportError):
+            if done:
+                raise
             self.close()
             self.spec = None
-            return [_expand_one(self.module, pos) for pos in level]
+            for pos in level:
+                yield _expand_one(self.module, pos)
 
     def close(self):
         if self.pool is not None:

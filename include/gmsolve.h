@@ -82,18 +82,13 @@ enum {
                                 context on one GPU (loopback transport instead of RCCL); for testing
                                 the multi-GPU partition on a single device */
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
-    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path, 4 blocks per workgroup: 11 = persistent workgroups, one
-                                  wave walks a byte LDS image with no barrier while four load the next (default),
-                                  10 = the same walk, one group per workgroup,
-                                  6 = byte LDS image, 256-thread barrier walk,
-                                  7 = byte image, whole solve as one dataflow launch (per-block child flags),
-                                  8 = byte image, one 64-lane wave per workgroup (no barriers),
-                                  9 = byte image, persistent, next group's loads pipelined into pass B,
-                                  4 = u16 image, 5 = u16 image + anti-diagonal pass B; 1 = one block */
+    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path, LOW = 3: 10 = the walker kernel on tiers of >= 4096
+                                  blocks, the four-block kernel below (default); 6 = the four-block kernel
+                                  (byte LDS image, 256-thread barrier walk) on every tier; 13 = the whole
+                                  solve as one row-granular dataflow launch (development option, measured
+                                  slower on one GPU); 1 = one block per workgroup of GM_OPT_SUB_THREADS */
     GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton,
-                               2 = Hilbert walk of the tier's free high nibbles (default), 3 = the
-                               Hilbert runs of the eight XCDs each walked layer by layer in one
-                               nibble (env GM_ORDER_LAYER; measured: more L2 misses) */
+                               2 = Hilbert walk of the tier's free high nibbles (default) */
     GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
     GM_OPT_DIST_SLOTS = 10, /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
     GM_OPT_DIST_SOLO = 12,  /* diagnostic, loopback sharded SUBTRACT path: r + 1 = enqueue only rank r's

@@ -13,9 +13,14 @@ solver_launcher.py:9-41; the plugin is loaded by path and published as
 Differences, on purpose:
 * ``--custom/--init_pos`` takes effect (the reference freezes the root at import,
   src/game_state.py:15, so it silently ignores them -- SURVEY §0.3);
-* the solve runs in libgmsolve.so on the GPU (one process per GPU; ranks come
-  from torch.distributed.run's environment instead of mpiexec), values and
-  remoteness are the canonical ones (SURVEY Appendix A);
+* the solve runs in libgmsolve.so on the GPU; ranks come from
+  torch.distributed.run's environment instead of mpiexec.  With one GPU per rank
+  the ranks shard the solve (RCCL); with more ranks than GPUs -- the reference's
+  own tests run ``mpiexec --oversubscribe -n 2`` on one host
+  (game_tests/four_to_one_test.py:20) -- rank 0 solves for all of them, running
+  the same sharded algorithm over ``world`` loopback ranks on its GPU, and the
+  other ranks wait at a barrier and exit 0.  Either way the root line is printed
+  once.  Values and remoteness are the canonical ones (SURVEY Appendix A);
 * ``-sd DIR`` writes the solved table in the reference's layout -- shelve
   databases ``DIR/stats/<rank>/resolved`` and ``remote`` keyed by ``str(pos)``,
   each position on rank ``md5(str(pos)) % world`` (src/cache_dict.py:19-42,
@@ -122,6 +127,23 @@ def dist_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
+MAX_VIRTUAL_RANKS = 64   # GM_OPT_VIRTUAL_RANKS range (include/gmsolve.h)
+
+
+def rank_plan(world, local_world, n_devices):
+    """How `world` launcher ranks share the solve (the reference's mpiexec -n N).
+
+    "solo"     one rank: it solves;
+    "sharded"  one GPU per rank on one node: every rank joins the RCCL solve;
+    "single"   more ranks than GPUs (mpiexec --oversubscribe): rank 0 solves for all,
+               the others wait at a barrier and exit 0."""
+    if world <= 1:
+        return "solo"
+    if local_world == world and world <= n_devices:
+        return "sharded"
+    return "single"
+
+
 def run(args, out=sys.stdout):
     rank, world, local = dist_env()
     if args.debug:
@@ -130,12 +152,24 @@ def run(args, out=sys.stdout):
     game, root = prepare_game(args)
 
     from gamesmanmpi_amd import Solver, _lib
-    engine = {"auto": None, "dense": _lib.ENGINE_DENSE, "sparse": _lib.ENGINE_SPARSE}[args.engine]
-    device = args.device if args.device is not None else (local if world > 1 else -1)
-    solver = Solver(game, root, device=device, engine=engine)
+    plan = "solo"
     if world > 1:
         from gamesmanmpi_amd import dist
+        dist.init_group()
+        plan = dist.broadcast(rank_plan(world, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
+                                        _lib.lib().gm_device_count()) if rank == 0 else None)
+        logging.debug("rank %d of %d: %s", rank, world, plan)
+        if plan == "single" and rank != 0:
+            dist.barrier()   # rank 0 solves for every rank; it prints the root line
+            return 0
+    engine = {"auto": None, "dense": _lib.ENGINE_DENSE, "sparse": _lib.ENGINE_SPARSE}[args.engine]
+    device = args.device if args.device is not None else (local if plan == "sharded" else -1)
+    solver = Solver(game, root, device=device, engine=engine)
+    if plan == "sharded":
         dist.join(solver.ctx, rank, world)
+    elif plan == "single" and solver.codec.game_id != _lib.GAME_GRAPH and world <= MAX_VIRTUAL_RANKS:
+        # the sharded algorithm over `world` loopback ranks on this one GPU
+        solver.ctx.set_option(_lib.OPT_VIRTUAL_RANKS, world)
     logging.debug("solving %s from %r on device %s", args.game_file, root, device)
     if args.cp:
         prof = cProfile.Profile()
@@ -151,14 +185,17 @@ def run(args, out=sys.stdout):
         st["rank"] = rank
         print(json.dumps(st), file=sys.stderr)
     if args.statsdir:
-        write_statsdir(args, solver, rank, world)
+        write_statsdir(args, solver, rank, world, gather=plan == "sharded")
     solver.close()
+    if plan == "single":
+        dist.barrier()
     return 0
 
 
-def write_statsdir(args, solver, rank, world):
+def write_statsdir(args, solver, rank, world, gather=True):
     """-sd DIR: this rank's npz table and/or the reference's shelve layout (rank 0
-    writes every rank's shelves, gathering the ranks' tables first)."""
+    writes every rank's shelves, gathering the sharded ranks' tables first; with
+    gather False rank 0 holds the whole table)."""
     from gamesmanmpi_amd.persist import write_reference_tables
     from gamesmanmpi_amd.solver import dump_table
     keys, recs = solver.table()
@@ -173,7 +210,7 @@ def write_statsdir(args, solver, rank, world):
         dump_table(os.path.join(args.statsdir, "stats", str(rank), "table.npz"), keys, recs,
                    {"game": args.game_file, "codec": solver.codec.name, "params": solver.codec.params})
     if fmt in ("reference", "both"):
-        if world > 1:
+        if world > 1 and gather:
             import numpy as np
             import torch.distributed as tdist
             parts = [None] * world

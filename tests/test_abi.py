@@ -122,6 +122,39 @@ def test_identify_rejects_a_modified_game():
     assert games.identify(mod) is None
 
 
+def test_identify_needs_certainty_not_a_sample():
+    """A plugin equal to mttt on every board of up to 6 pieces (all that the sampled
+    check sees first) must not bind to the TTT descriptor (exhaustive check,
+    games.identify); the sampled check alone would accept it."""
+    mod = load_plugin("tests/plugins/mttt_late_rule.py")
+    assert games.verify(mod, games.TTTStringCodec(), mod.initial_position(), samples=0)
+    assert games.identify(mod) is None
+
+
+def test_identify_binds_an_unknown_but_equal_plugin_exhaustively():
+    """mttt's rules rewritten (different code, same game): no known fingerprint, but
+    every reachable position agrees, so it binds -- and not when the exhaustive
+    check is capped below the game's 5,478 positions."""
+    mod = load_plugin("tests/plugins/mttt_late_rule.py")
+    orig = mod.primitive
+    mod.primitive = lambda pos: 1 if orig(pos) == 0 else orig(pos)   # WIN -> LOSS: exactly mttt
+    c = games.identify(mod)
+    assert c is not None and c.name == "mttt"
+    assert games.identify(mod, exhaustive_max=1000) is None
+
+
+def test_fingerprints_cover_this_repos_plugins():
+    """plugin_fingerprints.json is current (python -m gamesmanmpi_amd.fingerprint --write)."""
+    from gamesmanmpi_amd import fingerprint as fp
+    known = fp.known()
+    for rel, codec in fp.SOURCES:
+        got = known.get(fp.fingerprint(load_plugin(rel)))
+        assert got is not None and got["codec"] == codec, rel
+    # dimensions are parameters, not code: a patched board keeps its fingerprint
+    assert fp.fingerprint(load_plugin("test_games/othello_bit_new.py", length=4, height=4)) == \
+        fp.fingerprint(load_plugin("test_games/othello_bit_new.py"))
+
+
 def test_othello_8x8_has_no_descriptor():
     mod = load_plugin("test_games/othello_bit_new.py")     # reference default 8x8
     assert games.identify(mod) is None

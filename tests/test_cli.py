@@ -74,6 +74,73 @@ def test_dims_flag_patches_board_plugins():
     assert (game.length, game.height) == (4, 3) and len(root) == 6
 
 
+def test_rank_plan():
+    """mpiexec -n N semantics (reference solver_launcher.py:43-60): one GPU per rank ->
+    sharded; more ranks than GPUs (the reference's --oversubscribe tests) -> rank 0
+    solves for all."""
+    plan = solver_launcher.rank_plan
+    assert plan(1, 1, 0) == "solo" and plan(1, 1, 8) == "solo"
+    assert plan(2, 2, 8) == "sharded" and plan(8, 8, 8) == "sharded"
+    assert plan(5, 5, 1) == "single" and plan(2, 2, 1) == "single" and plan(9, 9, 8) == "single"
+    assert plan(4, 2, 8) == "single"   # two nodes: the RCCL solve is single-node
+
+
+_SINGLE_MODE_RANK = r'''
+import io, json, os, sys
+sys.path.insert(0, sys.argv[1])
+os.environ.update(RANK=sys.argv[2], LOCAL_RANK=sys.argv[2], WORLD_SIZE=sys.argv[3], LOCAL_WORLD_SIZE=sys.argv[3],
+                  MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[4])
+import solver_launcher, gamesmanmpi_amd
+seen = {}
+class FakeCtx:
+    def set_option(self, opt, v): seen[opt] = v
+    def stats(self): return {}
+class FakeSolver:   # stands in for the GPU solve (this container has no GPU)
+    def __init__(self, module, root, device=-1, engine=None):
+        from gamesmanmpi_amd import games
+        self.codec, self.ctx = games.FourToOneCodec(), FakeCtx()
+        seen["device"] = device
+    def solve(self): pass
+    def root_line(self): return "WIN in 3 moves"
+    def close(self): pass
+gamesmanmpi_amd.Solver = FakeSolver
+out = io.StringIO()
+args = solver_launcher.build_parser().parse_args([os.path.join(sys.argv[1], "test_games/four_to_one.py")])
+rc = solver_launcher.run(args, out=out)
+print(json.dumps({"rc": rc, "out": out.getvalue(), "seen": {str(k): v for k, v in seen.items()}}))
+'''
+
+
+def test_launcher_single_mode_ranks_gloo(tmp_path):
+    """More launcher ranks than GPUs (this container has none): rank 0 solves with
+    world loopback ranks (GM_OPT_VIRTUAL_RANKS) and prints the one root line; the
+    other ranks print nothing, wait at the barrier and return 0."""
+    import socket
+    import subprocess
+    import sys
+    from gamesmanmpi_amd import _lib
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    world = 3
+    procs = [subprocess.Popen([sys.executable, "-c", _SINGLE_MODE_RANK, REPO, str(r), str(world), str(port)],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    res = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=120)
+            assert p.returncode == 0, e
+            res.append(json.loads(o.strip().splitlines()[-1]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert all(r["rc"] == 0 for r in res)
+    assert res[0]["out"] == "WIN in 3 moves\n" and all(r["out"] == "" for r in res[1:])
+    assert res[0]["seen"] == {str(_lib.OPT_VIRTUAL_RANKS): world, "device": -1}
+    assert all(r["seen"] == {} for r in res[1:])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("argv,case", CASES)
 def test_launcher_root_lines(argv, case):
@@ -81,6 +148,33 @@ def test_launcher_root_lines(argv, case):
     args = solver_launcher.build_parser().parse_args(_abs(argv))
     assert solver_launcher.run(args, out=out) == 0
     assert out.getvalue() == ROOTS[case]["canonical"] + "\n"
+
+
+def _torchrun(nproc, argv, timeout=180):
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(REPO, "solver_launcher.py")] + _abs(argv)
+    return subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=timeout,
+                          env=dict(os.environ, PYTHONUNBUFFERED="1"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("argv,case", CASES)
+def test_launcher_under_torchrun_more_ranks_than_gpus(argv, case):
+    """The reference's game_tests run the launcher as `mpiexec --oversubscribe -n 2`
+    (four_to_one_test.py:14-23); BASELINE config 1 is `-n 5`.  Here: torch.distributed.run
+    with 5 ranks (Four-To-One) or 2 (mttt) on a one-GPU box; stdout must be exactly the
+    one root line."""
+    nproc = 5 if case.startswith("four_to_one") else 2
+    r = _torchrun(nproc, argv)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout == ROOTS[case]["canonical"] + "\n", (r.stdout, r.stderr[-2000:])
 
 
 @pytest.mark.gpu

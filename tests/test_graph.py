@@ -129,3 +129,20 @@ def test_enumeration_fails_fast_with_a_projection():
     with pytest.raises(TooLarge, match="projected"):
         enumerate_graph(mod, mod.initial_position(), limit=20_000, workers=1)
     assert time.perf_counter() - t < 60
+
+
+def test_parallel_walk_never_rebuilds_a_patched_plugin(monkeypatch):
+    """Workers rebuild the plugin from its file; a caller-replaced function must keep the
+    walk serial (else workers would expand the file's game), while a caller-changed table
+    travels to the workers.  Either way the graph equals the serial walk's."""
+    import gamesmanmpi_amd.graph as G
+    monkeypatch.setattr(G, "PAR_MIN", 16)
+    monkeypatch.setattr(G, "BATCH", 64)
+    mod = load_plugin("test_games/mttt.py")
+    orig = mod.primitive
+    mod.primitive = lambda pos: 1 if orig(pos) == 2 else orig(pos)   # misere: full board LOSS
+    assert G._module_spec(mod) is None
+    ser = enumerate_graph(mod, mod.initial_position(), workers=1)
+    par = enumerate_graph(mod, mod.initial_position(), workers=3)
+    assert ser[0] == par[0] and all(np.array_equal(a, b) for a, b in zip(ser[1:], par[1:]))
+    assert (par[1] == 1).sum() > (enumerate_graph(load_plugin("test_games/mttt.py"), "_" * 9, workers=1)[1] == 1).sum()
