@@ -65,6 +65,9 @@ def _oracle():
     P = ctypes.POINTER
     L.oracle_subtract_dense_mt.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     L.oracle_dense_digest.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, P(ctypes.c_uint64)]
+    L.oracle_dense_digest_blocks.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, P(ctypes.c_uint64),
+                                             P(ctypes.c_uint64)]
     L.oracle_initial.argtypes = [ctypes.c_int, P(ctypes.c_int32), ctypes.c_int, P(ctypes.c_uint64)]
     L.oracle_solve_layered.argtypes = [ctypes.c_int, P(ctypes.c_int32), ctypes.c_int, ctypes.c_uint64,
                                        ctypes.c_int, P(ctypes.c_uint64), P(ctypes.c_uint64),
@@ -132,28 +135,32 @@ def cpu_baseline(heaps=8):
             digest if heaps == 8 else None)
 
 
-def sparse_cpu_baseline(game, params):
+def sparse_cpu_baseline(game, params, root=None, what=None):
     """C oracle's sorted-layer OpenMP solver (oracle_solve_layered) on the host cores:
-    positions/s of one complete strong solve of `game` at `params`."""
+    positions/s of one complete strong solve of `game` at `params` from `root`
+    (default: the initial position)."""
     L = _oracle()
     if L is None:
         return None
     arr = (ctypes.c_int32 * len(params))(*params)
-    root = ctypes.c_uint64()
-    L.oracle_initial(game, arr, len(params), ctypes.byref(root))
+    if root is None:
+        r = ctypes.c_uint64()
+        L.oracle_initial(game, arr, len(params), ctypes.byref(r))
+        root = r.value
     npos, dg, rr, nt = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint16(), ctypes.c_int()
     t0 = time.perf_counter()
-    rc = L.oracle_solve_layered(game, arr, len(params), root, 0, ctypes.byref(npos), ctypes.byref(dg),
-                                ctypes.byref(rr), None, 0, ctypes.byref(nt))
+    rc = L.oracle_solve_layered(game, arr, len(params), ctypes.c_uint64(root), 0, ctypes.byref(npos),
+                                ctypes.byref(dg), ctypes.byref(rr), None, 0, ctypes.byref(nt))
     dt = time.perf_counter() - t0
     if rc != 0:
         return None
     return {"value": npos.value / dt, "unit": "positions/s", "cores": L.oracle_threads(), "kind": "port",
-            "positions": npos.value, "seconds": dt, "digest": dg.value,
-            "sample": "%s %s, all %d positions, %.2f s; C oracle sorted-layer retrograde "
+            "positions": npos.value, "seconds": dt, "digest": dg.value, "root_record": rr.value,
+            "sample": "%s %s, %s: all %d positions, %.2f s; C oracle sorted-layer retrograde "
                       "(oracle/gm_oracle.c oracle_solve_layered), OpenMP %d threads on %s; %s"
-                      % ({3: "Toot-and-Otto", 4: "Othello"}[game], "x".join(map(str, params)), npos.value, dt,
-                         L.oracle_threads(), _cpu_name(), THREAD_NOTE)}
+                      % ({3: "Toot-and-Otto", 4: "Othello"}[game], "x".join(map(str, params)),
+                         what or "from the initial position", npos.value, dt, L.oracle_threads(), _cpu_name(),
+                         THREAD_NOTE)}
 
 
 def committed_digest(name):
@@ -176,29 +183,65 @@ def summed_digest(ctx, world, dist, torch):
     return d, m
 
 
+def rank_digest_check(heaps, world, root, rank_digests, batch, slots, symmetry, owner):
+    """N > 1: each rank's gm_digest covers exactly its own blocks (csrc/dist_sub.hip
+    dist_sub_digest); compare every one with the C oracle's digest over the same
+    blocks (the rank's GM_PLAN_OWN list, host-only plan of the same options), so a
+    rank whose part of the table is wrong is named.  Rank 0 only; ~5 s of host work."""
+    L = _oracle()
+    if L is None:
+        return None
+    import numpy as np
+    from gamesmanmpi_amd import _lib
+    rec = np.empty(1 << (4 * heaps), dtype=np.uint16)
+    if L.oracle_subtract_dense_mt(heaps, rec.ctypes.data, 0) != 0:
+        return None
+    low = int(_lib.dist_plan(heaps, world, 0, _lib.PLAN_SHAPE, batch=batch, slots=slots, symmetry=symmetry,
+                             owner=owner)[1][0])
+    out = []
+    for r in range(world):
+        own = np.ascontiguousarray(_lib.dist_plan(heaps, world, r, _lib.PLAN_OWN, batch=batch, slots=slots,
+                                                  symmetry=symmetry, owner=owner)[1], dtype=np.uint32)
+        d, c = ctypes.c_uint64(), ctypes.c_uint64()
+        L.oracle_dense_digest_blocks(rec.ctypes.data, heaps, low, ctypes.c_uint64(root), own.ctypes.data,
+                                     ctypes.c_uint64(len(own)), 0, ctypes.byref(d), ctypes.byref(c))
+        got_d, got_n = rank_digests[r]
+        out.append({"rank": r, "blocks": int(len(own)), "positions": got_n,
+                    "ok": (got_d, got_n) == (d.value, c.value)})
+    return {"ranks": out, "wrong_ranks": [x["rank"] for x in out if not x["ok"]]}
+
+
 TOOT_6X4_PER_PLY = [1, 12, 114, 748, 4266, 19692, 81140, 285708, 928196, 2665424, 7098172, 17010952,
                     37792450, 64636776, 100084356, 136321692, 169785424, 180777508, 172831136,
                     135153280, 91440950, 45953432, 19196602, 4537828, 606968]   # SURVEY Appendix D
 
 
-def sparse_config(name, game, params, rank, world, dist, torch, repeats=2):
-    """Config 3 / 4 on the sparse engine, hash-sharded over the job's ranks (RCCL p2p,
-    csrc/dist_sparse.hip) when world > 1.  Checked: position count, root record,
-    per-ply counts (Toot 6x4: SURVEY Appendix D) and the full-table digest summed
-    over ranks against the C oracle's (tests/golden/oracle_digests.json).  Time =
-    max over ranks."""
-    from gamesmanmpi_amd import Context, _lib
-    ctx = Context(game, params, device=int(os.environ.get("LOCAL_RANK", 0)))
-    if world > 1:
-        uid = [None]
-        if rank == 0:
-            buf = ctypes.create_string_buffer(128)
-            _lib.check(_lib.lib().gm_comm_unique_id(buf, 128))
-            uid[0] = buf.raw
-        dist.broadcast_object_list(uid, src=0)
-        ctx.set_comm(rank, world, uid[0])
-    root = ctx.initial()
-    best = None
+SIDE_WARMUP, SIDE_REPEATS = 1, 5   # SURVEY §8d: median of 5 runs after 1 warm-up
+
+
+def toot_sample_root(params=(6, 4), plies=3):
+    """The bounded CPU sample of config 3: the Toot-and-Otto 6x4 position after `plies`
+    moves, taking at ply i the child (n // 2 + i) % n of the n children in gen_moves
+    order (csrc/games.hpp host twin, gm_expand_host).  After 3 plies the subgame has
+    106.4 M positions: ~7 s for the C oracle on the box's 16 host threads (after 4
+    plies 46.8 M, 3.3 s)."""
+    from gamesmanmpi_amd import games
+    hd = games.HostDescriptor(games.TootCodec(*params))
+    k = hd.initial()
+    try:
+        for i in range(plies):
+            kids = hd.expand(k)[1]
+            k = kids[(len(kids) // 2 + i) % len(kids)]
+    finally:
+        hd.close()
+    return k
+
+
+def timed_solves(ctx, root, rank, world, dist, torch, warmup=SIDE_WARMUP, repeats=SIDE_REPEATS):
+    """Solve times (s, max over ranks) of `repeats` solves after `warmup` untimed ones."""
+    for _ in range(warmup):
+        ctx.solve(root)
+    ts = []
     for _ in range(repeats):
         if world > 1:
             dist.barrier()
@@ -211,9 +254,33 @@ def sparse_config(name, game, params, rank, world, dist, torch, repeats=2):
             t = torch.tensor([dt], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
-        best = dt if best is None else min(best, dt)
+        ts.append(dt)
+    return n, rec, ts
+
+
+def sparse_config(name, game, params, rank, world, dist, torch):
+    """Config 3 / 4 on the sparse engine, hash-sharded over the job's ranks (RCCL p2p,
+    csrc/dist_sparse.hip) when world > 1.  Checked: position count, root record,
+    per-ply counts (Toot 6x4: SURVEY Appendix D) and the full-table digest summed
+    over ranks against the C oracle's (tests/golden/oracle_digests.json).  Time =
+    max over ranks, median of 5 after 1 warm-up."""
+    from gamesmanmpi_amd import Context, _lib
+    ctx = Context(game, params, device=int(os.environ.get("LOCAL_RANK", 0)))
+    if world > 1:
+        uid = [None]
+        if rank == 0:
+            buf = ctypes.create_string_buffer(128)
+            _lib.check(_lib.lib().gm_comm_unique_id(buf, 128))
+            uid[0] = buf.raw
+        dist.broadcast_object_list(uid, src=0)
+        ctx.set_comm(rank, world, uid[0])
+    root = ctx.initial()
+    n, rec, ts = timed_solves(ctx, root, rank, world, dist, torch)
+    med = sorted(ts)[len(ts) // 2]
     st = ctx.stats()
-    out = {"positions": n, "root_record": rec, "solve_ms": best * 1e3, "positions_per_s": n / best,
+    out = {"positions": n, "root_record": rec, "solve_ms": med * 1e3, "positions_per_s": n / med,
+           "statistic": "median of %d solves after %d warm-up (max over ranks)" % (SIDE_REPEATS, SIDE_WARMUP),
+           "solve_ms_all": [round(t * 1e3, 3) for t in ts],
            "ranks": world, "exchanged_bytes_rank%d" % rank: st["exchanged_bytes"]}
     ref = committed_digest(name)
     d, m = summed_digest(ctx, world, dist, torch)
@@ -226,6 +293,13 @@ def sparse_config(name, game, params, rank, world, dist, torch, repeats=2):
         out["ok"] = n == 1187212827 and out["per_ply_counts_match_appendix_d"] and out["digest_matches_oracle"]
         out["edges"] = st["n_edges"]
         out["algo_bytes_per_position"] = st["algo_bytes"] / n
+        if world == 1:   # the CPU leg's bounded sample, solved here too: the same workload on both
+            sub = toot_sample_root(params)
+            sn, srec, sts = timed_solves(ctx, sub, rank, world, dist, torch, warmup=1, repeats=3)
+            sm = sorted(sts)[1]
+            out["sample_on_gpu"] = {"root": "%#x" % sub, "positions": sn, "root_record": srec,
+                                    "solve_ms": sm * 1e3, "positions_per_s": sn / sm,
+                                    "statistic": "median of 3 after 1 warm-up"}
     else:
         out["workload"] = "Othello 4x4 (config 4), sparse engine" + (", hash-sharded" if world > 1 else "")
         out["ok"] = n == 54089 and (rec >> 14) == 1 and (rec & 0x3FFF) == 12 and out["digest_matches_oracle"]
@@ -234,7 +308,7 @@ def sparse_config(name, game, params, rank, world, dist, torch, repeats=2):
 
 
 SPARSE_CPU_SAMPLE = {"othello_4x4": (4, (4, 4)),    # the whole config-4 workload
-                     "toot_6x4": (3, (5, 4))}        # bounded sample: the 5x4 board (70 M positions, ~10-20 s)
+                     "toot_6x4": (3, (6, 4))}        # bounded sample: the 6x4 board from a ply-4 position
 
 
 def other_configs(rank, world, dist, torch, budget_s=240.0, emit=None):
@@ -258,15 +332,24 @@ def other_configs(rank, world, dist, torch, budget_s=240.0, emit=None):
     timer.start()
     for name, game, params in (("othello_4x4", _lib.GAME_OTHELLO, (4, 4)), ("toot_6x4", _lib.GAME_TOOT, (6, 4))):
         try:
-            res[name] = sparse_config(name, game, params, rank, world, dist, torch,
-                                      repeats=5 if name == "othello_4x4" else 2)
+            res[name] = sparse_config(name, game, params, rank, world, dist, torch)
         except Exception as e:  # reported in the line; a rank that fails here leaves the others to the watchdog
             res[name] = {"error": "%s: %s" % (type(e).__name__, e)}
             if world > 1:
                 break
         if rank == 0 and world == 1 and "error" not in res[name]:
             g, p = SPARSE_CPU_SAMPLE[name]
-            cb = sparse_cpu_baseline(g, p)
+            if name == "toot_6x4":
+                smp = res[name]["sample_on_gpu"]
+                cb = sparse_cpu_baseline(g, p, root=int(smp["root"], 16),
+                                         what="the subgame of the position %s after 3 plies (toot_sample_root)"
+                                              % smp["root"])
+                if cb is not None:
+                    cb["matches_gpu_sample"] = (cb["positions"] == smp["positions"]
+                                                and cb["root_record"] == smp["root_record"])
+                    res[name]["speedup_vs_cpu_baseline_same_sample"] = smp["positions_per_s"] / cb["value"]
+            else:
+                cb = sparse_cpu_baseline(g, p)
             if cb is not None:
                 res[name]["cpu_baseline"] = cb
                 res[name]["speedup_vs_cpu_baseline"] = res[name]["positions_per_s"] / cb["value"]
@@ -444,6 +527,17 @@ def main():
     # parity of the last timed solve: the whole table's digest (summed over ranks)
     # against the C oracle's digest of the same table
     digest, ndig = summed_digest(ctx, world, dist, torch)
+    rank_parity = None
+    if world > 1:
+        d0, m0 = ctx.digest()
+        mine = torch.tensor([d0 - (1 << 64) if d0 >= (1 << 63) else d0, m0], dtype=torch.int64, device="cuda")
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        if rank == 0 and args.virtual_ranks == 1:
+            rank_parity = rank_digest_check(args.heaps, world, root,
+                                            [(int(a[0].item()) & ((1 << 64) - 1), int(a[1].item())) for a in allr],
+                                            args.dist_batch, args.dist_slots, args.dist_symmetry, args.dist_owner)
+        barrier()
     watchdog.cancel()
     g = 0
     for i in range(args.heaps):
@@ -455,7 +549,8 @@ def main():
               "matches_committed_oracle_digest": (None if ref is None else
                                                   (digest, ndig, rec) == (ref["digest"], ref["positions"],
                                                                           ref["root_record"])),
-              "matches_live_oracle_digest": None}
+              "matches_live_oracle_digest": None,
+              "per_rank_vs_oracle": rank_parity}
 
     positions = n
     value = positions * args.steps / elapsed
@@ -522,7 +617,8 @@ def main():
         if live is not None and args.heaps == args.cpu_heaps == 8 and root == 0xFFFFFFFF:
             parity["matches_live_oracle_digest"] = live == digest
     parity["ok"] = bool(closed_form_ok and parity["matches_committed_oracle_digest"] is not False
-                        and parity["matches_live_oracle_digest"] is not False)
+                        and parity["matches_live_oracle_digest"] is not False
+                        and not (rank_parity and rank_parity["wrong_ranks"]))
     ctx.close()
     if args.virtual_ranks == 1 and not args.no_toot:
         del table

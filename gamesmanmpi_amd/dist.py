@@ -7,9 +7,28 @@ Replaces the reference's ``mpi4py.MPI.COMM_WORLD`` set-up
 communicator with ``gm_set_comm``.  All data-path exchange then happens inside
 libgmsolve.so (RCCL over xGMI).
 """
+import contextlib
 import ctypes
+import os
+import sys
 
 from . import _lib
+
+
+@contextlib.contextmanager
+def quiet_stdout():
+    """Send file descriptor 1 to stderr while the gloo group connects: gloo prints
+    "[Gloo] Rank r is connected to ..." on stdout, and the launcher's stdout must be
+    exactly the reference's root line (game_tests/four_to_one_test.py:23)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def unique_id():
@@ -23,20 +42,25 @@ def init_group(backend="gloo"):
     rendezvous comes from torch.distributed.run's MASTER_ADDR / MASTER_PORT."""
     import torch.distributed as tdist
     if not tdist.is_initialized():
-        tdist.init_process_group(backend)
+        with quiet_stdout():
+            tdist.init_process_group(backend)
     return tdist
 
 
 def broadcast(obj, src=0):
     """`obj` of rank `src` on every rank (reference: comm.bcast)."""
     box = [obj]
-    init_group().broadcast_object_list(box, src=src)
+    g = init_group()
+    with quiet_stdout():
+        g.broadcast_object_list(box, src=src)
     return box[0]
 
 
 def barrier():
     """All ranks (reference solver_launcher.py:60,114,166 comm.Barrier)."""
-    init_group().barrier()
+    g = init_group()
+    with quiet_stdout():
+        g.barrier()
 
 
 def share_unique_id(rank, backend="gloo"):

@@ -686,6 +686,36 @@ int oracle_dense_digest(const uint16_t *rec, uint64_t n, int threads, uint64_t *
     return 0;
 }
 
+/* The same digest restricted to whole blocks: positions hp << 4*low .. + 16^low - 1 of
+ * every listed high part hp that lie inside the root's box (every nibble <= the
+ * root's).  A sharded solve's rank digests its own blocks (gm_digest at N > 1), so
+ * this names the rank whose part of the table differs. */
+int oracle_dense_digest_blocks(const uint16_t *rec, int heaps, int low, uint64_t root, const uint32_t *blocks,
+                               uint64_t nblocks, int threads, uint64_t *digest, uint64_t *count) {
+    uint64_t sum = 0, cnt = 0;
+    const uint64_t bsz = 1ull << (4 * low);
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+#pragma omp parallel for reduction(+ : sum, cnt) schedule(dynamic, 64)
+    for (long long b = 0; b < (long long)nblocks; b++) {
+        const uint64_t base = (uint64_t)blocks[b] << (4 * low);
+        for (uint64_t i = 0; i < bsz; i++) {
+            const uint64_t k = base + i;
+            int in = 1;
+            for (int j = 0; j < heaps && in; j++) in = ((k >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
+            if (!in) continue;
+            sum += digest_term(k, rec[k]);
+            cnt++;
+        }
+    }
+    *digest = sum;
+    *count = cnt;
+    return 0;
+}
+
 /* ------------------------------------------------ layered solver (OpenMP) */
 /* The same Appendix-A fixed point as oracle_solve, on a different data
  * structure so the two check each other: per tier a SORTED array of distinct

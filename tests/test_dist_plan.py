@@ -258,3 +258,87 @@ def test_ring_slot_waits_name_the_last_nonempty_message(owner, heaps, world):
                     assert any(jp == prev and i < first_tier[t0] for i, jp in waits), \
                         "rank %d axis %d: message %d does not wait for %d" % (r, a, jj, prev)
                 assert len(waits) == max(0, len(nonempty) - 1)
+
+
+@pytest.mark.parametrize("world,owner", [(2, 0), (4, 0), (8, 0), (8, 1)])
+def test_rank_digests_partition_the_table(oracle, world, owner):
+    """bench.py at N > 1 names a wrong rank by comparing each rank's gm_digest (its own
+    blocks) with the oracle's digest over the same blocks (oracle_dense_digest_blocks on
+    the rank's GM_PLAN_OWN list).  The OWN lists partition the table, so those per-rank
+    oracle digests sum to the full-table digest; and rank_digest_check accepts them."""
+    import ctypes
+    import os
+    import sys
+    heaps, root = 6, (1 << 24) - 1
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    rec = oracle.subtract_dense_mt(heaps)
+    L = bench._oracle()
+    seen = np.zeros(1 << (4 * (heaps - 3)), dtype=np.int64)
+    per, total = [], 0
+    for r in range(world):
+        own = np.ascontiguousarray(_lib.dist_plan(heaps, world, r, _lib.PLAN_OWN, owner=owner)[1], dtype=np.uint32)
+        seen[own] += 1
+        d, c = ctypes.c_uint64(), ctypes.c_uint64()
+        L.oracle_dense_digest_blocks(rec.ctypes.data, heaps, 3, ctypes.c_uint64(root), own.ctypes.data,
+                                     ctypes.c_uint64(len(own)), 0, ctypes.byref(d), ctypes.byref(c))
+        per.append((d.value, c.value))
+        total = (total + d.value) & ((1 << 64) - 1)
+    assert (seen == 1).all()
+    assert (total, sum(c for _, c in per)) == (oracle.dense_digest(rec), 16 ** heaps)
+    chk = bench.rank_digest_check(heaps, world, root, per, 4, 4, 1, owner)
+    assert chk["wrong_ranks"] == [] and len(chk["ranks"]) == world
+    bad = list(per)
+    bad[world - 1] = (bad[world - 1][0] ^ 1, bad[world - 1][1])
+    assert bench.rank_digest_check(heaps, world, root, bad, 4, 4, 1, owner)["wrong_ranks"] == [world - 1]
+
+
+def _hang_rank(rank, world, phase, port):
+    import os
+    import time
+    import torch.distributed as tdist
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    phase("exchange")
+    if rank == 1:
+        phase("stuck on purpose")
+        while True:          # never reaches the collective: rank 0's all_reduce waits for ever
+            time.sleep(1)
+    import torch
+    t = torch.ones(1)
+    tdist.all_reduce(t)
+    return float(t.item())
+
+
+def test_rank_runner_stops_a_hung_rank():
+    """The multi-process runner of the RCCL GPU tests (tests/mp_ranks.py): a gloo rank that
+    hangs on purpose ends the run at its deadline, every rank process is gone, and the
+    failure names each rank's last phase."""
+    import time
+    from mp_ranks import RankFailure, run_ranks
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    t = time.monotonic()
+    with pytest.raises(RankFailure, match=r"timeout.*0=exchange, 1=stuck on purpose"):
+        run_ranks(_hang_rank, 2, (port,), timeout=20, grace=3)
+    assert time.monotonic() - t < 60
+
+
+def _ok_rank(rank, world, phase, port):
+    import os
+    import torch
+    import torch.distributed as tdist
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    t = torch.ones(1) * (rank + 1)
+    tdist.all_reduce(t)
+    return float(t.item())
+
+
+def test_rank_runner_collects_results():
+    from mp_ranks import run_ranks
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    assert run_ranks(_ok_rank, 3, (port,), timeout=60) == [6.0, 6.0, 6.0]

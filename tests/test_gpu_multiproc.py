@@ -29,46 +29,47 @@ def _devices():
     return torch.cuda.device_count()
 
 
-def _rank_main(rank, world, game, params, opts, uidq, out):
+def _rank_main(rank, world, phase, game, params, opts):
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")   # as bench.py: a queue per stream
-    try:
-        import ctypes
-        from gamesmanmpi_amd import Context, _lib
-        ctx = Context(game, params, device=rank)
-        if rank == 0:
-            buf = ctypes.create_string_buffer(128)
-            _lib.check(_lib.lib().gm_comm_unique_id(buf, 128))
-            for _ in range(world - 1):
-                uidq.put(buf.raw)
-            uid = buf.raw
-        else:
-            uid = uidq.get(timeout=120)
-        ctx.set_comm(rank, world, uid)
-        for k, v in opts.items():
-            ctx.set_option(getattr(_lib, "OPT_" + k.upper()), v)
-        n, rec = ctx.solve(ctx.initial())
-        d, m = ctx.digest()
-        out.put({"rank": rank, "n": n, "rec": rec, "digest": d, "m": m,
-                 "tiers": [int(x) for x in ctx.tier_counts()], "exchanged": ctx.stats()["exchanged_bytes"]})
-        ctx.close()
-    except Exception as e:  # reported to the parent
-        out.put({"rank": rank, "error": repr(e)})
+    import ctypes
+    import torch.distributed as tdist
+    from gamesmanmpi_amd import Context, _lib
+    tdist.init_process_group("gloo", rank=rank, world_size=world)   # MASTER_* from the parent
+    ctx = Context(game, params, device=rank)
+    phase("unique id")
+    uid = [None]
+    if rank == 0:
+        buf = ctypes.create_string_buffer(128)
+        _lib.check(_lib.lib().gm_comm_unique_id(buf, 128))
+        uid[0] = buf.raw
+    tdist.broadcast_object_list(uid, src=0)
+    phase("communicator")
+    ctx.set_comm(rank, world, uid[0])
+    for k, v in opts.items():
+        ctx.set_option(getattr(_lib, "OPT_" + k.upper()), v)
+    phase("solve")
+    n, rec = ctx.solve(ctx.initial())
+    phase("digest")
+    d, m = ctx.digest()
+    res = {"rank": rank, "n": n, "rec": rec, "digest": d, "m": m,
+           "tiers": [int(x) for x in ctx.tier_counts()], "exchanged": ctx.stats()["exchanged_bytes"]}
+    ctx.close()
+    return res
 
 
 def _run(world, game, params, opts=None):
+    """Every rank in its own process; on a timeout, an error or a dead rank, every
+    rank is terminated then killed and the failure names each rank's last phase
+    (tests/mp_ranks.py)."""
     if _devices() < world:
         pytest.skip("needs %d GPUs (one process per GPU over RCCL)" % world)
-    ctx = mp.get_context("spawn")
-    uidq, out = ctx.Queue(), ctx.Queue()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, game, params, opts or {}, uidq, out))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    res = [out.get(timeout=240) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-    assert all("error" not in r for r in res), res
-    return sorted(res, key=lambda r: r["rank"])
+    import socket
+    from mp_ranks import run_ranks
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = "127.0.0.1", str(port)
+    return run_ranks(_rank_main, world, (game, params, opts or {}), timeout=240)
 
 
 def _summed(res):
