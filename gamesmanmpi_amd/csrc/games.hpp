@@ -248,15 +248,83 @@ GM_HD DescToot unreduced(const DescToot &d) {
     return r;
 }
 
+
 // ---------------------------------------------------------------- Othello
 // reference test_games/othello_bit_new.py (square boards).  Key = all 2A+16
 // string bits: WHITE plane at [A+16, 2A+16), BLACK plane at [16, A+16), the
 // signed turn byte (1 BLACK, 2 WHITE) at bits 8..15, the pass byte at 0..7.
-struct DescOthello : NoSym {
+struct DescOthello {
     static constexpr int MAX_SKIP = 3;
     static constexpr int MAXC = 24;
     int L, A;
     uint32_t amask;
+    // Board symmetries (set per solve, gm_api.hip): bit g of `sym` = element g of the
+    // square's dihedral group D4 (0 identity, 1-3 rotations by 90/180/270 degrees, 4
+    // transpose, 5 anti-transpose, 6/7 mirrors in x/y) that maps the ROOT to itself.
+    // The rules -- flips along all 8 directions, the pass rule, the piece count -- are
+    // invariant under D4 with colours kept, so positions in one orbit share value and
+    // remoteness, and the positions reachable from a root that the subgroup fixes are
+    // closed under it: visit() returns canonical children (min over the orbit) and
+    // every count / export / digest expands the orbit.  From the standard start the
+    // subgroup is {identity, rotation by 180, transpose, anti-transpose}.  The
+    // reference's own declared symmetry, player_flip (othello_bit_new.py:224-235:
+    // colours swapped and the turn advanced), fixes no reachable position set: a
+    // reachable position's turn is fixed by its piece count (a pass keeps the mover,
+    // who then passes again and ends the game), and player_flip keeps the pieces but
+    // swaps the turn -- it maps every reachable position to an unreachable one, so it
+    // merges nothing.
+    uint32_t sym = 0;
+    GM_HD uint32_t xform_plane(uint32_t p, int g) const {
+        uint32_t out = 0;
+        for (int y = 0; y < L; y++)
+            for (int x = 0; x < L; x++) {
+                if (!((p >> (L * y + x)) & 1u)) continue;
+                int nx = x, ny = y;
+                switch (g) {
+                case 1: nx = L - 1 - y; ny = x; break;
+                case 2: nx = L - 1 - x; ny = L - 1 - y; break;
+                case 3: nx = y; ny = L - 1 - x; break;
+                case 4: nx = y; ny = x; break;
+                case 5: nx = L - 1 - y; ny = L - 1 - x; break;
+                case 6: nx = L - 1 - x; break;
+                case 7: ny = L - 1 - y; break;
+                }
+                out |= 1u << (L * ny + nx);
+            }
+        return out;
+    }
+    GM_HD uint64_t xform(uint64_t k, int g) const {
+        return ((uint64_t)xform_plane(wplane(k), g) << (A + 16)) | ((uint64_t)xform_plane(bplane(k), g) << 16) |
+               (k & 0xFFFFull);
+    }
+    GM_HD uint64_t canon(uint64_t k) const {
+        uint64_t m = k;
+        for (int g = 1; g < 8; g++)
+            if ((sym >> g) & 1u) {
+                const uint64_t t = xform(k, g);
+                m = t < m ? t : m;
+            }
+        return m;
+    }
+    template <class F>
+    GM_HD void orbit(uint64_t k, F &&f) const {
+        uint64_t seen[8];
+        int n = 0;
+        for (int g = 0; g < 8; g++) {
+            if (g && !((sym >> g) & 1u)) continue;
+            const uint64_t t = g ? xform(k, g) : k;
+            bool dup = false;
+            for (int i = 0; i < n; i++) dup |= seen[i] == t;
+            if (!dup) { seen[n++] = t; f(t); }
+        }
+    }
+    // the elements of D4 that fix k (bit 0 always set)
+    GM_HD uint32_t stabilizer(uint64_t k) const {
+        uint32_t s = 1u;
+        for (int g = 1; g < 8; g++)
+            if (xform(k, g) == k) s |= 1u << g;
+        return s;
+    }
 
     static bool make(int L_, int H_, DescOthello *d) {
         if (L_ != H_ || L_ < 2 || (L_ & 1) || 2 * L_ * H_ + 16 > 64) return false;
@@ -309,9 +377,9 @@ struct DescOthello : NoSym {
                 uint32_t nme = me | cell | f, nopp = opp & ~f;
                 uint32_t nw = black ? nopp : nme, nb = black ? nme : nopp;
                 n++;
-                if (!fn(((uint64_t)nw << (A + 16)) | ((uint64_t)nb << 16) | low)) return;
+                if (!fn(canon(((uint64_t)nw << (A + 16)) | ((uint64_t)nb << 16) | low))) return;
             }
-        if (!n) fn(k + 1);                                        // [None]: pass + 1 (:122-124)
+        if (!n) fn(canon(k + 1));                                 // [None]: pass + 1 (:122-124)
     }
     GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
     // The split kernels' per-lane share of visit(): the children from the empty squares
@@ -335,11 +403,11 @@ struct DescOthello : NoSym {
             uint32_t nme = me | cell | f, nopp = opp & ~f;
             uint32_t nw = black ? nopp : nme, nb = black ? nme : nopp;
             n++;
-            if (!fn(((uint64_t)nw << (A + 16)) | ((uint64_t)nb << 16) | low)) return n;
+            if (!fn(canon(((uint64_t)nw << (A + 16)) | ((uint64_t)nb << 16) | low))) return n;
         }
         return n;
     }
-    GM_HD uint64_t pass_child(uint64_t k) const { return k + 1; }
+    GM_HD uint64_t pass_child(uint64_t k) const { return canon(k + 1); }
     GM_HD int64_t tier(uint64_t k) const {
         return 3 * popc64(wplane(k) | bplane(k)) + sbyte(k, 0);
     }
@@ -350,6 +418,12 @@ struct DescOthello : NoSym {
         return (turn == 1 || turn == 2) && pass >= 0 && pass <= 2;
     }
 };
+
+GM_HD DescOthello unreduced(const DescOthello &d) {
+    DescOthello r = d;
+    r.sym = 0;
+    return r;
+}
 
 // ---------------------------------------------------------------- Subtract
 // The build's synthetic game: `heaps` heaps of 4 bits; a move

@@ -295,7 +295,12 @@ int gm_expand_host(gm_ctx *h, uint64_t key, uint64_t *children, int cap, int *n,
         p = d.primitive(key); t = d.tier(key); if (p == UNDECIDED) k = d.children(key, kids);
         break;
     }
-    case GM_GAME_OTHELLO: p = c->oth.primitive(key); t = c->oth.tier(key); if (p == UNDECIDED) k = c->oth.children(key, kids); break;
+    case GM_GAME_OTHELLO: {   // the plugin's own moves: no symmetry reduction
+        DescOthello d = c->oth;
+        d.sym = 0;
+        p = d.primitive(key); t = d.tier(key); if (p == UNDECIDED) k = d.children(key, kids);
+        break;
+    }
     case GM_GAME_SUBTRACT: p = c->sub.primitive(key); t = c->sub.tier(key); if (p == UNDECIDED) k = c->sub.children(key, kids); break;
     default: return GM_E_GAME;
     }
@@ -345,8 +350,10 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     c->stats.kernel_launches = c->timing ? launches : 0;
     c->stats.world = c->world;
     c->root = root;
-    // symmetry reduction (games.hpp): Toot-and-Otto's mirror, when the root is its own mirror image
+    // symmetry reduction (games.hpp): Toot-and-Otto's mirror, when the root is its own mirror image;
     if (c->game == GM_GAME_TOOT) c->toot.sym = (c->symmetry && c->toot.mirror(root) == root) ? 1u : 0u;
+    // Othello: the board symmetries that fix the root (games.hpp DescOthello::sym)
+    if (c->game == GM_GAME_OTHELLO) c->oth.sym = c->symmetry ? c->oth.stabilizer(root) : 0u;
     int eng = engine_for(c);
     // GM_ENGINE_DIST_SPARSE forces the hash-sharded engine, e.g. over a one-rank communicator
     const bool force_dist_sparse = c->engine_opt == GM_ENGINE_DIST_SPARSE;

@@ -281,7 +281,8 @@ static bool replay_enabled() {
 
 static void plan_key_of(const Ctx *c, uint64_t root, int64_t (&key)[7]) {
     const int64_t k[7] = {c->game, c->params[0], c->params[1], c->params[2], c->params[3], (int64_t)root,
-                          c->game == GM_GAME_TOOT ? (int64_t)c->toot.sym : 0};
+                          c->game == GM_GAME_TOOT ? (int64_t)c->toot.sym
+                          : c->game == GM_GAME_OTHELLO ? (int64_t)c->oth.sym : 0};
     std::copy(k, k + 7, key);
 }
 

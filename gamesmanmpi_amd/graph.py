@@ -21,7 +21,18 @@ walk would pass ``budget_s`` seconds: a plugin far too large for host
 enumeration (e.g. othello_bit_new.py at its 8x8 default) fails in seconds
 instead of running for days.  Positions must be hashable, or numpy arrays
 (keyed by dtype, shape and bytes).
+
+Symmetry.  A plugin may declare ``symmetry_functions()``, a list
+of ``(function, order)`` pairs (the reference's hook, othello_bit_new.py:224-225,
+which its engines never call).  The walk uses those functions that map the root
+to itself: the positions reachable from such a root are closed under them, so
+it numbers one representative per orbit (the least position of the orbit, in a
+fixed byte order), expands only representatives, and counts, exports and
+persists every member of every orbit.  A declared function that moves the root
+is not used: its images of reachable positions need not be reachable
+(Othello's player_flip maps every reachable position to an unreachable one).
 """
+import pickle
 import importlib.util
 import multiprocessing as mp
 import os
@@ -47,17 +58,71 @@ def position_key(pos):
     return pos
 
 
-def _expand_one(module, pos):
+def _order(pos):
+    return pickle.dumps(position_key(pos), protocol=4)
+
+
+def symmetry_generators(module, root):
+    """Indices of the plugin's symmetry_functions() that map `root` to itself."""
+    decl = getattr(module, "symmetry_functions", None)
+    if not callable(decl):
+        return []
+    out = []
+    try:
+        items = list(decl())
+    except Exception:
+        return []
+    for i, item in enumerate(items):
+        f = item[0] if isinstance(item, tuple) else item
+        try:
+            if callable(f) and position_key(f(root)) == position_key(root):
+                out.append(i)
+        except Exception:
+            pass
+    return out
+
+
+def _generators(module, idx):
+    if not idx:
+        return []
+    items = list(module.symmetry_functions())
+    return [items[i][0] if isinstance(items[i], tuple) else items[i] for i in idx]
+
+
+def orbit(pos, gens):
+    """Every image of pos under the group the functions generate, pos first."""
+    out, seen, todo = [pos], {position_key(pos)}, [pos]
+    while todo:
+        p = todo.pop()
+        for g in gens:
+            q = g(p)
+            k = position_key(q)
+            if k not in seen:
+                seen.add(k)
+                out.append(q)
+                todo.append(q)
+    return out
+
+
+def canonical(pos, gens):
+    """The orbit's representative: its least member in pickled-key byte order."""
+    return min(orbit(pos, gens), key=_order) if gens else pos
+
+
+def _expand_one(module, pos, gens=()):
     p = module.primitive(pos)
     if not isinstance(p, (int, np.integer)) or not 0 <= int(p) <= 4:
         raise ValueError("primitive(%r) returned %r, not a src.utils code" % (pos, p))
     p = int(p)
     kids = [module.do_move(pos, m) for m in module.gen_moves(pos)] if p == UNDECIDED else []
+    if gens:
+        kids = [canonical(c, gens) for c in kids]
     return p, kids
 
 
 # ---------------------------------------------------------------- worker pool
 _WORKER_MODULE = None
+_WORKER_GENS = []
 
 
 def _simple(v):
@@ -132,16 +197,17 @@ def _module_spec(module):
     return path, attrs
 
 
-def _worker_init(path, attrs):
-    global _WORKER_MODULE
+def _worker_init(path, attrs, gen_idx=()):
+    global _WORKER_MODULE, _WORKER_GENS
     mod = _load_fresh(path)
     for k, v in attrs.items():   # values the caller set on its module (board size, ...)
         setattr(mod, k, v)
     _WORKER_MODULE = mod
+    _WORKER_GENS = _generators(mod, list(gen_idx))
 
 
 def _worker_expand(batch):
-    return [_expand_one(_WORKER_MODULE, pos) for pos in batch]
+    return [_expand_one(_WORKER_MODULE, pos, _WORKER_GENS) for pos in batch]
 
 
 def _default_workers():
@@ -176,16 +242,17 @@ class _Expander:
     levels run serially).  A pool failure (a worker that cannot start or dies)
     before any result of a level was yielded falls back to the serial walk."""
 
-    def __init__(self, module, workers):
+    def __init__(self, module, workers, gen_idx=()):
         self.module = module
         self.workers = workers
+        self.gens = _generators(module, list(gen_idx))
         self.pool = None
         self.spec = _module_spec(module) if workers > 1 and _main_importable() else None
         if self.spec is not None:
             from concurrent.futures import ProcessPoolExecutor
             try:
                 self.pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("spawn"),
-                                                initializer=_worker_init, initargs=self.spec)
+                                                initializer=_worker_init, initargs=self.spec + (tuple(gen_idx),))
                 for _ in range(self.workers):   # start every worker now
                     self.pool.submit(_noop)
             except (OSError, ImportError):
@@ -195,7 +262,7 @@ class _Expander:
     def __call__(self, level):
         if self.spec is None or len(level) < PAR_MIN:
             for pos in level:
-                yield _expand_one(self.module, pos)
+                yield _expand_one(self.module, pos, self.gens)
             return
         from concurrent.futures.process import BrokenProcessPool
         batches = [level[i:i + BATCH] for i in range(0, len(level), BATCH)]
@@ -211,7 +278,7 @@ class _Expander:
             self.close()
             self.spec = None
             for pos in level:
-                yield _expand_one(self.module, pos)
+                yield _expand_one(self.module, pos, self.gens)
 
     def close(self):
         if self.pool is not None:
@@ -219,12 +286,15 @@ class _Expander:
             self.pool = None
 
 
-def enumerate_graph(module, root, limit=50_000_000, workers=None, budget_s=3600.0):
+def enumerate_graph(module, root, limit=50_000_000, workers=None, budget_s=3600.0, symmetry=()):
     """Positions reachable from ``root`` (index 0) with primitive codes and CSR children.
 
+    ``symmetry``: indices of ``symmetry_functions()`` that fix the root
+    (symmetry_generators); the positions are then the orbit representatives.
     Raises TooLarge as soon as the projected next level would pass ``limit``
     positions or the walk's projected time would pass ``budget_s`` seconds."""
     workers = _default_workers() if workers is None else max(1, int(workers))
+    root = canonical(root, _generators(module, list(symmetry)))
     index = {position_key(root): 0}
     positions = [root]
     prim = []
@@ -232,7 +302,7 @@ def enumerate_graph(module, root, limit=50_000_000, workers=None, budget_s=3600.
     kids = []
     sizes = []
     level = [root]
-    expand = _Expander(module, workers)
+    expand = _Expander(module, workers, symmetry)
     t0 = time.perf_counter()
     try:
         while level:
@@ -274,21 +344,33 @@ def enumerate_graph(module, root, limit=50_000_000, workers=None, budget_s=3600.
 
 
 class GraphCodec:
-    """Keys of a graph solve are position indices; ``pos`` maps them back."""
+    """Keys of a graph solve are position indices -- of orbit representatives when the
+    plugin declares symmetries that fix the root; ``pos`` maps a key back to its
+    representative and ``members`` to every position it stands for."""
     game_id = _lib.GAME_GRAPH
     params = ()
     name = "graph"
 
-    def __init__(self, module, root, workers=None):
+    def __init__(self, module, root, workers=None, symmetry=None):
         self.module = module
-        self.positions, self.prim, self.off, self.kids = enumerate_graph(module, root, workers=workers)
+        self.symmetry = symmetry_generators(module, root) if symmetry is None else list(symmetry)
+        self.gens = _generators(module, self.symmetry)
+        self.positions, self.prim, self.off, self.kids = enumerate_graph(module, root, workers=workers,
+                                                                         symmetry=self.symmetry)
         self._index = {position_key(p): i for i, p in enumerate(self.positions)}
+        self.n_positions = (sum(len(orbit(p, self.gens)) for p in self.positions) if self.gens
+                            else len(self.positions))
 
     def key(self, pos):
         try:
-            return self._index[position_key(pos)]
+            return self._index[position_key(canonical(pos, self.gens))]
         except KeyError:
             raise ValueError("position not reachable from the root") from None
 
     def pos(self, key):
         return self.positions[int(key)]
+
+    def members(self, key):
+        """The reachable positions key stands for (its orbit; just pos(key) without symmetry)."""
+        p = self.positions[int(key)]
+        return orbit(p, self.gens) if self.gens else [p]

@@ -54,12 +54,12 @@ def write_reference_tables(statsdir, codec, keys, records, world_size=1):
         for k, rec in zip(keys.tolist(), records.tolist()):
             if rec == _lib.REC_UNSOLVED:
                 continue
-            pos = codec.pos(k)
-            r = owner_rank(pos, world_size)
-            sk = shelf_key(pos)
-            shelves[r][0][sk] = rec >> 14
-            shelves[r][1][sk] = rec & 0x3FFF
-            counts[r] += 1
+            for pos in (codec.members(k) if hasattr(codec, "members") else (codec.pos(k),)):
+                r = owner_rank(pos, world_size)   # a symmetric graph key stands for its whole orbit
+                sk = shelf_key(pos)
+                shelves[r][0][sk] = rec >> 14
+                shelves[r][1][sk] = rec & 0x3FFF
+                counts[r] += 1
     finally:
         for a, b in shelves:
             a.close()

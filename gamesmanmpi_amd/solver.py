@@ -159,7 +159,8 @@ class Solver:
     def solve(self):
         if self.codec.game_id == _lib.GAME_GRAPH:
             c = self.codec
-            self.n_positions, self.root_record = self.ctx.solve_graph(c.prim, c.off, c.kids)
+            _, self.root_record = self.ctx.solve_graph(c.prim, c.off, c.kids)
+            self.n_positions = c.n_positions   # every orbit member (gamesmanmpi_amd/graph.py)
         else:
             self.n_positions, self.root_record = self.ctx.solve(self.root_key)
         return self.n_positions, self.root_record

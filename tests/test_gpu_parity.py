@@ -431,6 +431,33 @@ def test_toot_symmetry_off_matches_oracle_and_halves_tables(board, ranks):
     assert bytes_[1] < 0.8 * bytes_[0]
 
 
+@pytest.mark.parametrize("ranks", [1, 8])
+def test_othello_board_symmetry_on_off_matches_golden(ranks):
+    """Othello 4x4 with the reduction by the board symmetries that fix the root (games.hpp
+    DescOthello::sym; from the start: rotation by 180, transpose, anti-transpose): the same
+    golden table, digest and per-tier counts as without it, at one GPU and 8 loopback
+    ranks, with about a quarter of the edges expanded."""
+    keys, recs = golden("othello_4x4")
+    edges, tiers = {}, {}
+    for sym in (0, 1):
+        ctx = Context(OTH, (4, 4), device=0)
+        ctx.set_option(_lib.OPT_SYMMETRY, sym)
+        if ranks > 1:
+            ctx.set_option(_lib.OPT_VIRTUAL_RANKS, ranks)
+        for _ in range(2):   # the second solve is a replay on one GPU
+            n, rec = ctx.solve(ctx.initial())
+            k, r = ctx.export()
+            assert n == len(keys) and np.array_equal(k, keys) and np.array_equal(r, recs)
+            assert ctx.digest() == (digest(keys, recs), len(keys))
+            assert ctx.query(keys[::97]).tolist() == recs[::97].tolist()
+        edges[sym] = ctx.stats()["n_edges"]
+        tiers[sym] = [int(x) for x in ctx.tier_counts()]
+        ctx.close()
+    assert tiers[0] == tiers[1] and sum(tiers[1]) == len(keys)
+    if ranks == 1:
+        assert edges[1] < 0.4 * edges[0], edges
+
+
 @pytest.mark.parametrize("ranks", [1, 3])
 def test_toot_symmetry_custom_roots_vs_oracle(oracle, ranks):
     """Roots other than the empty board (Toot 4x3): a mirror-symmetric grandchild keeps the

@@ -146,3 +146,50 @@ def test_parallel_walk_never_rebuilds_a_patched_plugin(monkeypatch):
     par = enumerate_graph(mod, mod.initial_position(), workers=3)
     assert ser[0] == par[0] and all(np.array_equal(a, b) for a, b in zip(ser[1:], par[1:]))
     assert (par[1] == 1).sum() > (enumerate_graph(load_plugin("test_games/mttt.py"), "_" * 9, workers=1)[1] == 1).sum()
+
+
+def test_symmetry_functions_fixing_the_root_reduce_the_walk():
+    """symmetry_functions() (the reference's hook, othello_bit_new.py:224-225): the graph
+    walk keeps one representative per orbit of the declared functions that fix the root
+    and stands for every member (tests/plugins/ttt_symmetric.py: 765 orbits of 5,478
+    positions); functions that move the root are not used."""
+    from gamesmanmpi_amd.graph import GraphCodec, symmetry_generators
+    mod = load_plugin("tests/plugins/ttt_symmetric.py")
+    c = GraphCodec(mod, mod.initial_position(), workers=1)
+    assert c.symmetry == [0, 1] and len(c.positions) == 765 and c.n_positions == 5478
+    members = [p for i in range(len(c.positions)) for p in c.members(i)]
+    assert len(members) == len(set(members)) == 5478
+    table, _ = canonical.solve(load_plugin("test_games/mttt.py"))
+    assert set(members) == set(table)
+    assert all(c.key(p) == c.key(mod.rotate(p)) for p in members[:500])
+    assert symmetry_generators(mod, "X___O____") == []      # neither generator fixes it
+    oth = load_plugin("test_games/othello_bit_new.py", length=4, height=4)
+    assert not hasattr(oth, "symmetry_functions") or symmetry_generators(oth, oth.initial_position()) == []
+
+
+@pytest.mark.gpu
+def test_graph_engine_with_declared_symmetry_matches_golden(tmp_path):
+    """The symmetric plugin solved through the graph engine (765 orbits on the device):
+    every member's record equals the golden mttt table; -sd writes all 5,478 positions."""
+    import io
+    import solver_launcher
+    from gamesmanmpi_amd import Solver
+    mod = load_plugin("tests/plugins/ttt_symmetric.py")
+    s = Solver(mod, device=0, graph=True)
+    n, rec = s.solve()
+    keys, recs = golden("ttt")
+    want = dict(zip(keys.tolist(), recs.tolist()))
+    codec = games.TTTStringCodec()
+    idx, r = s.table()
+    assert n == 5478 and len(idx) == 765
+    got = {codec.key(p): rr for i, rr in zip(idx.tolist(), r.tolist()) for p in s.codec.members(i)}
+    assert got == want
+    assert s.lookup("XO_______") == (want[codec.key("XO_______")] >> 14, want[codec.key("XO_______")] & 0x3FFF)
+    s.close()
+    out = io.StringIO()
+    args = solver_launcher.build_parser().parse_args([os.path.join(REPO, "tests/plugins/ttt_symmetric.py"),
+                                                      "-sd", str(tmp_path)])
+    assert solver_launcher.run(args, out=out) == 0 and out.getvalue() == "TIE in 9 moves\n"
+    from gamesmanmpi_amd.persist import read_reference_tables
+    back = read_reference_tables(str(tmp_path))
+    assert len(back) == 5478 and back["X________"] == (want[1] >> 14, want[1] & 0x3FFF)

@@ -209,3 +209,21 @@ def test_dense_digest_matches_python_formula(oracle):
     rng = np.random.default_rng(3)
     recs = rng.integers(0, 1 << 16, size=100003, dtype=np.uint16)
     assert oracle.dense_digest(recs) == digest(np.arange(len(recs), dtype=np.uint64), recs)
+
+
+def test_othello_player_flip_maps_reachable_to_unreachable():
+    """The reference's declared Othello symmetry, player_flip (othello_bit_new.py:224-235:
+    every piece changes colour and the turn advances), merges no two reachable positions:
+    a reachable position's mover is fixed by its piece count (a pass keeps the mover, who
+    passes again and ends the game), and player_flip keeps the pieces but swaps the mover.
+    So the device reduces Othello by the board symmetries that fix the root instead
+    (DescOthello::sym); this pins the argument on the reference's own 54,089 positions."""
+    keys, _ = golden("othello_4x4")
+    A = 16
+    ks = set(int(k) for k in keys)
+    m = (1 << A) - 1
+    for k in ks:
+        w, b, turn, pas = (k >> (A + 16)) & m, (k >> 16) & m, (k >> 8) & 0xFF, k & 0xFF
+        flipped = (b << (A + 16)) | (w << 16) | ((3 - turn) << 8) | pas
+        assert flipped not in ks
+        assert (bin(w | b).count("1") % 2 == 0) == (turn == 2)   # WHITE moves on an even piece count
