@@ -289,31 +289,41 @@ __device__ __forceinline__ void p4_write_pair(uint32_t *s, uint32_t c, int pr, c
     }
 }
 // the 2*HIGH child blocks of block hp, chunk c: one whole-table descriptor, each child a
-// scalar offset; a missing child (heap nibble < 1 or < 2) reads through a zero-size
-// descriptor -- the load returns 0, which max ignores, without touching L1/L2 (9.06
-// child blocks per block on average instead of 10)
+// scalar offset (a block with no child at all, only high part 0, reads through a
+// zero-size descriptor).  Written so that the compiler keeps every load of the four
+// blocks in flight before the first fold (126-128 VGPRs); an equivalent form that chose
+// the offset per load let it drain after each block's loads (64-89 VGPRs: 4.71 ms per
+// 2^32 solve against 4.63-4.66, profiles/r03a_bench_subtract8.log).
 template <int HIGH, int LCPOL = 0>
 __device__ __forceinline__ void p4_issue(uint8_t *table, uint32_t hp, bool valid, uint32_t c,
                                          u32x4v (&v)[2 * HIGH > 0 ? 2 * HIGH : 1]) {
     constexpr int NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1;
     uint32_t soff[NMAX];
+    uint32_t first = 0;
+    bool any = false;
 #if defined(GM_EXP) && (GM_EXP & 2)
     valid = false;   // experiment: no child-block traffic (out-of-range loads return 0)
 #endif
 #pragma unroll
+    for (int j = HIGH - 1; j >= 0; j--)
+        if (valid && ((hp >> (4 * j)) & 15u) >= 1) { first = (hp - (1u << (4 * j))) << 12; any = true; }
+#pragma unroll
     for (int j = 0; j < HIGH; j++) {
-        soff[2 * j] = (hp - (1u << (4 * j))) << 12;
-        soff[2 * j + 1] = (hp - (2u << (4 * j))) << 12;
+        const uint32_t h = (hp >> (4 * j)) & 15u;
+        soff[2 * j] = (valid && h >= 1) ? (hp - (1u << (4 * j))) << 12 : first;
+        soff[2 * j + 1] = (valid && h >= 2) ? (hp - (2u << (4 * j))) << 12 : first;
     }
     if constexpr (HIGH == 0) soff[0] = 0;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(table, 0, 0xFFFFFFFFu, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(table, 0, any ? 0xFFFFFFFFu : 0u, 0x00020000);
+    // a missing child (heap nibble < 1 or < 2) reads through a zero-size descriptor: the
+    // load returns 0 (max ignores it) without touching L1/L2 -- 9.06 child blocks per
+    // block on average instead of 10 loads
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(table, 0, 0u, 0x00020000);
 #pragma unroll
     for (int m = 0; m < NMAX; m++) {
         const uint32_t h = HIGH > 0 ? (hp >> (4 * (m >> 1))) & 15u : 0u;
         const bool ok = HIGH > 0 && valid && h >= (uint32_t)(m & 1) + 1u;
-        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ok ? r : rz, 16u * c,
-                                                                                ok ? soff[m] : 0u, LCPOL));
+        v[m] = __builtin_bit_cast(u32x4v, __builtin_amdgcn_raw_buffer_load_b128(ok ? r : rz, 16u * c, soff[m], LCPOL));
     }
 }
 
