@@ -274,7 +274,38 @@ struct DescOthello {
     // swaps the turn -- it maps every reachable position to an unreachable one, so it
     // merges nothing.
     uint32_t sym = 0;
+    // 4x4 planes (the one Othello board above 2x2 a 64-bit key holds): bit permutations
+    // by masks and shifts instead of the cell loop below (the canonical form is taken
+    // for every child, in the latency-bound small-tier kernels)
+    GM_HD static uint32_t mirror_x4(uint32_t p) {   // (x, y) -> (3 - x, y)
+        return ((p & 0x1111u) << 3) | ((p & 0x8888u) >> 3) | ((p & 0x2222u) << 1) | ((p & 0x4444u) >> 1);
+    }
+    GM_HD static uint32_t mirror_y4(uint32_t p) {   // (x, y) -> (x, 3 - y)
+        return ((p & 0x000Fu) << 12) | ((p & 0x00F0u) << 4) | ((p & 0x0F00u) >> 4) | ((p & 0xF000u) >> 12);
+    }
+    GM_HD static uint32_t transpose4(uint32_t p) {   // (x, y) -> (y, x)
+        uint32_t t = (p ^ (p >> 3)) & 0x0A0Au;
+        p ^= t ^ (t << 3);
+        t = (p ^ (p >> 6)) & 0x00CCu;
+        return p ^ t ^ (t << 6);
+    }
+    GM_HD static uint32_t xform_plane4(uint32_t p, int g) {
+        switch (g) {
+        case 1: return mirror_x4(transpose4(p));
+        case 2: return mirror_x4(mirror_y4(p));
+        case 3: return transpose4(mirror_x4(p));
+        case 4: return transpose4(p);
+        case 5: return mirror_x4(mirror_y4(transpose4(p)));
+        case 6: return mirror_x4(p);
+        case 7: return mirror_y4(p);
+        }
+        return p;
+    }
     GM_HD uint32_t xform_plane(uint32_t p, int g) const {
+        if (L == 4) return xform_plane4(p, g);
+        return xform_plane_cells(p, g);
+    }
+    GM_HD uint32_t xform_plane_cells(uint32_t p, int g) const {
         uint32_t out = 0;
         for (int y = 0; y < L; y++)
             for (int x = 0; x < L; x++) {
