@@ -20,7 +20,7 @@ LIB = os.path.join(PKG, "libgmsolve.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("GM_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["gm_api.hip", "dense_sub.hip", "small_dense.hip", "sparse.hip", "dist_sub.hip", "dist_sparse.hip",
+SOURCES = ["gm_api.hip", "dense_sub.hip", "dense_box.hip", "small_dense.hip", "sparse.hip", "dist_sub.hip", "dist_sparse.hip",
            "graph.hip"]
 HEADERS = ["gm_common.hpp", "games.hpp", "gm_internal.hpp", "sparse_common.hpp", "sparse_tables.hpp"]
 

@@ -1,0 +1,684 @@
+// dense_box.hip -- box-tiled dense retrograde for the 8-heap synthetic subtraction game
+// (config 5, GM_OPT_SUB_INTERLEAVE 20).
+//
+// Replaces, like dense_sub.hip, the reference's per-edge job loop (Process.lookup /
+// distribute / resolve, src/new_process.py:102-265) and its shelve tables
+// (src/cache_dict.py) for the 2^32-position game: every position gets a 1-byte code
+// (gm_common.hpp: WIN R -> R+1, LOSS R -> 255-R), exported as u16 records.
+//
+// Decomposition.  dense_sub.hip's blocks are the 16^3 positions sharing the high five
+// nibbles, so half of a position's 16 children live in 10 other blocks spread over TWO
+// block tiers, and every block is read by ten parents in two launches.  Here the
+// 16^8 lattice is cut into BOXES of 4 x 4 x 4 x 4 x 2 x 2 x 2 x 2 positions (heaps
+// 0-3 in quarters "A", heaps 4-7 in halves "B"): 4,096 positions, 2^20 boxes.  A move
+// takes 1 or 2 from one heap, so every child outside a box lies in the box ONE step
+// below it along that heap, in that box's top two layers of the heap (half of it
+// along an A heap, all of it along a B heap).  Boxes are solved in box-tiers (sum of
+// the eight box coordinates, 0..40, one launch each); a launch reads only the tier
+// before it, each box once per parent, 5 B of child rows per position instead of 10
+// (tools/l2sim_box.cpp: 1.9 B/position of L2 misses modelled, against 3.8 for the
+// block order the block engine uses).
+//
+// Table layout: index = box << 12 | A << 4 | B, with A = a0 + 4 a1 + 16 a2 + 64 a3
+// (a_i = heap i mod 4) and B = b0 + 2 b1 + 4 b2 + 8 b3 (b_j = heap 4+j mod 2); the box
+// id packs the coordinates h_i >> 2 (2 bits each, bits 0-7) and h_{4+j} >> 1 (3 bits
+// each, bits 8-19).  A bit permutation of the key: export, query and digest map it.
+//
+// One workgroup = ONE wave, solving two boxes at a time (their codes share each LDS
+// dword as a u16 pair: low half box 0, high half box 1), persistent over its share of
+// the tier:
+//   fold   the child rows: per target row (16 positions, one A), the four B-children
+//          rows (whole 16-B rows, shifted by one B step where b_j = 0); then per A heap
+//          the two top layers of the child box below, merged into the rows a_i = 0, 1;
+//   walk   lane (b = lane & 15, a0 = lane >> 4) walks p = 0..63 (A = a0 + 4 p) starting
+//          d = popcount(b) + a0 steps late, so each child made inside the box is at
+//          least a step old: the B children by DPP row_shr 1/2/4/8 from the lanes one
+//          B step below, (a0-1, a0-2) from the image in LDS, (a1, a2) from this lane's
+//          own last 1/2/4/8 codes (masked at their digit boundaries) and (a3) from its
+//          codes 16 and 32 steps ago (zero before its start); 71 steps, no barrier;
+//   store  16-B rows of both boxes (write-through).
+// The max of up to 13 inputs uses v_pk_maximum3_f16: a code 0..255 in the low byte of
+// an f16 is a subnormal, ordered like the integer (the kernel keeps f16 denormals,
+// .amdhsa_float_denorm_mode_16_64 3).
+#include "gm_internal.hpp"
+#include "gm_common.hpp"
+
+#include <algorithm>
+#include <utility>
+
+namespace gm {
+
+typedef uint32_t bx_u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 bx_h2 __attribute__((ext_vector_type(2)));
+typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
+
+#ifndef GM_BOX_MAX3
+#define GM_BOX_MAX3 1          // 1: v_pk_maximum3_f16 on subnormal codes; 0: v_pk_max_u16
+#endif
+#ifndef GM_BOX_STORE_CPOL
+#define GM_BOX_STORE_CPOL 16   // sc1 write-through: a stored box is next read a launch later
+#endif
+#ifndef GM_BOX_WAVES
+#define GM_BOX_WAVES 2         // waves per SIMD the register budget must allow
+#endif
+#ifndef GM_BOX_PIPE
+#define GM_BOX_PIPE 1          // issue the next group's child loads before walking this one
+#endif
+
+// ---------------------------------------------------------------------------
+// key <-> table index
+GM_HD uint32_t box_index_of_key(uint32_t k) {
+    uint32_t off = 0, box = 0;
+    for (int i = 0; i < 4; i++) {
+        const uint32_t h = (k >> (4 * i)) & 15u;
+        off |= (h & 3u) << (4 + 2 * i);
+        box |= (h >> 2) << (2 * i);
+    }
+    for (int j = 0; j < 4; j++) {
+        const uint32_t h = (k >> (16 + 4 * j)) & 15u;
+        off |= (h & 1u) << j;
+        box |= (h >> 1) << (8 + 3 * j);
+    }
+    return (box << 12) | off;
+}
+GM_HD uint32_t box_key_of_index(uint32_t x) {
+    const uint32_t off = x & 4095u, box = x >> 12;
+    uint32_t k = 0;
+    for (int i = 0; i < 4; i++) {
+        const uint32_t h = (((box >> (2 * i)) & 3u) << 2) | ((off >> (4 + 2 * i)) & 3u);
+        k |= h << (4 * i);
+    }
+    for (int j = 0; j < 4; j++) {
+        const uint32_t h = (((box >> (8 + 3 * j)) & 7u) << 1) | ((off >> j) & 1u);
+        k |= h << (16 + 4 * j);
+    }
+    return k;
+}
+GM_HD int box_coord(uint32_t box, int dim) {
+    return dim < 4 ? (int)((box >> (2 * dim)) & 3u) : (int)((box >> (8 + 3 * (dim - 4))) & 7u);
+}
+GM_HD uint32_t box_unit(int dim) { return dim < 4 ? 1u << (2 * dim) : 1u << (8 + 3 * (dim - 4)); }
+
+// ---------------------------------------------------------------------------
+// device helpers
+__device__ __forceinline__ uint32_t bx_max2(uint32_t a, uint32_t b) {
+#if GM_BOX_MAX3
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_bit_cast(bx_h2, a),
+                                                                     __builtin_bit_cast(bx_h2, b)));
+#else
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(bx_u16x2, a),
+                                                                 __builtin_bit_cast(bx_u16x2, b)));
+#endif
+}
+__device__ __forceinline__ uint32_t bx_max3(uint32_t a, uint32_t b, uint32_t c) { return bx_max2(bx_max2(a, b), c); }
+// parent code of a pair of best-child codes (gm_common.hpp parent_code, per u16 half)
+__device__ __forceinline__ uint32_t bx_code(uint32_t m) { return (m ^ 0x00FF00FFu) + ((m >> 6) & 0x00020002u); }
+template <int CTRL>
+__device__ __forceinline__ uint32_t bx_dpp_shr(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+// x & sext(byte N of m): one masked child per instruction (SDWA), the masks held as bytes
+template <int N>
+__device__ __forceinline__ uint32_t bx_and_byte(uint32_t x, uint32_t m) {
+    uint32_t r;
+    if constexpr (N == 0)
+        asm("v_and_b32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+            : "=v"(r) : "v"(x), "v"(m));
+    else if constexpr (N == 1)
+        asm("v_and_b32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+            : "=v"(r) : "v"(x), "v"(m));
+    else if constexpr (N == 2)
+        asm("v_and_b32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+            : "=v"(r) : "v"(x), "v"(m));
+    else
+        asm("v_and_b32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+            : "=v"(r) : "v"(x), "v"(m));
+    return r;
+}
+// LDS ops of one wave complete in order; this keeps the compiler from moving them
+#define BX_LDS_ORDER() asm volatile("" ::: "memory")
+
+// 16 codes of box 0 (x0) and box 1 (x1), one 16-B row each -> 16 u16 pairs (b0 | b1 << 16)
+__device__ __forceinline__ void bx_pairs(const bx_u32x4 &x0, const bx_u32x4 &x1, uint32_t (&p)[16]) {
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+        const uint32_t r = (uint32_t)(b & 3);
+        p[b] = __builtin_amdgcn_perm(x1[b >> 2], x0[b >> 2], r | 0x0c00u | ((4u + r) << 16) | 0x0c000000u);
+    }
+}
+
+constexpr int BX_IMG = 4096;              // dwords: position (A, B) at 16 A + B
+constexpr int BX_PAD = 32;                // guard in front: the walk's (a0-1, a0-2) reads of row 0 at p = 0
+constexpr int BX_LDS = BX_PAD + BX_IMG + 64;   // + one dummy dword per lane for idle walk steps
+constexpr int BX_NLOAD = 48;              // 16-B child rows per lane per group
+
+struct BxGroup {
+    uint32_t box[2];
+    bool valid[2];
+};
+
+__device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, uint32_t nbox, uint32_t g) {
+    BxGroup G;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const uint32_t i = 2 * g + k;
+        G.valid[k] = i < nbox;
+        G.box[k] = G.valid[k] ? boxes[i] : 0u;
+    }
+    return G;
+}
+
+// Every child row of a group, in flight at once: R[0..31] the B children of target rows
+// m = lane + 64 i (R[8 i + 4 k + j]: box k, heap 4 + j), R[32..47] the A children's top
+// layers (R[32 + 4 i + 2 k + v]: heap i, box k, layer 3 - v) of the rows a_i in {2, 3}
+// whose other coordinates are the lane.
+__device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
+                                         bx_u32x4 (&R)[BX_NLOAD]) {
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0xFFFFFFFFu, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0u, 0x00020000);
+    // one (descriptor, offset) per child box, used by consecutive loads
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const bool ok = G.valid[k] && box_coord(G.box[k], 4 + j) >= 1;
+            const uint32_t soff = ok ? (G.box[k] - box_unit(4 + j)) << 12 : 0u;
+            const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                R[8 * i + 4 * k + j] = __builtin_bit_cast(
+                    bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * (lane + 64u * i), soff, 0));
+        }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t lo = lane & ((1u << (2 * i)) - 1u), hi = (lane >> (2 * i)) << (2 * i + 2);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const bool ok = G.valid[k] && box_coord(G.box[k], i) >= 1;
+            const uint32_t soff = ok ? (G.box[k] - box_unit(i)) << 12 : 0u;
+            const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
+                R[32 + 4 * i + 2 * k + v] =
+                    __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, 0));
+            }
+        }
+    }
+}
+
+// fold: the image's slot of every position gets the max of its children outside the box
+__device__ __forceinline__ void bx_fold(uint32_t *s, const BxGroup &G, uint32_t lane, const bx_u32x4 (&R)[BX_NLOAD]) {
+    // B children: row m of the child box below along heap 4 + j; a position with b_j = 0
+    // also takes b | e_j of that row (its child two below)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t m = lane + 64u * i;
+        // heap by heap into F (16 live pairs instead of 64)
+        uint32_t F[16];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            uint32_t P[16];
+            bx_pairs(R[8 * i + j], R[8 * i + 4 + j], P);
+#pragma unroll
+            for (int b = 0; b < 16; b++) {
+                const bool two = !((b >> j) & 1);
+                if (j == 0) F[b] = two ? bx_max2(P[b], P[b | 1]) : P[b];
+                else F[b] = two ? bx_max3(F[b], P[b], P[b | (1 << j)]) : bx_max2(F[b], P[b]);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *(bx_u32x4 *)(s + 16u * m + 4u * q) = bx_u32x4{F[4 * q], F[4 * q + 1], F[4 * q + 2], F[4 * q + 3]};
+    }
+    BX_LDS_ORDER();
+    // A children: layers 3 and 2 of the box below along heap i go to the rows a_i = 0
+    // (both) and a_i = 1 (layer 3); one heap after the other (a row can take from several)
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if (!((G.valid[0] && box_coord(G.box[0], i) >= 1) || (G.valid[1] && box_coord(G.box[1], i) >= 1))) continue;
+        const uint32_t lo = lane & ((1u << (2 * i)) - 1u), hi = (lane >> (2 * i)) << (2 * i + 2);
+        uint32_t L3[16], L2[16];
+        bx_pairs(R[32 + 4 * i + 0], R[32 + 4 * i + 2], L3);
+        bx_pairs(R[32 + 4 * i + 1], R[32 + 4 * i + 3], L2);
+        uint32_t *t0 = s + 16u * (lo | hi), *t1 = s + 16u * (lo | (1u << (2 * i)) | hi);
+        bx_u32x4 T0[4], T1[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            T0[q] = *(const bx_u32x4 *)(t0 + 4 * q);
+            T1[q] = *(const bx_u32x4 *)(t1 + 4 * q);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                T0[q][e] = bx_max3(T0[q][e], L3[4 * q + e], L2[4 * q + e]);
+                T1[q][e] = bx_max2(T1[q][e], L3[4 * q + e]);
+            }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            *(bx_u32x4 *)(t0 + 4 * q) = T0[q];
+            *(bx_u32x4 *)(t1 + 4 * q) = T1[q];
+        }
+        BX_LDS_ORDER();
+    }
+}
+
+// walk: see the file comment.  The image holds the fold of every position; each code
+// overwrites its slot as it is made.
+template <int T>
+struct BxT { static constexpr int v = T; };
+template <class F, int... I>
+__device__ __forceinline__ void bx_unroll(F &f, std::integer_sequence<int, I...>) { (f(BxT<I>{}), ...); }
+
+__device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t lane) {
+    uint32_t ln = lane;
+    asm volatile("" : "+v"(ln));   // per group: keeps the per-step addresses from being hoisted (registers)
+    const uint32_t b = ln & 15u, a0 = ln >> 4;
+    const int d = __popc(b) + (int)a0;
+    const uint32_t m01 = a0 >= 1 ? ~0u : 0u, m02 = a0 >= 2 ? ~0u : 0u;
+    const uint32_t mb0 = (b & 1u) ? ~0u : 0u, mb1 = (b & 2u) ? ~0u : 0u, mb2 = (b & 4u) ? ~0u : 0u;
+    // validity of this lane's own earlier codes as (a1, a2) children at step t (p = t - d,
+    // a1 = p & 3, a2 = (p >> 2) & 3), one byte (0 or 0xFF) per step phase: t & 3 for a1,
+    // t & 15 for a2 (byte t & 3 of word (t >> 2) & 3)
+    uint32_t v11 = 0, v12 = 0, v21[4] = {0, 0, 0, 0}, v22[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        const uint32_t q = (uint32_t)(t - d) & 15u;
+        if (t < 4) {
+            v11 |= ((q & 3u) >= 1 ? 0xFFu : 0u) << (8 * t);
+            v12 |= ((q & 3u) >= 2 ? 0xFFu : 0u) << (8 * t);
+        }
+        v21[t >> 2] |= ((q >> 2) >= 1 ? 0xFFu : 0u) << (8 * (t & 3));
+        v22[t >> 2] |= ((q >> 2) >= 2 ? 0xFFu : 0u) << (8 * (t & 3));
+    }
+    const int base = (int)ln - 64 * d;   // image dword of this lane's position at step t: base + 64 t
+    const int dummy = BX_IMG + (int)ln;
+    uint32_t h[8];   // this lane's codes of the last 8 steps (ring by step)
+#pragma unroll
+    for (int q = 0; q < 8; q++) h[q] = 0;
+    auto slot = [&](auto TT) {
+        constexpr int T = decltype(TT)::v;
+        int idx = base + 64 * T;
+        if constexpr (T < 7 || T >= 64) idx = (uint32_t)(T - d) < 64u ? idx : dummy;
+        return idx;
+    };
+    // (a3 - 1, a3 - 2) = this lane's codes 16 and 32 steps ago, from its slots in the image
+    // (they exist from steps 16 and 32 on; a lane started d <= 7 steps late)
+    auto a3kids = [&](auto TT, uint32_t &k16, uint32_t &k32) {
+        constexpr int T = decltype(TT)::v;
+        const int idx = base + 64 * T;
+        k16 = k32 = 0;
+        if constexpr (T >= 16 && T < 23) k16 = T - d >= 16 ? s[idx - 1024 > 0 ? idx - 1024 : 0] : 0u;
+        if constexpr (T >= 23 && T < 64 + 7) k16 = s[idx - 1024];
+        if constexpr (T >= 32 && T < 39) k32 = T - d >= 32 ? s[idx - 2048 > 0 ? idx - 2048 : 0] : 0u;
+        if constexpr (T >= 39 && T < 64 + 7) k32 = s[idx - 2048];
+    };
+    uint32_t Fv = s[slot(BxT<0>{})], Y2 = s[slot(BxT<0>{}) - 32], K16 = 0, K32 = 0;
+    auto step = [&](auto TT) {
+        constexpr int T = decltype(TT)::v;
+        constexpr bool peel = T < 7 || T >= 64;
+        const int idx = slot(TT);
+        const uint32_t Y1 = s[idx - 16];   // (a0 - 1): made last step by the row below
+        const uint32_t h1 = h[(T + 7) & 7], h2 = h[(T + 6) & 7], h4 = h[(T + 4) & 7], h8 = h[T & 7];
+        const uint32_t c0 = bx_dpp_shr<0x111>(h1) & mb0, c1 = bx_dpp_shr<0x112>(h1) & mb1;
+        const uint32_t c2 = bx_dpp_shr<0x114>(h1) & mb2, c3 = bx_dpp_shr<0x118>(h1);
+        uint32_t m = bx_max3(Fv, Y2 & m02, K16);
+        m = bx_max3(m, c0, c1);
+        m = bx_max3(m, c2, c3);
+        m = bx_max3(m, bx_and_byte<T & 3>(h2, v12), bx_and_byte<T & 3>(h4, v21[(T >> 2) & 3]));
+        m = bx_max3(m, bx_and_byte<T & 3>(h8, v22[(T >> 2) & 3]), K32);
+        m = bx_max3(m, bx_and_byte<T & 3>(h1, v11), Y1 & m01);
+        uint32_t c = bx_code(m);
+        if constexpr (peel) c = (uint32_t)(T - d) < 64u ? c : 0u;
+        h[T & 7] = c;
+        if constexpr (T < 70) {   // the next step's fold, (a0 - 2) row and a3 children are final already
+            const int nidx = slot(BxT<T + 1>{});
+            Fv = s[nidx];
+            Y2 = s[nidx - 32];
+            a3kids(BxT<T + 1>{}, K16, K32);
+        }
+        s[idx] = c;
+        BX_LDS_ORDER();
+    };
+    bx_unroll(step, std::make_integer_sequence<int, 71>{});
+}
+
+// store: rows m = lane + 64 i of both boxes, bytes regrouped per box
+__device__ __forceinline__ void bx_store(uint8_t *table, const BxGroup &G, const uint32_t *s, uint32_t lane) {
+    __amdgpu_buffer_rsrc_t w[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+        w[k] = __builtin_amdgcn_make_buffer_rsrc(table + ((uint64_t)G.box[k] << 12), 0, G.valid[k] ? 4096u : 0u,
+                                                 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t m = lane + 64u * i;
+        bx_u32x4 o0, o1;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bx_u32x4 x = *(const bx_u32x4 *)(s + 16u * m + 4u * q);
+            const uint32_t t01 = __builtin_amdgcn_perm(x[1], x[0], 0x06020400u);
+            const uint32_t t23 = __builtin_amdgcn_perm(x[3], x[2], 0x06020400u);
+            o0[q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+            o1[q] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(o0, w[0], 16u * m, 0, GM_BOX_STORE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(o1, w[1], 16u * m, 0, GM_BOX_STORE_CPOL);
+    }
+}
+
+// One launch per box-tier.  Workgroup w runs on XCD w % 8 and takes groups (box pairs)
+// of that XCD's contiguous run of the tier list (boxes sorted along a Hilbert walk), the
+// workgroups of an XCD side by side, so neighbouring groups share child boxes in its L2.
+__global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__restrict__ table,
+                                                                     const uint32_t *__restrict__ boxes,
+                                                                     uint32_t nbox) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BX_LDS];
+    uint32_t *s = lds + BX_PAD;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t ng = (nbox + 1) / 2, nw = gridDim.x, w = blockIdx.x;
+    const uint32_t x = w & 7u, kx = w >> 3, Kx = (nw - x + 7u) >> 3;
+    const uint32_t q = ng >> 3, r = ng & 7u;
+    const uint32_t g0 = x * q + (x < r ? x : r), g1 = g0 + q + (x < r ? 1u : 0u);
+    uint32_t g = g0 + kx;
+    if (g >= g1) return;
+    bx_u32x4 R[BX_NLOAD];
+    BxGroup G = bx_group(boxes, nbox, g);
+    bx_issue(table, G, lane, R);
+    for (;;) {
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));   // lane-derived addresses are recomputed per group, not held in registers
+        bx_fold(s, G, ln, R);
+        const uint32_t gn = g + Kx;
+        const bool more = gn < g1;
+        BxGroup Gn = G;
+#if GM_BOX_PIPE
+        if (more) {
+            Gn = bx_group(boxes, nbox, gn);
+            bx_issue(table, Gn, ln, R);
+        }
+#endif
+        BX_LDS_ORDER();
+        bx_walk(s, ln);
+        bx_store(table, G, s, ln);
+        BX_LDS_ORDER();
+        if (!more) break;
+        g = gn;
+#if GM_BOX_PIPE
+        G = Gn;
+#else
+        G = bx_group(boxes, nbox, g);
+        bx_issue(table, G, lane, R);
+#endif
+    }
+}
+
+__global__ void box_digest_kernel(const uint8_t *__restrict__ table, uint64_t root, unsigned long long *acc) {
+    uint64_t sum = 0, cnt = 0;
+    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < (1ull << 32);
+         x += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t k = box_key_of_index((uint32_t)x);
+        bool in = true;
+        for (int j = 0; j < 8; j++) in &= ((k >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
+        if (!in) continue;
+        sum += digest_term(k, record_of_code(table[x]));
+        cnt++;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o);
+        cnt += __shfl_xor(cnt, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(acc, (unsigned long long)sum);
+        atomicAdd(acc + 1, (unsigned long long)cnt);
+    }
+}
+
+__global__ void box_query_kernel(const uint8_t *__restrict__ table, const uint64_t *__restrict__ keys,
+                                 uint16_t *__restrict__ out, uint64_t n) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < n) out[i] = keys[i] < (1ull << 32) ? record_of_code(table[box_index_of_key((uint32_t)keys[i])]) : REC_UNSOLVED;
+}
+
+// ---------------------------------------------------------------------------
+// host
+struct DenseBox {
+    uint8_t *table = nullptr;
+    bool owned = false;
+    uint32_t root_hi = 0;                 // the root's box coordinates (box id form)
+    uint32_t *d_boxes = nullptr;          // the root region's boxes, sorted by (tier, Hilbert)
+    std::vector<uint32_t> tier_off;
+    int grid_cap = 2048;
+    uint64_t *d_acc = nullptr;
+    hipGraphExec_t graph = nullptr;
+    hipStream_t graph_stream = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+};
+
+// Hilbert index (Skilling's transpose form) of the first 7 box coordinates, 3 bits each
+static uint64_t box_hilbert(uint32_t box) {
+    const int n = 7;
+    uint32_t xv[8];
+    for (int i = 0; i < n; i++) xv[i] = (uint32_t)box_coord(box, i);
+    for (uint32_t qq = 4; qq > 1; qq >>= 1) {
+        const uint32_t p = qq - 1;
+        for (int i = 0; i < n; i++) {
+            if (xv[i] & qq) xv[0] ^= p;
+            else { const uint32_t t = (xv[0] ^ xv[i]) & p; xv[0] ^= t; xv[i] ^= t; }
+        }
+    }
+    for (int i = 1; i < n; i++) xv[i] ^= xv[i - 1];
+    uint32_t t = 0;
+    for (uint32_t qq = 4; qq > 1; qq >>= 1) if (xv[n - 1] & qq) t ^= qq - 1;
+    for (int i = 0; i < n; i++) xv[i] ^= t;
+    uint64_t hv = 0;
+    for (int bit = 2; bit >= 0; bit--)
+        for (int i = 0; i < n; i++) hv = (hv << 1) | ((xv[i] >> bit) & 1u);
+    return hv;
+}
+
+static int box_prepare(Ctx *c, DenseBox *d, uint64_t root) {
+    d->root_hi = box_index_of_key((uint32_t)root) >> 12;
+    int lim[8], tmax = 0;
+    for (int i = 0; i < 8; i++) { lim[i] = box_coord(d->root_hi, i); tmax += lim[i]; }
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> tiers(tmax + 1);
+    for (uint32_t box = 0; box < (1u << 20); box++) {
+        int t = 0;
+        bool in = true;
+        for (int i = 0; i < 8 && in; i++) {
+            const int cc = box_coord(box, i);
+            in = cc <= lim[i];
+            t += cc;
+        }
+        if (in) tiers[t].push_back({box_hilbert(box), box});
+    }
+    std::vector<uint32_t> order;
+    d->tier_off.assign(1, 0);
+    for (auto &tv : tiers) {
+        std::sort(tv.begin(), tv.end());
+        for (auto &e : tv) order.push_back(e.second);
+        d->tier_off.push_back((uint32_t)order.size());
+    }
+    GM_HIP(hipMalloc(&d->d_boxes, order.size() * sizeof(uint32_t)));
+    GM_HIP(hipMemcpy(d->d_boxes, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    GM_HIP(hipMalloc(&d->d_acc, 2 * sizeof(uint64_t)));
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
+    d->grid_cap = cus * 4 * GM_BOX_WAVES;
+    const uint64_t bytes = 1ull << 32;
+    if (c->adopted_dense) {
+        if (c->adopted_dense_bytes < bytes) {
+            set_error("adopted dense table holds %llu bytes, need %llu", (unsigned long long)c->adopted_dense_bytes,
+                      (unsigned long long)bytes);
+            return GM_E_CAP;
+        }
+        d->table = (uint8_t *)c->adopted_dense;
+        d->owned = false;
+    } else {
+        if (hipMalloc(&d->table, bytes) != hipSuccess) {
+            set_error("hipMalloc of the 4 GiB dense table failed");
+            return GM_E_NOMEM;
+        }
+        d->owned = true;
+    }
+    return GM_OK;
+}
+
+static int box_launch_tiers(Ctx *c, DenseBox *d) {
+    for (size_t t = 0; t + 1 < d->tier_off.size(); t++) {
+        const uint32_t nb = d->tier_off[t + 1] - d->tier_off[t];
+        if (!nb) continue;
+        const uint32_t ng = (nb + 1) / 2;
+        // at least 8 workgroups (one per XCD run), at most the resident capacity
+        const uint32_t grid = std::max<uint32_t>(8u, std::min<uint32_t>(ng, (uint32_t)d->grid_cap));
+        hipLaunchKernelGGL(box_tier_kernel, dim3(grid), dim3(64), 0, c->stream, d->table, d->d_boxes + d->tier_off[t], nb);
+    }
+    GM_HIP(hipGetLastError());
+    return GM_OK;
+}
+
+void dense_box_free(Ctx *c);
+
+int dense_box_solve(Ctx *c, uint64_t root) {
+    DenseBox *d = c->dbox;
+    const uint32_t rh = box_index_of_key((uint32_t)root) >> 12;
+    if (!d || (c->adopted_dense && d->table != c->adopted_dense) || d->root_hi != rh) {
+        dense_box_free(c);
+        d = c->dbox = new DenseBox();
+        GM_TRY(box_prepare(c, d, root));
+    }
+    const double t0 = now_ms();
+    if (c->timing && !d->ev[0]) {
+        GM_HIP(hipEventCreate(&d->ev[0]));
+        GM_HIP(hipEventCreate(&d->ev[1]));
+    }
+    if (c->use_graph) {
+        if (!d->graph || d->graph_stream != c->stream) {
+            if (d->graph) { (void)hipGraphExecDestroy(d->graph); d->graph = nullptr; }
+            hipGraph_t g;
+            GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            const int rc = box_launch_tiers(c, d);
+            const hipError_t e = hipStreamEndCapture(c->stream, &g);
+            if (rc != GM_OK) return rc;
+            if (e != hipSuccess) { set_error("graph capture failed: %s", hipGetErrorString(e)); return GM_E_HIP; }
+            GM_HIP(hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0));
+            GM_HIP(hipGraphDestroy(g));
+            d->graph_stream = c->stream;
+        }
+        if (c->timing) GM_HIP(hipEventRecord(d->ev[0], c->stream));
+        GM_HIP(hipGraphLaunch(d->graph, c->stream));
+        if (c->timing) GM_HIP(hipEventRecord(d->ev[1], c->stream));
+    } else {
+        if (c->timing) GM_HIP(hipEventRecord(d->ev[0], c->stream));
+        GM_TRY(box_launch_tiers(c, d));
+        if (c->timing) GM_HIP(hipEventRecord(d->ev[1], c->stream));
+    }
+    uint8_t rs = 0;
+    GM_HIP(hipMemcpyAsync(&rs, d->table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipStreamSynchronize(c->stream));
+    const double t1 = now_ms();
+    c->root_record = record_of_code(rs);
+    uint64_t n = 1;
+    for (int j = 0; j < 8; j++) n *= ((root >> (4 * j)) & 15u) + 1;
+    c->n_positions = n;
+    {
+        std::vector<uint64_t> acc(1, 1);
+        for (int j = 0; j < 8; j++) {
+            std::vector<uint64_t> nx(acc.size() + 15, 0);
+            for (size_t s = 0; s < acc.size(); s++)
+                for (int hh = 0; hh < 16; hh++) nx[s + hh] += acc[s];
+            acc.swap(nx);
+        }
+        c->tier_counts = acc;
+    }
+    int launches = 0;
+    for (size_t t = 0; t + 1 < d->tier_off.size(); t++) launches += d->tier_off[t + 1] > d->tier_off[t];
+    c->stats.n_positions = n;
+    c->stats.n_primitive = 1;
+    c->stats.n_tiers = launches;
+    c->stats.solve_ms = t1 - t0;
+    c->stats.backward_ms = t1 - t0;
+    c->stats.forward_ms = 0;
+    c->stats.algo_bytes = (uint64_t)((double)(1ull << 32) * (1.0 + 1.8125 * 8));
+    c->stats.table_bytes = 1ull << 32;
+    if (c->timing) {
+        float ms = 0;
+        GM_HIP(hipEventElapsedTime(&ms, d->ev[0], d->ev[1]));
+        c->stats.kernel_ms = ms;
+        c->stats.kernel_launches = launches;
+    }
+    return GM_OK;
+}
+
+int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
+    DenseBox *d = c->dbox;
+    *n = c->n_positions;
+    if (!keys) return GM_OK;
+    if (cap < c->n_positions) {
+        set_error("export buffer holds %llu, need %llu", (unsigned long long)cap, (unsigned long long)c->n_positions);
+        return GM_E_CAP;
+    }
+    std::vector<uint8_t> h(1ull << 32);
+    GM_HIP(hipMemcpy(h.data(), d->table, h.size(), hipMemcpyDeviceToHost));
+    uint64_t j = 0;
+    for (uint64_t k = 0; k < (1ull << 32); k++) {
+        bool in = true;
+        for (int i = 0; i < 8 && in; i++) in = ((k >> (4 * i)) & 15u) <= ((c->root >> (4 * i)) & 15u);
+        if (!in) continue;
+        keys[j] = k;
+        recs[j] = record_of_code(h[box_index_of_key((uint32_t)k)]);
+        j++;
+    }
+    return GM_OK;
+}
+
+int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
+    DenseBox *d = c->dbox;
+    if (!n) return GM_OK;
+    uint64_t *dk;
+    uint16_t *dr;
+    GM_HIP(hipMalloc(&dk, n * 8));
+    GM_HIP(hipMalloc(&dr, n * 2));
+    GM_HIP(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(box_query_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d->table, dk, dr, n);
+    GM_HIP(hipMemcpyAsync(recs, dr, n * 2, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(dk);
+    (void)hipFree(dr);
+    return GM_OK;
+}
+
+int dense_box_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
+    DenseBox *d = c->dbox;
+    GM_HIP(hipMemsetAsync(d->d_acc, 0, 16, c->stream));
+    hipLaunchKernelGGL(box_digest_kernel, dim3(4096), dim3(256), 0, c->stream, d->table, c->root,
+                       (unsigned long long *)d->d_acc);
+    uint64_t hst[2];
+    GM_HIP(hipMemcpyAsync(hst, d->d_acc, 16, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipStreamSynchronize(c->stream));
+    *digest = hst[0];
+    *n = hst[1];
+    return GM_OK;
+}
+
+int dense_box_table(Ctx *c, void **p, uint64_t *bytes) {
+    *p = c->dbox->table;
+    *bytes = 1ull << 32;
+    return GM_OK;
+}
+
+void dense_box_free(Ctx *c) {
+    DenseBox *d = c->dbox;
+    if (!d) return;
+    if (d->graph) (void)hipGraphExecDestroy(d->graph);
+    for (auto e : d->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (d->owned && d->table) (void)hipFree(d->table);
+    if (d->d_boxes) (void)hipFree(d->d_boxes);
+    if (d->d_acc) (void)hipFree(d->d_acc);
+    delete d;
+    c->dbox = nullptr;
+}
+
+}  // namespace gm

@@ -1288,6 +1288,13 @@ static int launch_tiers(Ctx *c, DenseSub *d, bool timed) {
 }
 
 int dense_sub_solve(Ctx *c, uint64_t root) {
+    if (c->sub.heaps == 8 && c->sub_interleave == 20) {   // the box engine (dense_box.hip)
+        dense_sub_free(c);
+        c->dbox_active = true;
+        return dense_box_solve(c, root);
+    }
+    dense_box_free(c);
+    c->dbox_active = false;
     DenseSub *d = c->dsub;
     if (!d || d->heaps != c->sub.heaps || d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave ||
         d->want_order != c->sub_order || d->low != std::min(std::max(c->sub_low, 1), std::min(3, c->sub.heaps)) ||
@@ -1402,6 +1409,7 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
 }
 
 int dense_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
+    if (c->dbox_active) return dense_box_export(c, keys, recs, cap, n);
     DenseSub *d = c->dsub;
     *n = c->n_positions;
     if (!keys) return GM_OK;
@@ -1424,6 +1432,7 @@ int dense_sub_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint6
 }
 
 int dense_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
+    if (c->dbox_active) return dense_box_query(c, keys, recs, n);
     DenseSub *d = c->dsub;
     if (!n) return GM_OK;
     uint64_t *dk;
@@ -1441,6 +1450,7 @@ int dense_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
 }
 
 int dense_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
+    if (c->dbox_active) return dense_box_digest(c, digest, n);
     DenseSub *d = c->dsub;
     GM_HIP(hipMemsetAsync(d->d_acc, 0, 16, c->stream));
     hipLaunchKernelGGL(sub_digest_kernel, dim3(2048), dim3(256), 0, c->stream, d->table, d->slots, d->heaps, c->root,
@@ -1454,6 +1464,7 @@ int dense_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
 }
 
 int dense_sub_table(Ctx *c, void **p, uint64_t *bytes) {
+    if (c->dbox_active) return dense_box_table(c, p, bytes);
     DenseSub *d = c->dsub;
     *p = d->table;
     *bytes = d->slots;

@@ -111,6 +111,7 @@ static bool key_valid(const Ctx *c, uint64_t k) {
 static void free_engines(Ctx *c) {
     graph_free(c);
     dense_sub_free(c);
+    dense_box_free(c);
     small_dense_free(c);
     sparse_free(c);
     dist_sub_free(c);
@@ -214,9 +215,9 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sub_threads = (int)v;
         return GM_OK;
     case GM_OPT_SUB_INTERLEAVE:
-        if (v != 1 && v != 6 && v != 10 && v != 13) {
-            set_error("sub_interleave must be 1 (one block per workgroup), 6 (four-block kernel), 10 (walker, "
-                      "default) or 13 (row-granular dataflow)");
+        if (v != 1 && v != 6 && v != 10 && v != 13 && v != 20) {
+            set_error("sub_interleave must be 1 (one block per workgroup), 6 (four-block kernel), 10 (walker), "
+                      "13 (row-granular dataflow) or 20 (box engine, 8 heaps)");
             return GM_E_ARG;
         }
         c->sub_interleave = (int)v;

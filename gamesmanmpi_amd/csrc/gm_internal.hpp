@@ -53,6 +53,7 @@ enum : uint32_t {
 int dev_error_to_gm(uint32_t flags);
 
 struct DenseSub;
+struct DenseBox;
 struct SmallDense;
 struct Sparse;
 struct DistSub;
@@ -109,6 +110,8 @@ struct Ctx {
     uint64_t adopted_dense_bytes = 0;
 
     DenseSub *dsub = nullptr;
+    DenseBox *dbox = nullptr;   // the box engine (GM_OPT_SUB_INTERLEAVE 20, 8 heaps)
+    bool dbox_active = false;   // the last dense SUBTRACT solve used dbox
     SmallDense *sd = nullptr;
     Sparse *sp = nullptr;
     DistSub *dist_sub = nullptr;
@@ -123,6 +126,13 @@ int dense_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
 int dense_sub_digest(Ctx *c, uint64_t *digest, uint64_t *n);
 void dense_sub_free(Ctx *c);
 int dense_sub_table(Ctx *c, void **p, uint64_t *bytes);
+// the box-tiled engine for 8 heaps (dense_box.hip), reached through dense_sub_*
+int dense_box_solve(Ctx *c, uint64_t root);
+int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int dense_box_digest(Ctx *c, uint64_t *digest, uint64_t *n);
+int dense_box_table(Ctx *c, void **p, uint64_t *bytes);
+void dense_box_free(Ctx *c);
 
 // the dense tier kernel, shared with the partitioned (multi-GPU) driver
 bool sub_kernel_exists(int low, int high, int nt);
