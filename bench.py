@@ -586,7 +586,10 @@ def main():
                      "traffic": traffic_launch,
                      "traffic_gbs": traffic_gbs,
                      "traffic_frac": (traffic_gbs / HBM_PEAK_GBS) if traffic_gbs else None,
-                     "kernel": "sub_tier_kernel_wk<%d> (tiers of >= 4096 blocks), sub_tier_kernel_b4<%d> (smaller)" % (args.heaps - 3, args.heaps - 3),
+                     "kernel": ("box_tier_kernel (csrc/dense_box.hip: 4x4x4x4x2x2x2x2 boxes, one launch per box-tier)"
+                                if (world == 1 and args.virtual_ranks == 1 and args.heaps == 8) else
+                                "sub_tier_kernel_wk<%d> (tiers of >= 4096 blocks), sub_tier_kernel_b4<%d> (smaller)"
+                                % (args.heaps - 3, args.heaps - 3)),
                      "algo_bytes_per_position": COMPULSORY_BYTES_PER_POSITION,
                      "algo_bytes_model": "compulsory: 1 B code written + 2 B producer-tier reads per position",
                      "launches_per_solve": launches_per_solve,

@@ -61,6 +61,10 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 #ifndef GM_BOX_WAVES
 #define GM_BOX_WAVES 2         // waves per SIMD the register budget must allow
 #endif
+// development ablations (results invalid): bit 1 no walk, 2 no child loads, 4 no stores, 8 no fold
+#ifndef GM_BOX_EXP
+#define GM_BOX_EXP 0
+#endif
 #ifndef GM_BOX_PIPE
 #define GM_BOX_PIPE 1          // issue the next group's child loads before walking this one
 #endif
@@ -147,9 +151,14 @@ __device__ __forceinline__ void bx_pairs(const bx_u32x4 &x0, const bx_u32x4 &x1,
     }
 }
 
-constexpr int BX_IMG = 4096;              // dwords: position (A, B) at 16 A + B
+// Image: position (A, B), A = a0 + 4 p, at dword PITCH p + 16 a0 + B.  A pitch of 68, not
+// 64, puts the 16-B chunks that 16 lanes touch in the fold and the store (whole rows A,
+// one per lane) in distinct banks; the walk's dword accesses then see 2-way conflicts.
+constexpr int BX_PITCH = 68;
+constexpr int BX_IMG = 64 * BX_PITCH;     // dwords
 constexpr int BX_PAD = 32;                // guard in front: the walk's (a0-1, a0-2) reads of row 0 at p = 0
 constexpr int BX_LDS = BX_PAD + BX_IMG + 64;   // + one dummy dword per lane for idle walk steps
+__device__ __forceinline__ uint32_t bx_row(uint32_t A) { return (A >> 2) * BX_PITCH + 16u * (A & 3u); }
 constexpr int BX_NLOAD = 48;              // 16-B child rows per lane per group
 
 struct BxGroup {
@@ -174,7 +183,8 @@ __device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, 
 // whose other coordinates are the lane.
 __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
                                          bx_u32x4 (&R)[BX_NLOAD]) {
-    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0xFFFFFFFFu, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rt =
+        __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, (GM_BOX_EXP & 2) ? 0u : 0xFFFFFFFFu, 0x00020000);
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0u, 0x00020000);
     // one (descriptor, offset) per child box, used by consecutive loads
 #pragma unroll
@@ -229,7 +239,7 @@ __device__ __forceinline__ void bx_fold(uint32_t *s, const BxGroup &G, uint32_t 
         }
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            *(bx_u32x4 *)(s + 16u * m + 4u * q) = bx_u32x4{F[4 * q], F[4 * q + 1], F[4 * q + 2], F[4 * q + 3]};
+            *(bx_u32x4 *)(s + bx_row(m) + 4u * q) = bx_u32x4{F[4 * q], F[4 * q + 1], F[4 * q + 2], F[4 * q + 3]};
     }
     BX_LDS_ORDER();
     // A children: layers 3 and 2 of the box below along heap i go to the rows a_i = 0
@@ -241,7 +251,7 @@ __device__ __forceinline__ void bx_fold(uint32_t *s, const BxGroup &G, uint32_t 
         uint32_t L3[16], L2[16];
         bx_pairs(R[32 + 4 * i + 0], R[32 + 4 * i + 2], L3);
         bx_pairs(R[32 + 4 * i + 1], R[32 + 4 * i + 3], L2);
-        uint32_t *t0 = s + 16u * (lo | hi), *t1 = s + 16u * (lo | (1u << (2 * i)) | hi);
+        uint32_t *t0 = s + bx_row(lo | hi), *t1 = s + bx_row(lo | (1u << (2 * i)) | hi);
         bx_u32x4 T0[4], T1[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -271,11 +281,32 @@ struct BxT { static constexpr int v = T; };
 template <class F, int... I>
 __device__ __forceinline__ void bx_unroll(F &f, std::integer_sequence<int, I...>) { (f(BxT<I>{}), ...); }
 
+#ifndef GM_BOX_SB
+#define GM_BOX_SB 2   // walk steps between a lane and the lanes one B step below it (DPP sources)
+#endif
+#ifndef GM_BOX_SR
+#define GM_BOX_SR 3   // walk steps between a lane and the row below it (LDS source)
+#endif
+constexpr int BX_SB = GM_BOX_SB, BX_SR = GM_BOX_SR;
+constexpr int BX_DMAX = 4 * BX_SB + 3 * BX_SR;   // latest start: SB popcount(b) + SR a0
+constexpr int BX_STEPS = 64 + BX_DMAX;
+constexpr int BX_AHEAD = BX_SR - 1;               // LDS inputs are fetched this many steps ahead
+static_assert(BX_AHEAD >= 1 && BX_AHEAD <= 2 && BX_SB >= 1 && BX_SB <= 2, "walk skews");
+// parent codes of a pair (gm_common.hpp parent_code per u16 half), two dependent ops deep
+__device__ __forceinline__ uint32_t bx_code2(uint32_t m) {
+    const bx_u16x2 v = __builtin_bit_cast(bx_u16x2, m);
+    const bx_u16x2 x = v ^ (bx_u16x2){255, 255}, t = v >> 7;
+    return __builtin_bit_cast(uint32_t, (bx_u16x2)(t * (bx_u16x2){2, 2} + x));
+}
 __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t lane) {
     uint32_t ln = lane;
     asm volatile("" : "+v"(ln));   // per group: keeps the per-step addresses from being hoisted (registers)
     const uint32_t b = ln & 15u, a0 = ln >> 4;
-    const int d = __popc(b) + (int)a0;
+    // A lane starts SB steps after the lanes one B step below it (it reads their codes by
+    // DPP SB steps after they were made) and SR steps after the row below (whose code it
+    // reads from LDS, fetched SR - 1 steps ahead); only its own last code (the a1 - 1
+    // child) is then on the step-to-step chain.
+    const int d = BX_SB * __popc(b) + BX_SR * (int)a0;
     const uint32_t m01 = a0 >= 1 ? ~0u : 0u, m02 = a0 >= 2 ? ~0u : 0u;
     const uint32_t mb0 = (b & 1u) ? ~0u : 0u, mb1 = (b & 2u) ? ~0u : 0u, mb2 = (b & 4u) ? ~0u : 0u;
     // validity of this lane's own earlier codes as (a1, a2) children at step t (p = t - d,
@@ -292,56 +323,67 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t lane) {
         v21[t >> 2] |= ((q >> 2) >= 1 ? 0xFFu : 0u) << (8 * (t & 3));
         v22[t >> 2] |= ((q >> 2) >= 2 ? 0xFFu : 0u) << (8 * (t & 3));
     }
-    const int base = (int)ln - 64 * d;   // image dword of this lane's position at step t: base + 64 t
+    const int base = (int)ln - BX_PITCH * d;   // image dword of this lane's position at step t: base + PITCH t
     const int dummy = BX_IMG + (int)ln;
-    uint32_t h[8];   // this lane's codes of the last 8 steps (ring by step)
+    // this lane's codes as (a1 - 1, a1 - 2, a2 - 1, a2 - 2) children of the positions 1, 2,
+    // 4 and 8 steps later, masked when they are made (0 where the digit wraps): rings by step
+    uint32_t g1 = 0, g2[2] = {0, 0}, g4[4] = {0, 0, 0, 0}, g8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // this lane's codes of the last 32 steps: (a3 - 1, a3 - 2) children and the DPP source
+    uint32_t hk[32];
 #pragma unroll
-    for (int q = 0; q < 8; q++) h[q] = 0;
+    for (int q = 0; q < 32; q++) hk[q] = 0;
     auto slot = [&](auto TT) {
         constexpr int T = decltype(TT)::v;
-        int idx = base + 64 * T;
-        if constexpr (T < 7 || T >= 64) idx = (uint32_t)(T - d) < 64u ? idx : dummy;
+        int idx = base + BX_PITCH * T;
+        if constexpr (T < BX_DMAX || T >= 64) idx = (uint32_t)(T - d) < 64u ? idx : dummy;
         return idx;
     };
-    // (a3 - 1, a3 - 2) = this lane's codes 16 and 32 steps ago, from its slots in the image
-    // (they exist from steps 16 and 32 on; a lane started d <= 7 steps late)
-    auto a3kids = [&](auto TT, uint32_t &k16, uint32_t &k32) {
-        constexpr int T = decltype(TT)::v;
-        const int idx = base + 64 * T;
-        k16 = k32 = 0;
-        if constexpr (T >= 16 && T < 23) k16 = T - d >= 16 ? s[idx - 1024 > 0 ? idx - 1024 : 0] : 0u;
-        if constexpr (T >= 23 && T < 64 + 7) k16 = s[idx - 1024];
-        if constexpr (T >= 32 && T < 39) k32 = T - d >= 32 ? s[idx - 2048 > 0 ? idx - 2048 : 0] : 0u;
-        if constexpr (T >= 39 && T < 64 + 7) k32 = s[idx - 2048];
+    // the LDS inputs of step T: the fold and the rows a0 - 1 / a0 - 2
+    struct In { uint32_t F, Y1, Y2; };
+    auto fetch = [&](auto TT) {
+        const int idx = slot(TT);
+        In x;
+        x.F = s[idx];
+        x.Y1 = s[idx - 16] & m01;
+        x.Y2 = s[idx - 32] & m02;
+        return x;
     };
-    uint32_t Fv = s[slot(BxT<0>{})], Y2 = s[slot(BxT<0>{}) - 32], K16 = 0, K32 = 0;
+    In pf[BX_AHEAD];
+    pf[0] = fetch(BxT<0>{});
+    if constexpr (BX_AHEAD > 1) pf[BX_AHEAD - 1] = fetch(BxT<BX_AHEAD - 1>{});
     auto step = [&](auto TT) {
         constexpr int T = decltype(TT)::v;
-        constexpr bool peel = T < 7 || T >= 64;
+        constexpr bool peel = T < BX_DMAX || T >= 64;
         const int idx = slot(TT);
-        const uint32_t Y1 = s[idx - 16];   // (a0 - 1): made last step by the row below
-        const uint32_t h1 = h[(T + 7) & 7], h2 = h[(T + 6) & 7], h4 = h[(T + 4) & 7], h8 = h[T & 7];
-        const uint32_t c0 = bx_dpp_shr<0x111>(h1) & mb0, c1 = bx_dpp_shr<0x112>(h1) & mb1;
-        const uint32_t c2 = bx_dpp_shr<0x114>(h1) & mb2, c3 = bx_dpp_shr<0x118>(h1);
-        uint32_t m = bx_max3(Fv, Y2 & m02, K16);
-        m = bx_max3(m, c0, c1);
-        m = bx_max3(m, c2, c3);
-        m = bx_max3(m, bx_and_byte<T & 3>(h2, v12), bx_and_byte<T & 3>(h4, v21[(T >> 2) & 3]));
-        m = bx_max3(m, bx_and_byte<T & 3>(h8, v22[(T >> 2) & 3]), K32);
-        m = bx_max3(m, bx_and_byte<T & 3>(h1, v11), Y1 & m01);
-        uint32_t c = bx_code(m);
+        const In cur = pf[T % BX_AHEAD];
+        // inputs made at least two steps ago: LDS reads, the B neighbours' codes (DPP of
+        // their code SB steps ago), this lane's older codes
+        const uint32_t hb = hk[(T + 32 - BX_SB) & 31];
+        const uint32_t c0 = bx_dpp_shr<0x111>(hb) & mb0, c1 = bx_dpp_shr<0x112>(hb) & mb1;
+        const uint32_t c2 = bx_dpp_shr<0x114>(hb) & mb2, c3 = bx_dpp_shr<0x118>(hb);
+        uint32_t e = bx_max3(cur.F, cur.Y1, cur.Y2);
+        if constexpr (T >= 32) e = bx_max3(e, hk[(T + 16) & 31], hk[T & 31]);
+        else if constexpr (T >= 16) e = bx_max2(e, hk[(T + 16) & 31]);
+        e = bx_max3(e, g2[T & 1], g4[T & 3]);
+        e = bx_max3(e, g8[T & 7], c0);
+        e = bx_max3(e, c1, c2);
+        // the last step's code of this lane: its (a1 - 1) child
+        const uint32_t m = bx_max3(e, c3, g1);
+        uint32_t c = bx_code2(m);
         if constexpr (peel) c = (uint32_t)(T - d) < 64u ? c : 0u;
-        h[T & 7] = c;
-        if constexpr (T < 70) {   // the next step's fold, (a0 - 2) row and a3 children are final already
-            const int nidx = slot(BxT<T + 1>{});
-            Fv = s[nidx];
-            Y2 = s[nidx - 32];
-            a3kids(BxT<T + 1>{}, K16, K32);
-        }
+        // the masks of the steps that will read c: byte (T + k) & 3 of the phase words
+        hk[T & 31] = c;
+        g1 = bx_and_byte<(T + 1) & 3>(c, v11);
+        g2[T & 1] = bx_and_byte<(T + 2) & 3>(c, v12);
+        g4[T & 3] = bx_and_byte<(T + 4) & 3>(c, v21[((T + 4) >> 2) & 3]);
+        g8[T & 7] = bx_and_byte<(T + 8) & 3>(c, v22[((T + 8) >> 2) & 3]);
         s[idx] = c;
         BX_LDS_ORDER();
+        // the row below made the code of step T + AHEAD at step T + AHEAD - SR = T - 1
+        if constexpr (T + BX_AHEAD < BX_STEPS) pf[T % BX_AHEAD] = fetch(BxT<T + BX_AHEAD>{});
+        __builtin_amdgcn_sched_barrier(0);   // no instruction crosses a step (a hoisted use would wait on the prefetch)
     };
-    bx_unroll(step, std::make_integer_sequence<int, 71>{});
+    bx_unroll(step, std::make_integer_sequence<int, BX_STEPS>{});
 }
 
 // store: rows m = lane + 64 i of both boxes, bytes regrouped per box
@@ -349,15 +391,15 @@ __device__ __forceinline__ void bx_store(uint8_t *table, const BxGroup &G, const
     __amdgpu_buffer_rsrc_t w[2];
 #pragma unroll
     for (int k = 0; k < 2; k++)
-        w[k] = __builtin_amdgcn_make_buffer_rsrc(table + ((uint64_t)G.box[k] << 12), 0, G.valid[k] ? 4096u : 0u,
-                                                 0x00020000);
+        w[k] = __builtin_amdgcn_make_buffer_rsrc(table + ((uint64_t)G.box[k] << 12), 0,
+                                                 (G.valid[k] && !(GM_BOX_EXP & 4)) ? 4096u : 0u, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t m = lane + 64u * i;
         bx_u32x4 o0, o1;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const bx_u32x4 x = *(const bx_u32x4 *)(s + 16u * m + 4u * q);
+            const bx_u32x4 x = *(const bx_u32x4 *)(s + bx_row(m) + 4u * q);
             const uint32_t t01 = __builtin_amdgcn_perm(x[1], x[0], 0x06020400u);
             const uint32_t t23 = __builtin_amdgcn_perm(x[3], x[2], 0x06020400u);
             o0[q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
@@ -389,7 +431,9 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
     for (;;) {
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));   // lane-derived addresses are recomputed per group, not held in registers
-        bx_fold(s, G, ln, R);
+        if (!(GM_BOX_EXP & 8)) bx_fold(s, G, ln, R);
+        else   // keep the loads live: one xor per row into the image
+            for (int q = 0; q < BX_NLOAD; q++) s[ln + 64 * (q & 7)] ^= R[q][0] ^ R[q][3];
         const uint32_t gn = g + Kx;
         const bool more = gn < g1;
         BxGroup Gn = G;
@@ -400,7 +444,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         }
 #endif
         BX_LDS_ORDER();
-        bx_walk(s, ln);
+        if (!(GM_BOX_EXP & 1)) bx_walk(s, ln);
         bx_store(table, G, s, ln);
         BX_LDS_ORDER();
         if (!more) break;

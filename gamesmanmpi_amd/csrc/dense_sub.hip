@@ -1078,13 +1078,13 @@ bool sub_kernel_x_exists(int high) { return pick_b4x(high) != nullptr && pick_wk
 void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_t *list, const uint8_t *zero,
                        const uint32_t *xoff, const uint64_t *xdst, hipStream_t s, int kind) {
     if (!nblocks) return;
-    hipLaunchKernelGGL(kind == 10 && nblocks >= wk_min_blocks() ? pick_wkx(high) : pick_b4x(high),
+    hipLaunchKernelGGL((kind == 10 || kind == 20) && nblocks >= wk_min_blocks() ? pick_wkx(high) : pick_b4x(high),
                        dim3((nblocks + 3) / 4), dim3(256), 0, s, table, list, nblocks, zero, xoff, xdst);
 }
 
 int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 6) return NT_B4;
-    if (low == 3 && c->sub_interleave == 10) return NT_WALK;
+    if (low == 3 && (c->sub_interleave == 10 || c->sub_interleave == 20)) return NT_WALK;   // 20: box engine at 8 heaps
     if (low == 3 && c->sub_interleave == 13) return NT_ROWFLOW;
     return c->sub_threads;
 }

@@ -76,7 +76,7 @@ struct Ctx {
     int engine_opt = GM_ENGINE_AUTO;
     int sub_low = 3;
     int sub_threads = 128;
-    int sub_interleave = 10;     // 10 walker (default), 6 four-block kernel, 13 row dataflow, 1 one block
+    int sub_interleave = 20;     // 20 box engine at 8 heaps, else the walker (default); 10 walker, 6 four-block, 13 row dataflow, 1 one block
     int sub_order = 2;   // block order inside a tier: 0 key, 1 Morton, 2 Hilbert (default)
     bool use_graph = true;
     bool timing = false;

@@ -82,8 +82,10 @@ enum {
                                 context on one GPU (loopback transport instead of RCCL); for testing
                                 the multi-GPU partition on a single device */
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
-    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path, LOW = 3: 10 = the walker kernel on tiers of >= 4096
-                                  blocks, the four-block kernel below (default); 6 = the four-block kernel
+    GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path: 20 (default) = the box engine at 8 heaps
+                                  (dense_box.hip: 4x4x4x4x2x2x2x2 boxes, 41 launches; other heap counts
+                                  and the sharded path use 10); 10 = the walker kernel on tiers of >= 4096
+                                  blocks, the four-block kernel below; 6 = the four-block kernel
                                   (byte LDS image, 256-thread barrier walk) on every tier; 13 = the whole
                                   solve as one row-granular dataflow launch (development option, measured
                                   slower on one GPU); 1 = one block per workgroup of GM_OPT_SUB_THREADS */

@@ -201,7 +201,7 @@ def test_subtract_block_orders_vs_oracle(oracle, heaps, order):
     assert np.array_equal(ctx.export()[1], ref)
 
 
-@pytest.mark.parametrize("variant", [10, 13])
+@pytest.mark.parametrize("variant", [10, 13, 20])
 def test_subtract_kernel_variants_full_2_32_match(variant):
     a, n1, r1 = _solve(SUB, (8,), sub_interleave=6)
     d1 = a.digest()
@@ -269,11 +269,11 @@ def test_subtract_custom_root_box(oracle):
 
 @pytest.mark.parametrize("root", [0x00000003, 0x000F0FFF, 0x12345678])
 def test_subtract_8_heaps_custom_root_solves_its_box_only(oracle, root):
-    """The dense engine launches only the blocks inside the root's box (every high
-    nibble <= the root's): a root with empty high heaps is one block, one launch.
-    Values are position-intrinsic, so the box equals the full 7-heap oracle table's
-    entries where the top nibble is 0 (roots below 16^7)."""
-    ctx, n, rec = _solve(SUB, (8,), root=root, timing=1)
+    """The block engine (GM_OPT_SUB_INTERLEAVE 10) launches only the blocks inside the
+    root's box (every high nibble <= the root's): a root with empty high heaps is one
+    block, one launch.  Values are position-intrinsic, so the box equals the full 7-heap
+    oracle table's entries where the top nibble is 0 (roots below 16^7)."""
+    ctx, n, rec = _solve(SUB, (8,), root=root, timing=1, sub_interleave=10)
     box = 1
     for j in range(8):
         box *= ((root >> (4 * j)) & 15) + 1
@@ -293,6 +293,28 @@ def test_subtract_8_heaps_custom_root_solves_its_box_only(oracle, root):
         for j in range(8):
             g ^= ((root >> (4 * j)) & 15) % 3
         assert (rec >> 14) == (1 if g == 0 else 0)
+
+
+def _box_tiers(root):
+    """Box-tiers of the box engine for a root: heaps 0-3 in quarters, 4-7 in halves."""
+    return sum(((root >> (4 * j)) & 15) >> (2 if j < 4 else 1) for j in range(8)) + 1
+
+
+@pytest.mark.parametrize("root", [0x00000003, 0x000F0FFF, 0x12345678, 0xFFFF0000, 0x0000FFFF, 0x9ABCDEF1, 0x7F7F7F7F])
+def test_subtract_8_heaps_box_engine_custom_roots(oracle, root):
+    """The box engine (GM_OPT_SUB_INTERLEAVE 20, the 8-heap default, csrc/dense_box.hip)
+    launches one box-tier per sum of the root box's coordinates and equals the block
+    engine on every root: same count, root record and digest; for roots below 16^7 the
+    exported records equal the 7-heap C-oracle table."""
+    a, n1, r1 = _solve(SUB, (8,), root=root, timing=1, sub_interleave=20)
+    assert a.stats()["kernel_launches"] == _box_tiers(root)
+    da = a.digest()
+    b, n2, r2 = _solve(SUB, (8,), root=root, sub_interleave=10)
+    assert (n1, r1, da) == (n2, r2, b.digest())
+    if root < 16 ** 7:
+        ref = oracle.subtract_dense_mt(7)
+        k, r = a.export()
+        assert np.array_equal(r, ref[k.astype(np.int64)])
 
 
 def test_subtract_single_heap_is_four_to_one():
@@ -329,9 +351,9 @@ def test_subtract_full_2_32_properties():
 
 
 def test_subtract_8_heaps_full_table_vs_oracle(oracle):
-    """Config 5 at FULL size: the 2^32 table of the headline kernel instance
-    (sub_tier_kernel_wk<5> on tiers of >= 4096 blocks, sub_tier_kernel_b4<5> below)
-    equals the C oracle's, through the order-independent
+    """Config 5 at FULL size: the 2^32 table of the headline kernel instance (the box
+    engine's box_tier_kernel, csrc/dense_box.hip, the 8-heap default) equals the C
+    oracle's, through the order-independent
     digest of every (key, record) -- against the committed oracle digest
     (tests/golden/make_oracle_digests.py) and a live oracle solve on the host.
     Semantics: reference src/new_process.py:189-198, 249-250."""

@@ -1,12 +1,21 @@
-"""Sum a rocprofv3 counter over the dispatches of one kernel (development aid).
-    python tools/pmc_sum.py DIR KERNEL_SUBSTRING [solves]"""
-import csv, sys, glob, os
-d, k = sys.argv[1], sys.argv[2]
-solves = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-tot = {}
-for r in csv.DictReader(open(f)):
-    if k in r["Kernel_Name"]:
-        tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-for n, v in tot.items():
-    print("%s per solve: %.4g" % (n, v / solves))
+"""Sum rocprofv3 --pmc counter_collection.csv rows per counter for kernels matching a name,
+over the last N dispatches (one solve).  python tools/pmc_sum.py DIR NAME [N]"""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+d, name = sys.argv[1], sys.argv[2]
+n = int(sys.argv[3]) if len(sys.argv) > 3 else 41
+files = glob.glob(d + "/**/*counter_collection.csv", recursive=True)
+rows = []
+for f in files:
+    rows += [r for r in csv.DictReader(open(f)) if name in r.get("Kernel_Name", "")]
+disp = sorted({int(r["Dispatch_Id"]) for r in rows})[-n:]
+keep = set(disp)
+acc = defaultdict(float)
+for r in rows:
+    if int(r["Dispatch_Id"]) in keep:
+        acc[r["Counter_Name"]] += float(r["Counter_Value"])
+for k in sorted(acc):
+    print("%-28s %.4g" % (k, acc[k]))
