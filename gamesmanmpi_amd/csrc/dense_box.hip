@@ -66,7 +66,7 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 #define GM_BOX_EXP 0
 #endif
 #ifndef GM_BOX_PIPE
-#define GM_BOX_PIPE 1          // issue the next group's child loads before walking this one
+#define GM_BOX_PIPE 0          // 1: issue the next group's child loads before walking this one (measured slower: registers)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -282,10 +282,10 @@ template <class F, int... I>
 __device__ __forceinline__ void bx_unroll(F &f, std::integer_sequence<int, I...>) { (f(BxT<I>{}), ...); }
 
 #ifndef GM_BOX_SB
-#define GM_BOX_SB 2   // walk steps between a lane and the lanes one B step below it (DPP sources)
+#define GM_BOX_SB 1   // walk steps between a lane and the lanes one B step below it (DPP sources)
 #endif
 #ifndef GM_BOX_SR
-#define GM_BOX_SR 3   // walk steps between a lane and the row below it (LDS source)
+#define GM_BOX_SR 2   // walk steps between a lane and the row below it (LDS source)
 #endif
 constexpr int BX_SB = GM_BOX_SB, BX_SR = GM_BOX_SR;
 constexpr int BX_DMAX = 4 * BX_SB + 3 * BX_SR;   // latest start: SB popcount(b) + SR a0
