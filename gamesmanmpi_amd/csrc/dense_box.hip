@@ -181,37 +181,42 @@ __device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, 
 // m = lane + 64 i (R[8 i + 4 k + j]: box k, heap 4 + j), R[32..47] the A children's top
 // layers (R[32 + 4 i + 2 k + v]: heap i, box k, layer 3 - v) of the rows a_i in {2, 3}
 // whose other coordinates are the lane.
+template <int PART>   // 1: the B children (R[0..31]), 2: the A children's top layers (R[32..47]), 3: both
 __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
                                          bx_u32x4 (&R)[BX_NLOAD]) {
     const __amdgpu_buffer_rsrc_t rt =
         __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, (GM_BOX_EXP & 2) ? 0u : 0xFFFFFFFFu, 0x00020000);
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0u, 0x00020000);
     // one (descriptor, offset) per child box, used by consecutive loads
+    if constexpr (PART & 1) {
 #pragma unroll
-    for (int k = 0; k < 2; k++)
+        for (int k = 0; k < 2; k++)
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const bool ok = G.valid[k] && box_coord(G.box[k], 4 + j) >= 1;
-            const uint32_t soff = ok ? (G.box[k] - box_unit(4 + j)) << 12 : 0u;
-            const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
+            for (int j = 0; j < 4; j++) {
+                const bool ok = G.valid[k] && box_coord(G.box[k], 4 + j) >= 1;
+                const uint32_t soff = ok ? (G.box[k] - box_unit(4 + j)) << 12 : 0u;
+                const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-                R[8 * i + 4 * k + j] = __builtin_bit_cast(
-                    bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * (lane + 64u * i), soff, 0));
-        }
+                for (int i = 0; i < 4; i++)
+                    R[8 * i + 4 * k + j] = __builtin_bit_cast(
+                        bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * (lane + 64u * i), soff, 0));
+            }
+    }
+    if constexpr (PART & 2) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t lo = lane & ((1u << (2 * i)) - 1u), hi = (lane >> (2 * i)) << (2 * i + 2);
+        for (int i = 0; i < 4; i++) {
+            const uint32_t lo = lane & ((1u << (2 * i)) - 1u), hi = (lane >> (2 * i)) << (2 * i + 2);
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const bool ok = G.valid[k] && box_coord(G.box[k], i) >= 1;
-            const uint32_t soff = ok ? (G.box[k] - box_unit(i)) << 12 : 0u;
-            const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
+            for (int k = 0; k < 2; k++) {
+                const bool ok = G.valid[k] && box_coord(G.box[k], i) >= 1;
+                const uint32_t soff = ok ? (G.box[k] - box_unit(i)) << 12 : 0u;
+                const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
 #pragma unroll
-            for (int v = 0; v < 2; v++) {
-                const uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
-                R[32 + 4 * i + 2 * k + v] =
-                    __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, 0));
+                for (int v = 0; v < 2; v++) {
+                    const uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
+                    R[32 + 4 * i + 2 * k + v] =
+                        __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, 0));
+                }
             }
         }
     }
@@ -224,17 +229,27 @@ __device__ __forceinline__ void bx_fold(uint32_t *s, const BxGroup &G, uint32_t 
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t m = lane + 64u * i;
-        // heap by heap into F (16 live pairs instead of 64)
+        // two heaps at a time into F: each position's inputs are its row's code in the four
+        // child boxes, and the code one B step up where b_j = 0 (48 maxes per row)
         uint32_t F[16];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            uint32_t P[16];
-            bx_pairs(R[8 * i + j], R[8 * i + 4 + j], P);
+        for (int jp = 0; jp < 4; jp += 2) {
+            uint32_t P[16], Q[16];
+            bx_pairs(R[8 * i + jp], R[8 * i + 4 + jp], P);
+            bx_pairs(R[8 * i + jp + 1], R[8 * i + 4 + jp + 1], Q);
 #pragma unroll
             for (int b = 0; b < 16; b++) {
-                const bool two = !((b >> j) & 1);
-                if (j == 0) F[b] = two ? bx_max2(P[b], P[b | 1]) : P[b];
-                else F[b] = two ? bx_max3(F[b], P[b], P[b | (1 << j)]) : bx_max2(F[b], P[b]);
+                uint32_t in[5];
+                int n = 0;
+                if (jp) in[n++] = F[b];
+                in[n++] = P[b];
+                in[n++] = Q[b];
+                if (!((b >> jp) & 1)) in[n++] = P[b | (1 << jp)];
+                if (!((b >> (jp + 1)) & 1)) in[n++] = Q[b | (2 << jp)];
+                uint32_t f = n >= 3 ? bx_max3(in[0], in[1], in[2]) : bx_max2(in[0], in[1]);
+                if (n == 4) f = bx_max2(f, in[3]);
+                if (n == 5) f = bx_max3(f, in[3], in[4]);
+                F[b] = f;
             }
         }
 #pragma unroll
@@ -298,31 +313,50 @@ __device__ __forceinline__ uint32_t bx_code2(uint32_t m) {
     const bx_u16x2 x = v ^ (bx_u16x2){255, 255}, t = v >> 7;
     return __builtin_bit_cast(uint32_t, (bx_u16x2)(t * (bx_u16x2){2, 2} + x));
 }
-__device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t lane) {
-    uint32_t ln = lane;
-    asm volatile("" : "+v"(ln));   // per group: keeps the per-step addresses from being hoisted (registers)
-    const uint32_t b = ln & 15u, a0 = ln >> 4;
+// per-lane constants of the walk, computed once per workgroup
+struct BxLaneC {
+    int d;                                   // start step
+    uint32_t m01, m02, mb0, mb1, mb2;        // row-below / B-neighbour validity
+    uint32_t v11, v12, v21[4], v22[4];       // (a1, a2) child validity bytes by step phase
+};
+__device__ __forceinline__ BxLaneC bx_lane_consts(uint32_t lane) {
+    BxLaneC L;
+    const uint32_t b = lane & 15u, a0 = lane >> 4;
     // A lane starts SB steps after the lanes one B step below it (it reads their codes by
     // DPP SB steps after they were made) and SR steps after the row below (whose code it
     // reads from LDS, fetched SR - 1 steps ahead); only its own last code (the a1 - 1
     // child) is then on the step-to-step chain.
     const int d = BX_SB * __popc(b) + BX_SR * (int)a0;
-    const uint32_t m01 = a0 >= 1 ? ~0u : 0u, m02 = a0 >= 2 ? ~0u : 0u;
-    const uint32_t mb0 = (b & 1u) ? ~0u : 0u, mb1 = (b & 2u) ? ~0u : 0u, mb2 = (b & 4u) ? ~0u : 0u;
+    L.d = d;
+    L.m01 = a0 >= 1 ? ~0u : 0u;
+    L.m02 = a0 >= 2 ? ~0u : 0u;
+    L.mb0 = (b & 1u) ? ~0u : 0u;
+    L.mb1 = (b & 2u) ? ~0u : 0u;
+    L.mb2 = (b & 4u) ? ~0u : 0u;
     // validity of this lane's own earlier codes as (a1, a2) children at step t (p = t - d,
     // a1 = p & 3, a2 = (p >> 2) & 3), one byte (0 or 0xFF) per step phase: t & 3 for a1,
     // t & 15 for a2 (byte t & 3 of word (t >> 2) & 3)
-    uint32_t v11 = 0, v12 = 0, v21[4] = {0, 0, 0, 0}, v22[4] = {0, 0, 0, 0};
+    L.v11 = L.v12 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) L.v21[q] = L.v22[q] = 0;
 #pragma unroll
     for (int t = 0; t < 16; t++) {
         const uint32_t q = (uint32_t)(t - d) & 15u;
         if (t < 4) {
-            v11 |= ((q & 3u) >= 1 ? 0xFFu : 0u) << (8 * t);
-            v12 |= ((q & 3u) >= 2 ? 0xFFu : 0u) << (8 * t);
+            L.v11 |= ((q & 3u) >= 1 ? 0xFFu : 0u) << (8 * t);
+            L.v12 |= ((q & 3u) >= 2 ? 0xFFu : 0u) << (8 * t);
         }
-        v21[t >> 2] |= ((q >> 2) >= 1 ? 0xFFu : 0u) << (8 * (t & 3));
-        v22[t >> 2] |= ((q >> 2) >= 2 ? 0xFFu : 0u) << (8 * (t & 3));
+        L.v21[t >> 2] |= ((q >> 2) >= 1 ? 0xFFu : 0u) << (8 * (t & 3));
+        L.v22[t >> 2] |= ((q >> 2) >= 2 ? 0xFFu : 0u) << (8 * (t & 3));
     }
+    return L;
+}
+__device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC &L) {
+    const int d = L.d;
+    const uint32_t m01 = L.m01, m02 = L.m02, mb0 = L.mb0, mb1 = L.mb1, mb2 = L.mb2;
+    const uint32_t v11 = L.v11, v12 = L.v12;
+    const uint32_t v21[4] = {L.v21[0], L.v21[1], L.v21[2], L.v21[3]};
+    const uint32_t v22[4] = {L.v22[0], L.v22[1], L.v22[2], L.v22[3]};
     const int base = (int)ln - BX_PITCH * d;   // image dword of this lane's position at step t: base + PITCH t
     const int dummy = BX_IMG + (int)ln;
     // this lane's codes as (a1 - 1, a1 - 2, a2 - 1, a2 - 2) children of the positions 1, 2,
@@ -425,9 +459,10 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
     const uint32_t g0 = x * q + (x < r ? x : r), g1 = g0 + q + (x < r ? 1u : 0u);
     uint32_t g = g0 + kx;
     if (g >= g1) return;
+    const BxLaneC L = bx_lane_consts(lane);
     bx_u32x4 R[BX_NLOAD];
     BxGroup G = bx_group(boxes, nbox, g);
-    bx_issue(table, G, lane, R);
+    bx_issue<3>(table, G, lane, R);
     for (;;) {
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));   // lane-derived addresses are recomputed per group, not held in registers
@@ -437,23 +472,27 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         const uint32_t gn = g + Kx;
         const bool more = gn < g1;
         BxGroup Gn = G;
-#if GM_BOX_PIPE
-        if (more) {
-            Gn = bx_group(boxes, nbox, gn);
-            bx_issue(table, Gn, ln, R);
-        }
+        if (more) Gn = bx_group(boxes, nbox, gn);
+#if GM_BOX_PIPE == 1
+        if (more) bx_issue<3>(table, Gn, ln, R);   // every child row of the next group during this walk
+#elif GM_BOX_PIPE >= 2
+        if (more) bx_issue<1>(table, Gn, ln, R);   // its B rows during this walk, its A rows after it
 #endif
         BX_LDS_ORDER();
-        if (!(GM_BOX_EXP & 1)) bx_walk(s, ln);
+        if (!(GM_BOX_EXP & 1)) bx_walk(s, ln, L);
+#if GM_BOX_PIPE == 2
+        if (more) bx_issue<2>(table, Gn, ln, R);
+#endif
         bx_store(table, G, s, ln);
+#if GM_BOX_PIPE == 3
+        if (more) bx_issue<2>(table, Gn, ln, R);   // A rows after the store
+#endif
         BX_LDS_ORDER();
         if (!more) break;
         g = gn;
-#if GM_BOX_PIPE
         G = Gn;
-#else
-        G = bx_group(boxes, nbox, g);
-        bx_issue(table, G, lane, R);
+#if GM_BOX_PIPE == 0
+        bx_issue<3>(table, G, lane, R);
 #endif
     }
 }
