@@ -13,7 +13,7 @@ ctx = Context(5, (8,), device=0)
 ctx.set_option(_lib.OPT_SUB_INTERLEAVE, int(os.environ.get("VARIANT", "20")))
 ctx.set_option(_lib.OPT_TIMING, 1)
 ts = []
-for _ in range(12):
+for _ in range(int(os.environ.get("SOLVES", "24"))):
     n, rec = ctx.solve(0xFFFFFFFF)
     ts.append(ctx.stats()["kernel_ms"])
 d = ctx.digest()
