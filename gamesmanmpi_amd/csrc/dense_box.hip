@@ -28,14 +28,16 @@
 // dword as a u16 pair: low half box 0, high half box 1), persistent over its share of
 // the tier:
 //   fold   the child rows: per target row (16 positions, one A), the four B-children
-//          rows (whole 16-B rows, shifted by one B step where b_j = 0); then per A heap
-//          the two top layers of the child box below, merged into the rows a_i = 0, 1;
-//   walk   lane (b = lane & 15, a0 = lane >> 4) walks p = 0..63 (A = a0 + 4 p) starting
-//          d = popcount(b) + a0 steps late, so each child made inside the box is at
-//          least a step old: the B children by DPP row_shr 1/2/4/8 from the lanes one
-//          B step below, (a0-1, a0-2) from the image in LDS, (a1, a2) from this lane's
-//          own last 1/2/4/8 codes (masked at their digit boundaries) and (a3) from its
-//          codes 16 and 32 steps ago (zero before its start); 71 steps, no barrier;
+//          rows (whole 16-B rows, shifted by one B step where b_j = 0) and, for the rows
+//          a3 = 0, 1 this lane owns, heap 3's two top layers of the box below; then per
+//          A heap 0-2 those layers merged into the rows a_i = 0, 1 of the image;
+//   walk   lane (a0 = lane & 3, b = lane >> 2) walks p = 0..63 (A = a0 + 4 p) starting
+//          d = b0 + b1 + 2 (b2 + b3) + a0 steps late, so each child made inside the box
+//          is old enough to fetch: the a0 - 1 / a0 - 2 / b0 / b1 children by DPP row_shr
+//          1/2/4/8 from the lanes below, the b2 / b3 children from the image in LDS (a
+//          zero slot where there is none), (a1, a2) from this lane's own last 1/2/4/8
+//          codes (masked at their digit boundaries) and (a3) from its codes 16 and 32
+//          steps ago (zero before its start); 73 steps, no barrier;
 //   store  16-B rows of both boxes (write-through).
 // The max of up to 13 inputs uses v_pk_maximum3_f16: a code 0..255 in the low byte of
 // an f16 is a subnormal, ordered like the integer (the kernel keeps f16 denormals,
@@ -64,18 +66,6 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 // development ablations (results invalid): bit 1 no walk, 2 no child loads, 4 no stores, 8 no fold
 #ifndef GM_BOX_EXP
 #define GM_BOX_EXP 0
-#endif
-#ifndef GM_BOX_WEXP
-#define GM_BOX_WEXP 0          // walk ablations (invalid results): 1 no LDS write, 2 no permlane, 4 no DPP, 8 no step barrier, 16 no fold read
-#endif
-#ifndef GM_BOX_REPW
-#define GM_BOX_REPW 1          // development: walk (1) / fold (REPF) repeated, to time one phase in the mix
-#endif
-#ifndef GM_BOX_REPF
-#define GM_BOX_REPF 1
-#endif
-#ifndef GM_BOX_PIPE
-#define GM_BOX_PIPE 0          // 1: issue the next group's child loads before walking this one (measured slower: registers)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -163,10 +153,7 @@ __device__ __forceinline__ void bx_pairs(const bx_u32x4 &x0, const bx_u32x4 &x1,
 // Image: position (A, B), A = a0 + 4 p, at dword PITCH p + 16 a0 + B.  A pitch of 68, not
 // 64, puts the 16-B chunks that 16 lanes touch in the fold and the store (whole rows A,
 // one per lane) in distinct banks; the walk's dword accesses then see 2-way conflicts.
-#ifndef GM_BOX_PITCH
-#define GM_BOX_PITCH 68
-#endif
-constexpr int BX_PITCH = GM_BOX_PITCH;
+constexpr int BX_PITCH = 68;
 constexpr int BX_IMG = 64 * BX_PITCH;     // dwords
 constexpr int BX_PAD = 32;                // guard in front: the walk's (a0-1, a0-2) reads of row 0 at p = 0
 constexpr int BX_LDS = BX_PAD + BX_IMG + 64;   // + one dummy dword per lane for idle walk steps
@@ -193,14 +180,13 @@ __device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, 
 // m = lane + 64 i (R[8 i + 4 k + j]: box k, heap 4 + j), R[32..47] the A children's top
 // layers (R[32 + 4 i + 2 k + v]: heap i, box k, layer 3 - v) of the rows a_i in {2, 3}
 // whose other coordinates are the lane.
-template <int PART>   // 1: the B children (R[0..31]), 2: the A children's top layers (R[32..47]), 3: both
 __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
                                          bx_u32x4 (&R)[BX_NLOAD]) {
     const __amdgpu_buffer_rsrc_t rt =
         __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, (GM_BOX_EXP & 2) ? 0u : 0xFFFFFFFFu, 0x00020000);
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0u, 0x00020000);
     // one (descriptor, offset) per child box, used by consecutive loads
-    if constexpr (PART & 1) {
+    {
 #pragma unroll
         for (int k = 0; k < 2; k++)
 #pragma unroll
@@ -214,7 +200,7 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
                         bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * (lane + 64u * i), soff, 0));
             }
     }
-    if constexpr (PART & 2) {
+    {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t lo = lane & ((1u << (2 * i)) - 1u), hi = (lane >> (2 * i)) << (2 * i + 2);
@@ -319,44 +305,18 @@ struct BxT { static constexpr int v = T; };
 template <class F, int... I>
 __device__ __forceinline__ void bx_unroll(F &f, std::integer_sequence<int, I...>) { (f(BxT<I>{}), ...); }
 
-#ifndef GM_BOX_XL
-#define GM_BOX_XL 2   // 2: b2/b3 neighbours from LDS (zero slots for none), the rest cross-lane; 1: all cross-lane; 0: rows a0-1/a0-2 from LDS
-#endif
-#ifndef GM_BOX_SB
-#define GM_BOX_SB 1   // walk steps between a lane and the lanes one B step below it (DPP sources)
-#endif
-#if GM_BOX_XL
-#ifndef GM_BOX_SR
-#define GM_BOX_SR 1   // walk steps between a lane and the lane one a0 step below it
-#endif
+// Lane (a0 = lane bits 0-1, b = lane bits 2-5) starts at step d = (b0 + b1) + 2 (b2 + b3)
+// + a0: a step after the lanes one a0 / b0 / b1 step below it, whose codes of the step
+// before it takes by DPP (row_shr 1, 2, 4, 8 inside a 16-lane row), and two steps after
+// the lanes one b2 / b3 step below (the rows 16 and 32 lanes down), whose codes it reads
+// from the image, fetched two steps ahead.
+constexpr int BX_S2 = 2;
+constexpr int BX_DMAX = 2 + 2 * BX_S2 + 3;   // latest start
+constexpr int BX_STEPS = 64 + BX_DMAX;
 #ifndef GM_BOX_FAHEAD
 #define GM_BOX_FAHEAD 4   // the fold value of a step is read from LDS this many steps ahead
 #endif
-#else
-#ifndef GM_BOX_SR
-#define GM_BOX_SR 2   // walk steps between a lane and the row below it (LDS source)
-#endif
-#endif
-#ifndef GM_BOX_S2
-#if GM_BOX_XL == 2
-#define GM_BOX_S2 2           // walk steps between a lane and the lanes one b2 / b3 step below (LDS sources)
-#else
-#define GM_BOX_S2 GM_BOX_SB   // XL 1: walk steps between a lane and the lanes one b2 / b3 step below (permlane sources)
-#endif
-#endif
-constexpr int BX_SB = GM_BOX_SB, BX_SR = GM_BOX_SR, BX_S2 = GM_BOX_XL ? GM_BOX_S2 : GM_BOX_SB;
-constexpr int BX_DMAX = 2 * BX_SB + 2 * BX_S2 + 3 * BX_SR;   // latest start
-constexpr int BX_STEPS = 64 + BX_DMAX;
-#if GM_BOX_XL == 2
-constexpr int BX_AHEAD = GM_BOX_S2;   // a b2 / b3 neighbour wrote its code S2 steps before it is needed
-static_assert(BX_AHEAD >= 2 && BX_SB == 1 && BX_SR == 1, "walk skews");
-#elif GM_BOX_XL
-constexpr int BX_AHEAD = GM_BOX_FAHEAD;
-static_assert(BX_AHEAD >= 1 && BX_SB >= 1 && BX_SR >= 1, "walk skews");
-#else
-constexpr int BX_AHEAD = BX_SR - 1;               // LDS inputs are fetched this many steps ahead
-static_assert(BX_AHEAD >= 1 && BX_AHEAD <= 2 && BX_SB >= 1 && BX_SB <= 2, "walk skews");
-#endif
+constexpr int BX_FA = GM_BOX_FAHEAD;
 // parent codes of a pair (gm_common.hpp parent_code per u16 half), two dependent ops deep
 __device__ __forceinline__ uint32_t bx_code2(uint32_t m) {
     // (m >> 7) * 2 + (m ^ 255) per half; written out so the compiler keeps the packed
@@ -368,30 +328,20 @@ __device__ __forceinline__ uint32_t bx_code2(uint32_t m) {
         : "=v"(g), "=&v"(t), "=&v"(x) : "v"(m));
     return g;
 }
-// The walk's lanes: XL 1: a0 = lane bits 0-1, b = lane bits 2-5 (b0, b1 inside a DPP row,
-// b2, b3 the row bits); XL 0: b = lane bits 0-3, a0 = lane bits 4-5.
-__device__ __forceinline__ uint32_t bx_walk_a0(uint32_t lane) { return GM_BOX_XL ? lane & 3u : lane >> 4; }
-__device__ __forceinline__ uint32_t bx_walk_b(uint32_t lane) { return GM_BOX_XL ? (lane >> 2) & 15u : lane & 15u; }
 // per-lane constants of the walk, computed once per workgroup
 struct BxLaneC {
     int d;                                   // start step
-    uint32_t m01, m02, mb0, mb1, mb2;        // a0-below / B-neighbour validity
+    uint32_t m01, m02, mb0;                  // a0 - 1 / a0 - 2 / b0 neighbour validity
     uint32_t v11, v12, v21[4], v22[4];       // (a1, a2) child validity bytes by step phase
 };
 __device__ __forceinline__ BxLaneC bx_lane_consts(uint32_t lane) {
     BxLaneC L;
-    const uint32_t b = bx_walk_b(lane), a0 = bx_walk_a0(lane);
-    // A lane starts SB steps after the lanes one B step below it (it takes their codes by
-    // a cross-lane op SB steps after they were made) and SR steps after the lane one a0
-    // step below; only its own last code (the a1 - 1 child) is then on the step-to-step
-    // chain besides the neighbours of the step before.
-    const int d = BX_SB * __popc(b & 3u) + BX_S2 * __popc(b & 12u) + BX_SR * (int)a0;
+    const uint32_t a0 = lane & 3u, b = (lane >> 2) & 15u;
+    const int d = (int)__popc(b & 3u) + BX_S2 * (int)__popc(b & 12u) + (int)a0;
     L.d = d;
     L.m01 = a0 >= 1 ? ~0u : 0u;
     L.m02 = a0 >= 2 ? ~0u : 0u;
-    L.mb0 = (b & 1u) ? ~0u : 0u;
-    L.mb1 = (b & 2u) ? ~0u : 0u;
-    L.mb2 = (b & 4u) ? ~0u : 0u;
+    L.mb0 = (b & 1u) ? ~0u : 0u;   // b1 needs none: row_shr 8 gives 0 to the lanes it leaves
     // opaque, so they stay VGPR masks (one v_and_b32_dpp per neighbour, not a DPP move
     // and a select on a lane-mask SGPR pair)
     asm volatile("" : "+v"(L.m01), "+v"(L.m02), "+v"(L.mb0));
@@ -413,25 +363,24 @@ __device__ __forceinline__ BxLaneC bx_lane_consts(uint32_t lane) {
     }
     return L;
 }
-#if GM_BOX_XL
-// rows 1 and 3 (lanes 16-31, 48-63) get lanes 16 below; rows 0 and 2 get 0
-__device__ __forceinline__ uint32_t bx_from16(uint32_t v) { return __builtin_amdgcn_permlane16_swap(0u, v, false, false)[0]; }
-// lanes 32-63 get lanes 32 below; lanes 0-31 get 0
-__device__ __forceinline__ uint32_t bx_from32(uint32_t v) { return __builtin_amdgcn_permlane32_swap(0u, v, false, false)[0]; }
-#endif
 __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC &L) {
     const int d = L.d;
-    const uint32_t m01 = L.m01, m02 = L.m02, mb0 = L.mb0, mb1 = L.mb1, mb2 = L.mb2;
+    const uint32_t m01 = L.m01, m02 = L.m02, mb0 = L.mb0;
     const uint32_t v11 = L.v11, v12 = L.v12;
     const uint32_t v21[4] = {L.v21[0], L.v21[1], L.v21[2], L.v21[3]};
     const uint32_t v22[4] = {L.v22[0], L.v22[1], L.v22[2], L.v22[3]};
-    // image dword of this lane's position at step t: base + PITCH t
-    const int base = (int)(16u * bx_walk_a0(ln) + bx_walk_b(ln)) - BX_PITCH * d;
-    const int dummy = BX_IMG + (int)ln;
+    // position (A = a0 + 4 p, B = b) of step t = p + d at dword base + PITCH t; the
+    // neighbour one b2 (b3) step below is 4 (8) dwords lower; a lane without one reads
+    // the row's padding (dwords 64-67, kept zero).  (From the opaque lane, per group:
+    // registers held across the group loop would spill in the fold.)
+    const uint32_t a0 = ln & 3u, b = (ln >> 2) & 15u;
+    const int base = (int)(16u * a0 + b) - BX_PITCH * d, zb = 64 + (int)a0 - BX_PITCH * d;
+    const int base2 = (b & 4u) ? base - 4 : zb, base3 = (b & 8u) ? base - 8 : zb;
+    const int dummy = BX_IMG + (int)ln;   // idle steps (before d, after d + 63) use a slot of their own
     // this lane's codes as (a1 - 1, a1 - 2, a2 - 1, a2 - 2) children of the positions 1, 2,
     // 4 and 8 steps later, masked when they are made (0 where the digit wraps): rings by step
     uint32_t g1 = 0, g2[2] = {0, 0}, g4[4] = {0, 0, 0, 0}, g8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // this lane's codes of the last 32 steps: (a3 - 1, a3 - 2) children and the cross-lane source
+    // this lane's codes of the last 32 steps: (a3 - 1, a3 - 2) children and the DPP source
     uint32_t hk[32];
 #pragma unroll
     for (int q = 0; q < 32; q++) hk[q] = 0;
@@ -441,113 +390,38 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
         if constexpr (T < BX_DMAX || T >= 64) idx = (uint32_t)(T - d) < 64u ? idx : dummy;
         return idx;
     };
-#if GM_BOX_XL == 2
-    // the LDS inputs of step T: the fold (nothing in the walk writes it before step T) and
-    // the b2 / b3 neighbours' codes (made S2 steps before), or a zero slot of the row
-    // padding (dwords 64-67) where this lane has no such neighbour
-    const uint32_t bw = bx_walk_b(ln);
-    const int zb = 64 + (int)(ln & 3u) - BX_PITCH * d;
-    const int base2 = (bw & 4u) ? base - 4 : zb, base3 = (bw & 8u) ? base - 8 : zb;
-    // (the fold is read FAHEAD steps ahead, the neighbours S2 = AHEAD steps ahead)
+    // LDS inputs: the fold (nothing in the walk writes it before its step), FA steps
+    // ahead; the b2 / b3 neighbours' codes, made S2 steps before they are needed
     struct In { uint32_t C2, C3; };
-    auto fetchc = [&](auto TT) {
-        In x;
-        x.C2 = s[slot(TT, base2)];
-        x.C3 = s[slot(TT, base3)];
-        return x;
-    };
+    auto fetchc = [&](auto TT) { return In{s[slot(TT, base2)], s[slot(TT, base3)]}; };
     auto fetchf = [&](auto TT) { return s[slot(TT, base)]; };
-    constexpr int FA = GM_BOX_FAHEAD;
-    uint32_t pff[FA];
-    In pf[BX_AHEAD];
+    uint32_t pff[BX_FA];
+    In pfc[BX_S2];
     auto firstf = [&](auto TT) { pff[decltype(TT)::v] = fetchf(TT); };
-    bx_unroll(firstf, std::make_integer_sequence<int, FA>{});
-    auto first = [&](auto TT) { pf[decltype(TT)::v] = fetchc(TT); };
-    bx_unroll(first, std::make_integer_sequence<int, BX_AHEAD>{});
-    // the max of a step's inputs made two or more steps before it and not read from LDS
-    // in the step before, formed a step early (off the step-to-step chain): the fold, the
-    // a0 - 2 neighbour, this lane's a1 - 2, a2 and a3 children
+    bx_unroll(firstf, std::make_integer_sequence<int, BX_FA>{});
+    auto firstc = [&](auto TT) { pfc[decltype(TT)::v] = fetchc(TT); };
+    bx_unroll(firstc, std::make_integer_sequence<int, BX_S2>{});
+    // the max of a step's inputs that exist a step before it (the fold, the a0 - 2
+    // neighbour, this lane's a1 - 2, a2 and a3 children), formed in that step, off the
+    // step-to-step chain
     uint32_t pre = pff[0];
-#elif GM_BOX_XL
-    // the LDS input of step T: the fold (nothing in the walk writes it before step T)
-    auto fetch = [&](auto TT) { return (GM_BOX_WEXP & 16) ? (uint32_t)slot(TT, base) : s[slot(TT, base)]; };
-    uint32_t pf[BX_AHEAD];
-    auto first = [&](auto TT) { pf[decltype(TT)::v] = fetch(TT); };
-    bx_unroll(first, std::make_integer_sequence<int, BX_AHEAD>{});
-#else
-    // the LDS inputs of step T: the fold and the rows a0 - 1 / a0 - 2
-    struct In { uint32_t F, Y1, Y2; };
-    auto fetch = [&](auto TT) {
-        const int idx = slot(TT, base);
-        In x;
-        x.F = s[idx];
-        x.Y1 = s[idx - 16] & m01;
-        x.Y2 = s[idx - 32] & m02;
-        return x;
-    };
-    In pf[BX_AHEAD];
-    pf[0] = fetch(BxT<0>{});
-    if constexpr (BX_AHEAD > 1) pf[BX_AHEAD - 1] = fetch(BxT<BX_AHEAD - 1>{});
-#endif
     auto step = [&](auto TT) {
         constexpr int T = decltype(TT)::v;
         constexpr bool peel = T < BX_DMAX || T >= 64;
-        const int idx = slot(TT, base);
-        // inputs made at least two steps ago first: the fold, this lane's older codes
-        // (a3, a2, a1 - 2 children) and, by cross-lane ops, the a0 - 2 neighbour; then the
-        // codes of the step before (the a0 - 1 and B neighbours, the a1 - 1 child)
-        const uint32_t hb = hk[(T + 32 - BX_SB) & 31];
-#if GM_BOX_XL == 2
         // the step-to-step chain: the a0 - 1, b0 and b1 neighbours' codes of the step
-        // before (DPP) and this lane's own (the a1 - 1 child)
+        // before (DPP), this lane's own (the a1 - 1 child), the b2 / b3 neighbours (LDS)
+        const uint32_t hb = hk[(T + 31) & 31];
         const uint32_t y1 = bx_dpp_shr<0x111>(hb) & m01, c0 = bx_dpp_shr<0x114>(hb) & mb0, c1 = bx_dpp_shr<0x118>(hb);
-        const In cn = pf[T % BX_AHEAD];
+        const In cn = pfc[T % BX_S2];
         const uint32_t m = bx_max3(bx_max3(bx_max3(pre, cn.C2, cn.C3), y1, c0), c1, g1);
         if constexpr (T + 1 < BX_STEPS) {
             constexpr int U = T + 1;
             const uint32_t y2 = bx_dpp_shr<0x112>(hb) & m02;   // the a0 - 2 neighbour of step U: its code of step U - 2
-            uint32_t q = bx_max3(pff[U % FA], g2[U & 1], g4[U & 3]);
+            uint32_t q = bx_max3(pff[U % BX_FA], g2[U & 1], g4[U & 3]);
             if constexpr (U >= 32) q = bx_max3(q, hk[(U + 16) & 31], hk[U & 31]);
             else if constexpr (U >= 16) q = bx_max2(q, hk[(U + 16) & 31]);
             pre = bx_max3(q, g8[U & 7], y2);
         }
-#elif GM_BOX_XL
-        const uint32_t F = pf[T % BX_AHEAD];
-#if GM_BOX_WEXP & 4
-        const uint32_t y1 = hk[(T + 32 - BX_SR) & 31] & m01, y2 = hk[(T + 64 - 2 * BX_SR) & 31] & m02;
-        const uint32_t c0 = hb & mb0, c1 = hb ^ m01;
-#else
-        const uint32_t y1 = bx_dpp_shr<0x111>(hk[(T + 32 - BX_SR) & 31]) & m01;
-        const uint32_t y2 = bx_dpp_shr<0x112>(hk[(T + 64 - 2 * BX_SR) & 31]) & m02;
-        const uint32_t c0 = bx_dpp_shr<0x114>(hb) & mb0, c1 = bx_dpp_shr<0x118>(hb);
-#endif
-#if GM_BOX_WEXP & 2
-        const uint32_t c2 = hb & mb1, c3 = hb & mb2;
-#else
-        const uint32_t h2 = hk[(T + 32 - BX_S2) & 31];
-        const uint32_t c2 = bx_from16(h2), c3 = bx_from32(h2);
-#endif
-        uint32_t e = F;
-        if constexpr (T >= 32) e = bx_max3(e, hk[(T + 16) & 31], hk[T & 31]);
-        else if constexpr (T >= 16) e = bx_max2(e, hk[(T + 16) & 31]);
-        e = bx_max3(e, g2[T & 1], g4[T & 3]);
-        e = bx_max3(e, g8[T & 7], y2);
-        e = bx_max3(e, y1, c0);
-        e = bx_max3(e, c1, c2);
-        const uint32_t m = bx_max3(e, c3, g1);
-#else
-        const In cur = pf[T % BX_AHEAD];
-        const uint32_t c0 = bx_dpp_shr<0x111>(hb) & mb0, c1 = bx_dpp_shr<0x112>(hb) & mb1;
-        const uint32_t c2 = bx_dpp_shr<0x114>(hb) & mb2, c3 = bx_dpp_shr<0x118>(hb);
-        uint32_t e = bx_max3(cur.F, cur.Y1, cur.Y2);
-        if constexpr (T >= 32) e = bx_max3(e, hk[(T + 16) & 31], hk[T & 31]);
-        else if constexpr (T >= 16) e = bx_max2(e, hk[(T + 16) & 31]);
-        e = bx_max3(e, g2[T & 1], g4[T & 3]);
-        e = bx_max3(e, g8[T & 7], c0);
-        e = bx_max3(e, c1, c2);
-        // the last step's code of this lane: its (a1 - 1) child
-        const uint32_t m = bx_max3(e, c3, g1);
-#endif
         uint32_t c = bx_code2(m);
         if constexpr (peel) c = (uint32_t)(T - d) < 64u ? c : 0u;
         // the masks of the steps that will read c: byte (T + k) & 3 of the phase words
@@ -556,18 +430,12 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
         g2[T & 1] = bx_and_byte<(T + 2) & 3>(c, v12);
         g4[T & 3] = bx_and_byte<(T + 4) & 3>(c, v21[((T + 4) >> 2) & 3]);
         g8[T & 7] = bx_and_byte<(T + 8) & 3>(c, v22[((T + 8) >> 2) & 3]);
-        if (!(GM_BOX_WEXP & 1) || T == BX_STEPS - 1) s[idx] = c;
+        s[slot(TT, base)] = c;
         BX_LDS_ORDER();
-#if !GM_BOX_XL
-        // the row below made the code of step T + AHEAD at step T + AHEAD - SR = T - 1
-#endif
-#if GM_BOX_XL == 2
-        if constexpr (T + FA < BX_STEPS) pff[T % FA] = fetchf(BxT<T + FA>{});
-        if constexpr (T + BX_AHEAD < BX_STEPS) pf[T % BX_AHEAD] = fetchc(BxT<T + BX_AHEAD>{});
-#else
-        if constexpr (T + BX_AHEAD < BX_STEPS) pf[T % BX_AHEAD] = fetch(BxT<T + BX_AHEAD>{});
-#endif
-        if (!(GM_BOX_WEXP & 8)) __builtin_amdgcn_sched_barrier(0);   // no instruction crosses a step (a hoisted use would wait on the prefetch)
+        // the b2 / b3 neighbours of step T + S2 made their codes in this step's write
+        if constexpr (T + BX_FA < BX_STEPS) pff[T % BX_FA] = fetchf(BxT<T + BX_FA>{});
+        if constexpr (T + BX_S2 < BX_STEPS) pfc[T % BX_S2] = fetchc(BxT<T + BX_S2>{});
+        __builtin_amdgcn_sched_barrier(0);   // no instruction crosses a step (a hoisted use would wait on a prefetch)
     };
     bx_unroll(step, std::make_integer_sequence<int, BX_STEPS>{});
 }
@@ -632,12 +500,14 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
     for (int k = 0; k < 4; k++) s[BX_PITCH * lane + 64 + k] = 0;
     bx_u32x4 R[BX_NLOAD];
     BxGroup G = bx_group(boxes, nbox, g);
-    bx_issue<3>(table, G, lane, R);
+    bx_issue(table, G, lane, R);
 #if GM_BOX_TRACE
     unsigned long long tt[5], acc[4] = {0, 0, 0, 0}, ngr = 0, tbeg, rbeg;
     BX_STAMP(tbeg);
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(rbeg)::"memory");
 #endif
+    // (issuing the next group's loads earlier -- during the walk or before the store --
+    // measured slower: the 192 registers they hold spill, or they queue behind the store)
     for (;;) {
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));   // lane-derived addresses are recomputed per group, not held in registers
@@ -646,35 +516,22 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         BX_STAMP(tt[1]);
 #endif
-        if (!(GM_BOX_EXP & 8))
-            for (int rp = 0; rp < GM_BOX_REPF; rp++) bx_fold(s, G, ln, R);
+        if (!(GM_BOX_EXP & 8)) bx_fold(s, G, ln, R);
         else   // keep the loads live: one xor per row into the image
             for (int q = 0; q < BX_NLOAD; q++) s[ln + 64 * (q & 7)] ^= R[q][0] ^ R[q][3];
         const uint32_t gn = g + Kx;
         const bool more = gn < g1;
         BxGroup Gn = G;
         if (more) Gn = bx_group(boxes, nbox, gn);
-#if GM_BOX_PIPE == 1
-        if (more) bx_issue<3>(table, Gn, ln, R);   // every child row of the next group during this walk
-#elif GM_BOX_PIPE >= 2
-        if (more) bx_issue<1>(table, Gn, ln, R);   // its B rows during this walk, its A rows after it
-#endif
         BX_LDS_ORDER();
 #if GM_BOX_TRACE
         BX_STAMP(tt[2]);
 #endif
-        if (!(GM_BOX_EXP & 1))
-            for (int rp = 0; rp < GM_BOX_REPW; rp++) bx_walk(s, ln, L);
+        if (!(GM_BOX_EXP & 1)) bx_walk(s, ln, L);
 #if GM_BOX_TRACE
         BX_STAMP(tt[3]);
 #endif
-#if GM_BOX_PIPE == 2
-        if (more) bx_issue<2>(table, Gn, ln, R);
-#endif
         bx_store(table, G, s, ln);
-#if GM_BOX_PIPE == 3
-        if (more) bx_issue<2>(table, Gn, ln, R);   // A rows after the store
-#endif
         BX_LDS_ORDER();
 #if GM_BOX_TRACE
         BX_STAMP(tt[4]);
@@ -684,9 +541,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         if (!more) break;
         g = gn;
         G = Gn;
-#if GM_BOX_PIPE == 0
-        bx_issue<3>(table, G, lane, R);
-#endif
+        bx_issue(table, G, lane, R);
     }
 #if GM_BOX_TRACE
     unsigned long long tend, rend;
