@@ -165,7 +165,10 @@ __device__ __forceinline__ void bx_pairs(const bx_u32x4 &x0, const bx_u32x4 &x1,
 // Image: position (A, B), A = a0 + 4 p, at dword PITCH p + 16 a0 + B.  A pitch of 68, not
 // 64, puts the 16-B chunks that 16 lanes touch in the fold and the store (whole rows A,
 // one per lane) in distinct banks; the walk's dword accesses then see 2-way conflicts.
-constexpr int BX_PITCH = 68;
+#ifndef GM_BOX_PITCH
+#define GM_BOX_PITCH 68
+#endif
+constexpr int BX_PITCH = GM_BOX_PITCH;
 constexpr int BX_IMG = 64 * BX_PITCH;     // dwords
 constexpr int BX_PAD = 32;                // guard in front: the walk's (a0-1, a0-2) reads of row 0 at p = 0
 constexpr int BX_LDS = BX_PAD + BX_IMG + 64;   // + one dummy dword per lane for idle walk steps
