@@ -785,6 +785,8 @@ int dense_box_solve(Ctx *c, uint64_t root) {
     return GM_OK;
 }
 
+int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+
 int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
     DenseBox *d = c->dbox;
     *n = c->n_positions;
@@ -793,17 +795,24 @@ int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint6
         set_error("export buffer holds %llu, need %llu", (unsigned long long)cap, (unsigned long long)c->n_positions);
         return GM_E_CAP;
     }
-    std::vector<uint8_t> h(1ull << 32);
-    GM_HIP(hipMemcpy(h.data(), d->table, h.size(), hipMemcpyDeviceToHost));
-    uint64_t j = 0;
-    for (uint64_t k = 0; k < (1ull << 32); k++) {
-        bool in = true;
-        for (int i = 0; i < 8 && in; i++) in = ((k >> (4 * i)) & 15u) <= ((c->root >> (4 * i)) & 15u);
-        if (!in) continue;
+    // the root's box of keys in ascending order (heap 0 fastest)
+    uint32_t lim[8];
+    for (int i = 0; i < 8; i++) lim[i] = (uint32_t)((c->root >> (4 * i)) & 15u);
+    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint64_t j = 0; j < c->n_positions; j++) {
+        uint32_t k = 0;
+        for (int i = 0; i < 8; i++) k |= h[i] << (4 * i);
         keys[j] = k;
-        recs[j] = record_of_code(h[box_index_of_key((uint32_t)k)]);
-        j++;
+        for (int i = 0; i < 8; i++) {
+            if (h[i] < lim[i]) { h[i]++; break; }
+            h[i] = 0;
+        }
     }
+    if (c->n_positions <= (1ull << 26)) return dense_box_query(c, keys, recs, c->n_positions);
+    // large boxes: one copy of the table, decoded on the host
+    std::vector<uint8_t> tab(1ull << 32);
+    GM_HIP(hipMemcpy(tab.data(), d->table, tab.size(), hipMemcpyDeviceToHost));
+    for (uint64_t j = 0; j < c->n_positions; j++) recs[j] = record_of_code(tab[box_index_of_key((uint32_t)keys[j])]);
     return GM_OK;
 }
 
