@@ -169,6 +169,8 @@ __device__ __forceinline__ void bx_pairs(const bx_u32x4 &x0, const bx_u32x4 &x1,
 #define GM_BOX_PITCH 68
 #endif
 constexpr int BX_PITCH = GM_BOX_PITCH;
+// rows stay 16-B aligned for ds_read/write_b128 (pitch 74, 8-B aligned rows: 5.3 ms, not 3.3)
+static_assert(BX_PITCH % 4 == 0, "16-B aligned image rows");
 constexpr int BX_IMG = 64 * BX_PITCH;     // dwords
 constexpr int BX_PAD = 32;                // guard in front: the walk's (a0-1, a0-2) reads of row 0 at p = 0
 constexpr int BX_LDS = BX_PAD + BX_IMG + 64;   // + one dummy dword per lane for idle walk steps
