@@ -300,12 +300,13 @@ def _box_tiers(root):
     return sum(((root >> (4 * j)) & 15) >> (2 if j < 4 else 1) for j in range(8)) + 1
 
 
-@pytest.mark.parametrize("root", [0x00000003, 0x000F0FFF, 0x12345678, 0xFFFF0000, 0x0000FFFF, 0x9ABCDEF1, 0x7F7F7F7F])
+@pytest.mark.parametrize("root", [0x00000003, 0x000F0FFF, 0x12345678, 0xFFFF0000, 0x0000FFFF, 0x9ABCDEF1, 0x7F7F7F7F, 0x0FFFFFFF])
 def test_subtract_8_heaps_box_engine_custom_roots(oracle, root):
     """The box engine (GM_OPT_SUB_INTERLEAVE 20, the 8-heap default, csrc/dense_box.hip)
     launches one box-tier per sum of the root box's coordinates and equals the block
     engine on every root: same count, root record and digest; for roots below 16^7 the
-    exported records equal the 7-heap C-oracle table."""
+    exported records equal the 7-heap C-oracle table (0x0FFFFFFF: 2^28 positions, the
+    export's table-copy path; smaller boxes go through the device query)."""
     a, n1, r1 = _solve(SUB, (8,), root=root, timing=1, sub_interleave=20)
     assert a.stats()["kernel_launches"] == _box_tiers(root)
     da = a.digest()
