@@ -67,9 +67,10 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 #ifndef GM_BOX_EXP
 #define GM_BOX_EXP 0
 #endif
-// wave priority per phase (s_setprio): the walk's dependent chain first, then the fold,
-// the store and the load issue last (the two waves of a SIMD otherwise share its issue
-// slots by age: 3.57 ms with none, 3.31 with the walk raised, 3.28 with walk 2 / fold 1)
+// wave priority per phase (s_setprio): the load issue first (48 instructions), then the
+// walk's dependent chain, then the fold, the store last.  The two waves of a SIMD
+// otherwise share its issue slots by age: 3.57 ms with none, 3.31 with the walk raised,
+// 3.28 with walk 2 / fold 1, ~2 % less again with the load issue at 3.
 #ifndef GM_BOX_PRIO_W
 #define GM_BOX_PRIO_W 2
 #endif
@@ -78,6 +79,9 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 #endif
 #ifndef GM_BOX_PRIO_S
 #define GM_BOX_PRIO_S 0
+#endif
+#ifndef GM_BOX_PRIO_I
+#define GM_BOX_PRIO_I 3        // issuing the next group's child loads
 #endif
 
 // ---------------------------------------------------------------------------
@@ -561,6 +565,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         if (!more) break;
         g = gn;
         G = Gn;
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_I);   // the next group's loads out first
         bx_issue(table, G, lane, R);
     }
 #if GM_BOX_TRACE
