@@ -211,6 +211,34 @@ def rank_digest_check(heaps, world, root, rank_digests, batch, slots, symmetry, 
     return {"ranks": out, "wrong_ranks": [x["rank"] for x in out if not x["ok"]]}
 
 
+def box_rank_digest_check(world, root, rank_digests):
+    """N > 1, box engine: each rank's gm_digest covers exactly the boxes it owns
+    (csrc/dense_box.hip, gm_box_plan GM_BOXPLAN_OWN); compare every one with the C
+    oracle's digest over the same boxes (oracle_dense_digest_boxes), so a rank whose part
+    of the table is wrong is named.  Rank 0 only; ~10 s of host work."""
+    L = _oracle()
+    if L is None:
+        return None
+    import numpy as np
+    from gamesmanmpi_amd import _lib
+    L.oracle_dense_digest_boxes.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                            ctypes.POINTER(ctypes.c_uint64)]
+    rec = np.empty(1 << 32, dtype=np.uint16)
+    if L.oracle_subtract_dense_mt(8, rec.ctypes.data, 0) != 0:
+        return None
+    out = []
+    for r in range(world):
+        own = np.ascontiguousarray(_lib.box_plan(world, r, _lib.BOXPLAN_OWN, root), dtype=np.uint32)
+        d, c = ctypes.c_uint64(), ctypes.c_uint64()
+        L.oracle_dense_digest_boxes(rec.ctypes.data, ctypes.c_uint64(root), own.ctypes.data,
+                                    ctypes.c_uint64(len(own)), 0, ctypes.byref(d), ctypes.byref(c))
+        got_d, got_n = rank_digests[r]
+        out.append({"rank": r, "boxes_owned": int(len(own)), "positions": got_n,
+                    "ok": (got_d, got_n) == (d.value, c.value)})
+    return {"ranks": out, "wrong_ranks": [x["rank"] for x in out if not x["ok"]]}
+
+
 TOOT_6X4_PER_PLY = [1, 12, 114, 748, 4266, 19692, 81140, 285708, 928196, 2665424, 7098172, 17010952,
                     37792450, 64636776, 100084356, 136321692, 169785424, 180777508, 172831136,
                     135153280, 91440950, 45953432, 19196602, 4537828, 606968]   # SURVEY Appendix D
@@ -402,6 +430,9 @@ def main():
     ap.add_argument("--dist-owner", type=int, default=0, choices=(0, 1),
                     help="N>1: block owner, 0 = split heaps in halves (default), 1 = tier-balanced (measured "
                          "slower per rank on one GPU, DESIGN.md §5)")
+    ap.add_argument("--block-engine", action="store_true",
+                    help="8 heaps: run the block engine (GM_OPT_SUB_INTERLEAVE 10) instead of the box engine, "
+                         "sharded with halo exchanges at N > 1 (the round-3 multi-GPU path, for comparison)")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     ap.add_argument("--watchdog", type=float, default=None,
@@ -443,6 +474,11 @@ def main():
     from gamesmanmpi_amd import Context, _lib
 
     ctx = Context(_lib.GAME_SUBTRACT, (args.heaps,), device=local)
+    # the box engine (csrc/dense_box.hip) at 8 heaps: one GPU, and at N > 1 each rank
+    # solving its orbit share of the boxes alone (no exchange); else the block engine
+    box = args.heaps == 8 and not args.block_engine
+    if not box:
+        ctx.set_option(_lib.OPT_SUB_INTERLEAVE, 10)
     if world > 1:
         uid = [None]
         if rank == 0:
@@ -474,7 +510,7 @@ def main():
             dist.barrier()
 
     autotune = None
-    if world > 1 and args.dist_batch is None:
+    if world > 1 and args.dist_batch is None and not box:
         # untimed: the halo batch trades the upper ranks' lag (B - 1 tiers) against the
         # number of RCCL messages; every rank measures the same candidates and takes
         # the same argmin of the max-over-ranks time, so all ranks keep one schedule
@@ -534,9 +570,10 @@ def main():
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         if rank == 0 and args.virtual_ranks == 1:
-            rank_parity = rank_digest_check(args.heaps, world, root,
-                                            [(int(a[0].item()) & ((1 << 64) - 1), int(a[1].item())) for a in allr],
-                                            args.dist_batch, args.dist_slots, args.dist_symmetry, args.dist_owner)
+            got = [(int(a[0].item()) & ((1 << 64) - 1), int(a[1].item())) for a in allr]
+            rank_parity = (box_rank_digest_check(world, root, got) if box else
+                           rank_digest_check(args.heaps, world, root, got, args.dist_batch, args.dist_slots,
+                                             args.dist_symmetry, args.dist_owner))
         barrier()
     watchdog.cancel()
     g = 0
@@ -561,7 +598,11 @@ def main():
     kernel_s_per_solve = kernel_ms / 1e3 / max(1, args.steps)
     avg_launch_s = (kernel_ms / 1e3) / max(1, launches)
     # algorithmic (compulsory) bytes per launch: 3 B x the positions this rank's launches solve
+    # (box engine at N > 1: its boxes, tie boxes included -- they are computed here too)
+    rstats = ctx.rank_stats() if box else []
     own_positions = positions if world == 1 else positions / world
+    if box and (world > 1 or args.virtual_ranks > 1) and rstats:
+        own_positions = rstats[0]["boxes"] * 4096.0
     compulsory_per_launch = COMPULSORY_BYTES_PER_POSITION * own_positions / launches_per_solve
     achieved = compulsory_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
     traffic_gbs = (traffic_launch / avg_launch_s / 1e9) if (traffic_launch and avg_launch_s > 0) else None
@@ -579,15 +620,19 @@ def main():
         "dtype": "u8",
         "data": "synthetic (the game itself: every position of the 2^32-state subtraction game)",
         "config": {"workload": "subtraction game, %d heaps x 4 bits, root %#x (config 5)" % (args.heaps, root),
-                   "positions": positions, "parallelism": "1 GPU" if world == 1 else "block-sharded x%d" % world},
+                   "positions": positions,
+                   "parallelism": "1 GPU" if world == 1 else ("box-orbit-sharded x%d" if box else "block-sharded x%d")
+                   % world},
         "parity": parity,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": traffic_launch,
                      "traffic_gbs": traffic_gbs,
                      "traffic_frac": (traffic_gbs / HBM_PEAK_GBS) if traffic_gbs else None,
-                     "kernel": ("box_tier_kernel (csrc/dense_box.hip: 4x4x4x4x2x2x2x2 boxes, one launch per box-tier)"
-                                if (world == 1 and args.virtual_ranks == 1 and args.heaps == 8) else
+                     "kernel": ("box_tier_kernel<%s> (csrc/dense_box.hip: 4x4x4x4x2x2x2x2 boxes, one launch per "
+                                "box-tier%s)" % (("false", "") if (world == 1 and args.virtual_ranks == 1) else
+                                                 ("true", "; this rank's orbit share of the boxes"))
+                                if box else
                                 "sub_tier_kernel_wk<%d> (tiers of >= 4096 blocks), sub_tier_kernel_b4<%d> (smaller)"
                                 % (args.heaps - 3, args.heaps - 3)),
                      "algo_bytes_per_position": COMPULSORY_BYTES_PER_POSITION,
@@ -604,10 +649,16 @@ def main():
                      "measured_copy_gbs": copy_gbs,
                      "timing": ("HIP events bracketing each solve's tier-launch graph replay on the launch "
                                 "stream; avg launch = span / launches (includes in-graph gaps)"
-                                if world == 1 else
+                                if (world == 1 or box) else
                                 "HIP events around this rank's whole sharded solve (includes halo waits)")},
         "exchanged_bytes_per_step_rank0": st["exchanged_bytes"],
         "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
+            "scheme": ("box engine: each rank computes one member of every orbit of heap permutations "
+                       "<rotate heaps 0-3> x <swap heaps 4/5 and 6/7> and reads the child boxes it does not "
+                       "compute through those permutations; no exchange (DESIGN.md §5)"),
+            "boxes_per_rank": rstats[0]["boxes"] if rstats else None,
+            "tie_boxes_per_rank": rstats[0]["ties"] if rstats else None,
+            "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank} if box else {
             "halo_batch_tiers": args.dist_batch, "halo_batch_autotune_ms": autotune, "halo_slots": args.dist_slots,
             "halo_symmetric_fill": bool(args.dist_symmetry),
             "block_owner": ("split heaps in halves", "tier-balanced")[args.dist_owner],

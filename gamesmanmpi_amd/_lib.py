@@ -24,6 +24,7 @@ OPT_DIST_OWNER = 13
 OPT_SYMMETRY = 14
 BUF_DENSE_TABLE = 1
 PLAN_SHAPE, PLAN_OWN, PLAN_FILL, PLAN_SEND, PLAN_RECV, PLAN_OPS, PLAN_XDEST = 0, 1, 2, 3, 4, 5, 6
+BOXPLAN_SHAPE, BOXPLAN_BOXES, BOXPLAN_FILLS, BOXPLAN_TIER_OFF, BOXPLAN_OWN, BOXPLAN_MAP = 0, 1, 2, 3, 4, 5
 REC_UNSOLVED = 0xFFFF
 
 ERRORS = {
@@ -35,7 +36,8 @@ ERRORS = {
 SYMBOLS = ("gm_version", "gm_last_error", "gm_device_count", "gm_open", "gm_set_stream",
            "gm_set_option", "gm_pack_initial", "gm_expand_host", "gm_comm_unique_id",
            "gm_set_comm", "gm_solve", "gm_solve_graph", "gm_export", "gm_query", "gm_digest", "gm_stats",
-           "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_dist_plan", "gm_close")
+           "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_dist_plan", "gm_box_plan",
+           "gm_rank_stats", "gm_close")
 
 
 class GMError(RuntimeError):
@@ -105,6 +107,8 @@ def lib():
         "gm_dense_table": (ctypes.c_int, [vp, P(vp), P(u64)]),
         "gm_dist_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                         vp, u64, P(u64), vp, u64, P(u64)]),
+        "gm_box_plan": (ctypes.c_int, [u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, u64, P(u64)]),
+        "gm_rank_stats": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, P(ctypes.c_int)]),
         "gm_close": (None, [vp]),
     }
     for name, (res, args) in sig.items():
@@ -135,3 +139,14 @@ def dist_plan(heaps, world, rank, what, axis=0, batch=4, slots=4, symmetry=1, ow
     check(L.gm_dist_plan(heaps, world, rank, opts, what, axis, off.ctypes.data, len(off), ctypes.byref(n_off),
                          data.ctypes.data, len(data), ctypes.byref(n_data)))
     return off[:n_off.value], data[:n_data.value]
+
+
+def box_plan(world, rank, what, root=0xFFFFFFFF):
+    """gm_box_plan -> uint32 numpy array (host only, no GPU): the sharded box solve's plan."""
+    import numpy as np
+    L = lib()
+    n = ctypes.c_uint64()
+    check(L.gm_box_plan(root, world, rank, what, None, 0, ctypes.byref(n)))
+    out = np.zeros(max(1, n.value), dtype=np.uint32)
+    check(L.gm_box_plan(root, world, rank, what, out.ctypes.data, len(out), ctypes.byref(n)))
+    return out[:n.value]

@@ -119,6 +119,35 @@ GM_HD int box_coord(uint32_t box, int dim) {
 GM_HD uint32_t box_unit(int dim) { return dim < 4 ? 1u << (2 * dim) : 1u << (8 + 3 * (dim - 4)); }
 
 // ---------------------------------------------------------------------------
+// Heap permutations of the sharded solve.  The game is the same on every
+// heap, so a permutation of heaps maps positions to positions of equal value; the ones
+// that map boxes to boxes permute A heaps among themselves and B heaps among themselves.
+// The sharded solve uses the group H = <r> x <t>: r rotates the A heaps (heap i -> heap
+// i + 1 mod 4), t swaps heaps 4 <-> 5 and 6 <-> 7.  Element code = k | e << 2 for r^k t^e.
+// On a box id: the A coordinates (bits 0-7, 2 bits per heap) rotate left by 2k bits; t
+// swaps the 3-bit B coordinates of heaps 4/5 (bits 8-10 / 11-13) and 6/7 (14-16 / 17-19).
+GM_HD uint32_t bsym_rot8(uint32_t f, uint32_t k) { return ((f | (f << 8)) >> (8 - 2 * k)) & 0xFFu; }
+GM_HD uint32_t bsym_tau_box(uint32_t b) {
+    const uint32_t x = ((b >> 3) ^ b) & 0x1C700u;
+    return b ^ x ^ (x << 3);
+}
+GM_HD uint32_t bsym_box(uint32_t code, uint32_t b) {
+    b = (b & ~0xFFu) | bsym_rot8(b & 0xFFu, code & 3u);
+    return (code & 4u) ? bsym_tau_box(b) : b;
+}
+// on a key (heap i at bits 4i): the low four nibbles rotate left by 4k bits; t swaps
+// nibbles 4/5 and 6/7
+GM_HD uint32_t bsym_key(uint32_t code, uint32_t key) {
+    const uint32_t k = code & 3u, lo = key & 0xFFFFu;
+    key = (key & 0xFFFF0000u) | (((lo | (lo << 16)) >> (16 - 4 * k)) & 0xFFFFu);
+    if (code & 4u) {
+        const uint32_t x = ((key >> 4) ^ key) & 0x0F0F0000u;
+        key ^= x ^ (x << 4);
+    }
+    return key;
+}
+
+// ---------------------------------------------------------------------------
 // device helpers
 __device__ __forceinline__ uint32_t bx_max2(uint32_t a, uint32_t b) {
 #if GM_BOX_MAX3
@@ -183,24 +212,46 @@ constexpr int BX_NLOAD = 48;              // 16-B child rows per lane per group
 
 struct BxGroup {
     uint32_t box[2];
+    uint32_t fill[2];   // sharded solve: per child direction d, 3 bits at 3 d: the code of the
+                        // permutation h whose image h(C) of the child box C this rank computes
     bool valid[2];
 };
 
-__device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, uint32_t nbox, uint32_t g) {
+template <bool SHARD>
+__device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, const uint32_t *__restrict__ fills,
+                                            uint32_t nbox, uint32_t g) {
     BxGroup G;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         const uint32_t i = 2 * g + k;
         G.valid[k] = i < nbox;
         G.box[k] = G.valid[k] ? boxes[i] : 0u;
+        G.fill[k] = (SHARD && G.valid[k]) ? fills[i] : 0u;
     }
     return G;
+}
+
+// Sharded solve: a B child read from the box t(C) is the child's row with B bits b0 <-> b1
+// and b2 <-> b3 swapped: byte e of dword q of the child row is byte sw(e) of dword sw(q) of
+// the loaded row, sw exchanging 1 and 2.
+__device__ __forceinline__ bx_u32x4 bx_tau_row(const bx_u32x4 &x) {
+    constexpr uint32_t S = 0x03010200u;
+    return bx_u32x4{__builtin_amdgcn_perm(x[0], x[0], S), __builtin_amdgcn_perm(x[2], x[2], S),
+                    __builtin_amdgcn_perm(x[1], x[1], S), __builtin_amdgcn_perm(x[3], x[3], S)};
 }
 
 // Every child row of a group, in flight at once: R[0..31] the B children of target rows
 // m = lane + 64 i (R[8 i + 4 k + j]: box k, heap 4 + j), R[32..47] the A children's top
 // layers (R[32 + 4 i + 2 k + v]: heap i, box k, layer 3 - v) of the rows a_i in {2, 3}
 // whose other coordinates are the lane.
+//
+// Sharded solve (SHARD): a child box C this rank does not compute is read from its image
+// S = h(C) under the permutation h of the group's fill code, which this rank computed in
+// the same box-tier.  The plan (box_plan) only uses t for B children and r^k for A
+// children: a B child's rows are then S's rows, byte-permuted in bx_fold (bx_tau_row);
+// an A child's row A is S's row rotl8(A, 2k) (the A digits move with the heaps), an
+// address change only.
+template <bool SHARD>
 __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
                                          bx_u32x4 (&R)[BX_NLOAD]) {
     const __amdgpu_buffer_rsrc_t rt =
@@ -213,7 +264,10 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const bool ok = G.valid[k] && box_coord(G.box[k], 4 + j) >= 1;
-                const uint32_t soff = ok ? (G.box[k] - box_unit(4 + j)) << 12 : 0u;
+                uint32_t src = G.box[k] - box_unit(4 + j);
+                if constexpr (SHARD)
+                    if ((G.fill[k] >> (3 * (4 + j))) & 4u) src = bsym_tau_box(src);
+                const uint32_t soff = ok ? src << 12 : 0u;
                 const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
 #pragma unroll
                 for (int i = 0; i < 4; i++)
@@ -228,13 +282,28 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
 #pragma unroll
             for (int k = 0; k < 2; k++) {
                 const bool ok = G.valid[k] && box_coord(G.box[k], i) >= 1;
-                const uint32_t soff = ok ? (G.box[k] - box_unit(i)) << 12 : 0u;
                 const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
+                if constexpr (!SHARD) {
+                    const uint32_t soff = ok ? (G.box[k] - box_unit(i)) << 12 : 0u;
 #pragma unroll
-                for (int v = 0; v < 2; v++) {
-                    const uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
-                    R[32 + 4 * i + 2 * k + v] =
-                        __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, 0));
+                    for (int v = 0; v < 2; v++) {
+                        const uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
+                        R[32 + 4 * i + 2 * k + v] =
+                            __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, 0));
+                    }
+                } else {
+                    // row rotl8(A, 2 rot): the lane's digits rotated (VGPR), digit i's layer
+                    // 3 - v moved to digit i + rot (uniform, in the scalar offset)
+                    const uint32_t rot = (G.fill[k] >> (3 * i)) & 3u;
+                    const uint32_t src = bsym_box(rot, G.box[k] - box_unit(i));
+                    const uint32_t soff = ok ? src << 12 : 0u;
+                    const uint32_t L = lo | hi;
+                    const uint32_t voff = __builtin_amdgcn_ubfe(L | (L << 8), 8u - 2u * rot, 8u) << 4;
+                    const uint32_t sh = 2u * ((i + rot) & 3u);
+#pragma unroll
+                    for (int v = 0; v < 2; v++)
+                        R[32 + 4 * i + 2 * k + v] = __builtin_bit_cast(
+                            bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff + ((3u - v) << (sh + 4u)), 0));
                 }
             }
         }
@@ -242,7 +311,17 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
 }
 
 // fold: the image's slot of every position gets the max of its children outside the box
-__device__ __forceinline__ void bx_fold(uint32_t *s, const BxGroup &G, uint32_t lane, const bx_u32x4 (&R)[BX_NLOAD]) {
+template <bool SHARD>
+__device__ __forceinline__ void bx_fold(uint32_t *s, const BxGroup &G, uint32_t lane, bx_u32x4 (&R)[BX_NLOAD]) {
+    if constexpr (SHARD) {   // B children read from t(C): back to C's byte order (uniform branches)
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if ((G.fill[k] >> (3 * (4 + j))) & 4u)
+#pragma unroll
+                    for (int i = 0; i < 4; i++) R[8 * i + 4 * k + j] = bx_tau_row(R[8 * i + 4 * k + j]);
+    }
     // B children: row m of the child box below along heap 4 + j; a position with b_j = 0
     // also takes b | e_j of that row (its child two below)
 #pragma unroll
@@ -501,8 +580,12 @@ __device__ unsigned long long bx_trace_acc[8];
 // One launch per box-tier.  Workgroup w runs on XCD w % 8 and takes groups (box pairs)
 // of that XCD's contiguous run of the tier list (boxes sorted along a Hilbert walk), the
 // workgroups of an XCD side by side, so neighbouring groups share child boxes in its L2.
+// SHARD: one rank of the sharded solve: its own box list, with a fill code
+// per box saying where each child box is read from.
+template <bool SHARD>
 __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__restrict__ table,
                                                                      const uint32_t *__restrict__ boxes,
+                                                                     const uint32_t *__restrict__ fills,
                                                                      uint32_t nbox) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[BX_LDS];
     uint32_t *s = lds + BX_PAD;
@@ -520,8 +603,8 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 #pragma unroll
     for (int k = 0; k < 4; k++) s[BX_PITCH * lane + 64 + k] = 0;
     bx_u32x4 R[BX_NLOAD];
-    BxGroup G = bx_group(boxes, nbox, g);
-    bx_issue(table, G, lane, R);
+    BxGroup G = bx_group<SHARD>(boxes, fills, nbox, g);
+    bx_issue<SHARD>(table, G, lane, R);
 #if GM_BOX_TRACE
     unsigned long long tt[5], acc[4] = {0, 0, 0, 0}, ngr = 0, tbeg, rbeg;
     BX_STAMP(tbeg);
@@ -538,13 +621,13 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         BX_STAMP(tt[1]);
 #endif
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_F);
-        if (!(GM_BOX_EXP & 8)) bx_fold(s, G, ln, R);
+        if (!(GM_BOX_EXP & 8)) bx_fold<SHARD>(s, G, ln, R);
         else   // keep the loads live: one xor per row into the image
             for (int q = 0; q < BX_NLOAD; q++) s[ln + 64 * (q & 7)] ^= R[q][0] ^ R[q][3];
         const uint32_t gn = g + Kx;
         const bool more = gn < g1;
         BxGroup Gn = G;
-        if (more) Gn = bx_group(boxes, nbox, gn);
+        if (more) Gn = bx_group<SHARD>(boxes, fills, nbox, gn);
         BX_LDS_ORDER();
 #if GM_BOX_TRACE
         BX_STAMP(tt[2]);
@@ -566,7 +649,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         g = gn;
         G = Gn;
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_I);   // the next group's loads out first
-        bx_issue(table, G, lane, R);
+        bx_issue<SHARD>(table, G, lane, R);
     }
 #if GM_BOX_TRACE
     unsigned long long tend, rend;
@@ -582,15 +665,19 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 #endif
 }
 
-__global__ void box_digest_kernel(const uint8_t *__restrict__ table, uint64_t root, unsigned long long *acc) {
+
+// digest of the positions of a box list that lie in the root's region
+__global__ void box_digest_kernel(const uint8_t *__restrict__ table, const uint32_t *__restrict__ boxes, uint64_t nbox,
+                                  uint64_t root, unsigned long long *acc) {
     uint64_t sum = 0, cnt = 0;
-    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < (1ull << 32);
+    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < (nbox << 12);
          x += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t k = box_key_of_index((uint32_t)x);
+        const uint32_t idx = (boxes[x >> 12] << 12) | (uint32_t)(x & 4095u);
+        const uint32_t k = box_key_of_index(idx);
         bool in = true;
         for (int j = 0; j < 8; j++) in &= ((k >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
         if (!in) continue;
-        sum += digest_term(k, record_of_code(table[x]));
+        sum += digest_term(k, record_of_code(table[idx]));
         cnt++;
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -603,26 +690,25 @@ __global__ void box_digest_kernel(const uint8_t *__restrict__ table, uint64_t ro
     }
 }
 
-__global__ void box_query_kernel(const uint8_t *__restrict__ table, const uint64_t *__restrict__ keys,
-                                 uint16_t *__restrict__ out, uint64_t n) {
+// Records of keys: REC_UNSOLVED outside the root's region (a key with a nibble above the
+// root's, whose slot the solve never wrote).  Sharded: `map` gives per box id the
+// permutation h whose image of the box this rank computed; the key's record is then its
+// image's (the game is symmetric under heap permutations).
+__global__ void box_query_kernel(const uint8_t *__restrict__ table, const uint8_t *__restrict__ map, uint64_t root,
+                                 const uint64_t *__restrict__ keys, uint16_t *__restrict__ out, uint64_t n) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i < n) out[i] = keys[i] < (1ull << 32) ? record_of_code(table[box_index_of_key((uint32_t)keys[i])]) : REC_UNSOLVED;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    bool in = k < (1ull << 32);
+    for (int j = 0; j < 8 && in; j++) in = ((k >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
+    if (!in) { out[i] = REC_UNSOLVED; return; }
+    uint32_t key = (uint32_t)k;
+    if (map) key = bsym_key(map[box_index_of_key(key) >> 12], key);
+    out[i] = record_of_code(table[box_index_of_key(key)]);
 }
 
 // ---------------------------------------------------------------------------
 // host
-struct DenseBox {
-    uint8_t *table = nullptr;
-    bool owned = false;
-    uint32_t root_hi = 0;                 // the root's box coordinates (box id form)
-    uint32_t *d_boxes = nullptr;          // the root region's boxes, sorted by (tier, Hilbert)
-    std::vector<uint32_t> tier_off;
-    int grid_cap = 2048;
-    uint64_t *d_acc = nullptr;
-    hipGraphExec_t graph = nullptr;
-    hipStream_t graph_stream = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-};
 
 // Hilbert index (Skilling's transpose form) of the first 7 box coordinates, 3 bits each
 static uint64_t box_hilbert(uint32_t box) {
@@ -646,64 +732,235 @@ static uint64_t box_hilbert(uint32_t box) {
     return hv;
 }
 
-static int box_prepare(Ctx *c, DenseBox *d, uint64_t root) {
-    d->root_hi = box_index_of_key((uint32_t)root) >> 12;
+// The order whose least orbit member is the orbit's representative: B coordinates first
+// (c4, c5, c6, c7, c0, c1, c2, c3), 3 bits each.  With it every fill is "pure" -- a B child
+// needs only t, an A child only a rotation -- which the kernel relies on (box_plan checks).
+static uint32_t bsym_ord(uint32_t b) {
+    uint32_t o = 0;
+    for (int n = 0; n < 8; n++) o = (o << 3) | (uint32_t)box_coord(b, n < 4 ? 4 + n : n - 4);
+    return o;
+}
+
+// The plan of one rank of a `world`-rank sharded box solve (host only, no HIP call).
+//
+// Partition.  H = <r^(4/m)> x <t> with |H| = 2m the largest power of two <= min(world, 8),
+// cut down to the permutations that fix the root's region (its stabiliser H').  Rank r
+// takes the element g = H'[r mod |H'|] and computes R_r = g^-1(F), F = the boxes that are
+// the least member (bsym_ord) of their H'-orbit: R_r holds exactly one member of every
+// orbit, and every R_r is a heap permutation of F, so all ranks have the same number of
+// boxes in every box-tier.  A box fixed by some h != id (a "tie") is in several R_r and
+// computed by each of them; it is OWNED (digest, export) by the first.  A child box C of a
+// box of R_r is either in R_r or some image h(C), h in H', is -- computed by this rank in
+// the same box-tier (h keeps the coordinate sum) -- so a rank never needs another rank's
+// values: no exchange at all.  The kernel reads such a child through h (fill codes).
+struct BoxPlan {
+    int nsym = 1;                                  // |H'|
+    uint32_t g = 0;                                // this rank's element
+    std::vector<uint32_t> boxes, fills, tier_off;  // computed boxes by (box-tier, Hilbert), fill codes
+    std::vector<uint32_t> own;                     // owned boxes, ascending
+    std::vector<uint8_t> map;                      // 2^20: per box of the region, h with h(box) in R_r
+    uint64_t ties = 0;                             // computed boxes also computed by another rank
+};
+
+static int box_plan(uint32_t root_hi, int world, int rank, bool want_map, BoxPlan *p) {
+    if (world < 1 || rank < 0 || rank >= world) { set_error("bad rank %d of %d", rank, world); return GM_E_ARG; }
+    int hs = 1;
+    while (hs * 2 <= std::min(world, 8)) hs *= 2;
+    static const uint32_t Hfull[4][8] = {{0}, {0, 4}, {0, 4, 2, 6}, {0, 4, 1, 5, 2, 6, 3, 7}};
+    const uint32_t *H = Hfull[hs == 1 ? 0 : hs == 2 ? 1 : hs == 4 ? 2 : 3];
+    std::vector<uint32_t> Hs;
+    for (int e = 0; e < hs; e++)
+        if (bsym_box(H[e], root_hi) == root_hi) Hs.push_back(H[e]);
+    const int n = (int)Hs.size();
+    p->nsym = n;
+    p->g = Hs[rank % n];
     int lim[8], tmax = 0;
-    for (int i = 0; i < 8; i++) { lim[i] = box_coord(d->root_hi, i); tmax += lim[i]; }
-    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> tiers(tmax + 1);
-    for (uint32_t box = 0; box < (1u << 20); box++) {
-        int t = 0;
-        bool in = true;
-        for (int i = 0; i < 8 && in; i++) {
-            const int cc = box_coord(box, i);
-            in = cc <= lim[i];
-            t += cc;
+    for (int i = 0; i < 8; i++) { lim[i] = box_coord(root_hi, i); tmax += lim[i]; }
+    auto in_region = [&](uint32_t b) {
+        for (int i = 0; i < 8; i++)
+            if (box_coord(b, i) > lim[i]) return false;
+        return true;
+    };
+    // R membership of every box of the region, and its owner element
+    std::vector<uint8_t> inR(1u << 20, 0);
+    std::vector<uint32_t> region;
+    for (uint32_t b = 0; b < (1u << 20); b++) {
+        if (!in_region(b)) continue;
+        region.push_back(b);
+        uint32_t mo = 0xFFFFFFFFu, og = 0, first = 0;
+        bool any = false;
+        for (int e = 0; e < n; e++) {
+            const uint32_t o = bsym_ord(bsym_box(Hs[e], b));
+            if (o < mo) { mo = o; }
         }
-        if (in) tiers[t].push_back({box_hilbert(box), box});
+        for (int e = 0; e < n; e++)
+            if (bsym_ord(bsym_box(Hs[e], b)) == mo) {
+                if (!any) first = (uint32_t)e;
+                any = true;
+                og++;
+            }
+        const bool mine = bsym_ord(bsym_box(p->g, b)) == mo;
+        inR[b] = mine ? (uint8_t)(1 + (rank < n && first == (uint32_t)rank)) : 0;   // 2 = owned
+        if (mine && og > 1) p->ties++;
     }
-    std::vector<uint32_t> order;
-    d->tier_off.assign(1, 0);
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> tiers(tmax + 1);
+    std::vector<std::vector<uint32_t>> tfill(tmax + 1);
+    p->own.clear();
+    for (uint32_t b : region) {
+        if (!inR[b]) continue;
+        if (inR[b] == 2) p->own.push_back(b);
+        int t = 0;
+        for (int i = 0; i < 8; i++) t += box_coord(b, i);
+        tiers[t].push_back({box_hilbert(b), b});
+    }
+    auto fill_of = [&](uint32_t b, uint32_t *code) {
+        uint32_t f = 0;
+        for (int d = 0; d < 8; d++) {
+            if (box_coord(b, d) < 1) continue;
+            const uint32_t cb = b - box_unit(d);
+            if (inR[cb]) continue;
+            bool found = false;
+            for (int e = 1; e < n && !found; e++) {
+                const uint32_t h = Hs[e];
+                const bool pure = d < 4 ? !(h & 4u) : !(h & 3u);
+                if (pure && inR[bsym_box(h, cb)]) { f |= h << (3 * d); found = true; }
+            }
+            if (!found) return false;
+        }
+        *code = f;
+        return true;
+    };
+    p->boxes.clear();
+    p->fills.clear();
+    p->tier_off.assign(1, 0);
     for (auto &tv : tiers) {
         std::sort(tv.begin(), tv.end());
-        for (auto &e : tv) order.push_back(e.second);
-        d->tier_off.push_back((uint32_t)order.size());
+        for (auto &e : tv) {
+            uint32_t f = 0;
+            if (!fill_of(e.second, &f)) {
+                set_error("box plan: no heap permutation in the kernel's form reads a child of box %#x (rank %d of %d)",
+                          e.second, rank, world);
+                return GM_E_STATE;
+            }
+            p->boxes.push_back(e.second);
+            p->fills.push_back(f);
+        }
+        p->tier_off.push_back((uint32_t)p->boxes.size());
     }
-    GM_HIP(hipMalloc(&d->d_boxes, order.size() * sizeof(uint32_t)));
-    GM_HIP(hipMemcpy(d->d_boxes, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    p->map.clear();
+    if (want_map && n > 1) {
+        p->map.assign(1u << 20, 0xFF);
+        for (uint32_t b : region)
+            for (int e = 0; e < n; e++)
+                if (inR[bsym_box(Hs[e], b)]) { p->map[b] = (uint8_t)Hs[e]; break; }
+    }
+    return GM_OK;
+}
+
+struct BoxRank {
+    int rank = 0;
+    uint8_t *table = nullptr;
+    bool owned = false;
+    uint32_t *d_boxes = nullptr, *d_fills = nullptr, *d_own = nullptr;
+    uint8_t *d_map = nullptr;
+    std::vector<uint32_t> tier_off;
+    std::vector<uint32_t> own;        // host copy (export)
+    uint64_t n_boxes = 0, ties = 0;
+    hipGraphExec_t graph = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    float kernel_ms = 0;
+};
+
+struct DenseBox {
+    uint32_t root_hi = 0;
+    int world = 1;                    // ranks of the solve (one per process, or virtual on this GPU)
+    int nsym = 1;                     // |H'|: ranks that compute different box sets
+    bool shard = false, virt = false;
+    std::vector<BoxRank> ranks;       // the ranks this context runs
+    int grid_cap = 2048;
+    uint64_t *d_acc = nullptr;
+    hipStream_t graph_stream = nullptr;
+};
+
+static int box_prepare(Ctx *c, DenseBox *d, uint64_t root) {
+    d->root_hi = box_index_of_key((uint32_t)root) >> 12;
+    d->virt = c->world <= 1 && c->virtual_ranks > 1;
+    d->world = c->world > 1 ? c->world : c->virtual_ranks;
+    d->shard = d->world > 1;
     GM_HIP(hipMalloc(&d->d_acc, 2 * sizeof(uint64_t)));
     int cus = 256;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
     d->grid_cap = cus * 4 * GM_BOX_WAVES;
     const uint64_t bytes = 1ull << 32;
-    if (c->adopted_dense) {
-        if (c->adopted_dense_bytes < bytes) {
-            set_error("adopted dense table holds %llu bytes, need %llu", (unsigned long long)c->adopted_dense_bytes,
-                      (unsigned long long)bytes);
-            return GM_E_CAP;
+    if (c->adopted_dense && c->adopted_dense_bytes < bytes) {
+        set_error("adopted dense table holds %llu bytes, need %llu", (unsigned long long)c->adopted_dense_bytes,
+                  (unsigned long long)bytes);
+        return GM_E_CAP;
+    }
+    const int r0 = d->virt ? 0 : c->rank, r1 = d->virt ? d->world : c->rank + 1;
+    d->ranks.resize(r1 - r0);
+    for (int r = r0; r < r1; r++) {
+        BoxRank &R = d->ranks[r - r0];
+        R.rank = r;
+        BoxPlan P;
+        GM_TRY(box_plan(d->root_hi, d->world, r, d->shard, &P));
+        d->nsym = P.nsym;
+        R.tier_off = P.tier_off;
+        R.own = P.own;
+        R.n_boxes = P.boxes.size();
+        R.ties = P.ties;
+        GM_HIP(hipMalloc(&R.d_boxes, std::max<size_t>(1, P.boxes.size()) * 4));
+        GM_HIP(hipMemcpy(R.d_boxes, P.boxes.data(), P.boxes.size() * 4, hipMemcpyHostToDevice));
+        GM_HIP(hipMalloc(&R.d_own, std::max<size_t>(1, P.own.size()) * 4));
+        GM_HIP(hipMemcpy(R.d_own, P.own.data(), P.own.size() * 4, hipMemcpyHostToDevice));
+        if (d->shard) {
+            GM_HIP(hipMalloc(&R.d_fills, std::max<size_t>(1, P.fills.size()) * 4));
+            GM_HIP(hipMemcpy(R.d_fills, P.fills.data(), P.fills.size() * 4, hipMemcpyHostToDevice));
+            if (!P.map.empty()) {
+                GM_HIP(hipMalloc(&R.d_map, P.map.size()));
+                GM_HIP(hipMemcpy(R.d_map, P.map.data(), P.map.size(), hipMemcpyHostToDevice));
+            }
         }
-        d->table = (uint8_t *)c->adopted_dense;
-        d->owned = false;
-    } else {
-        if (hipMalloc(&d->table, bytes) != hipSuccess) {
-            set_error("hipMalloc of the 4 GiB dense table failed");
-            return GM_E_NOMEM;
+        if (c->adopted_dense && r == r0) {
+            R.table = (uint8_t *)c->adopted_dense;
+            R.owned = false;
+        } else {
+            if (hipMalloc(&R.table, bytes) != hipSuccess) {
+                (void)hipGetLastError();
+                set_error("hipMalloc of a 4 GiB dense table failed (rank %d)", r);
+                return GM_E_NOMEM;
+            }
+            R.owned = true;
+            // a virtual rank's own table starts as 0xFF (LOSS in 0, the largest code): a read of
+            // a box the rank never computed would change its results, so tests catch it
+            if (d->virt) GM_HIP(hipMemsetAsync(R.table, 0xFF, bytes, c->stream));
         }
-        d->owned = true;
     }
     return GM_OK;
 }
 
-static int box_launch_tiers(Ctx *c, DenseBox *d) {
-    for (size_t t = 0; t + 1 < d->tier_off.size(); t++) {
-        const uint32_t nb = d->tier_off[t + 1] - d->tier_off[t];
+static int box_launch_tiers(Ctx *c, DenseBox *d, BoxRank &R) {
+    for (size_t t = 0; t + 1 < R.tier_off.size(); t++) {
+        const uint32_t nb = R.tier_off[t + 1] - R.tier_off[t];
         if (!nb) continue;
         const uint32_t ng = (nb + 1) / 2;
         // at least 8 workgroups (one per XCD run), at most the resident capacity
         const uint32_t grid = std::max<uint32_t>(8u, std::min<uint32_t>(ng, (uint32_t)d->grid_cap));
-        hipLaunchKernelGGL(box_tier_kernel, dim3(grid), dim3(64), 0, c->stream, d->table, d->d_boxes + d->tier_off[t], nb);
+        if (d->shard)
+            hipLaunchKernelGGL(box_tier_kernel<true>, dim3(grid), dim3(64), 0, c->stream, R.table,
+                               R.d_boxes + R.tier_off[t], R.d_fills + R.tier_off[t], nb);
+        else
+            hipLaunchKernelGGL(box_tier_kernel<false>, dim3(grid), dim3(64), 0, c->stream, R.table,
+                               R.d_boxes + R.tier_off[t], (const uint32_t *)nullptr, nb);
     }
     GM_HIP(hipGetLastError());
     return GM_OK;
+}
+
+static int box_launches(const BoxRank &R) {
+    int n = 0;
+    for (size_t t = 0; t + 1 < R.tier_off.size(); t++) n += R.tier_off[t + 1] > R.tier_off[t];
+    return n;
 }
 
 void dense_box_free(Ctx *c);
@@ -711,37 +968,46 @@ void dense_box_free(Ctx *c);
 int dense_box_solve(Ctx *c, uint64_t root) {
     DenseBox *d = c->dbox;
     const uint32_t rh = box_index_of_key((uint32_t)root) >> 12;
-    if (!d || (c->adopted_dense && d->table != c->adopted_dense) || d->root_hi != rh) {
+    const bool virt = c->world <= 1 && c->virtual_ranks > 1;
+    const int world = c->world > 1 ? c->world : c->virtual_ranks;
+    if (!d || (c->adopted_dense && d->ranks[0].table != c->adopted_dense) || d->root_hi != rh || d->world != world ||
+        d->virt != virt || (!virt && d->ranks[0].rank != c->rank)) {
         dense_box_free(c);
         d = c->dbox = new DenseBox();
         GM_TRY(box_prepare(c, d, root));
     }
     const double t0 = now_ms();
-    if (c->timing && !d->ev[0]) {
-        GM_HIP(hipEventCreate(&d->ev[0]));
-        GM_HIP(hipEventCreate(&d->ev[1]));
-    }
-    if (c->use_graph) {
-        if (!d->graph || d->graph_stream != c->stream) {
-            if (d->graph) { (void)hipGraphExecDestroy(d->graph); d->graph = nullptr; }
-            hipGraph_t g;
-            GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-            const int rc = box_launch_tiers(c, d);
-            const hipError_t e = hipStreamEndCapture(c->stream, &g);
-            if (rc != GM_OK) return rc;
-            if (e != hipSuccess) { set_error("graph capture failed: %s", hipGetErrorString(e)); return GM_E_HIP; }
-            GM_HIP(hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0));
-            GM_HIP(hipGraphDestroy(g));
-            d->graph_stream = c->stream;
+    if (c->timing)
+        for (auto &R : d->ranks)
+            if (!R.ev[0]) {
+                GM_HIP(hipEventCreate(&R.ev[0]));
+                GM_HIP(hipEventCreate(&R.ev[1]));
+            }
+    // one rank after the other (virtual ranks): each rank's launches are its whole
+    // multi-GPU job -- it never waits for another rank -- so its event span is its time
+    for (auto &R : d->ranks) {
+        if (c->use_graph) {
+            if (!R.graph || d->graph_stream != c->stream) {
+                if (R.graph) { (void)hipGraphExecDestroy(R.graph); R.graph = nullptr; }
+                hipGraph_t g;
+                GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+                const int rc = box_launch_tiers(c, d, R);
+                const hipError_t e = hipStreamEndCapture(c->stream, &g);
+                if (rc != GM_OK) return rc;
+                if (e != hipSuccess) { set_error("graph capture failed: %s", hipGetErrorString(e)); return GM_E_HIP; }
+                GM_HIP(hipGraphInstantiate(&R.graph, g, nullptr, nullptr, 0));
+                GM_HIP(hipGraphDestroy(g));
+            }
+            if (c->timing) GM_HIP(hipEventRecord(R.ev[0], c->stream));
+            GM_HIP(hipGraphLaunch(R.graph, c->stream));
+            if (c->timing) GM_HIP(hipEventRecord(R.ev[1], c->stream));
+        } else {
+            if (c->timing) GM_HIP(hipEventRecord(R.ev[0], c->stream));
+            GM_TRY(box_launch_tiers(c, d, R));
+            if (c->timing) GM_HIP(hipEventRecord(R.ev[1], c->stream));
         }
-        if (c->timing) GM_HIP(hipEventRecord(d->ev[0], c->stream));
-        GM_HIP(hipGraphLaunch(d->graph, c->stream));
-        if (c->timing) GM_HIP(hipEventRecord(d->ev[1], c->stream));
-    } else {
-        if (c->timing) GM_HIP(hipEventRecord(d->ev[0], c->stream));
-        GM_TRY(box_launch_tiers(c, d));
-        if (c->timing) GM_HIP(hipEventRecord(d->ev[1], c->stream));
     }
+    if (c->use_graph) d->graph_stream = c->stream;
 #if GM_BOX_TRACE
     {
         unsigned long long h[8];
@@ -755,8 +1021,10 @@ int dense_box_solve(Ctx *c, uint64_t root) {
                 h[7] / (double)(h[6] ? h[6] : 1) / 100.0, h[5] / (double)(h[7] ? h[7] : 1) / 10.0);
     }
 #endif
+    // the root box is fixed by every permutation of the plan, so every rank computes it
     uint8_t rs = 0;
-    GM_HIP(hipMemcpyAsync(&rs, d->table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipMemcpyAsync(&rs, d->ranks[0].table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToHost,
+                          c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     const double t1 = now_ms();
     c->root_record = record_of_code(rs);
@@ -774,28 +1042,73 @@ int dense_box_solve(Ctx *c, uint64_t root) {
         c->tier_counts = acc;
     }
     int launches = 0;
-    for (size_t t = 0; t + 1 < d->tier_off.size(); t++) launches += d->tier_off[t + 1] > d->tier_off[t];
+    for (auto &R : d->ranks) launches += box_launches(R);
     c->stats.n_positions = n;
     c->stats.n_primitive = 1;
-    c->stats.n_tiers = launches;
+    c->stats.n_tiers = box_launches(d->ranks[0]);
     c->stats.solve_ms = t1 - t0;
     c->stats.backward_ms = t1 - t0;
     c->stats.forward_ms = 0;
+    c->stats.exchanged_bytes = 0;   // the sharded solve exchanges nothing (box_plan)
     c->stats.algo_bytes = (uint64_t)((double)(1ull << 32) * (1.0 + 1.8125 * 8));
-    c->stats.table_bytes = 1ull << 32;
+    c->stats.table_bytes = (1ull << 32) * d->ranks.size();
     if (c->timing) {
-        float ms = 0;
-        GM_HIP(hipEventElapsedTime(&ms, d->ev[0], d->ev[1]));
-        c->stats.kernel_ms = ms;
+        float total = 0;
+        for (auto &R : d->ranks) {
+            GM_HIP(hipEventElapsedTime(&R.kernel_ms, R.ev[0], R.ev[1]));
+            total += R.kernel_ms;
+        }
+        c->stats.kernel_ms = total;
         c->stats.kernel_launches = launches;
     }
     return GM_OK;
 }
 
-int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
+    DenseBox *d = c->dbox;
+    if (!n) return GM_OK;
+    const BoxRank &R = d->ranks[0];
+    uint64_t *dk;
+    uint16_t *dr;
+    const uint64_t chunk = std::min<uint64_t>(n, 1ull << 26);
+    GM_HIP(hipMalloc(&dk, chunk * 8));
+    GM_HIP(hipMalloc(&dr, chunk * 2));
+    for (uint64_t o = 0; o < n; o += chunk) {
+        const uint64_t m = std::min(chunk, n - o);
+        GM_HIP(hipMemcpyAsync(dk, keys + o, m * 8, hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(box_query_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, R.table,
+                           R.d_map, c->root, dk, dr, m);
+        GM_HIP(hipMemcpyAsync(recs + o, dr, m * 2, hipMemcpyDeviceToHost, c->stream));
+    }
+    GM_HIP(hipStreamSynchronize(c->stream));
+    (void)hipFree(dk);
+    (void)hipFree(dr);
+    return GM_OK;
+}
 
+// Export: the root's region in ascending key order (one GPU, or every virtual rank), or,
+// for one rank of a multi-process solve, the positions of the boxes it owns.
 int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
     DenseBox *d = c->dbox;
+    uint32_t lim[8];
+    for (int i = 0; i < 8; i++) lim[i] = (uint32_t)((c->root >> (4 * i)) & 15u);
+    if (d->shard && !d->virt) {
+        std::vector<uint64_t> ks;
+        for (uint32_t b : d->ranks[0].own)
+            for (uint32_t o = 0; o < 4096; o++) {
+                const uint32_t k = box_key_of_index((b << 12) | o);
+                bool in = true;
+                for (int i = 0; i < 8 && in; i++) in = ((k >> (4 * i)) & 15u) <= lim[i];
+                if (in) ks.push_back(k);
+            }
+        *n = ks.size();
+        if (!keys) return GM_OK;
+        if (cap < ks.size()) { set_error("export buffer holds %llu, need %llu", (unsigned long long)cap,
+                                         (unsigned long long)ks.size()); return GM_E_CAP; }
+        std::sort(ks.begin(), ks.end());
+        std::copy(ks.begin(), ks.end(), keys);
+        return dense_box_query(c, keys, recs, ks.size());
+    }
     *n = c->n_positions;
     if (!keys) return GM_OK;
     if (cap < c->n_positions) {
@@ -803,8 +1116,6 @@ int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint6
         return GM_E_CAP;
     }
     // the root's box of keys in ascending order (heap 0 fastest)
-    uint32_t lim[8];
-    for (int i = 0; i < 8; i++) lim[i] = (uint32_t)((c->root >> (4 * i)) & 15u);
     uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint64_t j = 0; j < c->n_positions; j++) {
         uint32_t k = 0;
@@ -815,35 +1126,24 @@ int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint6
             h[i] = 0;
         }
     }
-    if (c->n_positions <= (1ull << 26)) return dense_box_query(c, keys, recs, c->n_positions);
+    if (c->n_positions <= (1ull << 26) || d->shard) return dense_box_query(c, keys, recs, c->n_positions);
     // large boxes: one copy of the table, decoded on the host
     std::vector<uint8_t> tab(1ull << 32);
-    GM_HIP(hipMemcpy(tab.data(), d->table, tab.size(), hipMemcpyDeviceToHost));
+    GM_HIP(hipMemcpy(tab.data(), d->ranks[0].table, tab.size(), hipMemcpyDeviceToHost));
     for (uint64_t j = 0; j < c->n_positions; j++) recs[j] = record_of_code(tab[box_index_of_key((uint32_t)keys[j])]);
     return GM_OK;
 }
 
-int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
-    DenseBox *d = c->dbox;
-    if (!n) return GM_OK;
-    uint64_t *dk;
-    uint16_t *dr;
-    GM_HIP(hipMalloc(&dk, n * 8));
-    GM_HIP(hipMalloc(&dr, n * 2));
-    GM_HIP(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(box_query_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d->table, dk, dr, n);
-    GM_HIP(hipMemcpyAsync(recs, dr, n * 2, hipMemcpyDeviceToHost, c->stream));
-    GM_HIP(hipStreamSynchronize(c->stream));
-    (void)hipFree(dk);
-    (void)hipFree(dr);
-    return GM_OK;
-}
-
+// Digest of the boxes this context's ranks own: the whole region on one GPU or over all
+// virtual ranks, this rank's part in a multi-process solve (the parts sum to the whole).
 int dense_box_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     DenseBox *d = c->dbox;
     GM_HIP(hipMemsetAsync(d->d_acc, 0, 16, c->stream));
-    hipLaunchKernelGGL(box_digest_kernel, dim3(4096), dim3(256), 0, c->stream, d->table, c->root,
-                       (unsigned long long *)d->d_acc);
+    for (auto &R : d->ranks)
+        if (!R.own.empty())
+            hipLaunchKernelGGL(box_digest_kernel, dim3(4096), dim3(256), 0, c->stream, R.table, R.d_own,
+                               (uint64_t)R.own.size(), c->root, (unsigned long long *)d->d_acc);
+    GM_HIP(hipGetLastError());
     uint64_t hst[2];
     GM_HIP(hipMemcpyAsync(hst, d->d_acc, 16, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
@@ -853,19 +1153,58 @@ int dense_box_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
 }
 
 int dense_box_table(Ctx *c, void **p, uint64_t *bytes) {
-    *p = c->dbox->table;
+    *p = c->dbox->ranks[0].table;
     *bytes = 1ull << 32;
+    return GM_OK;
+}
+
+int dense_box_rank_stats(Ctx *c, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n) {
+    DenseBox *d = c->dbox;
+    *n = (int)d->ranks.size();
+    if (cap < *n) { set_error("rank stats buffer holds %d, need %d", cap, *n); return GM_E_CAP; }
+    for (int i = 0; i < *n; i++) {
+        if (kernel_ms) kernel_ms[i] = d->ranks[i].kernel_ms;
+        if (boxes) boxes[i] = d->ranks[i].n_boxes;
+        if (ties) ties[i] = d->ranks[i].ties;
+    }
+    return GM_OK;
+}
+
+// host only: box_plan for tests and tools (gm_box_plan)
+int dense_box_plan(uint64_t root, int world, int rank, int what, uint32_t *out, uint64_t cap, uint64_t *n) {
+    if (root >> 32) { set_error("root must be a 32-bit key (8 heaps)"); return GM_E_KEY; }
+    BoxPlan P;
+    GM_TRY(box_plan(box_index_of_key((uint32_t)root) >> 12, world, rank, what == GM_BOXPLAN_MAP, &P));
+    std::vector<uint32_t> v;
+    switch (what) {
+    case GM_BOXPLAN_SHAPE: v = {(uint32_t)P.nsym, P.g, (uint32_t)P.boxes.size(), (uint32_t)P.own.size(),
+                                (uint32_t)P.ties, (uint32_t)(P.tier_off.size() - 1)}; break;
+    case GM_BOXPLAN_BOXES: v = P.boxes; break;
+    case GM_BOXPLAN_FILLS: v = P.fills; break;
+    case GM_BOXPLAN_TIER_OFF: v = P.tier_off; break;
+    case GM_BOXPLAN_OWN: v = P.own; break;
+    case GM_BOXPLAN_MAP: v.assign(P.map.begin(), P.map.end()); break;
+    default: set_error("unknown box plan item %d", what); return GM_E_ARG;
+    }
+    *n = v.size();
+    if (!out) return GM_OK;
+    if (cap < v.size()) { set_error("box plan buffer holds %llu, need %llu", (unsigned long long)cap,
+                                    (unsigned long long)v.size()); return GM_E_CAP; }
+    std::copy(v.begin(), v.end(), out);
     return GM_OK;
 }
 
 void dense_box_free(Ctx *c) {
     DenseBox *d = c->dbox;
     if (!d) return;
-    if (d->graph) (void)hipGraphExecDestroy(d->graph);
-    for (auto e : d->ev)
-        if (e) (void)hipEventDestroy(e);
-    if (d->owned && d->table) (void)hipFree(d->table);
-    if (d->d_boxes) (void)hipFree(d->d_boxes);
+    for (auto &R : d->ranks) {
+        if (R.graph) (void)hipGraphExecDestroy(R.graph);
+        for (auto e : R.ev)
+            if (e) (void)hipEventDestroy(e);
+        if (R.owned && R.table) (void)hipFree(R.table);
+        for (void *q : {(void *)R.d_boxes, (void *)R.d_fills, (void *)R.d_own, (void *)R.d_map})
+            if (q) (void)hipFree(q);
+    }
     if (d->d_acc) (void)hipFree(d->d_acc);
     delete d;
     c->dbox = nullptr;

@@ -363,9 +363,13 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
         set_error("virtual ranks and a multi-process communicator are exclusive");
         return GM_E_ARG;
     }
-    if (sharded) eng = (!force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT)
-                           ? GM_ENGINE_DIST_DENSE
-                           : GM_ENGINE_DIST_SPARSE;
+    // the 8-heap game on the box engine shards inside dense_box.hip (no exchange); other
+    // heap counts and GM_OPT_SUB_INTERLEAVE != 20 keep the block engine's sharded path
+    const bool box = !force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT &&
+                     c->sub.heaps == 8 && c->sub_interleave == 20;
+    if (sharded && !box) eng = (!force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT)
+                                   ? GM_ENGINE_DIST_DENSE
+                                   : GM_ENGINE_DIST_SPARSE;
     int rc;
     switch (eng) {
     case GM_ENGINE_DENSE:
@@ -377,7 +381,8 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     }
     if (rc != GM_OK) return rc;
     c->engine = eng;
-    c->stats.engine = eng;
+    c->stats.engine = (box && sharded) ? GM_ENGINE_DIST_DENSE : eng;
+    c->stats.world = sharded ? (c->world > 1 ? c->world : c->virtual_ranks) : 1;
     c->solved = true;
     if (n_positions) *n_positions = c->n_positions;
     if (root_record) *root_record = c->root_record;
@@ -489,6 +494,19 @@ int gm_dense_table(gm_ctx *h, void **p, uint64_t *bytes) {
 int gm_dist_plan(int heaps, int world, int rank, const int32_t *opts, int what, int axis, uint32_t *off,
                  uint64_t off_cap, uint64_t *n_off, uint32_t *data, uint64_t data_cap, uint64_t *n_data) {
     return dist_sub_plan(heaps, world, rank, opts, what, axis, off, off_cap, n_off, data, data_cap, n_data);
+}
+
+int gm_box_plan(uint64_t root, int world, int rank, int what, uint32_t *out, uint64_t cap, uint64_t *n) {
+    if (!n) return GM_E_ARG;
+    return dense_box_plan(root, world, rank, what, out, cap, n);
+}
+
+int gm_rank_stats(gm_ctx *h, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n) {
+    GM_TRY(need_solved(h));
+    if (!n) return GM_E_ARG;
+    Ctx *c = &h->c;
+    if (c->engine != GM_ENGINE_DENSE || !c->dbox_active || !c->dbox) { *n = 0; return GM_OK; }
+    return dense_box_rank_stats(c, kernel_ms, boxes, ties, cap, n);
 }
 
 void gm_close(gm_ctx *h) {

@@ -133,6 +133,8 @@ int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
 int dense_box_digest(Ctx *c, uint64_t *digest, uint64_t *n);
 int dense_box_table(Ctx *c, void **p, uint64_t *bytes);
 void dense_box_free(Ctx *c);
+int dense_box_rank_stats(Ctx *c, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n);
+int dense_box_plan(uint64_t root, int world, int rank, int what, uint32_t *out, uint64_t cap, uint64_t *n);
 
 // the dense tier kernel, shared with the partitioned (multi-GPU) driver
 bool sub_kernel_exists(int low, int high, int nt);

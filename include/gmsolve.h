@@ -253,6 +253,37 @@ int gm_dist_plan(int heaps, int world, int rank, const int32_t *opts, int what, 
                  uint32_t *off, uint64_t off_cap, uint64_t *n_off,
                  uint32_t *data, uint64_t data_cap, uint64_t *n_data);
 
+/* Host only (no HIP call): the plan of rank `rank` of a `world`-rank sharded solve of the
+ * 8-heap SUBTRACT game on the box engine (the default at 8 heaps).  The
+ * reference's counterpart is its owner hash, md5(str(pos)) % world (src/game_state.py:23-31):
+ * here a rank owns one member of every orbit of a group of heap permutations, and reads the
+ * children it does not compute from their images it does, so the ranks exchange nothing.
+ * Box ids pack the box coordinates (heap i >> 2 for heaps 0-3 at bits 2i, heap j >> 1 for
+ * heaps 4-7 at bits 8 + 3 (j - 4)).
+ *   GM_BOXPLAN_SHAPE     {|H'|, this rank's permutation code, boxes computed, boxes owned,
+ *                         tie boxes (also computed by another rank), box-tiers}
+ *   GM_BOXPLAN_BOXES     the boxes this rank computes, by box-tier (GM_BOXPLAN_TIER_OFF)
+ *   GM_BOXPLAN_FILLS     per computed box: 3 bits per child direction d at bit 3 d, the code
+ *                        k | e << 2 of the permutation r^k t^e (r rotates heaps 0-3, t swaps
+ *                        heaps 4/5 and 6/7) whose image of the child box is read instead; 0 =
+ *                        the child box itself
+ *   GM_BOXPLAN_TIER_OFF  offsets of the box-tiers in GM_BOXPLAN_BOXES
+ *   GM_BOXPLAN_OWN       the boxes this rank owns (digest, export); the ranks' lists partition
+ *                        the root's region
+ *   GM_BOXPLAN_MAP       per box id (2^20): the code h with h(box) computed by this rank, 0xFF
+ *                        outside the root's region (used by gm_query); empty when world is 1
+ * With out NULL only *n is set. */
+enum { GM_BOXPLAN_SHAPE = 0, GM_BOXPLAN_BOXES = 1, GM_BOXPLAN_FILLS = 2, GM_BOXPLAN_TIER_OFF = 3, GM_BOXPLAN_OWN = 4,
+       GM_BOXPLAN_MAP = 5 };
+int gm_box_plan(uint64_t root_key, int world, int rank, int what, uint32_t *out, uint64_t cap, uint64_t *n);
+
+/* Per rank this context ran in its last solve (all virtual ranks, or its own rank of a
+ * multi-process solve) on the sharded box engine: the GPU time of the rank's launches
+ * (GM_OPT_TIMING; with virtual ranks each rank runs alone, so this is its multi-GPU
+ * compute time), the boxes it computed, and how many of those another rank computes too.
+ * *n = 0 for every other engine. */
+int gm_rank_stats(gm_ctx *ctx, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n);
+
 /* Release everything. */
 void gm_close(gm_ctx *ctx);
 

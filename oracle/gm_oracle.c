@@ -716,6 +716,42 @@ int oracle_dense_digest_blocks(const uint16_t *rec, int heaps, int low, uint64_t
     return 0;
 }
 
+/* The same digest over the 8-heap game's BOXES (the sharded box solve's unit of
+ * ownership, include/gmsolve.h gm_box_plan): box id bits 2i..2i+1 = heap i >> 2 for
+ * heaps 0-3, bits 8+3j..10+3j = heap 4+j >> 1; a box holds the 4096 keys whose heaps
+ * 0-3 have those high two bits and heaps 4-7 those high three bits.  Restated here from
+ * that definition (not from the product's code) so a wrong rank of a sharded solve is
+ * named.  Positions outside the root's region are skipped, as above. */
+int oracle_dense_digest_boxes(const uint16_t *rec, uint64_t root, const uint32_t *boxes, uint64_t nboxes,
+                              int threads, uint64_t *digest, uint64_t *count) {
+    uint64_t sum = 0, cnt = 0;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#else
+    (void)threads;
+#endif
+#pragma omp parallel for reduction(+ : sum, cnt) schedule(dynamic, 64)
+    for (long long b = 0; b < (long long)nboxes; b++) {
+        const uint32_t id = boxes[b];
+        uint64_t base = 0;
+        for (int i = 0; i < 4; i++) base |= (uint64_t)(((id >> (2 * i)) & 3u) << 2) << (4 * i);
+        for (int j = 0; j < 4; j++) base |= (uint64_t)(((id >> (8 + 3 * j)) & 7u) << 1) << (16 + 4 * j);
+        for (uint32_t o = 0; o < 4096; o++) {
+            uint64_t k = base;
+            for (int i = 0; i < 4; i++) k |= (uint64_t)((o >> (2 * i)) & 3u) << (4 * i);
+            for (int j = 0; j < 4; j++) k |= (uint64_t)((o >> (8 + j)) & 1u) << (16 + 4 * j);
+            int in = 1;
+            for (int j = 0; j < 8 && in; j++) in = ((k >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
+            if (!in) continue;
+            sum += digest_term(k, rec[k]);
+            cnt++;
+        }
+    }
+    *digest = sum;
+    *count = cnt;
+    return 0;
+}
+
 /* ------------------------------------------------ layered solver (OpenMP) */
 /* The same Appendix-A fixed point as oracle_solve, on a different data
  * structure so the two check each other: per tier a SORTED array of distinct

@@ -2,8 +2,11 @@
 runs them at N > 1.  Needs at least two visible devices (the
 driver's 8-GPU node); on a one-GPU box every test here skips.
 
-* dense (config 5's engine, csrc/dist_sub.hip): per-axis split communicators, halo
-  messages as ncclSend / ncclRecv on the exchange streams;
+* dense, 8 heaps (config 5's engine, csrc/dense_box.hip): each rank solves its share of
+  the boxes alone -- it reads the child boxes it does not compute through heap
+  permutations of its own (DESIGN.md §5) -- so the ranks exchange nothing;
+* dense, block engine (other heap counts, or GM_OPT_SUB_INTERLEAVE 10; csrc/dist_sub.hip):
+  per-axis split communicators, halo messages as ncclSend / ncclRecv on the exchange streams;
 * sparse (configs 3/4, csrc/dist_sparse.hip): the reference's LOOK_UP / RESOLVE p2p pair
   (src/new_process.py:159,186) batched per tier as ncclGroup send / recv.
 
@@ -77,13 +80,15 @@ def _summed(res):
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_dense_rccl_2_32_matches_oracle_digest(world):
-    """Config 5 at full size, block-owner sharded over `world` processes."""
+@pytest.mark.parametrize("interleave", [20, 10])
+def test_dense_rccl_2_32_matches_oracle_digest(world, interleave):
+    """Config 5 at full size over `world` processes: the box engine (20, the default; no
+    exchange) and the block engine (10; halo messages over RCCL)."""
     ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["subtract_8"]
-    res = _run(world, SUB, (8,))
+    res = _run(world, SUB, (8,), {"sub_interleave": interleave})
     assert all(r["n"] == 1 << 32 and r["rec"] == ref["root_record"] for r in res)
     assert _summed(res) == (ref["digest"], 1 << 32)
-    assert sum(r["exchanged"] for r in res) > 0
+    assert (sum(r["exchanged"] for r in res) > 0) == (interleave == 10)
 
 
 @pytest.mark.parametrize("owner", [0, 1])

@@ -72,7 +72,8 @@ def test_dense_tier_balanced_full_2_32_matches_single_gpu(batch, slots):
     d1 = single.digest()
     single.close()
     for ranks in (2, 4, 8):
-        ctx, n, rec = _solve(SUB, (8,), ranks, dist_owner=1, dist_batch=batch, dist_slots=slots)
+        ctx, n, rec = _solve(SUB, (8,), ranks, sub_interleave=10, dist_owner=1, dist_batch=batch,
+                             dist_slots=slots)
         assert (n, rec) == (n1, rec1)
         assert ctx.digest() == d1
         # the halo blocks no heap permutation fills (tests/test_dist_plan.py pins the counts)
@@ -90,13 +91,14 @@ def test_dense_sharded_custom_root(oracle):
 
 
 def test_dense_sharded_full_2_32_matches_single_gpu():
+    """The block engine's sharded path (GM_OPT_SUB_INTERLEAVE 10) at full size."""
     single, n1, rec1 = _solve(SUB, (8,), 1)
     d1 = single.digest()
     single.close()
     halo = {2: 512 << 20, 4: 2 * (512 << 20), 8: 3 * (512 << 20)}   # full halo bytes per solve, all ranks
     for ranks in (2, 4, 8):
         for sym in (1, 0):
-            ctx, n, rec = _solve(SUB, (8,), ranks, dist_symmetry=sym)
+            ctx, n, rec = _solve(SUB, (8,), ranks, sub_interleave=10, dist_symmetry=sym)
             assert (n, rec) == (n1, rec1)
             assert ctx.digest() == d1
             sent = ctx.stats()["exchanged_bytes"]
@@ -104,6 +106,77 @@ def test_dense_sharded_full_2_32_matches_single_gpu():
             want = halo[ranks] // {2: 16, 4: 8, 8: 4}[ranks] if sym else halo[ranks]
             assert sent == want, (ranks, sym, sent, want)
             ctx.close()
+
+
+def _committed(name):
+    import json
+    import os
+    from conftest import GOLDEN
+    return json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))[name]
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 4, 8])
+def test_box_sharded_2_32_matches_oracle_digest(ranks):
+    """Config 5 on the box engine over virtual ranks: every rank solves its boxes alone, on
+    its own table (filled with 0xFF first, so a read of a box the rank never computed would
+    show), reading the child boxes it does not compute through heap permutations of its own
+    boxes.  The ranks' owned digests sum to the C oracle's digest of the whole table, the
+    root record is the oracle's, and nothing is exchanged."""
+    ref = _committed("subtract_8")
+    ctx, n, rec = _solve(SUB, (8,), ranks, timing=1)
+    st = ctx.stats()
+    assert st["engine"] == _lib.ENGINE_DIST_DENSE and st["exchanged_bytes"] == 0
+    assert (n, rec) == (1 << 32, ref["root_record"])
+    assert ctx.digest() == (ref["digest"], 1 << 32)
+    rs = ctx.rank_stats()
+    assert len(rs) == ranks and all(r["kernel_ms"] > 0 for r in rs)
+    want = {2: 532480, 3: 532480, 4: 282880, 8: 145600}[ranks]   # tests/test_box_plan.py pins these
+    assert [r["boxes"] for r in rs] == [want] * ranks   # at 3 ranks, rank 2 repeats rank 0's set
+    # a query answers every key through the rank-0 table's heap permutations
+    keys = np.array([0xFFFFFFFF, 0, 0x12345678, 0xFEDCBA98, 0x0F0F0F0F, 0x88888888], dtype=np.uint64)
+    single, _, _ = _solve(SUB, (8,), 1)
+    assert np.array_equal(ctx.query(keys), single.query(keys))
+    single.close()
+    ctx.close()
+
+
+_ORACLE_ROOTS = {}
+
+
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+@pytest.mark.parametrize("root", [0x33337777, 0x33557777, 0x333337BF, 0x13572468])
+def test_box_sharded_custom_roots_vs_oracle(oracle, ranks, root):
+    """Custom roots on the sharded box engine: regions every permutation of the plan maps
+    onto themselves (0x33337777, 0x33557777), one only t does (0x333337BF), one none does
+    (0x13572468: every rank computes everything).  Export, digest and query equal the C
+    oracle's table; keys outside the root's region query as unsolved."""
+    if root not in _ORACLE_ROOTS:
+        _ORACLE_ROOTS[root] = oracle.solve(SUB, (8,), root=root)
+    ok, orec = _ORACLE_ROOTS[root]
+    ctx, n, rec = _solve(SUB, (8,), ranks, root=root)
+    assert n == len(ok)
+    k, r = ctx.export()
+    assert np.array_equal(k, ok) and np.array_equal(r, orec)
+    assert ctx.digest() == (digest(ok, orec), len(ok))
+    sample = ok[:: max(1, len(ok) // 5000)]
+    assert np.array_equal(ctx.query(sample), orec[:: max(1, len(ok) // 5000)])
+    outside = np.array([root + 1 if (root & 15) < 15 else root | 0xF0000000, 0x1FFFFFFFF], dtype=np.uint64)
+    assert ctx.query(outside).tolist() == [_lib.REC_UNSOLVED] * 2
+    ctx.close()
+
+
+def test_box_engine_query_outside_the_root_region_is_unsolved():
+    """the box engine solves only the boxes of the root's region and never clears
+    the table, so a key with a nibble above the root's must query as 0xFFFF, not as whatever
+    the slot holds (include/gmsolve.h gm_query)."""
+    ctx, _, _ = _solve(SUB, (8,), 1)   # writes every slot; the next solve reuses the memory
+    root = 0x3F0A5C12
+    ctx.solve(root)
+    inside = np.array([root, 0x3F0A5C02, 0], dtype=np.uint64)
+    outside = np.array([0x3F0A5C13, 0x4F0A5C12, 0xFFFFFFFF, 1 << 32], dtype=np.uint64)
+    assert (ctx.query(inside) != _lib.REC_UNSOLVED).all()
+    assert ctx.query(outside).tolist() == [_lib.REC_UNSOLVED] * 4
+    ctx.close()
 
 
 @pytest.mark.parametrize("ranks", [2, 3, 8])
