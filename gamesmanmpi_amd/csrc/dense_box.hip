@@ -1161,6 +1161,7 @@ int dense_box_table(Ctx *c, void **p, uint64_t *bytes) {
 int dense_box_rank_stats(Ctx *c, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n) {
     DenseBox *d = c->dbox;
     *n = (int)d->ranks.size();
+    if (!kernel_ms && !boxes && !ties) return GM_OK;
     if (cap < *n) { set_error("rank stats buffer holds %d, need %d", cap, *n); return GM_E_CAP; }
     for (int i = 0; i < *n; i++) {
         if (kernel_ms) kernel_ms[i] = d->ranks[i].kernel_ms;

@@ -141,12 +141,26 @@ _known = None
 
 
 def known():
-    """{fingerprint: {"codec": name, "source": path}} of the stored plugin files."""
+    """{fingerprint: {"codec": name, "source": path}} of the stored plugin files.
+
+    Fingerprints hash bytecode, so they only match under the Python version the store was
+    made with; under another one this warns (once) that no known plugin file will be
+    recognised -- plugins then bind only by the exhaustive check, and large ones go to
+    the graph engine -- instead of losing the device path silently."""
     global _known
     if _known is None:
         try:
             with open(STORE) as f:
-                _known = json.load(f)["fingerprints"]
+                data = json.load(f)
+            _known = data["fingerprints"]
+            made = data.get("python")
+            here = "%d.%d" % sys.version_info[:2]
+            if made and made != here:
+                import warnings
+                warnings.warn("gamesmanmpi_amd: plugin fingerprints were made under Python %s, this is %s: "
+                              "no plugin file will be recognised by its code (run `python -m "
+                              "gamesmanmpi_amd.fingerprint --write` under this interpreter)" % (made, here),
+                              RuntimeWarning, stacklevel=2)
         except (OSError, ValueError, KeyError):
             _known = {}
     return _known

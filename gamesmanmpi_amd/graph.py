@@ -33,7 +33,6 @@ is not used: its images of reachable positions need not be reachable
 (Othello's player_flip maps every reachable position to an unreachable one).
 """
 import pickle
-import importlib.util
 import multiprocessing as mp
 import os
 import time
@@ -41,25 +40,17 @@ import time
 import numpy as np
 
 from . import _lib
+from .walk_worker import (_order, canonical, expand_one as _expand_one, fingerprint as _fingerprint,  # noqa: F401
+                          generators as _generators, load_fresh as _load_fresh, orbit, owner as _owner,
+                          position_key, worker_main)
 
 UNDECIDED = 4
-PAR_MIN = 1024        # positions in a level before it is expanded by the worker pool
-BATCH = 1024          # positions per worker task
+PAR_MIN = 2048        # positions in a level before the walk goes parallel
+PAR_START = 8192      # positions so far + the projected next level that start the worker processes
 
 
 class TooLarge(RuntimeError):
     """The plugin's reachable set is projected past the host-enumeration limits."""
-
-
-def position_key(pos):
-    """Hashable identity of a plugin position (numpy boards by dtype/shape/bytes)."""
-    if isinstance(pos, np.ndarray):
-        return ("ndarray", pos.dtype.str, pos.shape, pos.tobytes())
-    return pos
-
-
-def _order(pos):
-    return pickle.dumps(position_key(pos), protocol=4)
 
 
 def symmetry_generators(module, root):
@@ -82,60 +73,12 @@ def symmetry_generators(module, root):
     return out
 
 
-def _generators(module, idx):
-    if not idx:
-        return []
-    items = list(module.symmetry_functions())
-    return [items[i][0] if isinstance(items[i], tuple) else items[i] for i in idx]
-
-
-def orbit(pos, gens):
-    """Every image of pos under the group the functions generate, pos first."""
-    out, seen, todo = [pos], {position_key(pos)}, [pos]
-    while todo:
-        p = todo.pop()
-        for g in gens:
-            q = g(p)
-            k = position_key(q)
-            if k not in seen:
-                seen.add(k)
-                out.append(q)
-                todo.append(q)
-    return out
-
-
-def canonical(pos, gens):
-    """The orbit's representative: its least member in pickled-key byte order."""
-    return min(orbit(pos, gens), key=_order) if gens else pos
-
-
-def _expand_one(module, pos, gens=()):
-    p = module.primitive(pos)
-    if not isinstance(p, (int, np.integer)) or not 0 <= int(p) <= 4:
-        raise ValueError("primitive(%r) returned %r, not a src.utils code" % (pos, p))
-    p = int(p)
-    kids = [module.do_move(pos, m) for m in module.gen_moves(pos)] if p == UNDECIDED else []
-    if gens:
-        kids = [canonical(c, gens) for c in kids]
-    return p, kids
-
-
 # ---------------------------------------------------------------- worker pool
-_WORKER_MODULE = None
-_WORKER_GENS = []
-
 
 def _simple(v):
     if isinstance(v, (bool, int, float, str, type(None))):
         return True
     return isinstance(v, tuple) and all(_simple(x) for x in v)
-
-
-def _load_fresh(path, name="gm_graph_plugin"):
-    spec = importlib.util.spec_from_file_location(name, path)
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    return mod
 
 
 def _same(a, b):
@@ -197,19 +140,6 @@ def _module_spec(module):
     return path, attrs
 
 
-def _worker_init(path, attrs, gen_idx=()):
-    global _WORKER_MODULE, _WORKER_GENS
-    mod = _load_fresh(path)
-    for k, v in attrs.items():   # values the caller set on its module (board size, ...)
-        setattr(mod, k, v)
-    _WORKER_MODULE = mod
-    _WORKER_GENS = _generators(mod, list(gen_idx))
-
-
-def _worker_expand(batch):
-    return [_expand_one(_WORKER_MODULE, pos, _WORKER_GENS) for pos in batch]
-
-
 def _default_workers():
     """GM_HOST_WORKERS, else the CPUs this process may use (the GPU box grants each GPU a
     share of a large machine and says so in OMP_NUM_THREADS), at most 16."""
@@ -223,10 +153,6 @@ def _default_workers():
     return max(1, min(16, n))
 
 
-def _noop():
-    return 0
-
-
 def _main_importable():
     """Spawned workers re-import the parent's __main__; a script from stdin cannot be."""
     import sys
@@ -235,55 +161,249 @@ def _main_importable():
     return path is None or os.path.exists(path)
 
 
-class _Expander:
-    """Expands a level serially or, when large, in batches on a spawned worker pool,
-    yielding (primitive, children) per position in level order as batches complete.
-    The pool starts at construction (its processes import while the small first
-    levels run serially).  A pool failure (a worker that cannot start or dies)
-    before any result of a level was yielded falls back to the serial walk."""
+class _ShardPool:
+    """The parallel walk's worker processes (spawn), one pipe each."""
 
-    def __init__(self, module, workers, gen_idx=()):
-        self.module = module
-        self.workers = workers
-        self.gens = _generators(module, list(gen_idx))
-        self.pool = None
-        self.spec = _module_spec(module) if workers > 1 and _main_importable() else None
-        if self.spec is not None:
-            from concurrent.futures import ProcessPoolExecutor
-            try:
-                self.pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("spawn"),
-                                                initializer=_worker_init, initargs=self.spec + (tuple(gen_idx),))
-                for _ in range(self.workers):   # start every worker now
-                    self.pool.submit(_noop)
-            except (OSError, ImportError):
-                self.close()
-                self.spec = None
+    def __init__(self, spec, nw, gen_idx):
+        ctx = mp.get_context("spawn")
+        self.nw = nw
+        self.conns, self.procs = [], []
+        for w in range(nw):
+            a, b = ctx.Pipe()
+            pr = ctx.Process(target=worker_main, args=(b, spec[0], spec[1], tuple(gen_idx), nw), daemon=True)
+            pr.start()
+            b.close()
+            self.conns.append(a)
+            self.procs.append(pr)
+        self.ready = False
 
-    def __call__(self, level):
-        if self.spec is None or len(level) < PAR_MIN:
-            for pos in level:
-                yield _expand_one(self.module, pos, self.gens)
-            return
-        from concurrent.futures.process import BrokenProcessPool
-        batches = [level[i:i + BATCH] for i in range(0, len(level), BATCH)]
-        done = 0
-        try:
-            for res in self.pool.map(_worker_expand, batches):
-                for r in res:
-                    yield r
-                done += 1
-        except (BrokenProcessPool, OSError, ImportError):
-            if done:
-                raise
-            self.close()
-            self.spec = None
-            for pos in level:
-                yield _expand_one(self.module, pos, self.gens)
+    def _recv(self, w, kind):
+        msg = self.conns[w].recv()
+        if msg[0] == "error":
+            raise RuntimeError("graph walk worker %d failed:\n%s" % (w, msg[1]))
+        assert msg[0] == kind, msg[0]
+        return msg
+
+    def wait_ready(self):
+        if not self.ready:
+            for w in range(self.nw):
+                self._recv(w, "ready")
+            self.ready = True
+
+    def poll_ready(self):
+        """True once every worker has imported the plugin (does not block)."""
+        if not self.ready and all(c.poll() for c in self.conns):
+            self.wait_ready()
+        return self.ready
+
+    def all(self, msgs, kind):
+        for w, m in enumerate(msgs):
+            self.conns[w].send(m)
+        return [self._recv(w, kind) for w in range(self.nw)]
 
     def close(self):
-        if self.pool is not None:
-            self.pool.shutdown(wait=True, cancel_futures=True)
-            self.pool = None
+        """Tell the workers to stop; they leave on their own (daemon processes, reaped by
+        multiprocessing), so the walk does not wait for them."""
+        for c in self.conns:
+            try:
+                c.send(("stop",))
+                c.close()
+            except (OSError, EOFError, BrokenPipeError):
+                pass
+        self.conns, self.procs = [], []
+
+
+class _Walk:
+    """Level-synchronous enumeration, serial while the levels are small, then sharded
+    over worker processes (each owns the positions whose 128-bit fingerprint maps to
+    it).  In the sharded part the parent never touches a position object: per level it
+    merges the workers' (parent index, primitive, child count, child fingerprints),
+    deduplicates and numbers the children with numpy against the sorted fingerprints
+    of every position so far (new ones in first-occurrence order, so the numbering is
+    the serial walk's), and tells each owner which of them it keeps -- the reference's
+    owner-rank dedup (src/new_process.py:102-133, :145-162) with processes for ranks."""
+
+    def __init__(self, module, gen_idx, workers, limit, budget_s):
+        self.module, self.gen_idx, self.workers = module, list(gen_idx), workers
+        self.gens = _generators(module, self.gen_idx)
+        self.limit, self.budget_s = limit, budget_s
+        self.index, self.positions = {}, []     # serial part
+        self.prim, self.off, self.kids = [], [0], []
+        self.sizes = []
+        self.pool = None
+        self.spec = _module_spec(module) if workers > 1 and _main_importable() else None
+        self.n = 0                 # positions numbered so far
+        self.G = self.GI = None    # sorted fingerprints of every position, and their indices
+        self.members = 0           # orbit members of the positions the workers hold
+
+    def _project(self, level_len, nxt_len, tl, t0):
+        if not nxt_len:
+            return 0
+        growth = nxt_len / level_len
+        projected = self.n + nxt_len * growth
+        dt = time.perf_counter() - tl
+        elapsed = time.perf_counter() - t0
+        if projected > self.limit or (growth > 1 and elapsed + dt * growth * growth > self.budget_s):
+            raise TooLarge(
+                "plugin %s: after %d levels (sizes %s, %d positions, %.1f s) the next level is "
+                "projected at ~%.3g positions (growth x%.2f per level): past the host-enumeration "
+                "limits (%d positions, %.0f s); no device descriptor reproduces this plugin at these "
+                "parameters" % (getattr(self.module, "__name__", self.module), len(self.sizes),
+                                self.sizes + [nxt_len], self.n, elapsed, nxt_len * growth, growth, self.limit,
+                                self.budget_s))
+        return nxt_len * growth
+
+    def _serial_level(self, level):
+        nxt = []
+        for pos in level:
+            p, children = _expand_one(self.module, pos, self.gens)
+            self.prim.append(p)
+            for child in children:
+                k = position_key(child)
+                j = self.index.get(k)
+                if j is None:
+                    j = self.n
+                    if j >= self.limit:
+                        raise TooLarge("more than %d positions: too large for host enumeration (levels %s)"
+                                       % (self.limit, self.sizes))
+                    self.index[k] = j
+                    self.positions.append(child)
+                    self.n += 1
+                    nxt.append(child)
+                self.kids.append(j)
+            self.off.append(len(self.kids))
+        return nxt
+
+    def _go_parallel(self, level):
+        """Hand the current level to the workers' shards and the numbering to fingerprints."""
+        self.pool.wait_ready()
+        fps = [_fingerprint(p) for p in self.positions]
+        G = np.frombuffer(b"".join(fps), dtype="V16")
+        order = np.argsort(G, kind="stable")
+        self.G, self.GI = G[order], order.astype(np.int64)
+        first = self.n - len(level)
+        shards = [[] for _ in range(self.pool.nw)]
+        for i, pos in enumerate(level):
+            shards[_owner(fps[first + i], self.pool.nw)].append((first + i, pos))
+        self.pool.all([("seed", pickle.dumps(sh, protocol=4)) for sh in shards], "ok")
+
+    def _parallel_level(self):
+        t0 = time.perf_counter()
+        res = self.pool.all([("expand",)] * self.pool.nw, "expanded")
+        t1 = time.perf_counter()
+        idx = np.concatenate([np.frombuffer(r[1], dtype=np.int64) for r in res])
+        prims = np.concatenate([np.frombuffer(r[2], dtype=np.uint8) for r in res])
+        counts = np.concatenate([np.frombuffer(r[3], dtype=np.uint32) for r in res]).astype(np.int64)
+        E = np.concatenate([np.frombuffer(r[4], dtype="V16") for r in res])
+        # edges of the parents in index order (the serial walk's order)
+        start = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+        order = np.argsort(idx, kind="stable")
+        c = counts[order]
+        tot = int(c.sum())
+        csum = np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64)
+        perm = np.repeat(start[order] - csum, c) + np.arange(tot, dtype=np.int64)
+        E = E[perm]
+        for p in prims[order].tolist():
+            if p > 4:
+                raise ValueError("primitive() returned %r, not a src.utils code" % p)
+        self.prim.extend(prims[order].tolist())
+        self.off.extend((len(self.kids) + np.cumsum(c)).tolist())
+        # number the children: known ones by lookup, new ones in first-occurrence order
+        if tot:
+            uniq, first, inv = np.unique(E, return_index=True, return_inverse=True)
+            at = np.searchsorted(self.G, uniq)
+            found = np.zeros(len(uniq), dtype=bool)
+            ok = at < len(self.G)
+            found[ok] = self.G[at[ok]] == uniq[ok]
+            uidx = np.empty(len(uniq), dtype=np.int64)
+            uidx[found] = self.GI[at[found]]
+            new = np.flatnonzero(~found)
+            new = new[np.argsort(first[new], kind="stable")]
+            if self.n + len(new) > self.limit:
+                raise TooLarge("more than %d positions: too large for host enumeration (levels %s)"
+                               % (self.limit, self.sizes))
+            uidx[new] = self.n + np.arange(len(new), dtype=np.int64)
+            self.n += len(new)
+            self.kids.extend(uidx[inv.ravel()].tolist())
+            ins = np.sort(new)   # positions of the new fingerprints in uniq (sorted by fingerprint)
+            self.G = np.insert(self.G, at[ins], uniq[ins])
+            self.GI = np.insert(self.GI, at[ins], uidx[ins])
+            new_fp, new_idx = uniq[new], uidx[new]
+        else:
+            new_fp, new_idx = np.zeros(0, dtype="V16"), np.zeros(0, dtype=np.int64)
+        # each owner keeps its new positions; the objects it was sent come with them
+        nw = self.pool.nw
+        own = np.array([_owner(bytes(f), nw) for f in new_fp], dtype=np.int64) if len(new_fp) else \
+            np.zeros(0, dtype=np.int64)
+        msgs = []
+        for w in range(nw):
+            m = own == w
+            msgs.append(("adopt", new_fp[m].tobytes(), new_idx[m].tobytes(), [r[5][w] for r in res]))
+        t2 = time.perf_counter()
+        self.members += sum(r[1] for r in self.pool.all(msgs, "adopted"))
+        if os.environ.get("GM_GRAPH_TRACE"):
+            import sys
+            wt = [r[6] for r in res]
+            print("[graph] level %d: %d parents, %d edges, %d new | expand %.3f s (workers max %.3f min %.3f) "
+                  "number %.3f s adopt %.3f s" % (len(self.sizes), len(idx), tot, len(new_fp), t1 - t0, max(wt),
+                                                  min(wt), t2 - t1, time.perf_counter() - t2), file=sys.stderr)
+        return len(new_fp)
+
+    def _trace(self, what, t):
+        if os.environ.get("GM_GRAPH_TRACE"):
+            import sys
+            print("[graph] %s %.3f s" % (what, time.perf_counter() - t), file=sys.stderr)
+
+    def run(self, root):
+        self.index[position_key(root)] = 0
+        self.positions.append(root)
+        self.n = 1
+        level, level_len = [root], 1
+        t0 = time.perf_counter()
+        projected = 0
+        try:
+            while level_len:
+                tl = time.perf_counter()
+                self.sizes.append(level_len)
+                if self.G is None and self.spec is not None:
+                    # workers are spawned once the graph is projected past PAR_START positions
+                    # (tic-tac-toe never is: ADVICE r03); the parent keeps walking serially
+                    # while they import, and hands over at the first level of PAR_MIN
+                    # positions it meets with the workers ready (or 8 PAR_MIN, whatever)
+                    if self.pool is None and (self.n + projected >= PAR_START or level_len >= 4 * PAR_MIN):
+                        self.pool = _ShardPool(self.spec, self.workers, self.gen_idx)
+                        self._trace("spawn of %d workers at level %d" % (self.workers, len(self.sizes)), tl)
+                    if self.pool is not None and level_len >= PAR_MIN and (self.pool.poll_ready() or
+                                                                           level_len >= 8 * PAR_MIN):
+                        tw = time.perf_counter()
+                        self._go_parallel(level)
+                        self._trace("workers ready and seeded", tw)
+                if self.G is None:
+                    level = self._serial_level(level)
+                    nxt_len = len(level)
+                    self._trace("serial level %d (%d positions)" % (len(self.sizes), level_len), tl)
+                else:
+                    nxt_len = self._parallel_level()
+                projected = self._project(level_len, nxt_len, tl, t0)
+                level_len = nxt_len
+            self.serial_positions = list(self.positions)
+            if self.G is not None:   # the workers' positions, in index order
+                tg = time.perf_counter()
+                got = self.pool.all([("gather",)] * self.pool.nw, "positions")
+                pos = self.positions + [None] * (self.n - len(self.positions))
+                for r in got:
+                    for i, p in zip(np.frombuffer(r[1], dtype=np.int64).tolist(), pickle.loads(r[2])):
+                        pos[i] = p
+                self.positions = pos
+                self._trace("gather", tg)
+        finally:
+            if self.pool is not None:
+                tc = time.perf_counter()
+                self.pool.close()
+                self._trace("close", tc)
+        self._trace("walk", t0)
+        return (self.positions, np.array(self.prim, dtype=np.uint8), np.array(self.off, dtype=np.uint64),
+                np.array(self.kids, dtype=np.uint32))
 
 
 def enumerate_graph(module, root, limit=50_000_000, workers=None, budget_s=3600.0, symmetry=()):
@@ -295,52 +415,7 @@ def enumerate_graph(module, root, limit=50_000_000, workers=None, budget_s=3600.
     positions or the walk's projected time would pass ``budget_s`` seconds."""
     workers = _default_workers() if workers is None else max(1, int(workers))
     root = canonical(root, _generators(module, list(symmetry)))
-    index = {position_key(root): 0}
-    positions = [root]
-    prim = []
-    off = [0]
-    kids = []
-    sizes = []
-    level = [root]
-    expand = _Expander(module, workers, symmetry)
-    t0 = time.perf_counter()
-    try:
-        while level:
-            tl = time.perf_counter()
-            sizes.append(len(level))
-            nxt = []
-            for p, children in expand(level):
-                prim.append(p)
-                for child in children:
-                    k = position_key(child)
-                    j = index.get(k)
-                    if j is None:
-                        j = len(positions)
-                        if j >= limit:
-                            raise TooLarge("more than %d positions: too large for host enumeration (levels %s)"
-                                           % (limit, sizes))
-                        index[k] = j
-                        positions.append(child)
-                        nxt.append(child)
-                    kids.append(j)
-                off.append(len(kids))
-            # fail fast: project the level after this one from the last growth factor
-            if nxt and len(level) > 0:
-                growth = len(nxt) / len(level)
-                projected = len(positions) + len(nxt) * growth
-                dt = time.perf_counter() - tl
-                elapsed = time.perf_counter() - t0
-                if projected > limit or (growth > 1 and elapsed + dt * growth * growth > budget_s):
-                    raise TooLarge(
-                        "plugin %s: after %d levels (sizes %s, %d positions, %.1f s) the next level is "
-                        "projected at ~%.3g positions (growth x%.2f per level): past the host-enumeration "
-                        "limits (%d positions, %.0f s); no device descriptor reproduces this plugin at these "
-                        "parameters" % (getattr(module, "__name__", module), len(sizes), sizes + [len(nxt)],
-                                        len(positions), elapsed, len(nxt) * growth, growth, limit, budget_s))
-            level = nxt
-    finally:
-        expand.close()
-    return positions, np.array(prim, dtype=np.uint8), np.array(off, dtype=np.uint64), np.array(kids, dtype=np.uint32)
+    return _Walk(module, symmetry, workers, limit, budget_s).run(root)
 
 
 class GraphCodec:
@@ -355,11 +430,20 @@ class GraphCodec:
         self.module = module
         self.symmetry = symmetry_generators(module, root) if symmetry is None else list(symmetry)
         self.gens = _generators(module, self.symmetry)
-        self.positions, self.prim, self.off, self.kids = enumerate_graph(module, root, workers=workers,
-                                                                         symmetry=self.symmetry)
-        self._index = {position_key(p): i for i, p in enumerate(self.positions)}
-        self.n_positions = (sum(len(orbit(p, self.gens)) for p in self.positions) if self.gens
-                            else len(self.positions))
+        workers = _default_workers() if workers is None else max(1, int(workers))
+        walk = _Walk(module, self.symmetry, workers, 50_000_000, 3600.0)
+        self.positions, self.prim, self.off, self.kids = walk.run(canonical(root, self.gens))
+        self._index_map = None
+        if self.gens:   # every orbit member counts (the workers counted theirs)
+            self.n_positions = walk.members + sum(len(orbit(p, self.gens)) for p in walk.serial_positions)
+        else:
+            self.n_positions = len(self.positions)
+
+    @property
+    def _index(self):
+        if self._index_map is None:   # built on first lookup, not on the solve path
+            self._index_map = {position_key(p): i for i, p in enumerate(self.positions)}
+        return self._index_map
 
     def key(self, pos):
         try:

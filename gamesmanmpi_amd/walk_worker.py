@@ -1,0 +1,155 @@
+"""Worker side of the explicit-graph walk (gamesmanmpi_amd/graph.py), kept light.
+
+The parallel walk spawns one process per host core; each imports only this module
+(no numpy, no ctypes library -- the package's __init__ is lazy), rebuilds the plugin
+from its file and owns the positions whose fingerprint maps to it.  The plugin calls
+are the reference's expansion (GameState.expand, src/game_state.py:33-41: gen_moves +
+do_move; primitive positions are not expanded, src/new_process.py:120-130); the
+ownership mirrors its owner rank (src/game_state.py:23-31) and the one copy of each
+child its owner keeps (lookup / distribute, src/new_process.py:102-162).
+"""
+import array
+import hashlib
+import importlib.util
+import pickle
+import time
+
+UNDECIDED = 4
+
+
+def _is_ndarray(x):
+    t = type(x)
+    return t.__name__ == "ndarray" and t.__module__ == "numpy"
+
+
+def position_key(pos):
+    """Hashable identity of a plugin position (numpy boards by dtype/shape/bytes)."""
+    if _is_ndarray(pos):
+        return ("ndarray", pos.dtype.str, pos.shape, pos.tobytes())
+    return pos
+
+
+def _order(pos):
+    return pickle.dumps(position_key(pos), protocol=4)
+
+
+def fingerprint(pos):
+    """128-bit BLAKE2b digest of the position's pickled key: the identity positions are
+    deduplicated and numbered by in the parallel walk (a collision needs ~2^64
+    positions; the walk is limited to 5e7)."""
+    return hashlib.blake2b(_order(pos), digest_size=16).digest()
+
+
+def owner(fp, nw):
+    return fp[0] % nw if nw <= 256 else int.from_bytes(fp[:4], "little") % nw
+
+
+def generators(module, idx):
+    if not idx:
+        return []
+    items = list(module.symmetry_functions())
+    return [items[i][0] if isinstance(items[i], tuple) else items[i] for i in idx]
+
+
+def orbit(pos, gens):
+    """Every image of pos under the group the functions generate, pos first."""
+    out, seen, todo = [pos], {position_key(pos)}, [pos]
+    while todo:
+        p = todo.pop()
+        for g in gens:
+            q = g(p)
+            k = position_key(q)
+            if k not in seen:
+                seen.add(k)
+                out.append(q)
+                todo.append(q)
+    return out
+
+
+def canonical(pos, gens):
+    """The orbit's representative: its least member in pickled-key byte order."""
+    return min(orbit(pos, gens), key=_order) if gens else pos
+
+
+def expand_one(module, pos, gens=()):
+    p = module.primitive(pos)
+    if not (isinstance(p, int) or type(p).__module__ == "numpy") or not 0 <= int(p) <= 4:
+        raise ValueError("primitive(%r) returned %r, not a src.utils code" % (pos, p))
+    p = int(p)
+    kids = [module.do_move(pos, m) for m in module.gen_moves(pos)] if p == UNDECIDED else []
+    if gens:
+        kids = [canonical(c, gens) for c in kids]
+    return p, kids
+
+
+def load_fresh(path, name="gm_graph_plugin"):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def worker_main(conn, path, attrs, gen_idx, nw):
+    """One shard of the parallel walk (a spawned process).  It owns the positions whose
+    fingerprint maps to it: it keeps them, expands the ones of the current level when
+    told, and sends each child object once to the child's owner (relayed by the parent
+    as opaque bytes).  The parent sees only fingerprints, primitive codes and counts."""
+    import traceback
+    try:
+        mod = load_fresh(path)
+        for k, v in attrs.items():   # values the caller set on its module (board size, ...)
+            setattr(mod, k, v)
+        gens = generators(mod, list(gen_idx))
+    except BaseException:
+        conn.send(("error", traceback.format_exc()))
+        return
+    conn.send(("ready",))
+    frontier = []     # (index, position) of the level to expand, ascending index
+    owned_idx, owned_pos = array.array("q"), []
+    sent = set()      # fingerprints whose object this worker has already shipped
+    while True:
+        msg = conn.recv()
+        try:
+            if msg[0] == "seed":          # positions of the current level (from the serial walk)
+                frontier = sorted(pickle.loads(msg[1]), key=lambda t: t[0])
+                conn.send(("ok",))
+            elif msg[0] == "expand":
+                te = time.perf_counter()
+                idx = array.array("q", (i for i, _ in frontier))
+                prims = bytearray(len(frontier))
+                counts = array.array("I", bytes(4 * len(frontier)))
+                fps = []
+                out = [[] for _ in range(nw)]
+                for n, (_, pos) in enumerate(frontier):
+                    p, kids = expand_one(mod, pos, gens)
+                    prims[n] = p
+                    counts[n] = len(kids)
+                    for c in kids:
+                        f = fingerprint(c)
+                        fps.append(f)
+                        if f not in sent:
+                            sent.add(f)
+                            out[owner(f, nw)].append((f, c))
+                blobs = [pickle.dumps(o, protocol=4) if o else b"" for o in out]
+                conn.send(("expanded", idx.tobytes(), bytes(prims), counts.tobytes(), b"".join(fps), blobs,
+                           time.perf_counter() - te))
+            elif msg[0] == "adopt":       # the new positions this worker owns, and the objects sent to it
+                fp_b, idx_b = msg[1], array.array("q", msg[2])
+                want = {fp_b[16 * j:16 * j + 16]: idx_b[j] for j in range(len(idx_b))}
+                got = {}
+                for blob in msg[3]:
+                    if blob:
+                        for f, c in pickle.loads(blob):
+                            if f in want and f not in got:
+                                got[f] = c
+                frontier = sorted(((i, got[f]) for f, i in want.items()), key=lambda t: t[0])
+                owned_idx.extend(i for i, _ in frontier)
+                owned_pos.extend(c for _, c in frontier)
+                members = sum(len(orbit(c, gens)) for _, c in frontier) if gens else len(frontier)
+                conn.send(("adopted", members))
+            elif msg[0] == "gather":
+                conn.send(("positions", owned_idx.tobytes(), pickle.dumps(owned_pos, protocol=4)))
+            elif msg[0] == "stop":
+                return
+        except BaseException:
+            conn.send(("error", traceback.format_exc()))

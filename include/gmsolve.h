@@ -220,7 +220,15 @@ int gm_tier_counts(gm_ctx *ctx, uint64_t *counts, int cap, int *n);
 int gm_adopt_buffer(gm_ctx *ctx, int role, void *dev_ptr, uint64_t bytes);
 
 /* Device pointer and size of the dense table (GM_BUF_DENSE_TABLE) after a solve;
- * its slots hold 1-byte order-preserving codes ("HBM layout"), not records. */
+ * its slots hold 1-byte order-preserving codes ("HBM layout"), not records.
+ * The slot of a key depends on the engine:
+ *   - block engine (heaps != 8, or GM_OPT_SUB_INTERLEAVE != 20): slot = key;
+ *   - box engine (8 heaps, the default): slot = box << 12 | A << 4 | B, with box = the box
+ *     id of gm_box_plan (heap i >> 2 at bits 2i for heaps 0-3, heap j >> 1 at bits
+ *     8 + 3 (j - 4) for heaps 4-7), A = sum over heaps 0-3 of (heap i & 3) << 2i and
+ *     B = sum over heaps 4-7 of (heap j & 1) << (j - 4).  At N > 1 a rank's table holds
+ *     only the boxes it computed (gm_box_plan GM_BOXPLAN_BOXES); gm_query maps any key.
+ * Read records through gm_query / gm_export unless the layout is handled. */
 int gm_dense_table(gm_ctx *ctx, void **dev_ptr, uint64_t *bytes);
 
 /* Host only -- makes no HIP or RCCL call, so it runs without a GPU: the plan

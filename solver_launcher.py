@@ -160,8 +160,23 @@ def run(args, out=sys.stdout):
                                         _lib.lib().gm_device_count()) if rank == 0 else None)
         logging.debug("rank %d of %d: %s", rank, world, plan)
         if plan == "single" and rank != 0:
-            dist.barrier()   # rank 0 solves for every rank; it prints the root line
-            return 0
+            # rank 0 solves for every rank and prints the root line; wait for it by polling
+            # the group's store (a barrier would time out under a solve longer than the
+            # group timeout)
+            return dist.wait_for_root()
+    if plan == "single":
+        try:
+            return _solve_and_report(args, game, root, rank, world, local, plan, out)
+        except BaseException:
+            dist.release_waiters(world, ok=False)
+            raise
+    return _solve_and_report(args, game, root, rank, world, local, plan, out)
+
+
+def _solve_and_report(args, game, root, rank, world, local, plan, out):
+    from gamesmanmpi_amd import Solver, _lib
+    if world > 1:
+        from gamesmanmpi_amd import dist
     engine = {"auto": None, "dense": _lib.ENGINE_DENSE, "sparse": _lib.ENGINE_SPARSE}[args.engine]
     device = args.device if args.device is not None else (local if plan == "sharded" else -1)
     solver = Solver(game, root, device=device, engine=engine)
@@ -188,7 +203,7 @@ def run(args, out=sys.stdout):
         write_statsdir(args, solver, rank, world, gather=plan == "sharded")
     solver.close()
     if plan == "single":
-        dist.barrier()
+        dist.release_waiters(world)
     return 0
 
 

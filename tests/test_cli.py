@@ -100,7 +100,9 @@ class FakeSolver:   # stands in for the GPU solve (this container has no GPU)
         from gamesmanmpi_amd import games
         self.codec, self.ctx = games.FourToOneCodec(), FakeCtx()
         seen["device"] = device
-    def solve(self): pass
+    def solve(self):
+        import time
+        time.sleep(float(os.environ.get("FAKE_SOLVE_S", "0")))
     def root_line(self): return "WIN in 3 moves"
     def close(self): pass
 gamesmanmpi_amd.Solver = FakeSolver
@@ -111,10 +113,13 @@ print(json.dumps({"rc": rc, "out": out.getvalue(), "seen": {str(k): v for k, v i
 '''
 
 
-def test_launcher_single_mode_ranks_gloo(tmp_path):
+@pytest.mark.parametrize("solve_s,timeout_s", [(0, None), (6, 2)])
+def test_launcher_single_mode_ranks_gloo(tmp_path, solve_s, timeout_s):
     """More launcher ranks than GPUs (this container has none): rank 0 solves with
     world loopback ranks (GM_OPT_VIRTUAL_RANKS) and prints the one root line; the
-    other ranks print nothing, wait at the barrier and return 0."""
+    other ranks print nothing, wait for rank 0 and return 0 -- also when rank 0's solve
+    (6 s) outlasts the gloo group's timeout (2 s, GM_DIST_TIMEOUT_S): they poll the
+    group's store instead of waiting in a collective."""
     import socket
     import subprocess
     import sys
@@ -123,8 +128,12 @@ def test_launcher_single_mode_ranks_gloo(tmp_path):
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     world = 3
+    env = dict(os.environ, FAKE_SOLVE_S=str(solve_s))
+    if timeout_s is not None:
+        env["GM_DIST_TIMEOUT_S"] = str(timeout_s)
     procs = [subprocess.Popen([sys.executable, "-c", _SINGLE_MODE_RANK, REPO, str(r), str(world), str(port)],
-                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+             for r in range(world)]
     res = []
     try:
         for p in procs:

@@ -102,20 +102,49 @@ def test_launcher_solves_a_descriptorless_plugin(tmp_path):
     assert back[str((5, 6, 7))] == table[(5, 6, 7)]
 
 
-@pytest.mark.parametrize("rel", ["test_games/mttt.py", "test_games/tic_tac_toe_np.py", "tests/plugins/nim3.py"])
-def test_parallel_enumeration_equals_serial(monkeypatch, rel):
-    """Levels expanded by the spawned worker pool (forced on with PAR_MIN = 8) give the
-    serial walk's numbering, primitives and CSR exactly."""
+@pytest.mark.parametrize("workers", [2, 3])
+@pytest.mark.parametrize("rel", ["test_games/mttt.py", "test_games/tic_tac_toe_np.py", "tests/plugins/nim3.py",
+                                 "test_games/four_to_one.py"])
+def test_parallel_enumeration_equals_serial(monkeypatch, rel, workers):
+    """The sharded walk (forced on with PAR_MIN = 8: worker processes own the positions
+    by fingerprint, the parent numbers fingerprints with numpy) gives the serial walk's
+    numbering, primitives and CSR exactly."""
     from gamesmanmpi_amd import graph
     mod = load_plugin(rel)
     root = mod.initial_position()
     serial = enumerate_graph(mod, root, workers=1)
     monkeypatch.setattr(graph, "PAR_MIN", 8)
-    monkeypatch.setattr(graph, "BATCH", 64)
-    par = enumerate_graph(mod, root, workers=2)
+    monkeypatch.setattr(graph, "PAR_START", 8)
+    par = enumerate_graph(mod, root, workers=workers)
     assert [position_key(p) for p in par[0]] == [position_key(p) for p in serial[0]]
     for a, b in zip(par[1:], serial[1:]):
         assert np.array_equal(a, b)
+
+
+def test_parallel_walk_with_declared_symmetry(monkeypatch):
+    """The sharded walk on orbit representatives: the workers canonicalise children and
+    count the orbit members of the positions they keep (765 orbits, 5,478 positions)."""
+    from gamesmanmpi_amd import graph
+    monkeypatch.setattr(graph, "PAR_MIN", 8)
+    monkeypatch.setattr(graph, "PAR_START", 8)
+    mod = load_plugin("tests/plugins/ttt_symmetric.py")
+    ser = graph.GraphCodec(mod, mod.initial_position(), workers=1)
+    par = graph.GraphCodec(mod, mod.initial_position(), workers=3)
+    assert par.n_positions == ser.n_positions == 5478 and len(par.positions) == 765
+    assert par.positions == ser.positions
+    assert all(np.array_equal(a, b) for a, b in ((par.prim, ser.prim), (par.off, ser.off), (par.kids, ser.kids)))
+
+
+def test_small_plugins_start_no_worker(monkeypatch):
+    """a plugin whose levels stay small (tic-tac-toe: at most 1,520 positions
+    per level) never starts the worker processes."""
+    from gamesmanmpi_amd import graph
+    def pool(*a):
+        raise AssertionError("worker processes started for tic-tac-toe")
+    monkeypatch.setattr(graph, "_ShardPool", pool)
+    mod = load_plugin("test_games/mttt.py")
+    pos, prim, off, kids = graph.enumerate_graph(mod, mod.initial_position(), workers=8)
+    assert len(pos) == 5478
 
 
 def test_enumeration_fails_fast_with_a_projection():
@@ -137,7 +166,7 @@ def test_parallel_walk_never_rebuilds_a_patched_plugin(monkeypatch):
     travels to the workers.  Either way the graph equals the serial walk's."""
     import gamesmanmpi_amd.graph as G
     monkeypatch.setattr(G, "PAR_MIN", 16)
-    monkeypatch.setattr(G, "BATCH", 64)
+    monkeypatch.setattr(G, "PAR_START", 16)
     mod = load_plugin("test_games/mttt.py")
     orig = mod.primitive
     mod.primitive = lambda pos: 1 if orig(pos) == 2 else orig(pos)   # misere: full board LOSS
