@@ -54,6 +54,7 @@ EDGE_MODEL_BYTES_PER_POSITION = 15.5  # SURVEY §8d edge model, 1-B records: 1 w
 COMPULSORY_BYTES_PER_POSITION = 3.0  # SURVEY §8d compulsory bound with 1-B records: 1 write + 2 producer-tier reads
 ORACLE_DIGESTS = os.path.join(REPO, "tests", "golden", "oracle_digests.json")
 METRIC = "positions solved/sec (node) at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
+COLL_DEV = "cuda"   # device of the tensors bench.py's own collectives use ("cpu" under gloo)
 
 
 def _oracle():
@@ -177,7 +178,7 @@ def summed_digest(ctx, world, dist, torch):
     """gm_digest of this rank's table, summed over ranks (mod 2^64) when world > 1."""
     d, m = ctx.digest()
     if world > 1:
-        v = torch.tensor([d - (1 << 64) if d >= (1 << 63) else d, m], dtype=torch.int64, device="cuda")
+        v = torch.tensor([d - (1 << 64) if d >= (1 << 63) else d, m], dtype=torch.int64, device=COLL_DEV)
         dist.all_reduce(v)
         d, m = int(v[0].item()) & ((1 << 64) - 1), int(v[1].item())
     return d, m
@@ -279,7 +280,7 @@ def timed_solves(ctx, root, rank, world, dist, torch, warmup=SIDE_WARMUP, repeat
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+            t = torch.tensor([dt], dtype=torch.float64, device=COLL_DEV)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         ts.append(dt)
@@ -433,6 +434,10 @@ def main():
     ap.add_argument("--block-engine", action="store_true",
                     help="8 heaps: run the block engine (GM_OPT_SUB_INTERLEAVE 10) instead of the box engine, "
                          "sharded with halo exchanges at N > 1 (the round-3 multi-GPU path, for comparison)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N>1 rehearsal on a one-GPU box: every rank on device 0, bench.py's collectives over "
+                         "gloo, no RCCL communicator (the 8-heap box engine needs none), no side configs; the "
+                         "ranks share the GPU, so the time is not a multi-GPU result")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     ap.add_argument("--watchdog", type=float, default=None,
@@ -444,6 +449,11 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    global COLL_DEV
+    if args.rehearse_one_gpu:
+        if args.heaps != 8 or args.block_engine:
+            ap.error("--rehearse-one-gpu runs the 8-heap box engine (no exchange)")
+        local, COLL_DEV, args.no_toot = 0, "cpu", True
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
 
@@ -469,7 +479,10 @@ def main():
     import torch.distributed as dist
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from gamesmanmpi_amd import Context, _lib
 
@@ -479,7 +492,9 @@ def main():
     box = args.heaps == 8 and not args.block_engine
     if not box:
         ctx.set_option(_lib.OPT_SUB_INTERLEAVE, 10)
-    if world > 1:
+    if world > 1 and args.rehearse_one_gpu:
+        ctx.set_comm(rank, world)   # rank and world only: no communicator
+    elif world > 1:
         uid = [None]
         if rank == 0:
             buf = ctypes.create_string_buffer(128)
@@ -524,7 +539,7 @@ def main():
             for _ in range(3):
                 ctx.solve(root)
             torch.cuda.synchronize()
-            dt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3], dtype=torch.float64, device="cuda")
+            dt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3], dtype=torch.float64, device=COLL_DEV)
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
             autotune["batch%d" % b] = (round(float(dt.item()), 4), b)
         _, args.dist_batch = min(autotune.values())
@@ -550,12 +565,12 @@ def main():
     elapsed = time.perf_counter() - t0
     per_rank = None
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         # each rank's own view per step: GPU time of its sharded solve (HIP events on its
         # stream, halo waits included) and host time spent enqueueing it
-        mine = torch.tensor([kernel_ms / args.steps, enqueue_ms / args.steps], dtype=torch.float64, device="cuda")
+        mine = torch.tensor([kernel_ms / args.steps, enqueue_ms / args.steps], dtype=torch.float64, device=COLL_DEV)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         per_rank = [[round(float(x), 4) for x in a.tolist()] for a in allr]
@@ -566,7 +581,7 @@ def main():
     rank_parity = None
     if world > 1:
         d0, m0 = ctx.digest()
-        mine = torch.tensor([d0 - (1 << 64) if d0 >= (1 << 63) else d0, m0], dtype=torch.int64, device="cuda")
+        mine = torch.tensor([d0 - (1 << 64) if d0 >= (1 << 63) else d0, m0], dtype=torch.int64, device=COLL_DEV)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         if rank == 0 and args.virtual_ranks == 1:
@@ -652,6 +667,8 @@ def main():
                                 if (world == 1 or box) else
                                 "HIP events around this rank's whole sharded solve (includes halo waits)")},
         "exchanged_bytes_per_step_rank0": st["exchanged_bytes"],
+        "rehearsal": ("--rehearse-one-gpu: %d ranks sharing ONE GPU over gloo; not a multi-GPU measurement" % world
+                      if args.rehearse_one_gpu else None),
         "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
             "scheme": ("box engine: each rank computes one member of every orbit of heap permutations "
                        "<rotate heaps 0-3> x <swap heaps 4/5 and 6/7> and reads the child boxes it does not "

@@ -59,10 +59,6 @@ struct DenseSub {
     uint64_t *d_acc = nullptr;          // digest / counters
     hipGraphExec_t graph = nullptr;
     hipStream_t graph_stream = nullptr;
-    // row-granular dataflow option (NT_ROWFLOW): items in tier order, per-block progress
-    void *flow_items = nullptr;
-    uint32_t *flow_flags = nullptr, *flow_abort = nullptr;
-    unsigned flow_grid = 0;
     std::vector<hipEvent_t> ev;         // timing events
 };
 
@@ -794,195 +790,6 @@ __global__ __launch_bounds__(256, GM_WK_WAVES) void sub_tier_kernel_wkx(uint8_t 
     wk_solve<HIGH, 0, true>(table, blocks, nblk, s, xoff, xdst);
 }
 
-// ---------------------------------------------------------------------------
-// Waits of the dataflow option below are bounded in time (GM_FLOW_WAIT_TICKS of the
-// 100 MHz clock): a timeout raises `abort`, every later wait is skipped, and the
-// solve reports an error instead of hanging.
-constexpr uint64_t GM_FLOW_WAIT_TICKS = 5000000;   // 50 ms
-struct FlowItem {
-    uint32_t off;   // first block in the tier-sorted block list
-    uint32_t n;     // blocks in the group (1..4)
-};
-
-// ---------------------------------------------------------------------------
-// Row-granular dataflow (GM_OPT_SUB_INTERLEAVE 13, development option): the whole solve as
-// ONE launch of every tier's 4-block groups in tier order, no tier barrier.  Position
-// (a0, a1, c) of a block needs (a0, a1, c) of its child blocks, which pass B makes at the
-// same step tau = a0 + a1 + c, so the 16-B row (a1, c) of a child -- one of pass A's
-// loads -- is final once the child has passed step a1 + c + 15.  Each block publishes
-// `progress` (the last step whose completed rows are globally visible): at checkpoints
-// every few steps the workgroup stores the rows completed since the previous one
-// (write-through `sc1` stores, so pass C disappears), waits for its previous
-// checkpoint's stores, and one lane publishes that checkpoint (MI355X_MICROARCH.md
-// hand-off row 1: `sc1` payload, every storing wave's vmcnt(0), barrier, `sc1` flag;
-// `sc1` loads on the consumer).  A pass-A thread (one row) waits until every child block
-// has published the row's step.  Workgroups are launched in tier order, so a waiting
-// workgroup only waits on earlier ones (dispatched before it); a wait longer than
-// GM_FLOW_WAIT_TICKS raises `abort` and the solve fails loudly.
-constexpr uint32_t RF_DONE = 46;   // progress of a finished block
-#ifndef GM_RF_CK
-#define GM_RF_CK 4   // steps between checkpoints (the last one at step 45)
-#endif
-#ifndef GM_RF_LCPOL
-#define GM_RF_LCPOL CPOL_SC1   // child loads: sc1 (L1-bypassing) for the cross-workgroup hand-off
-#endif
-__device__ __forceinline__ uint32_t rf_load(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int HIGH>
-__global__ __launch_bounds__(256, GM_B4_WAVES) void sub_rowflow_kernel(uint8_t *__restrict__ table,
-                                                                         const uint32_t *__restrict__ blocks,
-                                                                         const FlowItem *__restrict__ items,
-                                                                         uint32_t *progress, uint32_t *abort_flag) {
-    constexpr int K = 4, NMAX = 2 * HIGH > 0 ? 2 * HIGH : 1, NPOS = 4096;
-    __shared__ __attribute__((aligned(16))) uint32_t s[4096];   // 16 KiB
-    __shared__ uint32_t prog_sh[4 * NMAX];
-    const FlowItem item = items[blockIdx.x];
-    if (item.n == 0) return;   // padding of a tier's workgroup count to a multiple of 8
-    const int tid = threadIdx.x;
-#ifdef GM_WK_TRACE
-    const uint64_t tr0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    uint32_t hp[K];
-    bool valid[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        valid[k] = (uint32_t)k < item.n;
-        hp[k] = valid[k] ? blocks[item.off + k] : 0u;
-    }
-    // ---- wait for the rows this thread loads: row (y, z) = chunk tid, final at step y + z + 15
-    auto child_of = [&](int j, uint32_t &ch) {   // child j = 2 * nibble + (s - 1) of block j / NMAX
-        const int k = j / NMAX, m = j % NMAX, nb = m >> 1, sub = (m & 1) + 1;
-        if (HIGH == 0 || !valid[k]) return false;
-        const uint32_t h = (hp[k] >> (4 * nb)) & 15u;
-        if (h < (uint32_t)sub) return false;
-        ch = hp[k] - ((uint32_t)sub << (4 * nb));
-        return true;
-    };
-    if (tid < 4 * NMAX) {
-        uint32_t ch = 0;
-        prog_sh[tid] = child_of(tid, ch) ? rf_load(progress + ch) : RF_DONE;
-    }
-    __syncthreads();
-    {
-        const uint32_t need = (uint32_t)(tid & 15) + (uint32_t)(tid >> 4) + 15u;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-#pragma unroll 1
-        for (int j = 0; j < 4 * NMAX; j++) {
-            if (prog_sh[j] >= need) continue;
-            uint32_t ch = 0;
-            child_of(j, ch);
-            while (rf_load(progress + ch) < need) {
-                __builtin_amdgcn_s_sleep(2);
-                if (rf_load(abort_flag) != 0u) return;
-                if (__builtin_amdgcn_s_memrealtime() - t0 > GM_FLOW_WAIT_TICKS) {
-                    __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    return;
-                }
-            }
-        }
-    }
-#ifdef GM_WK_TRACE
-    __syncthreads();
-    const uint64_t trw = __builtin_amdgcn_s_memrealtime();   // every row's children ready
-#endif
-    // ---- pass A: every child load in flight at once (L1-bypassing sc1 loads: hand-off bytes)
-    {
-        const uint32_t c = tid;
-        u32x4v v[K][NMAX];
-#pragma unroll
-        for (int k = 0; k < K; k++) p4_issue<HIGH, GM_RF_LCPOL>(table, hp[k], valid[k], c, v[k]);
-        uint32_t e[2][4], o[2][4];
-#pragma unroll
-        for (int k = 0; k < K; k += 2) {
-            p4_fold<NMAX>(v[k], e[0], o[0]);
-            p4_fold<NMAX>(v[k + 1], e[1], o[1]);
-            p4_write_pair(s, c, k >> 1, e, o);
-        }
-    }
-    // a thread that returned above (abort) leaves the barrier count short only when the
-    // whole solve is abandoned anyway; every thread of a live workgroup arrives here
-    __syncthreads();
-
-#ifdef GM_WK_TRACE
-    const uint64_t tra = __builtin_amdgcn_s_memrealtime();
-#endif
-    // ---- pass B as in b4_solve (split-register form), with row stores at checkpoints
-    const uint32_t row_done = (uint32_t)(tid & 15) + (uint32_t)(tid >> 4) + 15u;   // chunk tid's final step
-    uint32_t last_ck = 0;
-    auto checkpoint = [&](uint32_t tau) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's rows of the previous checkpoint
-        __syncthreads();
-        if (last_ck && tid < K && valid[tid])
-            __hip_atomic_store(progress + hp[tid], last_ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (row_done > last_ck && row_done <= tau) {   // store row tid of the four blocks
-            u32x4v out[K];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const u32x4v q = *(const u32x4v *)(s + 16 * tid + 4 * j);
-                const uint32_t t01 = __builtin_amdgcn_perm(q[1], q[0], 0x05010400u);
-                const uint32_t t23 = __builtin_amdgcn_perm(q[3], q[2], 0x05010400u);
-                const uint32_t u01 = __builtin_amdgcn_perm(q[1], q[0], 0x07030602u);
-                const uint32_t u23 = __builtin_amdgcn_perm(q[3], q[2], 0x07030602u);
-                out[0][j] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
-                out[1][j] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
-                out[2][j] = __builtin_amdgcn_perm(u23, u01, 0x05040100u);
-                out[3][j] = __builtin_amdgcn_perm(u23, u01, 0x07060302u);
-            }
-#pragma unroll
-            for (int k = 0; k < K; k++)
-                __builtin_amdgcn_raw_buffer_store_b128(out[k], block_rsrc(table + ((uint64_t)hp[k] << 12), valid[k] ? NPOS : 0),
-                                                       16u * tid, 0, CPOL_SC1);
-        }
-        last_ck = tau;
-    };
-    const int a0 = tid & 15, a1 = tid >> 4, s0 = a0 + a1;
-    uint32_t pe1 = 0, po1 = 0, pe2 = 0, po2 = 0;
-    const uint32_t d11 = a1 >= 1 ? 16u : 0u, d12 = a1 >= 2 ? 32u : 0u;
-    if (tid == 0) {
-        const uint32_t v = s[0];
-        uint32_t re = code_lo2(v & 0x00FF00FFu), ro = code_hi2(v & 0xFF00FF00u);
-        if (valid[0] && hp[0] == 0) re = (re & 0xFFFFFF00u) | 255u;   // all heaps empty: LOSS in 0
-        s[0] = re | ro;
-        pe1 = re;
-        po1 = ro;
-    }
-    __syncthreads();
-    for (int tau = 1; tau <= 45; tau++) {
-        const uint32_t n1e = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pe1, 0x111, 0xF, 0xF, true);
-        const uint32_t n1o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)po1, 0x111, 0xF, 0xF, true);
-        const uint32_t n2e = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pe2, 0x112, 0xF, 0xF, true);
-        const uint32_t n2o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)po2, 0x112, 0xF, 0xF, true);
-        const int c = tau - s0;
-        uint32_t re = 0, ro = 0;
-        if (c >= 0 && c <= 15) {
-            const uint32_t o = (uint32_t)(tid + 256 * c);
-            const uint32_t v0 = s[o], v3 = s[o - d11], v4 = s[o - d12];
-            const uint32_t me = pk_max(pk_max(pk_max(v0 & 0x00FF00FFu, v3 & 0x00FF00FFu), pk_max(v4 & 0x00FF00FFu, n1e)),
-                                       pk_max(pk_max(n2e, pe1), pe2));
-            const uint32_t mo = pk_max(pk_max(pk_max(v0, v3), pk_max(v4, n1o)), pk_max(pk_max(n2o, po1), po2));
-            re = code_lo2(me);
-            ro = code_hi2(mo & 0xFF00FF00u);
-            s[o] = re | ro;
-        }
-        pe2 = pe1;
-        po2 = po1;
-        pe1 = re;
-        po1 = ro;
-        __syncthreads();
-        if (tau >= 45 - GM_RF_CK * ((45 - 15) / GM_RF_CK) && (45 - tau) % GM_RF_CK == 0) checkpoint((uint32_t)tau);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid < K && valid[tid]) __hip_atomic_store(progress + hp[tid], RF_DONE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef GM_WK_TRACE
-    if (tid == 0) wk_trace(tr0, tra, trw, hp[0], trw, tra);
-#endif
-}
-
-typedef void (*rowflow_kernel_t)(uint8_t *, const uint32_t *, const FlowItem *, uint32_t *, uint32_t *);
-
 typedef void (*tier_kernel_t)(uint8_t *, const uint32_t *, uint32_t, const uint8_t *);
 typedef void (*tier_kernel_x_t)(uint8_t *, const uint32_t *, uint32_t, const uint8_t *, const uint32_t *,
                                 const uint64_t *);
@@ -1014,7 +821,6 @@ static tier_kernel_t pick_b4(int high) { GM_PICK_HIGH(sub_tier_kernel_b4) }
 static tier_kernel_t pick_wk(int high) { GM_PICK_HIGH(sub_tier_kernel_wk) }
 static tier_kernel_x_t pick_b4x(int high) { if (high < 1) return nullptr; GM_PICK_HIGH(sub_tier_kernel_b4x) }
 static tier_kernel_x_t pick_wkx(int high) { if (high < 1) return nullptr; GM_PICK_HIGH(sub_tier_kernel_wkx) }
-static rowflow_kernel_t pick_rowflow(int high) { GM_PICK_HIGH(sub_rowflow_kernel) }
 
 template <int LOW, int NT>
 static tier_kernel_t pick_high(int high) {
@@ -1052,11 +858,10 @@ static tier_kernel_t pick_kernel(int low, int high, int nt) {
 
 // nt > 0: one block per workgroup of nt threads (any LOW); LOW = 3 only:
 // NT_B4 the four-block kernel on every tier, NT_WALK the walker on tiers of at least
-// wk_min_blocks() blocks (b4 below), NT_ROWFLOW the one-launch row-granular dataflow
-enum { NT_B4 = -2, NT_WALK = -6, NT_ROWFLOW = -9 };
+// wk_min_blocks() blocks (b4 below)
+enum { NT_B4 = -2, NT_WALK = -6 };
 
 bool sub_kernel_exists(int low, int high, int nt) {
-    if (nt == NT_ROWFLOW) return low == 3 && pick_rowflow(high) != nullptr;
     if (nt == NT_B4 || nt == NT_WALK) return low == 3 && pick_b4(high) != nullptr;
     return nt > 0 && pick_kernel(low, high, nt) != nullptr;
 }
@@ -1085,7 +890,6 @@ void launch_sub_tier_x(int high, uint32_t nblocks, uint8_t *table, const uint32_
 int sub_kernel_threads(const Ctx *c, int low) {
     if (low == 3 && c->sub_interleave == 6) return NT_B4;
     if (low == 3 && (c->sub_interleave == 10 || c->sub_interleave == 20)) return NT_WALK;   // 20: box engine at 8 heaps
-    if (low == 3 && c->sub_interleave == 13) return NT_ROWFLOW;
     return c->sub_threads;
 }
 
@@ -1215,25 +1019,6 @@ static int prepare(Ctx *c, DenseSub *d, uint64_t root) {
     GM_HIP(hipMalloc(&d->zero, zbytes));
     GM_HIP(hipMemset(d->zero, 0, zbytes));
     GM_HIP(hipMalloc(&d->d_acc, 2 * sizeof(uint64_t)));
-    if (nt == NT_ROWFLOW) {
-        // one workgroup per group, tiers in order, each tier's workgroups padded to a
-        // multiple of 8 so workgroup b runs on XCD b % 8 with the run xcd_order gives it
-        std::vector<FlowItem> all;
-        for (size_t t = 0; t + 1 < d->tier_off.size(); t++) {
-            const uint32_t nb = d->tier_off[t + 1] - d->tier_off[t], ng = (nb + 3) / 4, q = ng >> 3, r = ng & 7;
-            const uint32_t ng8 = (ng + 7) & ~7u;
-            for (uint32_t b = 0; b < ng8; b++) {
-                const uint32_t x = b & 7u, i = b >> 3, len = x < r ? q + 1 : q;
-                const uint32_t g = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
-                all.push_back(i < len ? FlowItem{d->tier_off[t] + 4 * g, std::min(4u, nb - 4 * g)} : FlowItem{0, 0});
-            }
-        }
-        GM_HIP(hipMalloc(&d->flow_items, all.size() * sizeof(FlowItem)));
-        GM_HIP(hipMemcpy(d->flow_items, all.data(), all.size() * sizeof(FlowItem), hipMemcpyHostToDevice));
-        GM_HIP(hipMalloc(&d->flow_abort, 4));
-        GM_HIP(hipMalloc(&d->flow_flags, nhigh * 4));
-        d->flow_grid = (unsigned)all.size();
-    }
     uint64_t bytes = d->slots;
     if (c->adopted_dense) {
         if (c->adopted_dense_bytes < bytes) {
@@ -1265,17 +1050,6 @@ static int ensure_events(DenseSub *d) {
 
 static int launch_tiers(Ctx *c, DenseSub *d, bool timed) {
     int ntiers = (int)d->tier_off.size() - 1;
-    if (d->nt == NT_ROWFLOW) {
-        const uint64_t nhigh = 1ull << (4 * d->high);
-        if (timed) GM_HIP(hipEventRecord(d->ev[0], c->stream));
-        GM_HIP(hipMemsetAsync(d->flow_abort, 0, 4, c->stream));
-        GM_HIP(hipMemsetAsync(d->flow_flags, 0, nhigh * 4, c->stream));
-        hipLaunchKernelGGL(pick_rowflow(d->high), dim3(d->flow_grid), dim3(256), 0, c->stream, d->table, d->d_blocks,
-                           (const FlowItem *)d->flow_items, d->flow_flags, d->flow_abort);
-        if (timed) GM_HIP(hipEventRecord(d->ev[1], c->stream));
-        GM_HIP(hipGetLastError());
-        return GM_OK;
-    }
     for (int t = 0; t < ntiers; t++) {
         uint32_t nb = d->tier_off[t + 1] - d->tier_off[t];
         if (!nb) continue;
@@ -1343,15 +1117,9 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
         GM_TRY(launch_tiers(c, d, timed));
     }
     uint8_t rs;
-    uint32_t aborted = 0;
     GM_HIP(hipMemcpyAsync(&rs, d->table + root, 1, hipMemcpyDeviceToHost, c->stream));
-    if (d->nt == NT_ROWFLOW) GM_HIP(hipMemcpyAsync(&aborted, d->flow_abort, 4, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     double t1 = now_ms();
-    if (aborted) {
-        set_error("dataflow solve: a wait for a child block timed out");
-        return GM_E_STATE;
-    }
 
 #ifdef GM_WK_TRACE
     if (tpath && tbuf) {   // the entries of this solve, then reset for the next
@@ -1392,7 +1160,7 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
     if (timed) {
         float total = 0;
         int launches = 0;
-        for (int t = 0; t < ntiers && d->nt != NT_ROWFLOW; t++) {
+        for (int t = 0; t < ntiers; t++) {
             if (d->tier_off[t + 1] == d->tier_off[t]) continue;
             launches++;
             if (c->use_graph) continue;
@@ -1400,8 +1168,7 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
             GM_HIP(hipEventElapsedTime(&ms, d->ev[2 * t], d->ev[2 * t + 1]));
             total += ms;
         }
-        if (d->nt == NT_ROWFLOW) launches = 1;
-        if (c->use_graph || d->nt == NT_ROWFLOW) GM_HIP(hipEventElapsedTime(&total, d->ev[0], d->ev[1]));
+        if (c->use_graph) GM_HIP(hipEventElapsedTime(&total, d->ev[0], d->ev[1]));
         c->stats.kernel_ms = total;
         c->stats.kernel_launches = launches;
     }
@@ -1480,8 +1247,6 @@ void dense_sub_free(Ctx *c) {
     if (d->zero) (void)hipFree(d->zero);
     if (d->d_blocks) (void)hipFree(d->d_blocks);
     if (d->d_acc) (void)hipFree(d->d_acc);
-    for (void *p : {(void *)d->flow_items, (void *)d->flow_flags, (void *)d->flow_abort})
-        if (p) (void)hipFree(p);
     delete d;
     c->dsub = nullptr;
 }

@@ -215,9 +215,9 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sub_threads = (int)v;
         return GM_OK;
     case GM_OPT_SUB_INTERLEAVE:
-        if (v != 1 && v != 6 && v != 10 && v != 13 && v != 20) {
-            set_error("sub_interleave must be 1 (one block per workgroup), 6 (four-block kernel), 10 (walker), "
-                      "13 (row-granular dataflow) or 20 (box engine, 8 heaps)");
+        if (v != 1 && v != 6 && v != 10 && v != 20) {
+            set_error("sub_interleave must be 1 (one block per workgroup), 6 (four-block kernel), 10 (walker) "
+                      "or 20 (box engine, 8 heaps)");
             return GM_E_ARG;
         }
         c->sub_interleave = (int)v;
@@ -328,7 +328,9 @@ int gm_set_comm(gm_ctx *h, int rank, int world, const void *uid, int bytes) {
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
     c->rank = rank;
     c->world = world;
-    if (world == 1 && (!uid || bytes <= 0)) return GM_OK;   // no communicator needed
+    // no uid: rank and world only.  Enough for the 8-heap box engine, whose ranks exchange
+    // nothing; the RCCL engines refuse to solve without a communicator (gm_solve)
+    if (!uid || bytes <= 0) return GM_OK;
     if (!uid || bytes < (int)sizeof(ncclUniqueId)) { set_error("uid must hold %d bytes", (int)sizeof(ncclUniqueId)); return GM_E_ARG; }
     if (c->device < 0) { set_error("no HIP device"); return GM_E_HIP; }
     ncclUniqueId id;
@@ -367,6 +369,10 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     // heap counts and GM_OPT_SUB_INTERLEAVE != 20 keep the block engine's sharded path
     const bool box = !force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT &&
                      c->sub.heaps == 8 && c->sub_interleave == 20;
+    if (sharded && !box && c->world > 1 && !c->comm) {
+        set_error("a %d-rank solve of this game needs an RCCL communicator (gm_set_comm with a unique id)", c->world);
+        return GM_E_COMM;
+    }
     if (sharded && !box) eng = (!force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT)
                                    ? GM_ENGINE_DIST_DENSE
                                    : GM_ENGINE_DIST_SPARSE;

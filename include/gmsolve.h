@@ -83,12 +83,12 @@ enum {
                                 the multi-GPU partition on a single device */
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
     GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path: 20 (default) = the box engine at 8 heaps
-                                  (dense_box.hip: 4x4x4x4x2x2x2x2 boxes, 41 launches; other heap counts
-                                  and the sharded path use 10); 10 = the walker kernel on tiers of >= 4096
-                                  blocks, the four-block kernel below; 6 = the four-block kernel
-                                  (byte LDS image, 256-thread barrier walk) on every tier; 13 = the whole
-                                  solve as one row-granular dataflow launch (development option, measured
-                                  slower on one GPU); 1 = one block per workgroup of GM_OPT_SUB_THREADS */
+                                  (dense_box.hip: 4x4x4x4x2x2x2x2 boxes, 41 launches; sharded at N > 1 with
+                                  no exchange, gm_box_plan); other heap counts use 10; 10 = the block
+                                  engine's walker kernel on tiers of >= 4096 blocks, the four-block kernel
+                                  below (sharded at N > 1 with halo exchanges, gm_dist_plan); 6 = the
+                                  four-block kernel (byte LDS image, 256-thread barrier walk) on every tier;
+                                  1 = one block per workgroup of GM_OPT_SUB_THREADS */
     GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton,
                                2 = Hilbert walk of the tier's free high nibbles (default) */
     GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
@@ -172,6 +172,9 @@ int gm_expand_host(gm_ctx *ctx, uint64_t key, uint64_t *children, int cap,
  * world = 1 and a uid, a one-rank communicator is created: with GM_OPT_ENGINE =
  * GM_ENGINE_DIST_SPARSE the hash-sharded engine then runs its RCCL transport on
  * one GPU (self send/recv, all-gather, all-reduce), which tests use. */
+/* uid NULL sets rank and world only, with no communicator: enough for the 8-heap SUBTRACT game on
+ * the box engine (its ranks exchange nothing, gm_box_plan); the other sharded engines then refuse
+ * to solve (GM_E_COMM). */
 int gm_comm_unique_id(void *uid, int bytes);
 int gm_set_comm(gm_ctx *ctx, int rank, int world, const void *uid, int bytes);
 
