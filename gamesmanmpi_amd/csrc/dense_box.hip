@@ -195,19 +195,32 @@ __device__ __forceinline__ void bx_pairs(const bx_u32x4 &x0, const bx_u32x4 &x1,
     }
 }
 
-// Image: position (A, B), A = a0 + 4 p, at dword PITCH p + 16 a0 + B.  A pitch of 68, not
-// 64, puts the 16-B chunks that 16 lanes touch in the fold and the store (whole rows A,
-// one per lane) in distinct banks; the walk's dword accesses then see 2-way conflicts.
+// Image: position (A, B), A = a0 + 4 p, at dword PITCH p + ASTRIDE a0 + B; dword ZSLOT of
+// every p-row is used by no position and kept zero (the walk's slot for a missing b2 / b3
+// neighbour).  The walk reads at per-lane offsets + PITCH T (immediates), so the layout must
+// stay affine in p; among those layouts the LDS bank model (tools/lds_bank_model.py, the
+// CDNA4 rules of MI355X_MICROARCH.md) puts pitch 76 / a0-stride 20 at 15 % fewer LDS cycles
+// than round 3's 68 / 16 (walk 921 vs 1079, fold + store 848 vs 1000 per group).
 #ifndef GM_BOX_PITCH
-#define GM_BOX_PITCH 68
+#define GM_BOX_PITCH 76
 #endif
-constexpr int BX_PITCH = GM_BOX_PITCH;
+#ifndef GM_BOX_ASTRIDE
+#define GM_BOX_ASTRIDE 20
+#endif
+#ifndef GM_BOX_ZSLOT
+#define GM_BOX_ZSLOT 19
+#endif
+constexpr int BX_PITCH = GM_BOX_PITCH, BX_AS = GM_BOX_ASTRIDE, BX_Z = GM_BOX_ZSLOT;
 // rows stay 16-B aligned for ds_read/write_b128 (pitch 74, 8-B aligned rows: 5.3 ms, not 3.3)
-static_assert(BX_PITCH % 4 == 0, "16-B aligned image rows");
+static_assert(BX_PITCH % 4 == 0 && BX_AS % 4 == 0, "16-B aligned image rows");
+static_assert(BX_AS >= 16 && 3 * BX_AS + 16 <= BX_PITCH, "a0 sub-rows inside a p-row, disjoint");
+static_assert(BX_Z >= 0 && BX_Z < BX_PITCH && !(BX_Z < 16) && !(BX_Z >= BX_AS && BX_Z < BX_AS + 16) &&
+                  !(BX_Z >= 2 * BX_AS && BX_Z < 2 * BX_AS + 16) && !(BX_Z >= 3 * BX_AS && BX_Z < 3 * BX_AS + 16),
+              "the zero slot is used by no position");
 constexpr int BX_IMG = 64 * BX_PITCH;     // dwords
 constexpr int BX_PAD = 32;                // guard in front: the walk's (a0-1, a0-2) reads of row 0 at p = 0
 constexpr int BX_LDS = BX_PAD + BX_IMG + 64;   // + one dummy dword per lane for idle walk steps
-__device__ __forceinline__ uint32_t bx_row(uint32_t A) { return (A >> 2) * BX_PITCH + 16u * (A & 3u); }
+__device__ __forceinline__ uint32_t bx_row(uint32_t A) { return (A >> 2) * BX_PITCH + (uint32_t)BX_AS * (A & 3u); }
 constexpr int BX_NLOAD = 48;              // 16-B child rows per lane per group
 
 struct BxGroup {
@@ -471,10 +484,10 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
     const uint32_t v22[4] = {L.v22[0], L.v22[1], L.v22[2], L.v22[3]};
     // position (A = a0 + 4 p, B = b) of step t = p + d at dword base + PITCH t; the
     // neighbour one b2 (b3) step below is 4 (8) dwords lower; a lane without one reads
-    // the row's padding (dwords 64-67, kept zero).  (From the opaque lane, per group:
+    // the row's zero slot (dword ZSLOT).  (From the opaque lane, per group:
     // registers held across the group loop would spill in the fold.)
     const uint32_t a0 = ln & 3u, b = (ln >> 2) & 15u;
-    const int base = (int)(16u * a0 + b) - BX_PITCH * d, zb = 64 + (int)a0 - BX_PITCH * d;
+    const int base = (int)((uint32_t)BX_AS * a0 + b) - BX_PITCH * d, zb = BX_Z - BX_PITCH * d;
     const int base2 = (b & 4u) ? base - 4 : zb, base3 = (b & 8u) ? base - 8 : zb;
     const int dummy = BX_IMG + (int)ln;   // idle steps (before d, after d + 63) use a slot of their own
     // this lane's codes as (a1 - 1, a1 - 2, a2 - 1, a2 - 2) children of the positions 1, 2,
@@ -597,11 +610,9 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
     uint32_t g = g0 + kx;
     if (g >= g1) return;
     const BxLaneC L = bx_lane_consts(lane);
-    // the row padding (dwords 64-67 of each p-row) stays zero: the walk's slots for a
-    // missing b2 / b3 neighbour
-    static_assert(BX_PITCH >= 68, "zero slots");
-#pragma unroll
-    for (int k = 0; k < 4; k++) s[BX_PITCH * lane + 64 + k] = 0;
+    // the zero slot of each p-row (no position uses it): the walk's slot for a missing
+    // b2 / b3 neighbour
+    s[BX_PITCH * lane + BX_Z] = 0;
     bx_u32x4 R[BX_NLOAD];
     BxGroup G = bx_group<SHARD>(boxes, fills, nbox, g);
     bx_issue<SHARD>(table, G, lane, R);

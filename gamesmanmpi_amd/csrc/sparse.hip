@@ -23,6 +23,8 @@
 // SURVEY §0.2); here each distinct position is expanded once.
 #include "sparse_tables.hpp"
 
+#include <hipcub/hipcub.hpp>
+
 namespace gm {
 
 struct Sparse {
@@ -43,6 +45,8 @@ struct Sparse {
     ResRef *d_tabs = nullptr;                   // the tier tables, for the one-launch refill
     uint64_t replay_words = 0;
     hipGraphExec_t graph = nullptr;
+    void *sort_tmp = nullptr;                   // radix-sort scratch of the batch path (largest tier)
+    size_t sort_tmp_bytes = 0;
     gm_stats_t rec_stats{};                     // the recorded solve's counts, restored by a replay
     uint64_t rec_n_positions = 0;               // ... and its position count and per-tier counts: another
     std::vector<uint64_t> rec_tier_counts;      // engine may have solved on this context in between
@@ -133,7 +137,14 @@ __global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restr
 // lane runs the descriptor's move generator, which is arithmetic only), so the
 // memory round trips of one parent overlap.  The won flag (expand) is a ballot over
 // the row, the best child score (retro) a max over the row.
-constexpr uint64_t SPLIT_MAX = 1ull << 16;
+constexpr uint64_t SPLIT_MAX_DEFAULT = 1ull << 16;
+// GM_SPARSE_SPLIT_MAX (test aid) moves the threshold, e.g. to drive small games through the
+// batch kernels below
+static uint64_t split_max() {
+    static const uint64_t v = getenv("GM_SPARSE_SPLIT_MAX") ? strtoull(getenv("GM_SPARSE_SPLIT_MAX"), nullptr, 10)
+                                                             : SPLIT_MAX_DEFAULT;
+    return v;
+}
 constexpr int SPLIT_G = 16;
 
 template <class D>
@@ -220,12 +231,173 @@ __global__ __launch_bounds__(256) void retro_split_kernel(D d, const uint64_t *_
     }
 }
 
+// Large tiers (round 4): the interior list sorted by the key's top BATCH_SORT_BITS bits
+// (one radix-sort pass per 8 bits), and each workgroup takes BATCH_P consecutive parents
+// at a time.  Positions that agree on the top cells of the T and O planes sit together,
+// and they share many children: a workgroup-local hash set in LDS keeps one copy of each
+// child of the batch, so a child reached from several parents of the batch costs one
+// random probe of the multi-GB tier table instead of one per parent (the inserts and the
+// lookups are random 64-B accesses: the roofline of this engine).  The
+// model (tools/expand_dup_model.cpp, Toot 5x4) puts the duplicate inserts such batches
+// remove at ~40 % of all inserts (69 % of inserts are duplicates; in slot order a batch
+// of any size below 64 K parents removes < 1 %).  A child that does not fit the LDS set
+// (probe limit) goes to the global table directly: the set is a filter, never a source.
+constexpr int BATCH_T = 256;                 // threads per workgroup
+constexpr int BATCH_PER = 2;                 // parents per thread and batch
+constexpr int BATCH_P = BATCH_T * BATCH_PER;
+constexpr int BATCH_M = 4096;                // LDS set slots (32 KiB of keys)
+constexpr int BATCH_PROBE = 32;
+constexpr int BATCH_SORT_BITS = 16;
+
+__device__ __forceinline__ uint32_t bset_home(uint64_t k) {
+    return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 52) & (BATCH_M - 1);
+}
+// insert into the LDS set: true if k is now (or already was) in it
+__device__ __forceinline__ bool bset_insert(uint64_t *set, uint64_t k) {
+    uint32_t h = bset_home(k);
+#pragma unroll 1
+    for (int p = 0; p < BATCH_PROBE; p++) {
+        const unsigned long long prev = atomicCAS((unsigned long long *)&set[h], (unsigned long long)EMPTY_KEY,
+                                                  (unsigned long long)k);
+        if (prev == EMPTY_KEY || prev == k) return true;
+        h = (h + 1) & (BATCH_M - 1);
+    }
+    return false;
+}
+__device__ __forceinline__ int bset_find(const uint64_t *set, uint64_t k) {
+    uint32_t h = bset_home(k);
+#pragma unroll 1
+    for (int p = 0; p < BATCH_PROBE; p++) {
+        const uint64_t v = set[h];
+        if (v == k) return (int)h;
+        if (v == EMPTY_KEY) return -1;
+        h = (h + 1) & (BATCH_M - 1);
+    }
+    return -1;
+}
+
+template <class D>
+__global__ __launch_bounds__(BATCH_T) void expand_batch_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n,
+                                                               int64_t tk, Fronts<D::MAX_SKIP> next,
+                                                               uint8_t *__restrict__ iwon, uint32_t *err) {
+    constexpr int S = D::MAX_SKIP;
+    __shared__ uint64_t set[BATCH_M];
+    uint64_t fresh[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) fresh[s] = 0;
+    auto global_insert = [&](uint64_t c) {
+        const int64_t dt = d.tier(c) - tk;
+#pragma unroll
+        for (int s = 0; s < S; s++)
+            if (dt == s + 1 && front_insert(next.t[s], c, err)) fresh[s]++;
+    };
+    for (uint64_t base = blockIdx.x * (uint64_t)BATCH_P; base < n; base += (uint64_t)gridDim.x * BATCH_P) {
+        for (int j = threadIdx.x; j < BATCH_M; j += BATCH_T) set[j] = EMPTY_KEY;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < BATCH_PER; q++) {
+            const uint64_t i = base + (uint64_t)q * BATCH_T + threadIdx.x;
+            if (i >= n) continue;
+            const uint64_t k = ikeys[i];
+            bool won = false;
+            d.visit(k, [&](uint64_t c) {
+                if (!bset_insert(set, c)) global_insert(c);   // the set is full around c
+                if (!won) won = d.primitive(c) == LOSS;
+                return true;
+            });
+            iwon[i] = won ? 1 : 0;
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < BATCH_M; j += BATCH_T) {
+            const uint64_t c = set[j];
+            if (c != EMPTY_KEY) global_insert(c);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
+}
+
+template <class D>
+__global__ __launch_bounds__(BATCH_T) void retro_batch_kernel(D d, const uint64_t *__restrict__ ikeys,
+                                                              const uint32_t *__restrict__ islot,
+                                                              const uint8_t *__restrict__ iwon, uint64_t n, int64_t tk,
+                                                              ResRef self, Ress<D::MAX_SKIP> next, uint32_t *err) {
+    constexpr int S = D::MAX_SKIP;
+    __shared__ uint64_t set[BATCH_M];
+    __shared__ uint16_t score[BATCH_M];
+    auto global_score = [&](uint64_t c) {
+        const int64_t dt = d.tier(c) - tk;
+        int f = -1;
+#pragma unroll
+        for (int s = 0; s < S; s++)
+            if (dt == s + 1) f = res_find(next.t[s], c);
+        if (f < 0) { atomicOr(err, DEV_ERR_MISSING_CHILD); f = 0; }
+        return (uint32_t)f;
+    };
+    for (uint64_t base = blockIdx.x * (uint64_t)BATCH_P; base < n; base += (uint64_t)gridDim.x * BATCH_P) {
+        for (int j = threadIdx.x; j < BATCH_M; j += BATCH_T) set[j] = EMPTY_KEY;
+        __syncthreads();
+        // 1. the batch's undecided children, once each
+#pragma unroll
+        for (int q = 0; q < BATCH_PER; q++) {
+            const uint64_t i = base + (uint64_t)q * BATCH_T + threadIdx.x;
+            if (i >= n || iwon[i]) continue;
+            d.visit(ikeys[i], [&](uint64_t c) {
+                if (d.primitive(c) == UNDECIDED) bset_insert(set, c);   // one that does not fit is looked up later
+                return true;
+            });
+        }
+        __syncthreads();
+        // 2. one lookup per distinct child
+        for (int j = threadIdx.x; j < BATCH_M; j += BATCH_T) {
+            const uint64_t c = set[j];
+            if (c != EMPTY_KEY) score[j] = (uint16_t)global_score(c);
+        }
+        __syncthreads();
+        // 3. each parent's best child from the set (primitive children from primitive())
+#pragma unroll
+        for (int q = 0; q < BATCH_PER; q++) {
+            const uint64_t i = base + (uint64_t)q * BATCH_T + threadIdx.x;
+            if (i >= n) continue;
+            if (iwon[i]) {   // a LOSS-in-0 child: nothing beats it, no lookup needed
+                self.s[islot[i]].score = parent_score(0xFFFFu);
+                continue;
+            }
+            uint32_t best = 0;
+            d.visit(ikeys[i], [&](uint64_t c) {
+                const int p = d.primitive(c);
+                uint32_t sc;
+                if (p != UNDECIDED) {
+                    sc = score_of_primitive(p);
+                } else {
+                    const int h = bset_find(set, c);
+                    sc = h >= 0 ? (uint32_t)score[h] : global_score(c);
+                }
+                best = max(best, sc);
+                return best != 0xFFFFu;
+            });
+            if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
+            self.s[islot[i]].score = parent_score(best);
+        }
+        __syncthreads();
+    }
+}
+
+static bool batch_enabled() {
+    static const bool on = !getenv("GM_SPARSE_BATCH") || atoi(getenv("GM_SPARSE_BATCH")) != 0;
+    return on;
+}
+
 // expand / retro of one tier: the split kernels below SPLIT_MAX interior positions
 template <class D>
 static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fronts<D::MAX_SKIP> &nx, uint32_t *err) {
-    if (T.ni < SPLIT_MAX)
+    if (T.ni < split_max())
         hipLaunchKernelGGL(expand_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys, T.ni,
                            nx, T.iwon, err);
+    else if (T.skeys)
+        hipLaunchKernelGGL(expand_batch_kernel<D>, dim3(grid_for((T.ni + BATCH_PER - 1) / BATCH_PER)), dim3(BATCH_T), 0,
+                           st, d, T.skeys, T.ni, T.tier, nx, T.iwon, err);
     else
         hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.ikeys, T.ni, nx, T.iwon,
                            err);
@@ -234,15 +406,51 @@ static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fro
 template <class D>
 static void launch_retro(hipStream_t st, const D &d, const SpTier &T, const ResRef &self,
                          const Ress<D::MAX_SKIP> &nx, uint32_t *err) {
-    if (T.ni < SPLIT_MAX)
+    if (T.ni < split_max())
         hipLaunchKernelGGL(retro_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys,
                            T.islot, T.iwon, T.ni, self, nx, err);
+    else if (T.skeys)
+        hipLaunchKernelGGL(retro_batch_kernel<D>, dim3(grid_for((T.ni + BATCH_PER - 1) / BATCH_PER)), dim3(BATCH_T), 0,
+                           st, d, T.skeys, T.sslot, T.iwon, T.ni, T.tier, self, nx, err);
     else
         hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.ikeys, T.islot, T.iwon,
                            T.ni, self, nx, err);
 }
 
 // ----------------------------------------------------------------- host side
+// bits of the descriptor keys (the batch path sorts the interior list by the top ones)
+static int key_bits(const Ctx *c) {
+    switch (c->game) {
+    case GM_GAME_TOOT: return 2 * c->toot.A + 16;
+    case GM_GAME_OTHELLO: return 2 * c->oth.A + 16;
+    case GM_GAME_TTT: return 15;
+    case GM_GAME_SUBTRACT: return 4 * c->sub.heaps;
+    }
+    return 64;
+}
+
+// Sort a large tier's interior list by the key's top BATCH_SORT_BITS bits into
+// (skeys, sslot) for the batch kernels; the scratch is kept for the replay's sorts.
+static int batch_sort(Ctx *c, Sparse *sp, SpTier &T, bool alloc) {
+    const int kb = key_bits(c), b0 = std::max(0, kb - BATCH_SORT_BITS);
+    size_t need = 0;
+    GM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, need, T.ikeys, T.skeys, T.islot, T.sslot, (int)T.ni, b0, kb,
+                                             c->stream));
+    if (alloc) {
+        GM_TRY(dev_alloc(c, (void **)&T.skeys, T.ni * 8));
+        GM_TRY(dev_alloc(c, (void **)&T.sslot, T.ni * 4));
+        if (need > sp->sort_tmp_bytes) {
+            if (sp->sort_tmp) dev_free(c, sp->sort_tmp);
+            GM_TRY(dev_alloc(c, &sp->sort_tmp, need));
+            sp->sort_tmp_bytes = need;
+        }
+    }
+    size_t have = sp->sort_tmp_bytes;
+    GM_HIP(hipcub::DeviceRadixSort::SortPairs(sp->sort_tmp, have, T.ikeys, T.skeys, T.islot, T.sslot, (int)T.ni, b0,
+                                             kb, c->stream));
+    return GM_OK;
+}
+
 static int ensure_counts(Sparse *sp, size_t n) {
     if (n <= sp->counts_cap) return GM_OK;
     uint64_t cap = std::max<uint64_t>(64, pow2_at_least(n));
@@ -336,6 +544,7 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
             unsigned long long *scr = tscr + 16 * t;
             launch_classify<D, false>(c->stream, d, Tt.slots, Tt.cap, Tt.ikeys, Tt.islot, scr, err);
             if (!Tt.ni) continue;
+            if (Tt.skeys && batch_sort(c, sp, Tt, false) != GM_OK) return abort_capture(c, GM_E_HIP);
             Fronts<S> nx;   // a tier past the last one received nothing: no table (cap 0)
             for (int s = 0; s < S; s++) nx.t[s] = fref(t + 1 + s);
             launch_expand(c->stream, d, Tt, nx, err);
@@ -437,7 +646,9 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         sp->tiers[t].count = n;
         sp->tiers[t].count_all = sc[11];
         sp->tiers[t].ni = sc[9];
+        sp->tiers[t].tier = sp->t_root + (int64_t)t;
         if (!sp->tiers[t].ni) continue;
+        if (sp->tiers[t].ni >= split_max() && batch_enabled()) GM_TRY(batch_sort(c, sp, sp->tiers[t], true));
         // 2. size the tables of the tiers the children land in: load <= 0.7 for the
         //    predicted distinct children; a misprediction costs one re-run
         if (sp->tiers.size() < t + S + 1) sp->tiers.resize(t + S + 1);
@@ -664,6 +875,7 @@ void sparse_free(Ctx *c) {
     for (void *p : {(void *)sp->d_counts, (void *)sp->d_scratch, (void *)sp->d_err, (void *)sp->d_replay,
                     (void *)sp->d_tabs})
         if (p) (void)hipFree(p);
+    dev_free(c, sp->sort_tmp);
     if (sp->h_replay) (void)hipHostFree(sp->h_replay);
     delete sp;
     c->sp = nullptr;

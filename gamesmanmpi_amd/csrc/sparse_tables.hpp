@@ -57,6 +57,11 @@ struct SpTier {
     uint32_t *islot = nullptr;
     uint8_t *iwon = nullptr;     // per interior position: 1 = has a LOSS-in-0 child (set by expand)
     uint64_t ni = 0;
+    // single-GPU engine, large tiers: the interior list sorted by the key's top bits
+    // (sparse.hip, batch kernels); expand, retro and iwon then follow this order
+    uint64_t *skeys = nullptr;
+    uint32_t *sslot = nullptr;
+    int64_t tier = 0;            // the descriptor tier of the positions (root tier + index)
 };
 
 namespace {
@@ -346,7 +351,8 @@ inline int classify_tier_table(Ctx *c, const D &d, SpTier &T, unsigned long long
 }
 
 inline void free_tier(Ctx *c, SpTier &T) {
-    for (void *p : {(void *)T.slots, (void *)T.ikeys, (void *)T.islot, (void *)T.iwon}) dev_free(c, p);
+    for (void *p : {(void *)T.slots, (void *)T.ikeys, (void *)T.islot, (void *)T.iwon, (void *)T.skeys, (void *)T.sslot})
+        dev_free(c, p);
     T = SpTier{};
 }
 

@@ -242,6 +242,50 @@ def test_walker_kernel_on_every_tier_vs_oracle():
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
+_SPARSE_BATCH_EVERYWHERE = r'''
+import json, os, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+from conftest import golden, digest
+from gamesmanmpi_amd import Context, _lib
+for name, game, params in [("othello_4x4", 4, (4, 4)), ("toot_4x3", 3, (4, 3)), ("ttt", 2, ())]:
+    keys, recs = golden(name)
+    for sym in (1, 0):
+        ctx = Context(game, params, device=0)
+        ctx.set_option(_lib.OPT_ENGINE, _lib.ENGINE_SPARSE)
+        ctx.set_option(_lib.OPT_SYMMETRY, sym)
+        for rep in range(2):   # the synced solve, then the replay (its sorts run in the graph)
+            n, rec = ctx.solve(ctx.initial())
+            k, r = ctx.export()
+            assert n == len(keys) and np.array_equal(k, keys) and np.array_equal(r, recs), (name, sym, rep)
+        ctx.close()
+ref = json.load(open(os.path.join(sys.argv[1], "tests", "golden", "oracle_digests.json")))["toot_4x4"]
+ctx = Context(3, (4, 4), device=0)
+for rep in range(2):
+    n, rec = ctx.solve(ctx.initial())
+    assert ctx.digest() == (ref["digest"], ref["positions"]) and rec == ref["root_record"], rep
+print("ok")
+'''
+
+
+@pytest.mark.parametrize("split_max", ["1", "4096"])
+def test_sparse_batch_kernels_everywhere_vs_golden(split_max):
+    """The sparse engine's batch kernels (interior list sorted by the key's top bits, one
+    LDS-deduplicated insert / lookup per distinct child of a 512-parent batch; csrc/sparse.hip)
+    run only tiers of >= 65,536 interior positions; GM_SPARSE_SPLIT_MAX moves them onto
+    every tier (1) or the mid-size ones of these games (4096), synced solve and replay, with
+    and without the symmetry reduction: the reference plugins' golden tables and the Toot 4x4
+    oracle digest (fresh process: the threshold is read once)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GM_SPARSE_SPLIT_MAX=split_max)
+    r = subprocess.run([sys.executable, "-c", _SPARSE_BATCH_EVERYWHERE, repo], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
 def test_subtract_graph_replay_is_identical(oracle):
     ref = oracle.subtract_dense(5)
     for graph in (0, 1, 1):
