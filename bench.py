@@ -617,7 +617,13 @@ def main():
     rstats = ctx.rank_stats() if box else []
     own_positions = positions if world == 1 else positions / world
     if box and (world > 1 or args.virtual_ranks > 1) and rstats:
-        own_positions = rstats[0]["boxes"] * 4096.0
+        # the launches timed here are this process's: one rank's at N > 1, every virtual
+        # rank's (run one after another on this GPU) with --virtual-ranks
+        own_positions = sum(r["boxes"] for r in rstats) * 4096.0
+    sharded = world > 1 or args.virtual_ranks > 1
+    if sharded:
+        # the committed PMC summary is of the one-GPU solve's launches, not of a rank's
+        traffic_launch, traffic_solve = None, None
     compulsory_per_launch = COMPULSORY_BYTES_PER_POSITION * own_positions / launches_per_solve
     achieved = compulsory_per_launch / avg_launch_s / 1e9 if avg_launch_s > 0 else None
     traffic_gbs = (traffic_launch / avg_launch_s / 1e9) if (traffic_launch and avg_launch_s > 0) else None

@@ -360,8 +360,10 @@ __global__ __launch_bounds__(BATCH_T) void retro_batch_kernel(D d, const uint64_
         for (int q = 0; q < BATCH_PER; q++) {
             const uint64_t i = base + (uint64_t)q * BATCH_T + threadIdx.x;
             if (i >= n) continue;
+            const uint32_t at = islot[i];
+            if (at >= self.cap) { atomicOr(err, DEV_ERR_MISSING_CHILD); continue; }   // never: a corrupt list
             if (iwon[i]) {   // a LOSS-in-0 child: nothing beats it, no lookup needed
-                self.s[islot[i]].score = parent_score(0xFFFFu);
+                self.s[at].score = parent_score(0xFFFFu);
                 continue;
             }
             uint32_t best = 0;
@@ -378,15 +380,31 @@ __global__ __launch_bounds__(BATCH_T) void retro_batch_kernel(D d, const uint64_
                 return best != 0xFFFFu;
             });
             if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
-            self.s[islot[i]].score = parent_score(best);
+            self.s[at].score = parent_score(best);
         }
         __syncthreads();
     }
 }
 
-static bool batch_enabled() {
-    static const bool on = !getenv("GM_SPARSE_BATCH") || atoi(getenv("GM_SPARSE_BATCH")) != 0;
-    return on;
+// development check (GM_SPARSE_BATCH=3): the sorted list holds the same (key, slot) pairs
+__global__ void batch_verify_kernel(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sslot,
+                                    uint64_t n, const RSlot *__restrict__ slots, uint64_t cap,
+                                    unsigned long long *bad) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (sslot[i] >= cap || slots[sslot[i]].key != skeys[i]) atomicAdd(bad, 1ull);
+}
+
+// GM_SPARSE_BATCH: 1 (default) large tiers' interior lists sorted by the key's top bits, plain
+// kernels; 0 unsorted (round 3); 2 sorted + the LDS batch kernels (development option:
+// measured slower); 3 as 1 with a check of every sorted pair (debug)
+static int batch_mode() {
+    static const int m = getenv("GM_SPARSE_BATCH") ? atoi(getenv("GM_SPARSE_BATCH")) : 1;
+    return m;
+}
+static bool batch_enabled() { return batch_mode() != 0; }
+static int sort_bits() {   // GM_SPARSE_SORT_BITS (development): key bits the lists are sorted by
+    static const int b = getenv("GM_SPARSE_SORT_BITS") ? atoi(getenv("GM_SPARSE_SORT_BITS")) : BATCH_SORT_BITS;
+    return b;
 }
 
 // expand / retro of one tier: the split kernels below SPLIT_MAX interior positions
@@ -395,6 +413,9 @@ static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fro
     if (T.ni < split_max())
         hipLaunchKernelGGL(expand_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys, T.ni,
                            nx, T.iwon, err);
+    else if (T.skeys && batch_mode() != 2)
+        hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.skeys, T.ni, nx, T.iwon,
+                           err);
     else if (T.skeys)
         hipLaunchKernelGGL(expand_batch_kernel<D>, dim3(grid_for((T.ni + BATCH_PER - 1) / BATCH_PER)), dim3(BATCH_T), 0,
                            st, d, T.skeys, T.ni, T.tier, nx, T.iwon, err);
@@ -409,6 +430,9 @@ static void launch_retro(hipStream_t st, const D &d, const SpTier &T, const ResR
     if (T.ni < split_max())
         hipLaunchKernelGGL(retro_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys,
                            T.islot, T.iwon, T.ni, self, nx, err);
+    else if (T.skeys && batch_mode() != 2)
+        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.skeys, T.sslot, T.iwon,
+                           T.ni, self, nx, err);
     else if (T.skeys)
         hipLaunchKernelGGL(retro_batch_kernel<D>, dim3(grid_for((T.ni + BATCH_PER - 1) / BATCH_PER)), dim3(BATCH_T), 0,
                            st, d, T.skeys, T.sslot, T.iwon, T.ni, T.tier, self, nx, err);
@@ -432,7 +456,11 @@ static int key_bits(const Ctx *c) {
 // Sort a large tier's interior list by the key's top BATCH_SORT_BITS bits into
 // (skeys, sslot) for the batch kernels; the scratch is kept for the replay's sorts.
 static int batch_sort(Ctx *c, Sparse *sp, SpTier &T, bool alloc) {
-    const int kb = key_bits(c), b0 = std::max(0, kb - BATCH_SORT_BITS);
+    // end bit at most 63: ROCm 7's radix sort with end_bit 64 on u64 keys broke the
+    // (key, value) pairing of about half the pairs (Toot 6x4, whose keys use bit 63:
+    // GM_SPARSE_BATCH=3 counted 67,851 of 132,912 pairs wrong, profiles/r04d_*), so the
+    // top key bit is left out of the grouping (the locality only needs the cells below it)
+    const int kb = std::min(key_bits(c), 63), b0 = std::max(0, kb - sort_bits());
     size_t need = 0;
     GM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, need, T.ikeys, T.skeys, T.islot, T.sslot, (int)T.ni, b0, kb,
                                              c->stream));
@@ -446,8 +474,20 @@ static int batch_sort(Ctx *c, Sparse *sp, SpTier &T, bool alloc) {
         }
     }
     size_t have = sp->sort_tmp_bytes;
+    if (have < need) { set_error("batch sort: scratch of %zu bytes, need %zu", have, need); return GM_E_STATE; }
     GM_HIP(hipcub::DeviceRadixSort::SortPairs(sp->sort_tmp, have, T.ikeys, T.skeys, T.islot, T.sslot, (int)T.ni, b0,
                                              kb, c->stream));
+    if (batch_mode() == 3 && alloc) {
+        GM_HIP(hipMemsetAsync(sp->d_scratch + 13, 0, 8, c->stream));
+        hipLaunchKernelGGL(batch_verify_kernel, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, T.skeys, T.sslot, T.ni,
+                           T.slots, T.cap, sp->d_scratch + 13);
+        unsigned long long bad = 0;
+        GM_HIP(hipMemcpyAsync(&bad, sp->d_scratch + 13, 8, hipMemcpyDeviceToHost, c->stream));
+        GM_HIP(hipStreamSynchronize(c->stream));
+        fprintf(stderr, "[gm] batch sort of tier %lld: %llu interior, %llu pairs differ, scratch %zu of %zu bytes\n",
+                (long long)T.tier, (unsigned long long)T.ni, bad, need, have);
+        if (bad) { set_error("batch sort of tier %lld: %llu pairs differ", (long long)T.tier, bad); return GM_E_STATE; }
+    }
     return GM_OK;
 }
 

@@ -34,10 +34,18 @@ def _order(pos):
 
 
 def fingerprint(pos):
-    """128-bit BLAKE2b digest of the position's pickled key: the identity positions are
-    deduplicated and numbered by in the parallel walk (a collision needs ~2^64
-    positions; the walk is limited to 5e7)."""
-    return hashlib.blake2b(_order(pos), digest_size=16).digest()
+    """128-bit BLAKE2b digest of the position's identity: what the parallel walk
+    deduplicates and numbers positions by (a collision needs ~2^64 positions; the walk
+    is limited to 5e7).  str and int positions (the reference's plugins use both) hash
+    a type tag and their text directly; anything else its pickled key."""
+    t = type(pos)
+    if t is str:
+        b = b"s" + pos.encode("utf-8", "surrogatepass")
+    elif t is int:
+        b = b"i" + str(pos).encode()
+    else:
+        b = b"p" + _order(pos)
+    return hashlib.blake2b(b, digest_size=16).digest()
 
 
 def owner(fp, nw):
