@@ -232,22 +232,25 @@ __global__ __launch_bounds__(256) void retro_split_kernel(D d, const uint64_t *_
 }
 
 // Large tiers (round 4): the interior list sorted by the key's top BATCH_SORT_BITS bits
-// (one radix-sort pass per 8 bits), and each workgroup takes BATCH_P consecutive parents
-// at a time.  Positions that agree on the top cells of the T and O planes sit together,
-// and they share many children: a workgroup-local hash set in LDS keeps one copy of each
-// child of the batch, so a child reached from several parents of the batch costs one
-// random probe of the multi-GB tier table instead of one per parent (the inserts and the
-// lookups are random 64-B accesses: the roofline of this engine).  The
-// model (tools/expand_dup_model.cpp, Toot 5x4) puts the duplicate inserts such batches
-// remove at ~40 % of all inserts (69 % of inserts are duplicates; in slot order a batch
-// of any size below 64 K parents removes < 1 %).  A child that does not fit the LDS set
-// (probe limit) goes to the global table directly: the set is a filter, never a source.
+// (hipcub radix sort of (key, slot) pairs, a few ms per solve).  Positions that agree on
+// the top cells of the T and O planes then sit together and share many children (69 % of
+// the inserts are duplicates; tools/expand_dup_model.cpp), so the plain expand / retro
+// kernels, walking the sorted list, meet a duplicate child while its line is still in L2
+// instead of as one more random 64-B HBM access (the inserts and the lookups are the
+// roofline of this engine).  Default (GM_SPARSE_BATCH 1).
+//
+// Option 2 (measured slower, kept as a development option): each workgroup takes BATCH_P
+// consecutive parents at a time and a workgroup-local hash set in LDS keeps one copy of
+// each child of the batch, so a child reached from several parents costs one probe of
+// the tier table (the model puts the removed inserts at ~40 % of all; in slot order a
+// batch of any size below 64 K parents removes < 1 %).  A child that does not fit the LDS
+// set (probe limit) goes to the global table directly: the set is a filter, never a source.
 constexpr int BATCH_T = 256;                 // threads per workgroup
 constexpr int BATCH_PER = 2;                 // parents per thread and batch
 constexpr int BATCH_P = BATCH_T * BATCH_PER;
 constexpr int BATCH_M = 4096;                // LDS set slots (32 KiB of keys)
 constexpr int BATCH_PROBE = 32;
-constexpr int BATCH_SORT_BITS = 16;
+constexpr int BATCH_SORT_BITS = 24;       // Toot 6x4 per solve: 8 bits 133.3 ms, 16 132.3, 24 129.5, 32 133.9, 48 137.5
 
 __device__ __forceinline__ uint32_t bset_home(uint64_t k) {
     return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 52) & (BATCH_M - 1);

@@ -162,32 +162,46 @@ def _main_importable():
 
 
 class _ShardPool:
-    """The parallel walk's worker processes (spawn), one pipe each."""
+    """The parallel walk's worker processes (spawn): one pipe each to the parent, and a
+    pipe between every two workers for the children they send each other."""
 
     def __init__(self, spec, nw, gen_idx):
         ctx = mp.get_context("spawn")
         self.nw = nw
         self.conns, self.procs = [], []
+        peers = [[None] * nw for _ in range(nw)]
+        for x in range(nw):
+            for y in range(x + 1, nw):
+                peers[x][y], peers[y][x] = ctx.Pipe()
         for w in range(nw):
             a, b = ctx.Pipe()
-            pr = ctx.Process(target=worker_main, args=(b, spec[0], spec[1], tuple(gen_idx), nw), daemon=True)
+            pr = ctx.Process(target=worker_main, args=(b, peers[w], w, spec[0], spec[1], tuple(gen_idx)),
+                             daemon=True)
             pr.start()
             b.close()
             self.conns.append(a)
             self.procs.append(pr)
+        for row in peers:   # the workers hold their ends now
+            for c in row:
+                if c is not None:
+                    c.close()
         self.ready = False
 
-    def _recv(self, w, kind):
-        msg = self.conns[w].recv()
+    def recv(self, w, *kinds):
+        try:
+            msg = self.conns[w].recv()
+        except EOFError:
+            raise RuntimeError("graph walk worker %d exited unexpectedly (exit code %s)"
+                               % (w, self.procs[w].exitcode)) from None
         if msg[0] == "error":
             raise RuntimeError("graph walk worker %d failed:\n%s" % (w, msg[1]))
-        assert msg[0] == kind, msg[0]
+        assert msg[0] in kinds, msg[0]
         return msg
 
     def wait_ready(self):
         if not self.ready:
             for w in range(self.nw):
-                self._recv(w, "ready")
+                self.recv(w, "ready")
             self.ready = True
 
     def poll_ready(self):
@@ -196,20 +210,24 @@ class _ShardPool:
             self.wait_ready()
         return self.ready
 
-    def all(self, msgs, kind):
+    def send(self, msgs):
         for w, m in enumerate(msgs):
             self.conns[w].send(m)
-        return [self._recv(w, kind) for w in range(self.nw)]
 
-    def close(self):
+    def close(self, abort=False):
         """Tell the workers to stop; they leave on their own (daemon processes, reaped by
-        multiprocessing), so the walk does not wait for them."""
+        multiprocessing), so the walk does not wait for them.  After an error the
+        workers may be blocked on each other: they are terminated."""
         for c in self.conns:
             try:
                 c.send(("stop",))
                 c.close()
             except (OSError, EOFError, BrokenPipeError):
                 pass
+        if abort:
+            for pr in self.procs:
+                if pr.is_alive():
+                    pr.terminate()
         self.conns, self.procs = [], []
 
 
@@ -281,73 +299,100 @@ class _Walk:
         G = np.frombuffer(b"".join(fps), dtype="V16")
         order = np.argsort(G, kind="stable")
         self.G, self.GI = G[order], order.astype(np.int64)
+        nw = self.pool.nw
         first = self.n - len(level)
-        shards = [[] for _ in range(self.pool.nw)]
+        owned = [[] for _ in range(nw)]
+        for f in fps[:first]:
+            owned[_owner(f, nw)].append(f)
+        shards = [[] for _ in range(nw)]
         for i, pos in enumerate(level):
-            shards[_owner(fps[first + i], self.pool.nw)].append((first + i, pos))
-        self.pool.all([("seed", pickle.dumps(sh, protocol=4)) for sh in shards], "ok")
+            f = fps[first + i]
+            owned[_owner(f, nw)].append(f)
+            shards[_owner(f, nw)].append((f, pos))
+        self.pool.send([("seed", b"".join(owned[w]), pickle.dumps(shards[w], protocol=4)) for w in range(nw)])
+        self.pool.send([("run",)] * nw)
 
-    def _parallel_level(self):
-        t0 = time.perf_counter()
-        res = self.pool.all([("expand",)] * self.pool.nw, "expanded")
-        t1 = time.perf_counter()
-        idx = np.concatenate([np.frombuffer(r[1], dtype=np.int64) for r in res])
+    def _number_level(self, res):
+        """Number one level from the workers' reports: its parents (numbered a level
+        earlier) in index order, their children's fingerprints in that edge order; a child
+        seen before gets its index, a new one the next index in first-occurrence order --
+        the serial walk's numbering.  Returns the number of new positions."""
+        P = np.concatenate([np.frombuffer(r[1], dtype="V16") for r in res])
         prims = np.concatenate([np.frombuffer(r[2], dtype=np.uint8) for r in res])
         counts = np.concatenate([np.frombuffer(r[3], dtype=np.uint32) for r in res]).astype(np.int64)
         E = np.concatenate([np.frombuffer(r[4], dtype="V16") for r in res])
-        # edges of the parents in index order (the serial walk's order)
+        pat = np.searchsorted(self.G, P)
+        if len(P) and not (np.all(pat < len(self.G)) and np.all(self.G[np.minimum(pat, len(self.G) - 1)] == P)):
+            raise RuntimeError("graph walk: a worker expanded a position the walk never numbered")
+        idx = self.GI[pat]
         start = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
         order = np.argsort(idx, kind="stable")
+        if len(idx) and not np.array_equal(idx[order], np.arange(idx[order[0]], idx[order[0]] + len(idx))):
+            raise RuntimeError("graph walk: the workers' parents are not one level of the walk")
         c = counts[order]
         tot = int(c.sum())
         csum = np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64)
         perm = np.repeat(start[order] - csum, c) + np.arange(tot, dtype=np.int64)
         E = E[perm]
-        for p in prims[order].tolist():
-            if p > 4:
-                raise ValueError("primitive() returned %r, not a src.utils code" % p)
+        if len(prims) and int(prims.max()) > 4:
+            raise ValueError("primitive() returned %r, not a src.utils code" % int(prims.max()))
         self.prim.extend(prims[order].tolist())
         self.off.extend((len(self.kids) + np.cumsum(c)).tolist())
-        # number the children: known ones by lookup, new ones in first-occurrence order
-        if tot:
-            uniq, first, inv = np.unique(E, return_index=True, return_inverse=True)
-            at = np.searchsorted(self.G, uniq)
-            found = np.zeros(len(uniq), dtype=bool)
-            ok = at < len(self.G)
-            found[ok] = self.G[at[ok]] == uniq[ok]
-            uidx = np.empty(len(uniq), dtype=np.int64)
-            uidx[found] = self.GI[at[found]]
-            new = np.flatnonzero(~found)
-            new = new[np.argsort(first[new], kind="stable")]
-            if self.n + len(new) > self.limit:
-                raise TooLarge("more than %d positions: too large for host enumeration (levels %s)"
-                               % (self.limit, self.sizes))
-            uidx[new] = self.n + np.arange(len(new), dtype=np.int64)
-            self.n += len(new)
-            self.kids.extend(uidx[inv.ravel()].tolist())
-            ins = np.sort(new)   # positions of the new fingerprints in uniq (sorted by fingerprint)
-            self.G = np.insert(self.G, at[ins], uniq[ins])
-            self.GI = np.insert(self.GI, at[ins], uidx[ins])
-            new_fp, new_idx = uniq[new], uidx[new]
-        else:
-            new_fp, new_idx = np.zeros(0, dtype="V16"), np.zeros(0, dtype=np.int64)
-        # each owner keeps its new positions; the objects it was sent come with them
+        if not tot:
+            return 0
+        uniq, first, inv = np.unique(E, return_index=True, return_inverse=True)
+        at = np.searchsorted(self.G, uniq)
+        found = np.zeros(len(uniq), dtype=bool)
+        ok = at < len(self.G)
+        found[ok] = self.G[at[ok]] == uniq[ok]
+        uidx = np.empty(len(uniq), dtype=np.int64)
+        uidx[found] = self.GI[at[found]]
+        new = np.flatnonzero(~found)
+        new = new[np.argsort(first[new], kind="stable")]
+        if self.n + len(new) > self.limit:
+            raise TooLarge("more than %d positions: too large for host enumeration (levels %s)"
+                           % (self.limit, self.sizes))
+        uidx[new] = self.n + np.arange(len(new), dtype=np.int64)
+        self.n += len(new)
+        self.kids.extend(uidx[inv.ravel()].tolist())
+        ins = np.sort(new)   # positions of the new fingerprints in uniq (sorted by fingerprint)
+        self.G = np.insert(self.G, at[ins], uniq[ins])
+        self.GI = np.insert(self.GI, at[ins], uidx[ins])
+        return len(new)
+
+    def _parallel_levels(self, level_len, t0):
+        """The workers run the levels on their own; number each from their reports."""
         nw = self.pool.nw
-        own = np.array([_owner(bytes(f), nw) for f in new_fp], dtype=np.int64) if len(new_fp) else \
-            np.zeros(0, dtype=np.int64)
-        msgs = []
-        for w in range(nw):
-            m = own == w
-            msgs.append(("adopt", new_fp[m].tobytes(), new_idx[m].tobytes(), [r[5][w] for r in res]))
-        t2 = time.perf_counter()
-        self.members += sum(r[1] for r in self.pool.all(msgs, "adopted"))
-        if os.environ.get("GM_GRAPH_TRACE"):
-            import sys
-            wt = [r[6] for r in res]
-            print("[graph] level %d: %d parents, %d edges, %d new | expand %.3f s (workers max %.3f min %.3f) "
-                  "number %.3f s adopt %.3f s" % (len(self.sizes), len(idx), tot, len(new_fp), t1 - t0, max(wt),
-                                                  min(wt), t2 - t1, time.perf_counter() - t2), file=sys.stderr)
-        return len(new_fp)
+        trace = os.environ.get("GM_GRAPH_TRACE")
+        while True:
+            tl = time.perf_counter()
+            res = [self.pool.recv(w, "level", "done") for w in range(nw)]
+            kinds = {r[0] for r in res}
+            if kinds == {"done"}:
+                return
+            if kinds != {"level"}:
+                raise RuntimeError("graph walk: the workers disagree on the last level")
+            t1 = time.perf_counter()
+            self.sizes.append(level_len)
+            nxt_len = self._number_level(res)
+            # the next level's position objects, now numbered
+            pos = self.positions
+            pos.extend([None] * (self.n - len(pos)))
+            for w in range(nw):
+                r = self.pool.recv(w, "adopted")
+                F = np.frombuffer(r[1], dtype="V16")
+                if len(F):
+                    for i, p in zip(self.GI[np.searchsorted(self.G, F)].tolist(), pickle.loads(r[2])):
+                        pos[i] = p
+                self.members += r[3]
+            if trace:
+                import sys
+                wt = [r[5] for r in res]
+                print("[graph] level %d: %d parents, %d new | wait %.3f s (workers' expand max %.3f min %.3f) "
+                      "number %.3f s" % (len(self.sizes), level_len, nxt_len, t1 - tl, max(wt), min(wt),
+                                          time.perf_counter() - t1), file=sys.stderr)
+            self._project(level_len, nxt_len, tl, t0)
+            level_len = nxt_len
 
     def _trace(self, what, t):
         if os.environ.get("GM_GRAPH_TRACE"):
@@ -361,45 +406,39 @@ class _Walk:
         level, level_len = [root], 1
         t0 = time.perf_counter()
         projected = 0
+        ok = False
         try:
             while level_len:
                 tl = time.perf_counter()
-                self.sizes.append(level_len)
-                if self.G is None and self.spec is not None:
+                if self.spec is not None:
                     # workers are spawned once the graph is projected past PAR_START positions
                     # (tic-tac-toe never is: ADVICE r03); the parent keeps walking serially
                     # while they import, and hands over at the first level of PAR_MIN
                     # positions it meets with the workers ready (or 8 PAR_MIN, whatever)
                     if self.pool is None and (self.n + projected >= PAR_START or level_len >= 4 * PAR_MIN):
                         self.pool = _ShardPool(self.spec, self.workers, self.gen_idx)
-                        self._trace("spawn of %d workers at level %d" % (self.workers, len(self.sizes)), tl)
+                        self._trace("spawn of %d workers at level %d" % (self.workers, len(self.sizes) + 1), tl)
                     if self.pool is not None and level_len >= PAR_MIN and (self.pool.poll_ready() or
                                                                            level_len >= 8 * PAR_MIN):
                         tw = time.perf_counter()
                         self._go_parallel(level)
                         self._trace("workers ready and seeded", tw)
-                if self.G is None:
-                    level = self._serial_level(level)
-                    nxt_len = len(level)
-                    self._trace("serial level %d (%d positions)" % (len(self.sizes), level_len), tl)
-                else:
-                    nxt_len = self._parallel_level()
+                        break
+                self.sizes.append(level_len)
+                level = self._serial_level(level)
+                nxt_len = len(level)
+                self._trace("serial level %d (%d positions)" % (len(self.sizes), level_len), tl)
                 projected = self._project(level_len, nxt_len, tl, t0)
                 level_len = nxt_len
             self.serial_positions = list(self.positions)
-            if self.G is not None:   # the workers' positions, in index order
-                tg = time.perf_counter()
-                got = self.pool.all([("gather",)] * self.pool.nw, "positions")
-                pos = self.positions + [None] * (self.n - len(self.positions))
-                for r in got:
-                    for i, p in zip(np.frombuffer(r[1], dtype=np.int64).tolist(), pickle.loads(r[2])):
-                        pos[i] = p
-                self.positions = pos
-                self._trace("gather", tg)
+            if self.G is not None:   # the workers run the rest; the parent numbers it
+                del level
+                self._parallel_levels(level_len, t0)
+            ok = True
         finally:
             if self.pool is not None:
                 tc = time.perf_counter()
-                self.pool.close()
+                self.pool.close(abort=not ok)
                 self._trace("close", tc)
         self._trace("walk", t0)
         return (self.positions, np.array(self.prim, dtype=np.uint8), np.array(self.off, dtype=np.uint64),

@@ -97,12 +97,40 @@ def load_fresh(path, name="gm_graph_plugin"):
     return mod
 
 
-def worker_main(conn, path, attrs, gen_idx, nw):
-    """One shard of the parallel walk (a spawned process).  It owns the positions whose
-    fingerprint maps to it: it keeps them, expands the ones of the current level when
-    told, and sends each child object once to the child's owner (relayed by the parent
-    as opaque bytes).  The parent sees only fingerprints, primitive codes and counts."""
+def _exchange(peers, me, blobs):
+    """All-to-all of one message per peer: a thread sends (a pipe holds ~64 KiB, so every
+    worker sending before it receives would deadlock), this thread receives."""
+    import threading
+    nw = len(peers)
+
+    def send():
+        for k in range(1, nw):
+            w = (me + k) % nw
+            peers[w].send_bytes(blobs[w])
+    th = threading.Thread(target=send, daemon=True)
+    th.start()
+    got = [b""] * nw
+    for k in range(1, nw):
+        w = (me - k) % nw
+        got[w] = peers[w].recv_bytes()
+    th.join()
+    return got
+
+
+def worker_main(conn, peers, me, path, attrs, gen_idx):
+    """One shard of the parallel walk (a spawned process), the reference's rank
+    (src/new_process.py:102-162) with pipes for MPI: it owns the positions whose
+    fingerprint maps to it.  Seeded by the parent with the fingerprints it owns so far
+    and its share of the current level, it then runs the levels on its own: expand its
+    frontier, report (parent fingerprints, primitive codes, child counts, child
+    fingerprints) to the parent, send each child object once to the child's owner
+    (directly, one all-to-all per level over `peers`), keep the children it receives
+    that it does not own yet as the next frontier (and send them to the parent, which
+    keeps the position objects), and stop when every worker's frontier is empty.  The
+    parent numbers the positions from the reports while the workers run the next
+    level, off their critical path."""
     import traceback
+    nw = len(peers)
     try:
         mod = load_fresh(path)
         for k, v in attrs.items():   # values the caller set on its module (board size, ...)
@@ -112,52 +140,51 @@ def worker_main(conn, path, attrs, gen_idx, nw):
         conn.send(("error", traceback.format_exc()))
         return
     conn.send(("ready",))
-    frontier = []     # (index, position) of the level to expand, ascending index
-    owned_idx, owned_pos = array.array("q"), []
+    owned = set()
+    frontier = []                       # (fingerprint, position) of the level to expand
     sent = set()      # fingerprints whose object this worker has already shipped
-    while True:
-        msg = conn.recv()
-        try:
-            if msg[0] == "seed":          # positions of the current level (from the serial walk)
-                frontier = sorted(pickle.loads(msg[1]), key=lambda t: t[0])
-                conn.send(("ok",))
-            elif msg[0] == "expand":
-                te = time.perf_counter()
-                idx = array.array("q", (i for i, _ in frontier))
-                prims = bytearray(len(frontier))
-                counts = array.array("I", bytes(4 * len(frontier)))
-                fps = []
-                out = [[] for _ in range(nw)]
-                for n, (_, pos) in enumerate(frontier):
-                    p, kids = expand_one(mod, pos, gens)
-                    prims[n] = p
-                    counts[n] = len(kids)
-                    for c in kids:
-                        f = fingerprint(c)
-                        fps.append(f)
-                        if f not in sent:
-                            sent.add(f)
-                            out[owner(f, nw)].append((f, c))
-                blobs = [pickle.dumps(o, protocol=4) if o else b"" for o in out]
-                conn.send(("expanded", idx.tobytes(), bytes(prims), counts.tobytes(), b"".join(fps), blobs,
-                           time.perf_counter() - te))
-            elif msg[0] == "adopt":       # the new positions this worker owns, and the objects sent to it
-                fp_b, idx_b = msg[1], array.array("q", msg[2])
-                want = {fp_b[16 * j:16 * j + 16]: idx_b[j] for j in range(len(idx_b))}
-                got = {}
-                for blob in msg[3]:
-                    if blob:
-                        for f, c in pickle.loads(blob):
-                            if f in want and f not in got:
-                                got[f] = c
-                frontier = sorted(((i, got[f]) for f, i in want.items()), key=lambda t: t[0])
-                owned_idx.extend(i for i, _ in frontier)
-                owned_pos.extend(c for _, c in frontier)
-                members = sum(len(orbit(c, gens)) for _, c in frontier) if gens else len(frontier)
-                conn.send(("adopted", members))
-            elif msg[0] == "gather":
-                conn.send(("positions", owned_idx.tobytes(), pickle.dumps(owned_pos, protocol=4)))
+    try:
+        while True:
+            msg = conn.recv()
+            if msg[0] == "seed":          # what it owns so far, and its share of the current level
+                fp_b = msg[1]
+                owned.update(fp_b[16 * j:16 * j + 16] for j in range(len(fp_b) // 16))
+                frontier = pickle.loads(msg[2])
+            elif msg[0] == "run":
+                while True:
+                    te = time.perf_counter()
+                    prims = bytearray(len(frontier))
+                    counts = array.array("I", bytes(4 * len(frontier)))
+                    fps = []
+                    out = [[] for _ in range(nw)]
+                    for n, (_, pos) in enumerate(frontier):
+                        p, kids = expand_one(mod, pos, gens)
+                        prims[n] = p
+                        counts[n] = len(kids)
+                        for c in kids:
+                            f = fingerprint(c)
+                            fps.append(f)
+                            if f not in sent:
+                                sent.add(f)
+                                out[owner(f, nw)].append((f, c))
+                    conn.send(("level", b"".join(f for f, _ in frontier), bytes(prims), counts.tobytes(),
+                               b"".join(fps), time.perf_counter() - te))
+                    mine = out[me]
+                    got = _exchange(peers, me, [pickle.dumps(o, protocol=4) if o else b"" for o in out])
+                    frontier = []
+                    for w in range(nw):   # fixed order: the frontier is the same on every run
+                        for f, c in (mine if w == me else (pickle.loads(got[w]) if got[w] else ())):
+                            if f not in owned:
+                                owned.add(f)
+                                frontier.append((f, c))
+                    conn.send(("adopted", b"".join(f for f, _ in frontier),
+                               pickle.dumps([c for _, c in frontier], protocol=4),
+                               sum(len(orbit(c, gens)) for _, c in frontier) if gens else len(frontier)))
+                    sizes = _exchange(peers, me, [b"%d" % len(frontier)] * nw)
+                    if len(frontier) + sum(int(x) for w, x in enumerate(sizes) if w != me) == 0:
+                        conn.send(("done",))
+                        break
             elif msg[0] == "stop":
                 return
-        except BaseException:
-            conn.send(("error", traceback.format_exc()))
+    except BaseException:
+        conn.send(("error", traceback.format_exc()))

@@ -269,18 +269,20 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("split_max", ["1", "4096"])
-def test_sparse_batch_kernels_everywhere_vs_golden(split_max):
-    """The sparse engine's batch kernels (interior list sorted by the key's top bits, one
-    LDS-deduplicated insert / lookup per distinct child of a 512-parent batch; csrc/sparse.hip)
-    run only tiers of >= 65,536 interior positions; GM_SPARSE_SPLIT_MAX moves them onto
-    every tier (1) or the mid-size ones of these games (4096), synced solve and replay, with
-    and without the symmetry reduction: the reference plugins' golden tables and the Toot 4x4
-    oracle digest (fresh process: the threshold is read once)."""
+@pytest.mark.parametrize("split_max,mode", [("1", "1"), ("4096", "1"), ("1", "2"), ("4096", "2"), ("4096", "3")])
+def test_sparse_sorted_lists_everywhere_vs_golden(split_max, mode):
+    """The sparse engine's sorted interior lists (radix-sorted by the key's top bits, then
+    the plain expand / retro kernels: GM_SPARSE_BATCH 1, the default; 2: the LDS batch
+    kernels, one deduplicated insert / lookup per distinct child of a 512-parent batch;
+    3: 1 with every sorted pair checked on the device; csrc/sparse.hip) apply only to
+    tiers of >= 65,536 interior positions; GM_SPARSE_SPLIT_MAX moves them onto every tier
+    (1) or the mid-size ones of these games (4096), synced solve and replay, with and
+    without the symmetry reduction: the reference plugins' golden tables and the Toot 4x4
+    oracle digest (fresh process: the knobs are read once)."""
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, GM_SPARSE_SPLIT_MAX=split_max)
+    env = dict(os.environ, GM_SPARSE_SPLIT_MAX=split_max, GM_SPARSE_BATCH=mode)
     r = subprocess.run([sys.executable, "-c", _SPARSE_BATCH_EVERYWHERE, repo], env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
