@@ -492,8 +492,10 @@ def main():
     box = args.heaps == 8 and not args.block_engine
     if not box:
         ctx.set_option(_lib.OPT_SUB_INTERLEAVE, 10)
-    if world > 1 and args.rehearse_one_gpu:
-        ctx.set_comm(rank, world)   # rank and world only: no communicator
+    if world > 1 and (args.rehearse_one_gpu or box):
+        # the box engine exchanges nothing: rank and world only, no
+        # RCCL communicator of the library's own (torch's process group times the run)
+        ctx.set_comm(rank, world)
     elif world > 1:
         uid = [None]
         if rank == 0:

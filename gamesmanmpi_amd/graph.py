@@ -49,6 +49,13 @@ PAR_MIN = 2048        # positions in a level before the walk goes parallel
 PAR_START = 8192      # positions so far + the projected next level that start the worker processes
 
 
+def _halves(F):
+    """(first 8 bytes, last 8 bytes) of 16-byte fingerprints as big-endian u64, so that the
+    pair orders like the bytes."""
+    w = np.frombuffer(np.ascontiguousarray(F).tobytes(), dtype=">u8")
+    return w[0::2].astype(np.uint64), w[1::2].astype(np.uint64)
+
+
 class TooLarge(RuntimeError):
     """The plugin's reachable set is projected past the host-enumeration limits."""
 
@@ -253,6 +260,7 @@ class _Walk:
         self.n = 0                 # positions numbered so far
         self.G = self.GI = None    # sorted fingerprints of every position, and their indices
         self.members = 0           # orbit members of the positions the workers hold
+        self.prim_parts, self.off_parts, self.kid_parts = [], [], []   # the parallel levels' CSR
 
     def _project(self, level_len, nxt_len, tl, t0):
         if not nxt_len:
@@ -299,6 +307,9 @@ class _Walk:
         G = np.frombuffer(b"".join(fps), dtype="V16")
         order = np.argsort(G, kind="stable")
         self.G, self.GI = G[order], order.astype(np.int64)
+        self.G64, self.Glo = _halves(self.G)
+        self.exact = bool(len(self.G64) > 1 and np.any(self.G64[1:] == self.G64[:-1]))
+        self.nkids = len(self.kids)
         nw = self.pool.nw
         first = self.n - len(level)
         owned = [[] for _ in range(nw)]
@@ -312,19 +323,27 @@ class _Walk:
         self.pool.send([("seed", b"".join(owned[w]), pickle.dumps(shards[w], protocol=4)) for w in range(nw)])
         self.pool.send([("run",)] * nw)
 
+    def _lookup(self, F):
+        """Indices of fingerprints every one of which the walk has numbered."""
+        at = np.searchsorted(self.G, F) if self.exact else np.searchsorted(self.G64, _halves(F)[0])
+        if len(F) and not (np.all(at < len(self.G)) and np.all(self.G[np.minimum(at, len(self.G) - 1)] == F)):
+            raise RuntimeError("graph walk: a worker reported a position the walk never numbered")
+        return self.GI[at]
+
     def _number_level(self, res):
         """Number one level from the workers' reports: its parents (numbered a level
         earlier) in index order, their children's fingerprints in that edge order; a child
         seen before gets its index, a new one the next index in first-occurrence order --
-        the serial walk's numbering.  Returns the number of new positions."""
+        the serial walk's numbering.  Returns the number of new positions.
+
+        Fingerprints are compared by their first 8 bytes (one u64 sort per level) and
+        checked on all 16; should two differ only in the last 8 (p ~ n^2 / 2^65), the
+        level -- and every later one -- is numbered on the whole 16 bytes."""
         P = np.concatenate([np.frombuffer(r[1], dtype="V16") for r in res])
         prims = np.concatenate([np.frombuffer(r[2], dtype=np.uint8) for r in res])
         counts = np.concatenate([np.frombuffer(r[3], dtype=np.uint32) for r in res]).astype(np.int64)
         E = np.concatenate([np.frombuffer(r[4], dtype="V16") for r in res])
-        pat = np.searchsorted(self.G, P)
-        if len(P) and not (np.all(pat < len(self.G)) and np.all(self.G[np.minimum(pat, len(self.G) - 1)] == P)):
-            raise RuntimeError("graph walk: a worker expanded a position the walk never numbered")
-        idx = self.GI[pat]
+        idx = self._lookup(P)
         start = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
         order = np.argsort(idx, kind="stable")
         if len(idx) and not np.array_equal(idx[order], np.arange(idx[order[0]], idx[order[0]] + len(idx))):
@@ -336,15 +355,38 @@ class _Walk:
         E = E[perm]
         if len(prims) and int(prims.max()) > 4:
             raise ValueError("primitive() returned %r, not a src.utils code" % int(prims.max()))
-        self.prim.extend(prims[order].tolist())
-        self.off.extend((len(self.kids) + np.cumsum(c)).tolist())
+        self.prim_parts.append(prims[order])
+        self.off_parts.append(self.nkids + np.cumsum(c))
+        self.nkids += tot
         if not tot:
             return 0
-        uniq, first, inv = np.unique(E, return_index=True, return_inverse=True)
-        at = np.searchsorted(self.G, uniq)
-        found = np.zeros(len(uniq), dtype=bool)
-        ok = at < len(self.G)
-        found[ok] = self.G[at[ok]] == uniq[ok]
+        hi, lo = _halves(E)
+        fast = not self.exact
+        if fast:
+            o = np.argsort(hi)
+            h = hi[o]
+            flag = np.empty(tot, dtype=bool)
+            flag[0] = True
+            np.not_equal(h[1:], h[:-1], out=flag[1:])
+            starts = np.flatnonzero(flag)
+            uhi, first = h[starts], np.minimum.reduceat(o, starts)
+            inv = np.empty(tot, dtype=np.int64)
+            inv[o] = np.cumsum(flag) - 1
+            ulo = lo[first]
+            at = np.searchsorted(self.G64, uhi)
+            found = np.zeros(len(uhi), dtype=bool)
+            ok = at < len(self.G64)
+            found[ok] = self.G64[at[ok]] == uhi[ok]
+            fast = np.array_equal(lo, ulo[inv]) and np.array_equal(self.Glo[at[found]], ulo[found])
+            uniq = E[first]
+        if not fast:   # two fingerprints share their first 8 bytes: whole 16 from here on
+            self.exact = True
+            uniq, first, inv = np.unique(E, return_index=True, return_inverse=True)
+            inv = inv.ravel()
+            at = np.searchsorted(self.G, uniq)
+            found = np.zeros(len(uniq), dtype=bool)
+            ok = at < len(self.G)
+            found[ok] = self.G[at[ok]] == uniq[ok]
         uidx = np.empty(len(uniq), dtype=np.int64)
         uidx[found] = self.GI[at[found]]
         new = np.flatnonzero(~found)
@@ -354,9 +396,12 @@ class _Walk:
                            % (self.limit, self.sizes))
         uidx[new] = self.n + np.arange(len(new), dtype=np.int64)
         self.n += len(new)
-        self.kids.extend(uidx[inv.ravel()].tolist())
+        self.kid_parts.append(uidx[inv])
         ins = np.sort(new)   # positions of the new fingerprints in uniq (sorted by fingerprint)
+        nh, nl = _halves(uniq[ins])
         self.G = np.insert(self.G, at[ins], uniq[ins])
+        self.G64 = np.insert(self.G64, at[ins], nh)
+        self.Glo = np.insert(self.Glo, at[ins], nl)
         self.GI = np.insert(self.GI, at[ins], uidx[ins])
         return len(new)
 
@@ -373,8 +418,10 @@ class _Walk:
             if kinds != {"level"}:
                 raise RuntimeError("graph walk: the workers disagree on the last level")
             t1 = time.perf_counter()
-            self.sizes.append(level_len)
+            if level_len:
+                self.sizes.append(level_len)
             nxt_len = self._number_level(res)
+            t2 = time.perf_counter()
             # the next level's position objects, now numbered
             pos = self.positions
             pos.extend([None] * (self.n - len(pos)))
@@ -382,16 +429,19 @@ class _Walk:
                 r = self.pool.recv(w, "adopted")
                 F = np.frombuffer(r[1], dtype="V16")
                 if len(F):
-                    for i, p in zip(self.GI[np.searchsorted(self.G, F)].tolist(), pickle.loads(r[2])):
+                    for i, p in zip(self._lookup(F).tolist(), pickle.loads(r[2])):
                         pos[i] = p
                 self.members += r[3]
             if trace:
                 import sys
                 wt = [r[5] for r in res]
-                print("[graph] level %d: %d parents, %d new | wait %.3f s (workers' expand max %.3f min %.3f) "
-                      "number %.3f s" % (len(self.sizes), level_len, nxt_len, t1 - tl, max(wt), min(wt),
-                                          time.perf_counter() - t1), file=sys.stderr)
-            self._project(level_len, nxt_len, tl, t0)
+                print("[graph] level %d: %d parents, %d new | wait %.3f s (workers' expand max %.3f (w%d) min %.3f "
+                      "(w%d); parents per worker %d-%d) number %.3f s adopted %.3f s"
+                      % (len(self.sizes), level_len, nxt_len, t1 - tl, max(wt), wt.index(max(wt)), min(wt),
+                         wt.index(min(wt)), min(len(r[2]) for r in res), max(len(r[2]) for r in res),
+                         t2 - t1, time.perf_counter() - t2), file=sys.stderr)
+            if level_len:
+                self._project(level_len, nxt_len, tl, t0)
             level_len = nxt_len
 
     def _trace(self, what, t):
@@ -441,8 +491,10 @@ class _Walk:
                 self.pool.close(abort=not ok)
                 self._trace("close", tc)
         self._trace("walk", t0)
-        return (self.positions, np.array(self.prim, dtype=np.uint8), np.array(self.off, dtype=np.uint64),
-                np.array(self.kids, dtype=np.uint32))
+        return (self.positions,
+                np.concatenate([np.array(self.prim, dtype=np.uint8)] + self.prim_parts),
+                np.concatenate([np.array(self.off, dtype=np.uint64)] + [a.astype(np.uint64) for a in self.off_parts]),
+                np.concatenate([np.array(self.kids, dtype=np.uint32)] + [a.astype(np.uint32) for a in self.kid_parts]))
 
 
 def enumerate_graph(module, root, limit=50_000_000, workers=None, budget_s=3600.0, symmetry=()):

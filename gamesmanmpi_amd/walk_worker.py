@@ -10,6 +10,7 @@ child its owner keeps (lookup / distribute, src/new_process.py:102-162).
 """
 import array
 import hashlib
+import os
 import importlib.util
 import pickle
 import time
@@ -97,39 +98,67 @@ def load_fresh(path, name="gm_graph_plugin"):
     return mod
 
 
-def _exchange(peers, me, blobs):
-    """All-to-all of one message per peer: a thread sends (a pipe holds ~64 KiB, so every
-    worker sending before it receives would deadlock), this thread receives."""
-    import threading
-    nw = len(peers)
+class _Sender:
+    """Sends from a thread, in order: the worker's own thread never blocks on a full pipe
+    (a pipe holds ~64 KiB; two workers blocked on sends to each other would deadlock)."""
 
-    def send():
-        for k in range(1, nw):
-            w = (me + k) % nw
-            peers[w].send_bytes(blobs[w])
-    th = threading.Thread(target=send, daemon=True)
-    th.start()
-    got = [b""] * nw
-    for k in range(1, nw):
-        w = (me - k) % nw
-        got[w] = peers[w].recv_bytes()
-    th.join()
-    return got
+    def __init__(self):
+        import queue
+        import threading
+        self.q = queue.Queue()
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def _run(self):
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            conn, data = item
+            if isinstance(data, bytes):
+                conn.send_bytes(data)
+            else:
+                conn.send(data)
+
+    def put(self, conn, data):
+        self.q.put((conn, data))
+
+    def close(self):
+        self.q.put(None)
+        self.th.join()
+
+
+class _Level:
+    """What a worker reports to the parent for one level it expanded."""
+
+    def __init__(self):
+        self.pfps, self.kfps = [], []
+        self.prims = bytearray()
+        self.counts = array.array("I")
+        self.t = 0.0
+
+
+CHUNK = 256   # positions expanded between two looks at the incoming pipes
 
 
 def worker_main(conn, peers, me, path, attrs, gen_idx):
     """One shard of the parallel walk (a spawned process), the reference's rank
     (src/new_process.py:102-162) with pipes for MPI: it owns the positions whose
     fingerprint maps to it.  Seeded by the parent with the fingerprints it owns so far
-    and its share of the current level, it then runs the levels on its own: expand its
-    frontier, report (parent fingerprints, primitive codes, child counts, child
-    fingerprints) to the parent, send each child object once to the child's owner
-    (directly, one all-to-all per level over `peers`), keep the children it receives
-    that it does not own yet as the next frontier (and send them to the parent, which
-    keeps the position objects), and stop when every worker's frontier is empty.  The
-    parent numbers the positions from the reports while the workers run the next
-    level, off their critical path."""
+    and its share of the current level, it then runs on its own: it expands its
+    frontier a chunk at a time, sends each child object once to the child's owner
+    (directly, tagged with the level), keeps the children it receives that it does not
+    own yet as the next level's frontier, and reports every level to the parent
+    (parent fingerprints, primitive codes, child counts, child fingerprints; then the
+    positions it took for the next level).  Levels overlap: a worker expands the part of
+    level L + 1 it already has while a slower worker finishes level L; a level-L child
+    is taken (or found known) only once every worker's level L - 1 children are in, so a
+    position's level is its breadth-first depth and the parent's numbering, a level
+    behind, is the serial walk's.  It stops when every worker's frontier of one level is
+    empty."""
     import traceback
+    from multiprocessing.connection import wait
+    from collections import defaultdict
     nw = len(peers)
     try:
         mod = load_fresh(path)
@@ -140,51 +169,119 @@ def worker_main(conn, peers, me, path, attrs, gen_idx):
         conn.send(("error", traceback.format_exc()))
         return
     conn.send(("ready",))
-    owned = set()
-    frontier = []                       # (fingerprint, position) of the level to expand
-    sent = set()      # fingerprints whose object this worker has already shipped
+    chunk_n = int(os.environ.get("GM_GRAPH_CHUNK", CHUNK))
+    if os.environ.get("GM_GRAPH_NICE"):
+        os.nice(int(os.environ["GM_GRAPH_NICE"]))
     try:
-        while True:
-            msg = conn.recv()
-            if msg[0] == "seed":          # what it owns so far, and its share of the current level
-                fp_b = msg[1]
-                owned.update(fp_b[16 * j:16 * j + 16] for j in range(len(fp_b) // 16))
-                frontier = pickle.loads(msg[2])
-            elif msg[0] == "run":
-                while True:
-                    te = time.perf_counter()
-                    prims = bytearray(len(frontier))
-                    counts = array.array("I", bytes(4 * len(frontier)))
-                    fps = []
-                    out = [[] for _ in range(nw)]
-                    for n, (_, pos) in enumerate(frontier):
-                        p, kids = expand_one(mod, pos, gens)
-                        prims[n] = p
-                        counts[n] = len(kids)
-                        for c in kids:
-                            f = fingerprint(c)
-                            fps.append(f)
-                            if f not in sent:
-                                sent.add(f)
-                                out[owner(f, nw)].append((f, c))
-                    conn.send(("level", b"".join(f for f, _ in frontier), bytes(prims), counts.tobytes(),
-                               b"".join(fps), time.perf_counter() - te))
-                    mine = out[me]
-                    got = _exchange(peers, me, [pickle.dumps(o, protocol=4) if o else b"" for o in out])
-                    frontier = []
-                    for w in range(nw):   # fixed order: the frontier is the same on every run
-                        for f, c in (mine if w == me else (pickle.loads(got[w]) if got[w] else ())):
-                            if f not in owned:
-                                owned.add(f)
-                                frontier.append((f, c))
-                    conn.send(("adopted", b"".join(f for f, _ in frontier),
-                               pickle.dumps([c for _, c in frontier], protocol=4),
-                               sum(len(orbit(c, gens)) for _, c in frontier) if gens else len(frontier)))
-                    sizes = _exchange(peers, me, [b"%d" % len(frontier)] * nw)
-                    if len(frontier) + sum(int(x) for w, x in enumerate(sizes) if w != me) == 0:
-                        conn.send(("done",))
-                        break
-            elif msg[0] == "stop":
+        msg = conn.recv()
+        if msg[0] != "seed":
+            return
+        fp_b = msg[1]
+        owned = set(fp_b[16 * j:16 * j + 16] for j in range(len(fp_b) // 16))
+        frontier = {0: pickle.loads(msg[2])}
+        if conn.recv()[0] != "run":
+            return
+        out = _Sender()      # to the peers, in order
+        up = _Sender()       # to the parent (which reads the workers in turn)
+        others = [peers[w] for w in range(nw) if w != me]
+        sent = set()         # fingerprints whose object this worker has already shipped
+        acc = 0              # level-acc children are applied on arrival; frontier[acc + 1] is filling
+        ends = defaultdict(int)          # level -> workers done expanding it
+        busy = defaultdict(bool)         # level -> some worker's frontier was non-empty
+        held = defaultdict(list)         # level -> children that arrived early
+        lvl, i, rep = 0, 0, _Level()     # expansion cursor and its report
+        state = {"done": False}
+
+        def apply(tag, items):
+            nxt = frontier.setdefault(tag + 1, [])
+            for f, c in items:
+                if f not in owned:
+                    owned.add(f)
+                    nxt.append((f, c))
+
+        def take(tag, items):
+            if tag == acc:
+                apply(tag, items)
+            else:
+                held[tag].append(items)
+
+        def advance():
+            nonlocal acc
+            while ends[acc] == nw and not state["done"]:
+                nxt = frontier.setdefault(acc + 1, [])   # complete: every level-acc child is in
+                up.put(conn, ("adopted", b"".join(f for f, _ in nxt), pickle.dumps([c for _, c in nxt], protocol=4),
+                              sum(len(orbit(c, gens)) for _, c in nxt) if gens else len(nxt)))
+                if not busy[acc]:
+                    state["done"] = True
+                    return
+                acc += 1
+                for items in held.pop(acc, []):
+                    apply(acc, items)
+
+        def on_message(c):
+            if c is conn:
+                m = conn.recv()
+                if m[0] == "stop":
+                    raise SystemExit
                 return
+            kind, tag, payload = pickle.loads(c.recv_bytes())
+            if kind == "kids":
+                take(tag, payload)
+            else:   # "end": the sender expanded all of its level `tag`
+                ends[tag] += 1
+                busy[tag] = busy[tag] or payload
+                advance()
+
+        while not state["done"]:
+            F = frontier.setdefault(lvl, [])
+            if i < len(F):
+                te = time.perf_counter()
+                chunk = F[i:i + chunk_n]
+                i += len(chunk)
+                dest = [[] for _ in range(nw)]
+                for f0, pos in chunk:
+                    p, kids = expand_one(mod, pos, gens)
+                    rep.pfps.append(f0)
+                    rep.prims.append(p)
+                    rep.counts.append(len(kids))
+                    for c in kids:
+                        f = fingerprint(c)
+                        rep.kfps.append(f)
+                        if f not in sent:
+                            sent.add(f)
+                            dest[owner(f, nw)].append((f, c))
+                for w in range(nw):
+                    if w == me:
+                        if dest[w]:
+                            take(lvl, dest[w])
+                    elif dest[w]:
+                        out.put(peers[w], pickle.dumps(("kids", lvl, dest[w]), protocol=4))
+                rep.t += time.perf_counter() - te
+                for c in wait(others + [conn], timeout=0):
+                    on_message(c)
+            elif lvl <= acc:   # level lvl is complete and expanded
+                up.put(conn, ("level", b"".join(rep.pfps), bytes(rep.prims), rep.counts.tobytes(),
+                              b"".join(rep.kfps), rep.t))
+                end = pickle.dumps(("end", lvl, len(F) > 0), protocol=4)
+                for c in others:
+                    out.put(c, end)
+                ends[lvl] += 1
+                busy[lvl] = busy[lvl] or len(F) > 0
+                del frontier[lvl]
+                lvl, i, rep = lvl + 1, 0, _Level()
+                advance()
+            else:              # wait for the rest of this level's frontier
+                for c in wait(others + [conn]):
+                    on_message(c)
+        out.close()
+        up.put(conn, ("done",))
+        up.close()
+        while conn.recv()[0] != "stop":
+            pass
+    except SystemExit:
+        return
     except BaseException:
-        conn.send(("error", traceback.format_exc()))
+        try:
+            conn.send(("error", traceback.format_exc()))
+        except Exception:
+            pass

@@ -121,6 +121,30 @@ def test_parallel_enumeration_equals_serial(monkeypatch, rel, workers):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("collide", ["first_level", "always"])
+def test_parallel_numbering_survives_8_byte_fingerprint_collisions(monkeypatch, collide):
+    """The parent compares fingerprints by their first 8 bytes and checks all 16; with
+    the first 8 forced equal (as if two positions collided there) the level falls back to
+    the whole 16 bytes -- before the walk goes parallel, or from its first parallel level
+    -- and the numbering is still the serial walk's."""
+    from gamesmanmpi_amd import graph
+    mod = load_plugin("test_games/mttt.py")
+    root = mod.initial_position()
+    serial = enumerate_graph(mod, root, workers=1)
+    real = graph._halves
+
+    def halves(F):
+        hi, lo = real(F)
+        return np.zeros_like(hi) if collide == "always" or len(F) > 2000 else hi, lo
+    monkeypatch.setattr(graph, "_halves", halves)
+    monkeypatch.setattr(graph, "PAR_MIN", 8)
+    monkeypatch.setattr(graph, "PAR_START", 8)
+    par = enumerate_graph(mod, root, workers=2)
+    assert [position_key(p) for p in par[0]] == [position_key(p) for p in serial[0]]
+    for a, b in zip(par[1:], serial[1:]):
+        assert np.array_equal(a, b)
+
+
 def test_parallel_walk_with_declared_symmetry(monkeypatch):
     """The sharded walk on orbit representatives: the workers canonicalise children and
     count the orbit members of the positions they keep (765 orbits, 5,478 positions)."""
