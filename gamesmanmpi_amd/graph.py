@@ -7,14 +7,15 @@ expansion as GameState.expand, src/game_state.py:33-41, primitive positions not
 expanded, src/new_process.py:120-130) -- numbers every distinct position, and
 hands the graph to ``gm_solve_graph``, whose kernels run the retrograde.
 
-Host enumeration is level-synchronous.  A level of at least ``PAR_MIN``
-positions is expanded in batches by a pool of worker processes (the plugin's
-Python runs in parallel; ``GM_HOST_WORKERS``, default the process's CPU share,
-at most 16); the pool is started while the first levels run serially, and the
-parent deduplicates each batch's children as it arrives, in level order, so the
-numbering is the serial walk's.  Workers rebuild the plugin from its file; when
-the caller's module differs from a fresh import in anything that cannot be
-passed along (a replaced function, a changed table), the walk stays serial.  Before each level the walk projects the next one from the
+Host enumeration is breadth-first.  Once the graph is projected past a few
+thousand positions, worker processes take over (``GM_HOST_WORKERS``, default the
+process's CPU share, at most 16; walk_worker.py): each owns the positions whose
+fingerprint maps to it, expands its frontier, sends every child to the child's
+owner and keeps the new ones, and the parent numbers each level from the workers'
+fingerprint reports, so the numbering is the serial walk's.  Workers rebuild the
+plugin from its file; when the caller's module differs from a fresh import in
+anything that cannot be passed along (a replaced function, a changed table), the
+walk stays serial.  Before each level the walk projects the next one from the
 growth so far and stops at once -- with the level sizes and the projection in
 the message -- when the reachable set would pass ``limit`` positions or the
 walk would pass ``budget_s`` seconds: a plugin far too large for host
@@ -46,7 +47,8 @@ from .walk_worker import (_order, canonical, expand_one as _expand_one, fingerpr
 
 UNDECIDED = 4
 PAR_MIN = 2048        # positions in a level before the walk goes parallel
-PAR_START = 8192      # positions so far + the projected next level that start the worker processes
+PAR_START = 8192      # positions so far + the projected next level (or twice that level) that start the
+                      # worker processes
 
 
 def _halves(F):
@@ -169,30 +171,27 @@ def _main_importable():
 
 
 class _ShardPool:
-    """The parallel walk's worker processes (spawn): one pipe each to the parent, and a
-    pipe between every two workers for the children they send each other."""
+    """The parallel walk's worker processes (spawn): one pipe each to the parent; the
+    workers connect to each other themselves (walk_worker._mesh)."""
 
     def __init__(self, spec, nw, gen_idx):
         ctx = mp.get_context("spawn")
         self.nw = nw
         self.conns, self.procs = [], []
-        peers = [[None] * nw for _ in range(nw)]
-        for x in range(nw):
-            for y in range(x + 1, nw):
-                peers[x][y], peers[y][x] = ctx.Pipe()
+        tag = "gm-walk-%d-%d-%s" % (os.getpid(), id(self), os.urandom(4).hex())
+        self.start_s = []
+        self.t_start = time.time()
         for w in range(nw):
+            t = time.perf_counter()
             a, b = ctx.Pipe()
-            pr = ctx.Process(target=worker_main, args=(b, peers[w], w, spec[0], spec[1], tuple(gen_idx)),
-                             daemon=True)
+            pr = ctx.Process(target=worker_main, args=(b, w, nw, tag, spec[0], spec[1], tuple(gen_idx)), daemon=True)
             pr.start()
             b.close()
             self.conns.append(a)
             self.procs.append(pr)
-        for row in peers:   # the workers hold their ends now
-            for c in row:
-                if c is not None:
-                    c.close()
+            self.start_s.append(time.perf_counter() - t)
         self.ready = False
+        self.ready_at = []
 
     def recv(self, w, *kinds):
         try:
@@ -208,7 +207,7 @@ class _ShardPool:
     def wait_ready(self):
         if not self.ready:
             for w in range(self.nw):
-                self.recv(w, "ready")
+                self.ready_at.append(self.recv(w, "ready")[1] - self.t_start)
             self.ready = True
 
     def poll_ready(self):
@@ -456,6 +455,7 @@ class _Walk:
         level, level_len = [root], 1
         t0 = time.perf_counter()
         projected = 0
+        spawned_at = None
         ok = False
         try:
             while level_len:
@@ -465,14 +465,20 @@ class _Walk:
                     # (tic-tac-toe never is: ADVICE r03); the parent keeps walking serially
                     # while they import, and hands over at the first level of PAR_MIN
                     # positions it meets with the workers ready (or 8 PAR_MIN, whatever)
-                    if self.pool is None and (self.n + projected >= PAR_START or level_len >= 4 * PAR_MIN):
+                    if self.pool is None and (self.n + projected >= PAR_START or 2 * projected >= PAR_START
+                                              or level_len >= 4 * PAR_MIN):
                         self.pool = _ShardPool(self.spec, self.workers, self.gen_idx)
-                        self._trace("spawn of %d workers at level %d" % (self.workers, len(self.sizes) + 1), tl)
-                    if self.pool is not None and level_len >= PAR_MIN and (self.pool.poll_ready() or
-                                                                           level_len >= 8 * PAR_MIN):
+                        spawned_at = len(self.sizes)
+                        self._trace("spawn of %d workers at level %d (starts %s)" % (
+                            self.workers, len(self.sizes) + 1, " ".join("%.3f" % x for x in self.pool.start_s)), tl)
+                    # a pool started a level earlier is waited for (its workers start in ~50 ms,
+                    # less than a serial level of PAR_MIN positions)
+                    if self.pool is not None and level_len >= PAR_MIN and (
+                            self.pool.poll_ready() or spawned_at < len(self.sizes) or level_len >= 8 * PAR_MIN):
                         tw = time.perf_counter()
                         self._go_parallel(level)
-                        self._trace("workers ready and seeded", tw)
+                        self._trace("workers ready (%s s after the spawn) and seeded" % " ".join(
+                            "%.3f" % x for x in self.pool.ready_at), tw)
                         break
                 self.sizes.append(level_len)
                 level = self._serial_level(level)

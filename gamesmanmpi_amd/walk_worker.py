@@ -138,10 +138,39 @@ class _Level:
         self.t = 0.0
 
 
-CHUNK = 256   # positions expanded between two looks at the incoming pipes
+CHUNK = 64    # positions expanded between two looks at the incoming pipes (GM_GRAPH_CHUNK)
 
 
-def worker_main(conn, peers, me, path, attrs, gen_idx):
+def _mesh(me, nw, tag, timeout_s=120.0):
+    """Pipes to every other worker: worker w listens on an abstract unix socket named by
+    the walk's tag and w, connects to every lower-numbered worker's and accepts every
+    higher-numbered one's.  The workers build the mesh themselves so the parent never holds
+    the n(n-1) descriptors (growing a threaded process's descriptor table waits for an RCU
+    grace period, ~0.1 s a doubling on a busy host)."""
+    from multiprocessing.connection import Client, Listener
+    name = "\0" + tag + "-%d"
+    lst = Listener(name % me, family="AF_UNIX", backlog=max(1, nw))
+    peers = [None] * nw
+    deadline = time.time() + timeout_s
+    for p in range(me):
+        while True:
+            try:
+                c = Client(name % p, family="AF_UNIX")
+                break
+            except (FileNotFoundError, ConnectionRefusedError):
+                if time.time() > deadline:
+                    raise
+                time.sleep(0.002)
+        c.send_bytes(b"%d" % me)
+        peers[p] = c
+    for _ in range(me + 1, nw):
+        c = lst.accept()
+        peers[int(c.recv_bytes())] = c
+    lst.close()
+    return peers
+
+
+def worker_main(conn, me, nw, tag, path, attrs, gen_idx):
     """One shard of the parallel walk (a spawned process), the reference's rank
     (src/new_process.py:102-162) with pipes for MPI: it owns the positions whose
     fingerprint maps to it.  Seeded by the parent with the fingerprints it owns so far
@@ -159,8 +188,8 @@ def worker_main(conn, peers, me, path, attrs, gen_idx):
     import traceback
     from multiprocessing.connection import wait
     from collections import defaultdict
-    nw = len(peers)
     try:
+        peers = _mesh(me, nw, tag)
         mod = load_fresh(path)
         for k, v in attrs.items():   # values the caller set on its module (board size, ...)
             setattr(mod, k, v)
@@ -168,10 +197,8 @@ def worker_main(conn, peers, me, path, attrs, gen_idx):
     except BaseException:
         conn.send(("error", traceback.format_exc()))
         return
-    conn.send(("ready",))
+    conn.send(("ready", time.time()))
     chunk_n = int(os.environ.get("GM_GRAPH_CHUNK", CHUNK))
-    if os.environ.get("GM_GRAPH_NICE"):
-        os.nice(int(os.environ["GM_GRAPH_NICE"]))
     try:
         msg = conn.recv()
         if msg[0] != "seed":

@@ -184,6 +184,25 @@ def test_enumeration_fails_fast_with_a_projection():
     assert time.perf_counter() - t < 60
 
 
+def test_parallel_walk_fails_fast_and_ends_its_workers(monkeypatch):
+    """The projection stops a sharded walk too: TooLarge is raised from the parent's
+    numbering while the workers run ahead, and the workers are ended (none outlives it)."""
+    import multiprocessing as mp
+    import time
+    from gamesmanmpi_amd import graph
+    monkeypatch.setattr(graph, "PAR_MIN", 64)
+    monkeypatch.setattr(graph, "PAR_START", 64)
+    mod = load_plugin("test_games/othello_bit_new.py")
+    t = time.perf_counter()
+    with pytest.raises(graph.TooLarge):
+        enumerate_graph(mod, mod.initial_position(), limit=20_000, workers=3)
+    assert time.perf_counter() - t < 60
+    deadline = time.time() + 10
+    while mp.active_children() and time.time() < deadline:
+        time.sleep(0.05)
+    assert not mp.active_children()
+
+
 def test_parallel_walk_never_rebuilds_a_patched_plugin(monkeypatch):
     """Workers rebuild the plugin from its file; a caller-replaced function must keep the
     walk serial (else workers would expand the file's game), while a caller-changed table
