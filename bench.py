@@ -652,9 +652,12 @@ def main():
                      "traffic": traffic_launch,
                      "traffic_gbs": traffic_gbs,
                      "traffic_frac": (traffic_gbs / HBM_PEAK_GBS) if traffic_gbs else None,
-                     "kernel": ("box_tier_kernel<%s> (csrc/dense_box.hip: 4x4x4x4x2x2x2x2 boxes, one launch per "
-                                "box-tier%s)" % (("false", "") if (world == 1 and args.virtual_ranks == 1) else
-                                                 ("true", "; this rank's orbit share of the boxes"))
+                     "kernel": (("box_tier_kernel<%s> (csrc/dense_box.hip: 4x4x4x4x2x2x2x2 boxes, one launch "
+                                 "per box-tier)" % ("true" if sharded else "false")
+                                 if launches_per_solve > max(1, args.virtual_ranks) else
+                                 "box_flow_kernel<%s> (csrc/dense_box.hip: 4x4x4x4x2x2x2x2 boxes, every box-tier in "
+                                 "one launch, a box group starting when its child boxes are stored%s)"
+                                 % (("true", "; this rank's orbit share of the boxes") if sharded else ("false", "")))
                                 if box else
                                 "sub_tier_kernel_wk<%d> (tiers of >= 4096 blocks), sub_tier_kernel_b4<%d> (smaller)"
                                 % (args.heaps - 3, args.heaps - 3)),

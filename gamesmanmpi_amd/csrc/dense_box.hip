@@ -264,7 +264,7 @@ __device__ __forceinline__ bx_u32x4 bx_tau_row(const bx_u32x4 &x) {
 // children: a B child's rows are then S's rows, byte-permuted in bx_fold (bx_tau_row);
 // an A child's row A is S's row rotl8(A, 2k) (the A digits move with the heaps), an
 // address change only.
-template <bool SHARD>
+template <bool SHARD, int CPOL = 0>
 __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
                                          bx_u32x4 (&R)[BX_NLOAD]) {
     const __amdgpu_buffer_rsrc_t rt =
@@ -285,7 +285,7 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
 #pragma unroll
                 for (int i = 0; i < 4; i++)
                     R[8 * i + 4 * k + j] = __builtin_bit_cast(
-                        bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * (lane + 64u * i), soff, 0));
+                        bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * (lane + 64u * i), soff, CPOL));
             }
     }
     {
@@ -302,7 +302,7 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
                     for (int v = 0; v < 2; v++) {
                         const uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
                         R[32 + 4 * i + 2 * k + v] =
-                            __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, 0));
+                            __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, CPOL));
                     }
                 } else {
                     // row rotl8(A, 2 rot): the lane's digits rotated (VGPR), digit i's layer
@@ -316,7 +316,7 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
 #pragma unroll
                     for (int v = 0; v < 2; v++)
                         R[32 + 4 * i + 2 * k + v] = __builtin_bit_cast(
-                            bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff + ((3u - v) << (sh + 4u)), 0));
+                            bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff + ((3u - v) << (sh + 4u)), CPOL));
                 }
             }
         }
@@ -677,6 +677,132 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 }
 
 
+// ---------------------------------------------------------------------------
+// One-launch (dataflow) solve, GM_BOX_FLOW: the box-tier launches' groups, tier after
+// tier, go into 8 queues (workgroup w takes from queue w % 8, which hold the same XCD
+// runs as the tiered launches; workgroup k of a queue takes its groups k, k + K, ...), and
+// a group starts as soon as its child boxes are stored
+// instead of when the whole box-tier before it is: the partial last round of each
+// launch fills with the next tier's groups.  Hand-off per box (MI355X_MICROARCH.md,
+// the first row of the sc1 hand-off table): the group's stores are sc1, the wave waits for
+// them, then one lane stores the box's flag (the solve's epoch) sc1; a consumer polls
+// its child boxes' flags with sc1 loads and then reads them with sc1 loads.  A workgroup
+// takes its groups in tier order, so the workgroup whose current group has the lowest tier
+// has all its children stored and never waits (no deadlock while every workgroup is
+// resident: the grid is at most the resident capacity); a wait that outlasts
+// GM_BOX_FLOW_TIMEOUT flags an error that every wave sees and leaves by, and the host then
+// re-solves with the tiered launches.
+#ifndef GM_BOX_FLOW_TIMEOUT
+#define GM_BOX_FLOW_TIMEOUT 20000000ull   // s_memrealtime ticks (100 MHz): 200 ms
+#endif
+struct BxFlow {
+    const uint32_t *groups;   // queue q: groups[qbase[q] + j], j < qlen[q]: box-list index | second box << 31
+    uint32_t qbase[8], qlen[8];
+    uint32_t *ctr;            // [8] error; zeroed before each solve
+    uint32_t *flag;           // per box id: the epoch of the solve that stored it
+    const uint32_t *epoch;    // this solve's epoch
+    uint32_t dev;             // development: 1 = no waits (wrong results; times the rest)
+};
+
+template <bool SHARD>
+__device__ __forceinline__ BxGroup bx_group_rec(const uint32_t *__restrict__ boxes, const uint32_t *__restrict__ fills,
+                                                uint32_t rec) {
+    BxGroup G;
+    const uint32_t i = rec & 0x7FFFFFFFu;
+    const bool two = rec >> 31;
+    G.valid[0] = true;
+    G.box[0] = boxes[i];
+    G.fill[0] = SHARD ? fills[i] : 0u;
+    G.valid[1] = two;
+    G.box[1] = two ? boxes[i + 1] : 0u;
+    G.fill[1] = (SHARD && two) ? fills[i + 1] : 0u;
+    return G;
+}
+
+// the box the group's box k reads for its child along heap dir (bx_issue's choice), ~0 if none
+template <bool SHARD>
+__device__ __forceinline__ uint32_t bx_child_src(const BxGroup &G, uint32_t k, uint32_t dir) {
+    const uint32_t box = k ? G.box[1] : G.box[0], fill = k ? G.fill[1] : G.fill[0];
+    if (!(k ? G.valid[1] : G.valid[0]) || box_coord(box, (int)dir) < 1) return ~0u;
+    uint32_t src = box - box_unit((int)dir);
+    if constexpr (SHARD) {
+        if (dir >= 4) {
+            if ((fill >> (3 * dir)) & 4u) src = bsym_tau_box(src);
+        } else {
+            src = bsym_box((fill >> (3 * dir)) & 3u, src);
+        }
+    }
+    return src;
+}
+
+// lanes 0-15 each wait for one child box of G (k = lane >> 3, heap lane & 7): src, and the
+// flag value `seen` loaded earlier (~0 = none); false when an error (a timeout, here or
+// in another wave) ends the solve
+__device__ __forceinline__ uint32_t bx_flag_src_load(const BxFlow &F, uint32_t src) {
+    return src == ~0u ? 0u : __hip_atomic_load(&F.flag[src], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool bx_wait(const BxFlow &F, uint32_t src, uint32_t seen, uint32_t lane, uint32_t ep) {
+    if (__all(src == ~0u || seen == ep)) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (__all(src == ~0u || bx_flag_src_load(F, src) == ep)) return true;
+        if (__hip_atomic_load(&F.ctr[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > GM_BOX_FLOW_TIMEOUT) {
+            if (lane == 0) atomicOr(&F.ctr[8], 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+template <bool SHARD>
+__global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__restrict__ table,
+                                                                     const uint32_t *__restrict__ boxes,
+                                                                     const uint32_t *__restrict__ fills, BxFlow F) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BX_LDS];
+    uint32_t *s = lds + BX_PAD;
+    const uint32_t lane = threadIdx.x, q = blockIdx.x & 7u, qn = F.qlen[q];
+    const uint32_t *gq = F.groups + F.qbase[q];
+    const uint32_t ep = __builtin_amdgcn_readfirstlane(*F.epoch);
+    // workgroup k of queue q takes its groups k, k + K, k + 2 K, ... (K workgroups per
+    // queue): static, like the tier launches, so no atomic per group
+    const uint32_t K = (gridDim.x - q + 7u) >> 3;
+    uint32_t j = blockIdx.x >> 3;
+    if (j >= qn) return;
+    const BxLaneC L = bx_lane_consts(lane);
+    s[BX_PITCH * lane + BX_Z] = 0;
+    bx_u32x4 R[BX_NLOAD];
+    for (;;) {
+        const BxGroup G = bx_group_rec<SHARD>(boxes, fills, gq[j]);
+        const uint32_t src = lane < 16u ? bx_child_src<SHARD>(G, lane >> 3, lane & 7u) : ~0u;
+        if (!(F.dev & 1u) && !bx_wait(F, src, bx_flag_src_load(F, src), lane, ep)) return;
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_I);
+        bx_issue<SHARD, GM_BOX_STORE_CPOL>(table, G, lane, R);
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_F);
+        bx_fold<SHARD>(s, G, ln, R);
+        BX_LDS_ORDER();
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_W);
+        bx_walk(s, ln, L);
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_S);
+        bx_store(table, G, s, ln);
+        BX_LDS_ORDER();
+        // publish: the wave's sc1 stores done, then one lane stores each box's flag sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            __hip_atomic_store(&F.flag[G.box[0]], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (G.valid[1]) __hip_atomic_store(&F.flag[G.box[1]], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        j += K;
+        if (j >= qn) break;
+    }
+}
+
+__global__ void box_epoch_kernel(uint32_t *epoch) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *epoch += 1u;
+}
+
 // digest of the positions of a box list that lie in the root's region
 __global__ void box_digest_kernel(const uint8_t *__restrict__ table, const uint32_t *__restrict__ boxes, uint64_t nbox,
                                   uint64_t root, unsigned long long *acc) {
@@ -880,6 +1006,8 @@ struct BoxRank {
     hipGraphExec_t graph = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
     float kernel_ms = 0;
+    uint32_t *d_groups = nullptr;     // one-launch solve: the 8 group queues (BxFlow)
+    uint32_t qbase[8] = {}, qlen[8] = {};
 };
 
 struct DenseBox {
@@ -891,7 +1019,86 @@ struct DenseBox {
     int grid_cap = 2048;
     uint64_t *d_acc = nullptr;
     hipStream_t graph_stream = nullptr;
+    bool flow = false;                // one-launch (dataflow) solve (GM_OPT_BOX_FLOW)
+    bool flow_failed = false;         // a dataflow solve timed out: tier launches from then on
+    uint32_t *d_flow = nullptr;       // [0, 9) queue cursors + error, [16] epoch, [64, 64 + 2^20) box flags
 };
+
+// GM_BOX_FLOW (development, overrides GM_OPT_BOX_FLOW): 0 tier launches, 1 dataflow, 2 dataflow
+// without its waits (wrong results: times everything else)
+static int box_flow_env() {
+    static const int v = getenv("GM_BOX_FLOW") ? atoi(getenv("GM_BOX_FLOW")) : -1;
+    return v;
+}
+static bool box_flow_wanted(const Ctx *c, bool shard) {
+    const int e = box_flow_env();
+    if (e >= 0) return e != 0;
+    return c->box_flow < 0 ? shard : c->box_flow != 0;
+}
+
+// The tier launches' groups in 8 queues: queue x = every tier's XCD run x, tier after
+// tier.  Inside a run the groups are ordered by when their child boxes are stored: a
+// group's key is the latest normalised position (0..1 along its queue's run) of its
+// children in the tier before, and the run is sorted by key (stable: Hilbert order among
+// equals), so the first rounds of a tier take the groups whose children the first rounds
+// of the tier before made (GM_BOX_FLOW_ORDER 0: Hilbert order only).
+static void box_flow_queues(BoxRank &R, const std::vector<uint32_t> &boxes, const std::vector<uint32_t> &fills,
+                            bool shard, std::vector<uint32_t> &out) {
+    static const int order = getenv("GM_BOX_FLOW_ORDER") ? atoi(getenv("GM_BOX_FLOW_ORDER")) : 1;
+    std::vector<uint32_t> q[8];
+    std::vector<float> when(1u << 20, 0.0f);   // per box id: normalised position of its group
+    auto child = [&](uint32_t i, int dir) -> uint32_t {
+        const uint32_t box = boxes[i];
+        if (box_coord(box, dir) < 1) return ~0u;
+        uint32_t src = box - box_unit(dir);
+        if (shard) {
+            const uint32_t fill = fills[i];
+            if (dir >= 4) {
+                if ((fill >> (3 * dir)) & 4u) src = bsym_tau_box(src);
+            } else {
+                src = bsym_box((fill >> (3 * dir)) & 3u, src);
+            }
+        }
+        return src;
+    };
+    for (size_t t = 0; t + 1 < R.tier_off.size(); t++) {
+        const uint32_t o = R.tier_off[t], nb = R.tier_off[t + 1] - o, ng = (nb + 1) / 2;
+        const uint32_t qq = ng >> 3, r = ng & 7u;
+        for (uint32_t x = 0; x < 8; x++) {
+            const uint32_t g0 = x * qq + (x < r ? x : r), g1 = g0 + qq + (x < r ? 1u : 0u);
+            std::vector<std::pair<float, uint32_t>> run;
+            for (uint32_t g = g0; g < g1; g++) {
+                const uint32_t i = o + 2 * g;
+                const bool two = i + 1 < o + nb;
+                float key = 0.0f;
+                if (order)
+                    for (uint32_t k = 0; k < (two ? 2u : 1u); k++)
+                        for (int dir = 0; dir < 8; dir++) {
+                            const uint32_t c = child(i + k, dir);
+                            if (c != ~0u) key = std::max(key, when[c]);
+                        }
+                run.push_back({key, i | (two ? 0x80000000u : 0u)});
+            }
+            std::stable_sort(run.begin(), run.end(),
+                             [](const std::pair<float, uint32_t> &a, const std::pair<float, uint32_t> &b) {
+                                 return a.first < b.first;
+                             });
+            for (size_t n = 0; n < run.size(); n++) {
+                const uint32_t rec = run[n].second, i = rec & 0x7FFFFFFFu;
+                const float w = (float)(n + 1) / (float)run.size();
+                when[boxes[i]] = w;
+                if (rec >> 31) when[boxes[i + 1]] = w;
+                q[x].push_back(rec);
+            }
+        }
+    }
+    out.clear();
+    for (int x = 0; x < 8; x++) {
+        R.qbase[x] = (uint32_t)out.size();
+        R.qlen[x] = (uint32_t)q[x].size();
+        out.insert(out.end(), q[x].begin(), q[x].end());
+    }
+}
 
 static int box_prepare(Ctx *c, DenseBox *d, uint64_t root) {
     d->root_hi = box_index_of_key((uint32_t)root) >> 12;
@@ -910,6 +1117,12 @@ static int box_prepare(Ctx *c, DenseBox *d, uint64_t root) {
     }
     const int r0 = d->virt ? 0 : c->rank, r1 = d->virt ? d->world : c->rank + 1;
     d->ranks.resize(r1 - r0);
+    d->flow = box_flow_wanted(c, d->shard);
+    if (d->flow) {
+        const size_t words = 64 + (1u << 20);
+        GM_HIP(hipMalloc(&d->d_flow, words * 4));
+        GM_HIP(hipMemset(d->d_flow, 0, words * 4));
+    }
     for (int r = r0; r < r1; r++) {
         BoxRank &R = d->ranks[r - r0];
         R.rank = r;
@@ -932,6 +1145,12 @@ static int box_prepare(Ctx *c, DenseBox *d, uint64_t root) {
                 GM_HIP(hipMemcpy(R.d_map, P.map.data(), P.map.size(), hipMemcpyHostToDevice));
             }
         }
+        if (d->flow) {
+            std::vector<uint32_t> qs;
+            box_flow_queues(R, P.boxes, P.fills, d->shard, qs);
+            GM_HIP(hipMalloc(&R.d_groups, std::max<size_t>(1, qs.size()) * 4));
+            GM_HIP(hipMemcpy(R.d_groups, qs.data(), qs.size() * 4, hipMemcpyHostToDevice));
+        }
         if (c->adopted_dense && r == r0) {
             R.table = (uint8_t *)c->adopted_dense;
             R.owned = false;
@@ -950,7 +1169,31 @@ static int box_prepare(Ctx *c, DenseBox *d, uint64_t root) {
     return GM_OK;
 }
 
+static int box_launch_flow(Ctx *c, DenseBox *d, BoxRank &R) {
+    BxFlow F;
+    F.groups = R.d_groups;
+    for (int x = 0; x < 8; x++) {
+        F.qbase[x] = R.qbase[x];
+        F.qlen[x] = R.qlen[x];
+    }
+    F.ctr = d->d_flow;
+    F.epoch = d->d_flow + 16;
+    F.flag = d->d_flow + 64;
+    F.dev = box_flow_env() == 2 ? 1u : 0u;
+    GM_HIP(hipMemsetAsync(d->d_flow, 0, 9 * 4, c->stream));
+    hipLaunchKernelGGL(box_epoch_kernel, dim3(1), dim3(64), 0, c->stream, d->d_flow + 16);
+    const uint32_t grid = (uint32_t)d->grid_cap & ~7u;
+    if (d->shard)
+        hipLaunchKernelGGL(box_flow_kernel<true>, dim3(grid), dim3(64), 0, c->stream, R.table, R.d_boxes, R.d_fills, F);
+    else
+        hipLaunchKernelGGL(box_flow_kernel<false>, dim3(grid), dim3(64), 0, c->stream, R.table, R.d_boxes,
+                           (const uint32_t *)nullptr, F);
+    GM_HIP(hipGetLastError());
+    return GM_OK;
+}
+
 static int box_launch_tiers(Ctx *c, DenseBox *d, BoxRank &R) {
+    if (d->flow) return box_launch_flow(c, d, R);
     for (size_t t = 0; t + 1 < R.tier_off.size(); t++) {
         const uint32_t nb = R.tier_off[t + 1] - R.tier_off[t];
         if (!nb) continue;
@@ -968,7 +1211,8 @@ static int box_launch_tiers(Ctx *c, DenseBox *d, BoxRank &R) {
     return GM_OK;
 }
 
-static int box_launches(const BoxRank &R) {
+static int box_launches(const DenseBox *d, const BoxRank &R) {
+    if (d->flow) return 1;
     int n = 0;
     for (size_t t = 0; t + 1 < R.tier_off.size(); t++) n += R.tier_off[t + 1] > R.tier_off[t];
     return n;
@@ -982,7 +1226,8 @@ int dense_box_solve(Ctx *c, uint64_t root) {
     const bool virt = c->world <= 1 && c->virtual_ranks > 1;
     const int world = c->world > 1 ? c->world : c->virtual_ranks;
     if (!d || (c->adopted_dense && d->ranks[0].table != c->adopted_dense) || d->root_hi != rh || d->world != world ||
-        d->virt != virt || (!virt && d->ranks[0].rank != c->rank)) {
+        d->virt != virt || (!virt && d->ranks[0].rank != c->rank) ||
+        (d->flow != box_flow_wanted(c, world > 1) && !d->flow_failed)) {
         dense_box_free(c);
         d = c->dbox = new DenseBox();
         GM_TRY(box_prepare(c, d, root));
@@ -1037,6 +1282,19 @@ int dense_box_solve(Ctx *c, uint64_t root) {
     GM_HIP(hipMemcpyAsync(&rs, d->ranks[0].table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToHost,
                           c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
+    if (d->flow) {
+        uint32_t e = 0;
+        GM_HIP(hipMemcpy(&e, d->d_flow + 8, 4, hipMemcpyDeviceToHost));
+        if (e) {   // a wait timed out: solve again with the tier launches
+            fprintf(stderr, "gmsolve: the one-launch box solve timed out waiting for a child box; "
+                            "re-solving with tier launches\n");
+            for (auto &R : d->ranks)
+                if (R.graph) { (void)hipGraphExecDestroy(R.graph); R.graph = nullptr; }
+            d->flow = false;
+            d->flow_failed = true;
+            return dense_box_solve(c, root);
+        }
+    }
     const double t1 = now_ms();
     c->root_record = record_of_code(rs);
     uint64_t n = 1;
@@ -1053,10 +1311,10 @@ int dense_box_solve(Ctx *c, uint64_t root) {
         c->tier_counts = acc;
     }
     int launches = 0;
-    for (auto &R : d->ranks) launches += box_launches(R);
+    for (auto &R : d->ranks) launches += box_launches(d, R);
     c->stats.n_positions = n;
     c->stats.n_primitive = 1;
-    c->stats.n_tiers = box_launches(d->ranks[0]);
+    c->stats.n_tiers = (int)d->ranks[0].tier_off.size() - 1;
     c->stats.solve_ms = t1 - t0;
     c->stats.backward_ms = t1 - t0;
     c->stats.forward_ms = 0;
@@ -1214,10 +1472,11 @@ void dense_box_free(Ctx *c) {
         for (auto e : R.ev)
             if (e) (void)hipEventDestroy(e);
         if (R.owned && R.table) (void)hipFree(R.table);
-        for (void *q : {(void *)R.d_boxes, (void *)R.d_fills, (void *)R.d_own, (void *)R.d_map})
+        for (void *q : {(void *)R.d_boxes, (void *)R.d_fills, (void *)R.d_own, (void *)R.d_map, (void *)R.d_groups})
             if (q) (void)hipFree(q);
     }
     if (d->d_acc) (void)hipFree(d->d_acc);
+    if (d->d_flow) (void)hipFree(d->d_flow);
     delete d;
     c->dbox = nullptr;
 }

@@ -246,6 +246,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         if (v < 0 || v > 64) { set_error("dist_solo must be 0..64"); return GM_E_ARG; }
         c->dist_solo = (int)v;
         return GM_OK;
+    case GM_OPT_BOX_FLOW:
+        if (v < -1 || v > 1) { set_error("box flow must be -1, 0 or 1"); return GM_E_ARG; }
+        c->box_flow = (int)v;
+        return GM_OK;
     case GM_OPT_SYMMETRY:
         if (v < 0 || v > 1) { set_error("symmetry must be 0 or 1"); return GM_E_ARG; }
         c->symmetry = (int)v;

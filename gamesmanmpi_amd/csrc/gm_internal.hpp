@@ -91,6 +91,7 @@ struct Ctx {
     int dist_solo = 0;       // diagnostic (loopback): enqueue only rank dist_solo-1's tier launches
     int dist_symmetry = 1;   // sharded dense path: halo blocks derivable by a heap swap are filled locally
     int dist_owner = 0;      // sharded dense path: 0 = split heaps in halves, 1 = tier-balanced comparisons
+    int box_flow = -1;       // box engine: -1 dataflow when sharded, 0 tier launches, 1 dataflow (GM_OPT_BOX_FLOW)
     int symmetry = 1;        // sparse engines: store one representative per symmetry orbit (games.hpp)
 
     // results

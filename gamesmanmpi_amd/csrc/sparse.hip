@@ -130,6 +130,119 @@ __global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restr
     }
 }
 
+// Large tiers of descriptors with child_at (Toot): NB children at a time are made in
+// registers and their first table probes issued together, so a lane has NB random
+// accesses in flight instead of one (each visit() callback above waits for its probe
+// before the generator makes the next child).  Same inserts, lookups and scores as
+// expand_kernel / retro_kernel.
+template <class D, int NB>
+__global__ __launch_bounds__(256) void expand_mlp_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n,
+                                                         Fronts<1> next, uint8_t *__restrict__ iwon, uint32_t *err) {
+    static_assert(D::MAX_SKIP == 1, "one tier step");
+    const FrontRef t = next.t[0];
+    const uint64_t lim = t.cap < MAX_PROBE ? t.cap : MAX_PROBE;
+    uint64_t fresh = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL) break;   // the pass is re-run into larger tables
+        const uint64_t k = ikeys[i];
+        bool won = false;
+#pragma unroll
+        for (int j0 = 0; j0 < D::MAXC; j0 += NB) {
+            uint64_t ck[NB], h[NB], cur[NB];
+            bool has[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                has[j] = j0 + j < D::MAXC && d.child_at(k, j0 + j, ck[j]);
+                if (has[j]) {
+                    h[j] = home_slot(ck[j], t.cap);
+                    cur[j] = t.s[h[j]].key;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                if (!has[j]) continue;
+                if (!won) won = d.primitive(ck[j]) == LOSS;
+                for (uint64_t probe = 0;; probe++) {
+                    if (cur[j] == ck[j]) break;
+                    if (cur[j] == EMPTY_KEY) {
+                        const unsigned long long prev = atomicCAS((unsigned long long *)&t.s[h[j]].key,
+                                                                  (unsigned long long)EMPTY_KEY,
+                                                                  (unsigned long long)ck[j]);
+                        if (prev == EMPTY_KEY) { fresh++; break; }
+                        if (prev == ck[j]) break;
+                    }
+                    if (probe + 1 >= lim) { atomicOr(err, DEV_ERR_TABLE_FULL); break; }
+                    h[j] = h[j] + 1 == t.cap ? 0 : h[j] + 1;
+                    cur[j] = t.s[h[j]].key;
+                }
+            }
+        }
+        iwon[i] = won ? 1 : 0;
+    }
+    wave_add(t.count, fresh);
+}
+
+template <class D, int NB>
+__global__ __launch_bounds__(256) void retro_mlp_kernel(D d, const uint64_t *__restrict__ ikeys,
+                                                        const uint32_t *__restrict__ islot,
+                                                        const uint8_t *__restrict__ iwon, uint64_t n, ResRef self,
+                                                        Ress<1> next, uint32_t *err) {
+    static_assert(D::MAX_SKIP == 1, "one tier step");
+    const ResRef t = next.t[0];
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (iwon[i]) {   // a LOSS-in-0 child: nothing beats it, no lookup needed
+            self.s[islot[i]].score = parent_score(0xFFFFu);
+            continue;
+        }
+        const uint64_t k = ikeys[i];
+        uint32_t best = 0;
+#pragma unroll
+        for (int j0 = 0; j0 < D::MAXC; j0 += NB) {
+            uint64_t ck[NB], h[NB];
+            u64x2 v[NB];
+            bool look[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                uint64_t c = 0;
+                look[j] = false;
+                if (j0 + j < D::MAXC && d.child_at(k, j0 + j, c)) {
+                    const int p = d.primitive(c);
+                    if (p != UNDECIDED) best = max(best, score_of_primitive(p));
+                    else look[j] = true;
+                }
+                ck[j] = c;
+                if (look[j] && t.s) {
+                    h[j] = home_slot(c, t.cap);
+                    v[j] = *(const u64x2 *)&t.s[h[j]];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NB; j++) {
+                if (!look[j]) continue;
+                int f = -1;
+                for (uint64_t probe = 0; t.s && probe < t.cap; probe++) {
+                    if (v[j][0] == ck[j]) { f = (int)(v[j][1] & 0xFFFFu); break; }
+                    if (v[j][0] == EMPTY_KEY) break;
+                    h[j] = h[j] + 1 == t.cap ? 0 : h[j] + 1;
+                    v[j] = *(const u64x2 *)&t.s[h[j]];
+                }
+                if (f < 0) { atomicOr(err, DEV_ERR_MISSING_CHILD); f = 0; }
+                best = max(best, (uint32_t)f);
+            }
+        }
+        if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
+        self.s[islot[i]].score = parent_score(best);
+    }
+}
+
+// GM_SPARSE_MLP: children per probe batch of the MLP kernels (0 = off; 4, 6, 8, 12, 16)
+static int mlp_nb() {
+    static const int v = getenv("GM_SPARSE_MLP") ? atoi(getenv("GM_SPARSE_MLP")) : 0;
+    return v;
+}
+
 // Small tiers (fewer than SPLIT_MAX interior positions): latency, not throughput,
 // bounds a tier, and with one lane per parent a lane walks its children's inserts
 // (or lookups) one after the other.  The split kernels give each parent G = 16
@@ -412,7 +525,45 @@ static int sort_bits() {   // GM_SPARSE_SORT_BITS (development): key bits the li
 
 // expand / retro of one tier: the split kernels below SPLIT_MAX interior positions
 template <class D>
+static bool launch_expand_mlp(hipStream_t st, const D &d, const SpTier &T, const Fronts<D::MAX_SKIP> &nx,
+                              uint32_t *err) {
+    if constexpr (child_at_t<D>::value && D::MAX_SKIP == 1) {
+        const uint64_t *keys = T.skeys ? T.skeys : T.ikeys;
+        const dim3 g(grid_for(T.ni)), b(256);
+        switch (mlp_nb()) {
+        case 4: hipLaunchKernelGGL((expand_mlp_kernel<D, 4>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
+        case 6: hipLaunchKernelGGL((expand_mlp_kernel<D, 6>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
+        case 8: hipLaunchKernelGGL((expand_mlp_kernel<D, 8>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
+        case 12: hipLaunchKernelGGL((expand_mlp_kernel<D, 12>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
+        case 16: hipLaunchKernelGGL((expand_mlp_kernel<D, 16>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
+        default: return false;
+        }
+    }
+    return false;
+}
+
+template <class D>
+static bool launch_retro_mlp(hipStream_t st, const D &d, const SpTier &T, const ResRef &self,
+                             const Ress<D::MAX_SKIP> &nx, uint32_t *err) {
+    if constexpr (child_at_t<D>::value && D::MAX_SKIP == 1) {
+        const uint64_t *keys = T.skeys ? T.skeys : T.ikeys;
+        const uint32_t *slots = T.skeys ? T.sslot : T.islot;
+        const dim3 g(grid_for(T.ni)), b(256);
+        switch (mlp_nb()) {
+        case 4: hipLaunchKernelGGL((retro_mlp_kernel<D, 4>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
+        case 6: hipLaunchKernelGGL((retro_mlp_kernel<D, 6>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
+        case 8: hipLaunchKernelGGL((retro_mlp_kernel<D, 8>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
+        case 12: hipLaunchKernelGGL((retro_mlp_kernel<D, 12>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
+        case 16: hipLaunchKernelGGL((retro_mlp_kernel<D, 16>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
+        default: return false;
+        }
+    }
+    return false;
+}
+
+template <class D>
 static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fronts<D::MAX_SKIP> &nx, uint32_t *err) {
+    if (T.ni >= split_max() && batch_mode() != 2 && launch_expand_mlp(st, d, T, nx, err)) return;
     if (T.ni < split_max())
         hipLaunchKernelGGL(expand_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys, T.ni,
                            nx, T.iwon, err);
@@ -430,6 +581,7 @@ static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fro
 template <class D>
 static void launch_retro(hipStream_t st, const D &d, const SpTier &T, const ResRef &self,
                          const Ress<D::MAX_SKIP> &nx, uint32_t *err) {
+    if (T.ni >= split_max() && batch_mode() != 2 && launch_retro_mlp(st, d, T, self, nx, err)) return;
     if (T.ni < split_max())
         hipLaunchKernelGGL(retro_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys,
                            T.islot, T.iwon, T.ni, self, nx, err);

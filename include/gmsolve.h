@@ -102,10 +102,14 @@ enum {
                                (rank bit a = [heap >= 8]); 1 = tier-balanced: rank bits compare two
                                heaps ([h_x < h_y]) while enough heaps remain, [heap >= 8] after, so
                                every rank holds a share of every tier (needs GM_OPT_DIST_SYMMETRY 1) */
-    GM_OPT_SYMMETRY = 14    /* sparse engines, symmetry reduction (the reference's unused
+    GM_OPT_SYMMETRY = 14,   /* sparse engines, symmetry reduction (the reference's unused
                                hook othello_bit_new.py:224-235): 1 (default) = TOOT stores one position
                                per left-right mirror pair when the root is its own mirror image; every
                                count, export, query and digest still covers both positions.  0 = off */
+    GM_OPT_BOX_FLOW = 15    /* box engine (SUBTRACT, 8 heaps): -1 (default) = one-launch dataflow solve
+                               (box_flow_kernel: a box group starts when its child boxes are stored)
+                               for a sharded solve, tier launches on one GPU; 0 = tier launches; 1 =
+                               dataflow always */
 };
 
 /* Buffer roles for gm_adopt_buffer. */

@@ -115,16 +115,19 @@ def _committed(name):
     return json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))[name]
 
 
+@pytest.mark.parametrize("flow", [-1, 0])
 @pytest.mark.parametrize("ranks", [2, 3, 4, 8])
-def test_box_sharded_2_32_matches_oracle_digest(ranks):
+def test_box_sharded_2_32_matches_oracle_digest(ranks, flow):
     """Config 5 on the box engine over virtual ranks: every rank solves its boxes alone, on
     its own table (filled with 0xFF first, so a read of a box the rank never computed would
     show), reading the child boxes it does not compute through heap permutations of its own
     boxes.  The ranks' owned digests sum to the C oracle's digest of the whole table, the
-    root record is the oracle's, and nothing is exchanged."""
+    root record is the oracle's, and nothing is exchanged.  flow -1 (the default: a sharded
+    solve is one dataflow launch per rank, box_flow_kernel) and 0 (tier launches)."""
     ref = _committed("subtract_8")
-    ctx, n, rec = _solve(SUB, (8,), ranks, timing=1)
+    ctx, n, rec = _solve(SUB, (8,), ranks, timing=1, box_flow=flow)
     st = ctx.stats()
+    assert st["kernel_launches"] == (ranks if flow else 41 * ranks)
     assert st["engine"] == _lib.ENGINE_DIST_DENSE and st["exchanged_bytes"] == 0
     assert (n, rec) == (1 << 32, ref["root_record"])
     assert ctx.digest() == (ref["digest"], 1 << 32)
@@ -162,6 +165,29 @@ def test_box_sharded_custom_roots_vs_oracle(oracle, ranks, root):
     assert np.array_equal(ctx.query(sample), orec[:: max(1, len(ok) // 5000)])
     outside = np.array([root + 1 if (root & 15) < 15 else root | 0xF0000000, 0x1FFFFFFFF], dtype=np.uint64)
     assert ctx.query(outside).tolist() == [_lib.REC_UNSOLVED] * 2
+    ctx.close()
+
+
+@pytest.mark.parametrize("root", [0xFFFFFFFF, 0x33337777, 0x000F0FFF, 0x9ABCDEF1])
+def test_box_dataflow_on_one_gpu_vs_oracle(oracle, root):
+    """GM_OPT_BOX_FLOW 1 on one GPU: the whole box-tier chain in one launch, each box group
+    waiting for its child boxes' flags (csrc/dense_box.hip box_flow_kernel), equals the
+    tier launches and, for the full table, the committed C-oracle digest; twice in a row
+    (the second solve's epoch must not accept the first solve's flags)."""
+    tiers, n0, r0 = _solve(SUB, (8,), 1, root=root, box_flow=0)
+    d0 = tiers.digest()
+    tiers.close()
+    ctx, n, rec = _solve(SUB, (8,), 1, root=root, box_flow=1, timing=1)
+    assert ctx.stats()["kernel_launches"] == 1
+    assert (n, rec, ctx.digest()) == (n0, r0, d0)
+    n2, rec2 = ctx.solve(root)
+    assert (n2, rec2, ctx.digest()) == (n0, r0, d0)
+    if root == 0xFFFFFFFF:
+        ref = _committed("subtract_8")
+        assert d0 == (ref["digest"], 1 << 32) and r0 == ref["root_record"]
+    elif root < 16 ** 7:
+        k, r = ctx.export()
+        assert np.array_equal(r, oracle.subtract_dense_mt(7)[k.astype(np.int64)])
     ctx.close()
 
 
