@@ -49,18 +49,6 @@ struct part_visit_t<D, std::void_t<decltype(D::PART_VISIT)>> {
     static constexpr bool value = D::PART_VISIT;
 };
 
-// descriptors that can make their j-th child directly (child_at(k, j, &c), j < MAXC, in
-// visit() order): the sparse engine's large-tier kernels then hold several children in
-// registers and issue their table probes together (sparse.hip, MLP kernels)
-template <class D, class = void>
-struct child_at_t {
-    static constexpr bool value = false;
-};
-template <class D>
-struct child_at_t<D, std::void_t<decltype(D::CHILD_AT)>> {
-    static constexpr bool value = D::CHILD_AT;
-};
-
 struct NoSym {
     GM_HD uint64_t canon(uint64_t k) const { return k; }
     template <class F>
@@ -231,21 +219,6 @@ struct DescToot {
             if (have_t && !f(canon(k - (1ull << tsh) + (1ull << (A + 16 + bit))))) return;
             if (have_o && !f(canon(k - (1ull << osh) + (1ull << (16 + bit))))) return;
         }
-    }
-    // child j of visit()'s order (column x = j / 2 from the right, T piece for even j)
-    static constexpr bool CHILD_AT = true;
-    GM_HD bool child_at(uint64_t k, int j, uint64_t &c) const {
-        const int x = j >> 1;
-        if (x >= L) return false;
-        const uint32_t occ = tplane(k) | oplane(k);
-        const bool p1 = popc64(occ) & 1;
-        const int sh = (j & 1) ? (p1 ? 8 : 0) : (p1 ? 12 : 4);
-        const uint32_t hand = (uint32_t)(k >> sh) & 15u;
-        const int xr = L - 1 - x;
-        if (hand < 1 || hand > 7 || (occ & (1u << xr))) return false;
-        const int bit = L * (H - 1 - popc64(occ & (colmask << xr))) + xr;
-        c = canon(k - (1ull << sh) + (1ull << ((j & 1) ? 16 + bit : A + 16 + bit)));
-        return true;
     }
     GM_HD int children(uint64_t k, uint64_t *out) const { return collect(*this, k, out); }
     GM_HD int64_t tier(uint64_t k) const { return popc64(tplane(k) | oplane(k)); }

@@ -130,119 +130,6 @@ __global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restr
     }
 }
 
-// Large tiers of descriptors with child_at (Toot): NB children at a time are made in
-// registers and their first table probes issued together, so a lane has NB random
-// accesses in flight instead of one (each visit() callback above waits for its probe
-// before the generator makes the next child).  Same inserts, lookups and scores as
-// expand_kernel / retro_kernel.
-template <class D, int NB>
-__global__ __launch_bounds__(256) void expand_mlp_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n,
-                                                         Fronts<1> next, uint8_t *__restrict__ iwon, uint32_t *err) {
-    static_assert(D::MAX_SKIP == 1, "one tier step");
-    const FrontRef t = next.t[0];
-    const uint64_t lim = t.cap < MAX_PROBE ? t.cap : MAX_PROBE;
-    uint64_t fresh = 0;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        if (*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL) break;   // the pass is re-run into larger tables
-        const uint64_t k = ikeys[i];
-        bool won = false;
-#pragma unroll
-        for (int j0 = 0; j0 < D::MAXC; j0 += NB) {
-            uint64_t ck[NB], h[NB], cur[NB];
-            bool has[NB];
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                has[j] = j0 + j < D::MAXC && d.child_at(k, j0 + j, ck[j]);
-                if (has[j]) {
-                    h[j] = home_slot(ck[j], t.cap);
-                    cur[j] = t.s[h[j]].key;
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                if (!has[j]) continue;
-                if (!won) won = d.primitive(ck[j]) == LOSS;
-                for (uint64_t probe = 0;; probe++) {
-                    if (cur[j] == ck[j]) break;
-                    if (cur[j] == EMPTY_KEY) {
-                        const unsigned long long prev = atomicCAS((unsigned long long *)&t.s[h[j]].key,
-                                                                  (unsigned long long)EMPTY_KEY,
-                                                                  (unsigned long long)ck[j]);
-                        if (prev == EMPTY_KEY) { fresh++; break; }
-                        if (prev == ck[j]) break;
-                    }
-                    if (probe + 1 >= lim) { atomicOr(err, DEV_ERR_TABLE_FULL); break; }
-                    h[j] = h[j] + 1 == t.cap ? 0 : h[j] + 1;
-                    cur[j] = t.s[h[j]].key;
-                }
-            }
-        }
-        iwon[i] = won ? 1 : 0;
-    }
-    wave_add(t.count, fresh);
-}
-
-template <class D, int NB>
-__global__ __launch_bounds__(256) void retro_mlp_kernel(D d, const uint64_t *__restrict__ ikeys,
-                                                        const uint32_t *__restrict__ islot,
-                                                        const uint8_t *__restrict__ iwon, uint64_t n, ResRef self,
-                                                        Ress<1> next, uint32_t *err) {
-    static_assert(D::MAX_SKIP == 1, "one tier step");
-    const ResRef t = next.t[0];
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        if (iwon[i]) {   // a LOSS-in-0 child: nothing beats it, no lookup needed
-            self.s[islot[i]].score = parent_score(0xFFFFu);
-            continue;
-        }
-        const uint64_t k = ikeys[i];
-        uint32_t best = 0;
-#pragma unroll
-        for (int j0 = 0; j0 < D::MAXC; j0 += NB) {
-            uint64_t ck[NB], h[NB];
-            u64x2 v[NB];
-            bool look[NB];
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                uint64_t c = 0;
-                look[j] = false;
-                if (j0 + j < D::MAXC && d.child_at(k, j0 + j, c)) {
-                    const int p = d.primitive(c);
-                    if (p != UNDECIDED) best = max(best, score_of_primitive(p));
-                    else look[j] = true;
-                }
-                ck[j] = c;
-                if (look[j] && t.s) {
-                    h[j] = home_slot(c, t.cap);
-                    v[j] = *(const u64x2 *)&t.s[h[j]];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < NB; j++) {
-                if (!look[j]) continue;
-                int f = -1;
-                for (uint64_t probe = 0; t.s && probe < t.cap; probe++) {
-                    if (v[j][0] == ck[j]) { f = (int)(v[j][1] & 0xFFFFu); break; }
-                    if (v[j][0] == EMPTY_KEY) break;
-                    h[j] = h[j] + 1 == t.cap ? 0 : h[j] + 1;
-                    v[j] = *(const u64x2 *)&t.s[h[j]];
-                }
-                if (f < 0) { atomicOr(err, DEV_ERR_MISSING_CHILD); f = 0; }
-                best = max(best, (uint32_t)f);
-            }
-        }
-        if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
-        self.s[islot[i]].score = parent_score(best);
-    }
-}
-
-// GM_SPARSE_MLP: children per probe batch of the MLP kernels (0 = off; 4, 6, 8, 12, 16)
-static int mlp_nb() {
-    static const int v = getenv("GM_SPARSE_MLP") ? atoi(getenv("GM_SPARSE_MLP")) : 0;
-    return v;
-}
-
 // Small tiers (fewer than SPLIT_MAX interior positions): latency, not throughput,
 // bounds a tier, and with one lane per parent a lane walks its children's inserts
 // (or lookups) one after the other.  The split kernels give each parent G = 16
@@ -351,156 +238,8 @@ __global__ __launch_bounds__(256) void retro_split_kernel(D d, const uint64_t *_
 // kernels, walking the sorted list, meet a duplicate child while its line is still in L2
 // instead of as one more random 64-B HBM access (the inserts and the lookups are the
 // roofline of this engine).  Default (GM_SPARSE_BATCH 1).
-//
-// Option 2 (measured slower, kept as a development option): each workgroup takes BATCH_P
-// consecutive parents at a time and a workgroup-local hash set in LDS keeps one copy of
-// each child of the batch, so a child reached from several parents costs one probe of
-// the tier table (the model puts the removed inserts at ~40 % of all; in slot order a
-// batch of any size below 64 K parents removes < 1 %).  A child that does not fit the LDS
-// set (probe limit) goes to the global table directly: the set is a filter, never a source.
-constexpr int BATCH_T = 256;                 // threads per workgroup
-constexpr int BATCH_PER = 2;                 // parents per thread and batch
-constexpr int BATCH_P = BATCH_T * BATCH_PER;
-constexpr int BATCH_M = 4096;                // LDS set slots (32 KiB of keys)
-constexpr int BATCH_PROBE = 32;
+
 constexpr int BATCH_SORT_BITS = 24;       // Toot 6x4 per solve: 8 bits 133.3 ms, 16 132.3, 24 129.5, 32 133.9, 48 137.5
-
-__device__ __forceinline__ uint32_t bset_home(uint64_t k) {
-    return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 52) & (BATCH_M - 1);
-}
-// insert into the LDS set: true if k is now (or already was) in it
-__device__ __forceinline__ bool bset_insert(uint64_t *set, uint64_t k) {
-    uint32_t h = bset_home(k);
-#pragma unroll 1
-    for (int p = 0; p < BATCH_PROBE; p++) {
-        const unsigned long long prev = atomicCAS((unsigned long long *)&set[h], (unsigned long long)EMPTY_KEY,
-                                                  (unsigned long long)k);
-        if (prev == EMPTY_KEY || prev == k) return true;
-        h = (h + 1) & (BATCH_M - 1);
-    }
-    return false;
-}
-__device__ __forceinline__ int bset_find(const uint64_t *set, uint64_t k) {
-    uint32_t h = bset_home(k);
-#pragma unroll 1
-    for (int p = 0; p < BATCH_PROBE; p++) {
-        const uint64_t v = set[h];
-        if (v == k) return (int)h;
-        if (v == EMPTY_KEY) return -1;
-        h = (h + 1) & (BATCH_M - 1);
-    }
-    return -1;
-}
-
-template <class D>
-__global__ __launch_bounds__(BATCH_T) void expand_batch_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n,
-                                                               int64_t tk, Fronts<D::MAX_SKIP> next,
-                                                               uint8_t *__restrict__ iwon, uint32_t *err) {
-    constexpr int S = D::MAX_SKIP;
-    __shared__ uint64_t set[BATCH_M];
-    uint64_t fresh[S];
-#pragma unroll
-    for (int s = 0; s < S; s++) fresh[s] = 0;
-    auto global_insert = [&](uint64_t c) {
-        const int64_t dt = d.tier(c) - tk;
-#pragma unroll
-        for (int s = 0; s < S; s++)
-            if (dt == s + 1 && front_insert(next.t[s], c, err)) fresh[s]++;
-    };
-    for (uint64_t base = blockIdx.x * (uint64_t)BATCH_P; base < n; base += (uint64_t)gridDim.x * BATCH_P) {
-        for (int j = threadIdx.x; j < BATCH_M; j += BATCH_T) set[j] = EMPTY_KEY;
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < BATCH_PER; q++) {
-            const uint64_t i = base + (uint64_t)q * BATCH_T + threadIdx.x;
-            if (i >= n) continue;
-            const uint64_t k = ikeys[i];
-            bool won = false;
-            d.visit(k, [&](uint64_t c) {
-                if (!bset_insert(set, c)) global_insert(c);   // the set is full around c
-                if (!won) won = d.primitive(c) == LOSS;
-                return true;
-            });
-            iwon[i] = won ? 1 : 0;
-        }
-        __syncthreads();
-        for (int j = threadIdx.x; j < BATCH_M; j += BATCH_T) {
-            const uint64_t c = set[j];
-            if (c != EMPTY_KEY) global_insert(c);
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
-}
-
-template <class D>
-__global__ __launch_bounds__(BATCH_T) void retro_batch_kernel(D d, const uint64_t *__restrict__ ikeys,
-                                                              const uint32_t *__restrict__ islot,
-                                                              const uint8_t *__restrict__ iwon, uint64_t n, int64_t tk,
-                                                              ResRef self, Ress<D::MAX_SKIP> next, uint32_t *err) {
-    constexpr int S = D::MAX_SKIP;
-    __shared__ uint64_t set[BATCH_M];
-    __shared__ uint16_t score[BATCH_M];
-    auto global_score = [&](uint64_t c) {
-        const int64_t dt = d.tier(c) - tk;
-        int f = -1;
-#pragma unroll
-        for (int s = 0; s < S; s++)
-            if (dt == s + 1) f = res_find(next.t[s], c);
-        if (f < 0) { atomicOr(err, DEV_ERR_MISSING_CHILD); f = 0; }
-        return (uint32_t)f;
-    };
-    for (uint64_t base = blockIdx.x * (uint64_t)BATCH_P; base < n; base += (uint64_t)gridDim.x * BATCH_P) {
-        for (int j = threadIdx.x; j < BATCH_M; j += BATCH_T) set[j] = EMPTY_KEY;
-        __syncthreads();
-        // 1. the batch's undecided children, once each
-#pragma unroll
-        for (int q = 0; q < BATCH_PER; q++) {
-            const uint64_t i = base + (uint64_t)q * BATCH_T + threadIdx.x;
-            if (i >= n || iwon[i]) continue;
-            d.visit(ikeys[i], [&](uint64_t c) {
-                if (d.primitive(c) == UNDECIDED) bset_insert(set, c);   // one that does not fit is looked up later
-                return true;
-            });
-        }
-        __syncthreads();
-        // 2. one lookup per distinct child
-        for (int j = threadIdx.x; j < BATCH_M; j += BATCH_T) {
-            const uint64_t c = set[j];
-            if (c != EMPTY_KEY) score[j] = (uint16_t)global_score(c);
-        }
-        __syncthreads();
-        // 3. each parent's best child from the set (primitive children from primitive())
-#pragma unroll
-        for (int q = 0; q < BATCH_PER; q++) {
-            const uint64_t i = base + (uint64_t)q * BATCH_T + threadIdx.x;
-            if (i >= n) continue;
-            const uint32_t at = islot[i];
-            if (at >= self.cap) { atomicOr(err, DEV_ERR_MISSING_CHILD); continue; }   // never: a corrupt list
-            if (iwon[i]) {   // a LOSS-in-0 child: nothing beats it, no lookup needed
-                self.s[at].score = parent_score(0xFFFFu);
-                continue;
-            }
-            uint32_t best = 0;
-            d.visit(ikeys[i], [&](uint64_t c) {
-                const int p = d.primitive(c);
-                uint32_t sc;
-                if (p != UNDECIDED) {
-                    sc = score_of_primitive(p);
-                } else {
-                    const int h = bset_find(set, c);
-                    sc = h >= 0 ? (uint32_t)score[h] : global_score(c);
-                }
-                best = max(best, sc);
-                return best != 0xFFFFu;
-            });
-            if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
-            self.s[at].score = parent_score(best);
-        }
-        __syncthreads();
-    }
-}
 
 // development check (GM_SPARSE_BATCH=3): the sorted list holds the same (key, slot) pairs
 __global__ void batch_verify_kernel(const uint64_t *__restrict__ skeys, const uint32_t *__restrict__ sslot,
@@ -510,9 +249,9 @@ __global__ void batch_verify_kernel(const uint64_t *__restrict__ skeys, const ui
         if (sslot[i] >= cap || slots[sslot[i]].key != skeys[i]) atomicAdd(bad, 1ull);
 }
 
-// GM_SPARSE_BATCH: 1 (default) large tiers' interior lists sorted by the key's top bits, plain
-// kernels; 0 unsorted (round 3); 2 sorted + the LDS batch kernels (development option:
-// measured slower); 3 as 1 with a check of every sorted pair (debug)
+// GM_SPARSE_BATCH: 1 (default) large tiers' interior lists sorted by the key's top bits;
+// 0 unsorted (round 3); 3 as 1 with a check of every sorted pair (debug).  (2, the LDS
+// batch kernels of round 4, measured slower and was removed: DESIGN.md §4.2.)
 static int batch_mode() {
     static const int m = getenv("GM_SPARSE_BATCH") ? atoi(getenv("GM_SPARSE_BATCH")) : 1;
     return m;
@@ -523,77 +262,27 @@ static int sort_bits() {   // GM_SPARSE_SORT_BITS (development): key bits the li
     return b;
 }
 
-// expand / retro of one tier: the split kernels below SPLIT_MAX interior positions
-template <class D>
-static bool launch_expand_mlp(hipStream_t st, const D &d, const SpTier &T, const Fronts<D::MAX_SKIP> &nx,
-                              uint32_t *err) {
-    if constexpr (child_at_t<D>::value && D::MAX_SKIP == 1) {
-        const uint64_t *keys = T.skeys ? T.skeys : T.ikeys;
-        const dim3 g(grid_for(T.ni)), b(256);
-        switch (mlp_nb()) {
-        case 4: hipLaunchKernelGGL((expand_mlp_kernel<D, 4>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
-        case 6: hipLaunchKernelGGL((expand_mlp_kernel<D, 6>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
-        case 8: hipLaunchKernelGGL((expand_mlp_kernel<D, 8>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
-        case 12: hipLaunchKernelGGL((expand_mlp_kernel<D, 12>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
-        case 16: hipLaunchKernelGGL((expand_mlp_kernel<D, 16>), g, b, 0, st, d, keys, T.ni, nx, T.iwon, err); return true;
-        default: return false;
-        }
-    }
-    return false;
-}
-
-template <class D>
-static bool launch_retro_mlp(hipStream_t st, const D &d, const SpTier &T, const ResRef &self,
-                             const Ress<D::MAX_SKIP> &nx, uint32_t *err) {
-    if constexpr (child_at_t<D>::value && D::MAX_SKIP == 1) {
-        const uint64_t *keys = T.skeys ? T.skeys : T.ikeys;
-        const uint32_t *slots = T.skeys ? T.sslot : T.islot;
-        const dim3 g(grid_for(T.ni)), b(256);
-        switch (mlp_nb()) {
-        case 4: hipLaunchKernelGGL((retro_mlp_kernel<D, 4>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
-        case 6: hipLaunchKernelGGL((retro_mlp_kernel<D, 6>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
-        case 8: hipLaunchKernelGGL((retro_mlp_kernel<D, 8>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
-        case 12: hipLaunchKernelGGL((retro_mlp_kernel<D, 12>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
-        case 16: hipLaunchKernelGGL((retro_mlp_kernel<D, 16>), g, b, 0, st, d, keys, slots, T.iwon, T.ni, self, nx, err); return true;
-        default: return false;
-        }
-    }
-    return false;
-}
-
+// expand / retro of one tier: the split kernels below SPLIT_MAX interior positions, else
+// the plain kernels over the sorted interior list (or the unsorted one, GM_SPARSE_BATCH 0)
 template <class D>
 static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fronts<D::MAX_SKIP> &nx, uint32_t *err) {
-    if (T.ni >= split_max() && batch_mode() != 2 && launch_expand_mlp(st, d, T, nx, err)) return;
     if (T.ni < split_max())
         hipLaunchKernelGGL(expand_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys, T.ni,
                            nx, T.iwon, err);
-    else if (T.skeys && batch_mode() != 2)
-        hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.skeys, T.ni, nx, T.iwon,
-                           err);
-    else if (T.skeys)
-        hipLaunchKernelGGL(expand_batch_kernel<D>, dim3(grid_for((T.ni + BATCH_PER - 1) / BATCH_PER)), dim3(BATCH_T), 0,
-                           st, d, T.skeys, T.ni, T.tier, nx, T.iwon, err);
     else
-        hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.ikeys, T.ni, nx, T.iwon,
-                           err);
+        hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.skeys ? T.skeys : T.ikeys,
+                           T.ni, nx, T.iwon, err);
 }
 
 template <class D>
 static void launch_retro(hipStream_t st, const D &d, const SpTier &T, const ResRef &self,
                          const Ress<D::MAX_SKIP> &nx, uint32_t *err) {
-    if (T.ni >= split_max() && batch_mode() != 2 && launch_retro_mlp(st, d, T, self, nx, err)) return;
     if (T.ni < split_max())
         hipLaunchKernelGGL(retro_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys,
                            T.islot, T.iwon, T.ni, self, nx, err);
-    else if (T.skeys && batch_mode() != 2)
-        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.skeys, T.sslot, T.iwon,
-                           T.ni, self, nx, err);
-    else if (T.skeys)
-        hipLaunchKernelGGL(retro_batch_kernel<D>, dim3(grid_for((T.ni + BATCH_PER - 1) / BATCH_PER)), dim3(BATCH_T), 0,
-                           st, d, T.skeys, T.sslot, T.iwon, T.ni, T.tier, self, nx, err);
     else
-        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.ikeys, T.islot, T.iwon,
-                           T.ni, self, nx, err);
+        hipLaunchKernelGGL(retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.skeys ? T.skeys : T.ikeys,
+                           T.skeys ? T.sslot : T.islot, T.iwon, T.ni, self, nx, err);
 }
 
 // ----------------------------------------------------------------- host side

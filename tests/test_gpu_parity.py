@@ -269,12 +269,11 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("split_max,mode", [("1", "1"), ("4096", "1"), ("1", "2"), ("4096", "2"), ("4096", "3")])
+@pytest.mark.parametrize("split_max,mode", [("1", "1"), ("4096", "1"), ("4096", "3"), ("1", "0")])
 def test_sparse_sorted_lists_everywhere_vs_golden(split_max, mode):
     """The sparse engine's sorted interior lists (radix-sorted by the key's top bits, then
-    the plain expand / retro kernels: GM_SPARSE_BATCH 1, the default; 2: the LDS batch
-    kernels, one deduplicated insert / lookup per distinct child of a 512-parent batch;
-    3: 1 with every sorted pair checked on the device; csrc/sparse.hip) apply only to
+    the plain expand / retro kernels: GM_SPARSE_BATCH 1, the default; 3: 1 with every
+    sorted pair checked on the device; 0: unsorted; csrc/sparse.hip) apply only to
     tiers of >= 65,536 interior positions; GM_SPARSE_SPLIT_MAX moves them onto every tier
     (1) or the mid-size ones of these games (4096), synced solve and replay, with and
     without the symmetry reduction: the reference plugins' golden tables and the Toot 4x4
