@@ -701,7 +701,7 @@ struct BxFlow {
     uint32_t *ctr;            // [8] error; zeroed before each solve
     uint32_t *flag;           // per box id: the epoch of the solve that stored it
     const uint32_t *epoch;    // this solve's epoch
-    uint32_t dev;             // development: 1 = no waits (wrong results; times the rest), 2 = window of two
+    uint32_t dev;             // development: 1 = no waits (wrong results; times the rest)
 };
 
 template <bool SHARD>
@@ -767,29 +767,15 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
     // workgroup k of queue q takes its groups k, k + K, k + 2 K, ... (K workgroups per
     // queue): static, like the tier launches, so no atomic per group
     const uint32_t K = (gridDim.x - q + 7u) >> 3;
-    // a = the earliest of this workgroup's groups not yet solved, b = the next after it
-    // (development, F.dev & 2: when a's children are not all stored but b's are, b goes
-    // first; a stays the earliest, so the lowest-tier argument still holds)
-    uint32_t a = blockIdx.x >> 3, b = a + K;
-    if (a >= qn) return;
+    uint32_t j = blockIdx.x >> 3;
+    if (j >= qn) return;
     const BxLaneC L = bx_lane_consts(lane);
     s[BX_PITCH * lane + BX_Z] = 0;
     bx_u32x4 R[BX_NLOAD];
     for (;;) {
-        uint32_t j = a;
-        BxGroup G = bx_group_rec<SHARD>(boxes, fills, gq[a]);
-        uint32_t src = lane < 16u ? bx_child_src<SHARD>(G, lane >> 3, lane & 7u) : ~0u;
-        uint32_t seen = bx_flag_src_load(F, src);
-        if ((F.dev & 2u) && b < qn && !__all(src == ~0u || seen == ep)) {
-            const BxGroup Gb = bx_group_rec<SHARD>(boxes, fills, gq[b]);
-            const uint32_t srcb = lane < 16u ? bx_child_src<SHARD>(Gb, lane >> 3, lane & 7u) : ~0u;
-            if (__all(srcb == ~0u || bx_flag_src_load(F, srcb) == ep)) {
-                j = b;
-                G = Gb;
-                src = srcb;
-                seen = ep;
-            }
-        }
+        const BxGroup G = bx_group_rec<SHARD>(boxes, fills, gq[j]);
+        const uint32_t src = lane < 16u ? bx_child_src<SHARD>(G, lane >> 3, lane & 7u) : ~0u;
+        const uint32_t seen = bx_flag_src_load(F, src);
         if (!(F.dev & 1u) && !bx_wait(F, src, seen, lane, ep)) return;
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_I);
         bx_issue<SHARD, GM_BOX_STORE_CPOL>(table, G, lane, R);
@@ -809,13 +795,8 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
             __hip_atomic_store(&F.flag[G.box[0]], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (G.valid[1]) __hip_atomic_store(&F.flag[G.box[1]], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (j == a) {
-            a = b;
-            b += K;
-        } else {
-            b += K;
-        }
-        if (a >= qn) break;
+        j += K;
+        if (j >= qn) break;
     }
 }
 
@@ -1200,7 +1181,6 @@ static int box_launch_flow(Ctx *c, DenseBox *d, BoxRank &R) {
     F.epoch = d->d_flow + 16;
     F.flag = d->d_flow + 64;
     F.dev = box_flow_env() == 2 ? 1u : 0u;
-    if (getenv("GM_BOX_FLOW_WINDOW") && atoi(getenv("GM_BOX_FLOW_WINDOW"))) F.dev |= 2u;
     GM_HIP(hipMemsetAsync(d->d_flow, 0, 9 * 4, c->stream));
     hipLaunchKernelGGL(box_epoch_kernel, dim3(1), dim3(64), 0, c->stream, d->d_flow + 16);
     const uint32_t grid = (uint32_t)d->grid_cap & ~7u;
