@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ 
             bool interior = false;
             if (k[r] != EMPTY_KEY) {
                 nseen++;
-                d.orbit(k[r], [&](uint64_t) { nall++; });
+                if (COUNT) d.orbit(k[r], [&](uint64_t) { nall++; });   // a replay knows its orbit counts
                 const uint64_t i = chunk + 256ull * r + threadIdx.x;
                 const int p = d.primitive(k[r]);
                 if (p == DRAW) atomicOr(err, DEV_ERR_DRAW);
