@@ -108,13 +108,16 @@ __global__ __launch_bounds__(256) void retro_kernel(D d, const uint64_t *__restr
         const uint64_t k = ikeys[i];
         const int64_t tk = d.tier(k);
         uint32_t best = 0;
-        d.visit(k, [&](uint64_t c) {
+        // children as the moves make them; only one that needs a lookup is brought to its
+        // stored (canonical) form -- primitive() and tier() are symmetric (games.hpp)
+        unreduced(d).visit(k, [&](uint64_t c) {
             const int p = d.primitive(c);
             uint32_t sc;
             if (p != UNDECIDED) {
                 sc = score_of_primitive(p);
             } else {
                 const int64_t dt = d.tier(c) - tk;
+                c = d.canon(c);
                 int f = -1;
 #pragma unroll
                 for (int s = 0; s < S; s++)
