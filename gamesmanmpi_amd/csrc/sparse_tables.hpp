@@ -330,8 +330,12 @@ struct DedupEstimate {
 template <class D, bool COUNT = true>
 inline void launch_classify(hipStream_t st, const D &d, RSlot *slots, uint64_t cap, uint64_t *ikeys, uint32_t *islot,
                             unsigned long long *scr, uint32_t *err) {
+    // a replay's classify (no edge or orbit counts) does less per row: 32 rows
+    // per thread there (Toot 6x4 replay: 8.8 vs 9.5 ms; rows 8 / 4: 12.6 / 19.6 ms -- each
+    // chunk's barriers and reservation atomic are paid fewer times)
+    constexpr int rows = COUNT ? CROWS : 32;
     if (cap >= CLASSIFY_ROWS_MIN)
-        hipLaunchKernelGGL((classify_kernel<D, CROWS, COUNT>), dim3(grid_for(cap / CROWS + 1)), dim3(256), 0, st, d,
+        hipLaunchKernelGGL((classify_kernel<D, rows, COUNT>), dim3(grid_for(cap / rows + 1)), dim3(256), 0, st, d,
                            slots, cap, ikeys, islot, scr + 9, scr, scr + 10, err);
     else
         hipLaunchKernelGGL((classify_kernel<D, 1, COUNT>), dim3(grid_for(cap)), dim3(256), 0, st, d, slots, cap, ikeys,
