@@ -487,8 +487,11 @@ class _Walk:
                     # (tic-tac-toe never is: ADVICE r03); the parent keeps walking serially
                     # while they import, and hands over at the first level of PAR_MIN
                     # positions it meets with the workers ready (or 8 PAR_MIN, whatever)
-                    if not prestarted and (self.n + projected) * 16 >= PAR_START:
-                        _prestart()   # one process, started a level or two before the workers
+                    # the fork server (one process) a level ahead of the workers, once the next
+                    # level is projected past PAR_START / 8 positions at a growth of 4 or more
+                    # per level (tic-tac-toe never is)
+                    if not prestarted and 8 * projected >= PAR_START and projected >= 4 * level_len:
+                        _prestart()
                         prestarted = True
                     if self.pool is None and (self.n + projected >= PAR_START or 2 * projected >= PAR_START
                                               or level_len >= 4 * PAR_MIN):

@@ -166,6 +166,7 @@ def test_small_plugins_start_no_worker(monkeypatch):
     def pool(*a):
         raise AssertionError("worker processes started for tic-tac-toe")
     monkeypatch.setattr(graph, "_ShardPool", pool)
+    monkeypatch.setattr(graph, "_prestart", pool)
     mod = load_plugin("test_games/mttt.py")
     pos, prim, off, kids = graph.enumerate_graph(mod, mod.initial_position(), workers=8)
     assert len(pos) == 5478
