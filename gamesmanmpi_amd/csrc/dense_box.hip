@@ -692,6 +692,9 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 // resident: the grid is at most the resident capacity); a wait that outlasts
 // GM_BOX_FLOW_TIMEOUT flags an error that every wave sees and leaves by, and the host then
 // re-solves with the tiered launches.
+#ifndef GM_BOX_FLOW_LOAD_CPOL
+#define GM_BOX_FLOW_LOAD_CPOL 16   // child rows read sc1 (the hand-off table's consumer loads)
+#endif
 #ifndef GM_BOX_FLOW_TIMEOUT
 #define GM_BOX_FLOW_TIMEOUT 20000000ull   // s_memrealtime ticks (100 MHz): 200 ms
 #endif
@@ -778,7 +781,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
         const uint32_t seen = bx_flag_src_load(F, src);
         if (!(F.dev & 1u) && !bx_wait(F, src, seen, lane, ep)) return;
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_I);
-        bx_issue<SHARD, GM_BOX_STORE_CPOL>(table, G, lane, R);
+        bx_issue<SHARD, GM_BOX_FLOW_LOAD_CPOL>(table, G, lane, R);
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_F);
