@@ -211,7 +211,9 @@ def worker_main(conn, me, nw, tag, path, attrs, gen_idx):
         out = _Sender()      # to the peers, in order
         up = _Sender()       # to the parent (which reads the workers in turn)
         others = [peers[w] for w in range(nw) if w != me]
-        sent = set()         # fingerprints whose object this worker has already shipped
+        sent = set()         # fingerprints whose object this worker shipped in this level (kept
+                             # per level: a child of a tiered game is one level down only, and the
+                             # owner deduplicates anyway; a walk-long set would grow with the edges)
         acc = 0              # level-acc children are applied on arrival; frontier[acc + 1] is filling
         ends = defaultdict(int)          # level -> workers done expanding it
         busy = defaultdict(bool)         # level -> some worker's frontier was non-empty
@@ -296,6 +298,7 @@ def worker_main(conn, me, nw, tag, path, attrs, gen_idx):
                 busy[lvl] = busy[lvl] or len(F) > 0
                 del frontier[lvl]
                 lvl, i, rep = lvl + 1, 0, _Level()
+                sent.clear()
                 advance()
             else:              # wait for the rest of this level's frontier
                 for c in wait(others + [conn]):
