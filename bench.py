@@ -669,6 +669,12 @@ def main():
                      "traffic_bytes_per_position": (traffic_solve / positions) if traffic_solve else None,
                      "traffic_source": "profiles/traffic_subtract%d.json (rocprofv3 --pmc FETCH_SIZE x2 + "
                                        "WRITE_SIZE, per launch)" % args.heaps,
+                     "diag_survey_edge_model_bytes_per_position": 2 * EDGE_MODEL_BYTES_PER_POSITION,
+                     "diag_survey_edge_model_gbs": (2 * EDGE_MODEL_BYTES_PER_POSITION * own_positions
+                                                    / kernel_s_per_solve / 1e9 if kernel_s_per_solve > 0 else None),
+                     "diag_survey_edge_model_note": "SURVEY §8d's graded edge model with u16 records (31 B/position): "
+                                                    "above the HBM peak because the box kernel serves child edges from "
+                                                    "LDS and registers; compulsory bytes are graded (DESIGN.md §6)",
                      "diag_edge_model_bytes_per_position": EDGE_MODEL_BYTES_PER_POSITION,
                      "diag_edge_model_gbs": (EDGE_MODEL_BYTES_PER_POSITION * own_positions / kernel_s_per_solve / 1e9
                                              if kernel_s_per_solve > 0 else None),
