@@ -1,0 +1,40 @@
+"""The bench.py contract on the GPU: one JSON line with the driver's fields, the roofline
+and parity objects, at N = 1 and with 4 virtual ranks (the sharded dataflow launch)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIELDS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+          "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+
+
+def _bench(*args):
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "3", "--warmup", "1", "--no-toot",
+                        "--no-cpu-baseline", *args], capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_line_one_gpu():
+    d = _bench()
+    assert all(k in d for k in FIELDS)
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0 and d["parity"]["ok"]
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1 and rf["peak"] == 8000.0
+    assert rf["launches_per_solve"] == 41 and rf["kernel"].startswith("box_tier_kernel<false>")
+
+
+def test_bench_line_virtual_ranks_dataflow():
+    d = _bench("--virtual-ranks", "4")
+    assert d["parity"]["ok"] and d["sharding"]["boxes_per_rank"] == 282880
+    rf = d["roofline"]
+    assert rf["launches_per_solve"] == 4 and rf["kernel"].startswith("box_flow_kernel<true>")
+    assert rf["traffic"] is None   # the committed PMC summary is the one-GPU solve's
