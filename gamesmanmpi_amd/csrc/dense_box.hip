@@ -690,13 +690,10 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 // takes its groups in tier order, so the workgroup whose current group has the lowest tier
 // has all its children stored and never waits (no deadlock while every workgroup is
 // resident: the grid is at most the resident capacity); a wait that outlasts
-// GM_BOX_FLOW_TIMEOUT flags an error that every wave sees and leaves by, and the host then
+// 200 ms (GM_BOX_FLOW_TIMEOUT_MS) flags an error that every wave sees and leaves by, and the host then
 // re-solves with the tiered launches.
 #ifndef GM_BOX_FLOW_LOAD_CPOL
 #define GM_BOX_FLOW_LOAD_CPOL 16   // child rows read sc1 (the hand-off table's consumer loads)
-#endif
-#ifndef GM_BOX_FLOW_TIMEOUT
-#define GM_BOX_FLOW_TIMEOUT 20000000ull   // s_memrealtime ticks (100 MHz): 200 ms
 #endif
 struct BxFlow {
     const uint32_t *groups;   // queue q: groups[qbase[q] + j], j < qlen[q]: box-list index | second box << 31
@@ -704,7 +701,9 @@ struct BxFlow {
     uint32_t *ctr;            // [8] error; zeroed before each solve
     uint32_t *flag;           // per box id: the epoch of the solve that stored it
     const uint32_t *epoch;    // this solve's epoch
-    uint32_t dev;             // development: 1 = no waits (wrong results; times the rest)
+    uint64_t timeout;         // s_memrealtime ticks (100 MHz) a wait may last (GM_BOX_FLOW_TIMEOUT_MS)
+    uint32_t dev;             // development: 1 = no waits (wrong results; times the rest); test: 8 = wait
+                              // for an epoch no flag holds (every wait times out: the fallback path)
 };
 
 template <bool SHARD>
@@ -745,12 +744,13 @@ __device__ __forceinline__ uint32_t bx_flag_src_load(const BxFlow &F, uint32_t s
     return src == ~0u ? 0u : __hip_atomic_load(&F.flag[src], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ bool bx_wait(const BxFlow &F, uint32_t src, uint32_t seen, uint32_t lane, uint32_t ep) {
+    if (F.dev & 8u) ep += 1u;
     if (__all(src == ~0u || seen == ep)) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (__all(src == ~0u || bx_flag_src_load(F, src) == ep)) return true;
         if (__hip_atomic_load(&F.ctr[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > GM_BOX_FLOW_TIMEOUT) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > F.timeout) {
             if (lane == 0) atomicOr(&F.ctr[8], 1u);
             return false;
         }
@@ -1184,6 +1184,9 @@ static int box_launch_flow(Ctx *c, DenseBox *d, BoxRank &R) {
     F.epoch = d->d_flow + 16;
     F.flag = d->d_flow + 64;
     F.dev = box_flow_env() == 2 ? 1u : 0u;
+    if (getenv("GM_BOX_FLOW_TEST_STALL") && atoi(getenv("GM_BOX_FLOW_TEST_STALL"))) F.dev |= 8u;
+    const char *tm = getenv("GM_BOX_FLOW_TIMEOUT_MS");
+    F.timeout = (uint64_t)(tm ? atof(tm) : 200.0) * 100000ull;
     GM_HIP(hipMemsetAsync(d->d_flow, 0, 9 * 4, c->stream));
     hipLaunchKernelGGL(box_epoch_kernel, dim3(1), dim3(64), 0, c->stream, d->d_flow + 16);
     const uint32_t grid = (uint32_t)d->grid_cap & ~7u;

@@ -191,6 +191,39 @@ def test_box_dataflow_on_one_gpu_vs_oracle(oracle, root):
     ctx.close()
 
 
+_FLOW_STALL = r'''
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+from gamesmanmpi_amd import Context, _lib
+ref = json.load(open(os.path.join(sys.argv[1], "tests", "golden", "oracle_digests.json")))["subtract_8"]
+ctx = Context(5, (8,), device=0)
+ctx.set_option(_lib.OPT_VIRTUAL_RANKS, 2)
+ctx.set_option(_lib.OPT_TIMING, 1)
+for rep in range(2):
+    n, rec = ctx.solve(0xFFFFFFFF)
+    assert ctx.digest() == (ref["digest"], 1 << 32) and rec == ref["root_record"], rep
+    assert ctx.stats()["kernel_launches"] == 82, ctx.stats()["kernel_launches"]
+print("ok")
+'''
+
+
+def test_box_dataflow_timeout_falls_back_to_tier_launches():
+    """A dataflow wait that outlasts its limit (GM_BOX_FLOW_TEST_STALL makes every wait
+    look for an epoch no flag holds; GM_BOX_FLOW_TIMEOUT_MS 20) ends the launch -- every
+    wave sees the error and leaves -- and the solve is redone with tier launches: the
+    oracle's digest, a line on stderr, and tier launches from then on (fresh process: the
+    hooks are read at launch capture)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GM_BOX_FLOW_TEST_STALL="1", GM_BOX_FLOW_TIMEOUT_MS="20")
+    r = subprocess.run([sys.executable, "-c", _FLOW_STALL, repo], env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+    assert "re-solving with tier launches" in r.stderr
+
+
 def test_box_engine_query_outside_the_root_region_is_unsolved():
     """ADVICE r03: the box engine solves only the boxes of the root's region and never clears
     the table, so a key with a nibble above the root's must query as 0xFFFF, not as whatever
