@@ -335,7 +335,7 @@ int gm_set_comm(gm_ctx *h, int rank, int world, const void *uid, int bytes) {
     // no uid: rank and world only.  Enough for the 8-heap box engine, whose ranks exchange
     // nothing; the RCCL engines refuse to solve without a communicator (gm_solve)
     if (!uid || bytes <= 0) return GM_OK;
-    if (!uid || bytes < (int)sizeof(ncclUniqueId)) { set_error("uid must hold %d bytes", (int)sizeof(ncclUniqueId)); return GM_E_ARG; }
+    if (bytes < (int)sizeof(ncclUniqueId)) { set_error("uid must hold %d bytes", (int)sizeof(ncclUniqueId)); return GM_E_ARG; }
     if (c->device < 0) { set_error("no HIP device"); return GM_E_HIP; }
     ncclUniqueId id;
     memcpy(&id, uid, sizeof id);
