@@ -200,12 +200,14 @@ class _ShardPool:
         self.nw = nw
         self.conns, self.procs = [], []
         tag = "gm-walk-%d-%d-%s" % (os.getpid(), id(self), os.urandom(4).hex())
+        key = os.urandom(32)   # authenticates the workers' mesh connections (walk_worker._mesh)
         self.start_s = []
         self.t_start = time.time()
         for w in range(nw):
             t = time.perf_counter()
             a, b = ctx.Pipe()
-            pr = ctx.Process(target=worker_main, args=(b, w, nw, tag, spec[0], spec[1], tuple(gen_idx)), daemon=True)
+            pr = ctx.Process(target=worker_main, args=(b, w, nw, tag, key, spec[0], spec[1], tuple(gen_idx)),
+                             daemon=True)
             pr.start()
             b.close()
             self.conns.append(a)

@@ -141,21 +141,25 @@ class _Level:
 CHUNK = 64    # positions expanded between two looks at the incoming pipes (GM_GRAPH_CHUNK)
 
 
-def _mesh(me, nw, tag, timeout_s=120.0):
+def _mesh(me, nw, tag, key, timeout_s=120.0):
     """Pipes to every other worker: worker w listens on an abstract unix socket named by
     the walk's tag and w, connects to every lower-numbered worker's and accepts every
-    higher-numbered one's.  The workers build the mesh themselves so the parent never holds
+    higher-numbered one's.  Abstract socket names are visible to every process of the
+    network namespace (/proc/net/unix) and the peers exchange pickles, so each connection
+    is authenticated with the walk's random key (multiprocessing's HMAC challenge); one
+    that fails it is dropped.  The workers build the mesh themselves so the parent never holds
     the n(n-1) descriptors (growing a threaded process's descriptor table waits for an RCU
     grace period, ~0.1 s a doubling on a busy host)."""
+    from multiprocessing import AuthenticationError
     from multiprocessing.connection import Client, Listener
     name = "\0" + tag + "-%d"
-    lst = Listener(name % me, family="AF_UNIX", backlog=max(1, nw))
+    lst = Listener(name % me, family="AF_UNIX", backlog=max(1, nw), authkey=key)
     peers = [None] * nw
     deadline = time.time() + timeout_s
     for p in range(me):
         while True:
             try:
-                c = Client(name % p, family="AF_UNIX")
+                c = Client(name % p, family="AF_UNIX", authkey=key)
                 break
             except (FileNotFoundError, ConnectionRefusedError):
                 if time.time() > deadline:
@@ -163,14 +167,19 @@ def _mesh(me, nw, tag, timeout_s=120.0):
                 time.sleep(0.002)
         c.send_bytes(b"%d" % me)
         peers[p] = c
-    for _ in range(me + 1, nw):
-        c = lst.accept()
+    left = nw - 1 - me
+    while left:
+        try:
+            c = lst.accept()
+        except (AuthenticationError, EOFError, OSError):
+            continue
         peers[int(c.recv_bytes())] = c
+        left -= 1
     lst.close()
     return peers
 
 
-def worker_main(conn, me, nw, tag, path, attrs, gen_idx):
+def worker_main(conn, me, nw, tag, key, path, attrs, gen_idx):
     """One shard of the parallel walk (a spawned process), the reference's rank
     (src/new_process.py:102-162) with pipes for MPI: it owns the positions whose
     fingerprint maps to it.  Seeded by the parent with the fingerprints it owns so far
@@ -189,7 +198,7 @@ def worker_main(conn, me, nw, tag, path, attrs, gen_idx):
     from multiprocessing.connection import wait
     from collections import defaultdict
     try:
-        peers = _mesh(me, nw, tag)
+        peers = _mesh(me, nw, tag, key)
         mod = load_fresh(path)
         for k, v in attrs.items():   # values the caller set on its module (board size, ...)
             setattr(mod, k, v)

@@ -266,3 +266,51 @@ def test_graph_engine_with_declared_symmetry_matches_golden(tmp_path):
     from gamesmanmpi_amd.persist import read_reference_tables
     back = read_reference_tables(str(tmp_path))
     assert len(back) == 5478 and back["X________"] == (want[1] >> 14, want[1] & 0x3FFF)
+
+
+def test_worker_mesh_drops_unauthenticated_connections():
+    """The workers' mesh (walk_worker._mesh) listens on abstract unix sockets, whose names
+    any local process can list; a connection without the walk's key is refused and the
+    mesh still forms."""
+    import threading
+    from multiprocessing import AuthenticationError
+    from multiprocessing.connection import Client
+    from gamesmanmpi_amd import walk_worker
+
+    tag, key, nw = "gm-walk-test-%d-%s" % (os.getpid(), os.urandom(4).hex()), os.urandom(32), 3
+    out, errs = [None] * nw, []
+
+    def run(w):
+        try:
+            out[w] = walk_worker._mesh(w, nw, tag, key, timeout_s=30.0)
+        except BaseException as e:   # pragma: no cover - reported below
+            errs.append(e)
+
+    # a rogue client first: worker 0's listener must exist before it can connect
+    th = [threading.Thread(target=run, args=(0,))]
+    th[0].start()
+    rogue = None
+    for _ in range(2000):
+        try:
+            with pytest.raises(AuthenticationError):
+                Client("\0%s-0" % tag, family="AF_UNIX", authkey=b"wrong key")
+            rogue = True
+            break
+        except (FileNotFoundError, ConnectionRefusedError):
+            import time
+            time.sleep(0.005)
+    assert rogue
+    for w in range(1, nw):
+        th.append(threading.Thread(target=run, args=(w,)))
+        th[-1].start()
+    for t in th:
+        t.join(60)
+    assert not errs
+    for w in range(nw):
+        for p in range(nw):
+            if p != w:
+                out[w][p].send_bytes(b"%d>%d" % (w, p))
+    for w in range(nw):
+        for p in range(nw):
+            if p != w:
+                assert out[w][p].recv_bytes() == b"%d>%d" % (p, w)
