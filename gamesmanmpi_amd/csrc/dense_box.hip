@@ -692,6 +692,9 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 // resident: the grid is at most the resident capacity); a wait that outlasts
 // 200 ms (GM_BOX_FLOW_TIMEOUT_MS) flags an error that every wave sees and leaves by, and the host then
 // re-solves with the tiered launches.
+#ifndef GM_BOX_FLOW_SLEEP
+#define GM_BOX_FLOW_SLEEP 2        // s_sleep between two polls of a child's flag (64 clocks a unit)
+#endif
 #ifndef GM_BOX_FLOW_LOAD_CPOL
 #define GM_BOX_FLOW_LOAD_CPOL 16   // child rows read sc1 (the hand-off table's consumer loads)
 #endif
@@ -754,9 +757,23 @@ __device__ __forceinline__ bool bx_wait(const BxFlow &F, uint32_t src, uint32_t 
             if (lane == 0) atomicOr(&F.ctr[8], 1u);
             return false;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(GM_BOX_FLOW_SLEEP);
     }
 }
+
+#ifndef GM_BOX_FLOW_TRACE
+#define GM_BOX_FLOW_TRACE 0   // development: per-group realtime stamps (tools/flow_trace.py)
+#endif
+#if GM_BOX_FLOW_TRACE
+constexpr uint32_t BX_FT_WORDS = 6;   // picked, children ready, folded, walked, flagged, box | workgroup << 32
+__device__ unsigned long long bx_ftrace[BX_FT_WORDS << 19];
+#define BX_RT(v)                                                                        \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");  \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+    } while (0)
+#endif
 
 template <bool SHARD>
 __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__restrict__ table,
@@ -776,10 +793,17 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
     s[BX_PITCH * lane + BX_Z] = 0;
     bx_u32x4 R[BX_NLOAD];
     for (;;) {
+#if GM_BOX_FLOW_TRACE
+        unsigned long long ft[5];
+        BX_RT(ft[0]);
+#endif
         const BxGroup G = bx_group_rec<SHARD>(boxes, fills, gq[j]);
         const uint32_t src = lane < 16u ? bx_child_src<SHARD>(G, lane >> 3, lane & 7u) : ~0u;
         const uint32_t seen = bx_flag_src_load(F, src);
         if (!(F.dev & 1u) && !bx_wait(F, src, seen, lane, ep)) return;
+#if GM_BOX_FLOW_TRACE
+        BX_RT(ft[1]);
+#endif
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_I);
         bx_issue<SHARD, GM_BOX_FLOW_LOAD_CPOL>(table, G, lane, R);
         uint32_t ln = lane;
@@ -787,9 +811,15 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_F);
         bx_fold<SHARD>(s, G, ln, R);
         BX_LDS_ORDER();
+#if GM_BOX_FLOW_TRACE
+        BX_RT(ft[2]);
+#endif
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_W);
         bx_walk(s, ln, L);
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_S);
+#if GM_BOX_FLOW_TRACE
+        BX_RT(ft[3]);
+#endif
         bx_store(table, G, s, ln);
         BX_LDS_ORDER();
         // publish: the wave's sc1 stores done, then one lane stores each box's flag sc1
@@ -798,6 +828,14 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
             __hip_atomic_store(&F.flag[G.box[0]], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (G.valid[1]) __hip_atomic_store(&F.flag[G.box[1]], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+#if GM_BOX_FLOW_TRACE
+        BX_RT(ft[4]);
+        if (lane == 0) {
+            unsigned long long *o = bx_ftrace + BX_FT_WORDS * (F.qbase[q] + j);
+            for (int k = 0; k < 5; k++) o[k] = ft[k];
+            o[5] = G.box[0] | ((unsigned long long)blockIdx.x << 32);
+        }
+#endif
         j += K;
         if (j >= qn) break;
     }
@@ -1271,6 +1309,20 @@ int dense_box_solve(Ctx *c, uint64_t root) {
         }
     }
     if (c->use_graph) d->graph_stream = c->stream;
+#if GM_BOX_FLOW_TRACE
+    if (d->flow && getenv("GM_BOX_FLOW_TRACE_OUT")) {   // the last rank's launch (virtual ranks run in order)
+        const BoxRank &R = d->ranks.back();
+        uint64_t ng = 0;
+        for (int x = 0; x < 8; x++) ng += R.qlen[x];
+        std::vector<unsigned long long> h(BX_FT_WORDS * ng);
+        GM_HIP(hipStreamSynchronize(c->stream));
+        GM_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(bx_ftrace), h.size() * 8));
+        if (FILE *f = fopen(getenv("GM_BOX_FLOW_TRACE_OUT"), "wb")) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+    }
+#endif
 #if GM_BOX_TRACE
     {
         unsigned long long h[8];
