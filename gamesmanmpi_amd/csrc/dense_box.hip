@@ -766,7 +766,8 @@ __device__ __forceinline__ bool bx_wait(const BxFlow &F, uint32_t src, uint32_t 
 #endif
 #if GM_BOX_FLOW_TRACE
 constexpr uint32_t BX_FT_WORDS = 6;   // picked, children ready, folded, walked, flagged, box | workgroup << 32
-__device__ unsigned long long bx_ftrace[BX_FT_WORDS << 19];
+constexpr uint32_t BX_FT_GROUPS = (1u << 19) + 4096u;   // 2^20 boxes in pairs, plus an odd box per tier run
+__device__ unsigned long long bx_ftrace[BX_FT_WORDS * BX_FT_GROUPS];
 #define BX_RT(v)                                                                        \
     do {                                                                                \
         __builtin_amdgcn_sched_barrier(0);                                              \
@@ -830,7 +831,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
         }
 #if GM_BOX_FLOW_TRACE
         BX_RT(ft[4]);
-        if (lane == 0) {
+        if (lane == 0 && F.qbase[q] + j < BX_FT_GROUPS) {
             unsigned long long *o = bx_ftrace + BX_FT_WORDS * (F.qbase[q] + j);
             for (int k = 0; k < 5; k++) o[k] = ft[k];
             o[5] = G.box[0] | ((unsigned long long)blockIdx.x << 32);
@@ -1314,7 +1315,7 @@ int dense_box_solve(Ctx *c, uint64_t root) {
         const BoxRank &R = d->ranks.back();
         uint64_t ng = 0;
         for (int x = 0; x < 8; x++) ng += R.qlen[x];
-        std::vector<unsigned long long> h(BX_FT_WORDS * ng);
+        std::vector<unsigned long long> h(BX_FT_WORDS * std::min<uint64_t>(ng, BX_FT_GROUPS));
         GM_HIP(hipStreamSynchronize(c->stream));
         GM_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(bx_ftrace), h.size() * 8));
         if (FILE *f = fopen(getenv("GM_BOX_FLOW_TRACE_OUT"), "wb")) {
