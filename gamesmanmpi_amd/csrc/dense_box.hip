@@ -1065,6 +1065,7 @@ struct DenseBox {
     bool flow = false;                // one-launch (dataflow) solve (GM_OPT_BOX_FLOW)
     bool flow_failed = false;         // a dataflow solve timed out: tier launches from then on
     uint32_t *d_flow = nullptr;       // [0, 9) queue cursors + error, [16] epoch, [64, 64 + 2^20) box flags
+    uint32_t *h_res = nullptr;        // pinned: [0] the root's code (low byte), [1] the dataflow error word
 };
 
 // GM_BOX_FLOW (development, overrides GM_OPT_BOX_FLOW): 0 tier launches, 1 dataflow, 2 dataflow
@@ -1338,14 +1339,16 @@ int dense_box_solve(Ctx *c, uint64_t root) {
     }
 #endif
     // the root box is fixed by every permutation of the plan, so every rank computes it
-    uint8_t rs = 0;
-    GM_HIP(hipMemcpyAsync(&rs, d->ranks[0].table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToHost,
+    // (both words in one pinned buffer: one wait for the stream per solve)
+    if (!d->h_res) GM_HIP(hipHostMalloc((void **)&d->h_res, 8, hipHostMallocDefault));
+    d->h_res[0] = d->h_res[1] = 0;
+    GM_HIP(hipMemcpyAsync(d->h_res, d->ranks[0].table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToHost,
                           c->stream));
+    if (d->flow) GM_HIP(hipMemcpyAsync(d->h_res + 1, d->d_flow + 8, 4, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
+    const uint8_t rs = (uint8_t)(d->h_res[0] & 0xFFu);
     if (d->flow) {
-        uint32_t e = 0;
-        GM_HIP(hipMemcpy(&e, d->d_flow + 8, 4, hipMemcpyDeviceToHost));
-        if (e) {   // a wait timed out: solve again with the tier launches
+        if (d->h_res[1]) {   // a wait timed out: solve again with the tier launches
             fprintf(stderr, "gmsolve: the one-launch box solve timed out waiting for a child box; "
                             "re-solving with tier launches\n");
             for (auto &R : d->ranks)
@@ -1537,6 +1540,7 @@ void dense_box_free(Ctx *c) {
     }
     if (d->d_acc) (void)hipFree(d->d_acc);
     if (d->d_flow) (void)hipFree(d->d_flow);
+    if (d->h_res) (void)hipHostFree(d->h_res);
     delete d;
     c->dbox = nullptr;
 }
