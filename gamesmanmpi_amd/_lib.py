@@ -23,9 +23,14 @@ OPT_DIST_SOLO = 12
 OPT_DIST_OWNER = 13
 OPT_SYMMETRY = 14
 OPT_BOX_FLOW = 15
+OPT_BOX_SPLIT = 16
 BUF_DENSE_TABLE = 1
 PLAN_SHAPE, PLAN_OWN, PLAN_FILL, PLAN_SEND, PLAN_RECV, PLAN_OPS, PLAN_XDEST = 0, 1, 2, 3, 4, 5, 6
-BOXPLAN_SHAPE, BOXPLAN_BOXES, BOXPLAN_FILLS, BOXPLAN_TIER_OFF, BOXPLAN_OWN, BOXPLAN_MAP = 0, 1, 2, 3, 4, 5
+BOXPLAN_SHAPE, BOXPLAN_BOXES, BOXPLAN_FILLS, BOXPLAN_TIER_OFF, BOXPLAN_OWN = 0, 1, 2, 3, 4
+BOXPLAN_SEND, BOXPLAN_SEND_OFF, BOXPLAN_RECV, BOXPLAN_RECV_OFF, BOXPLAN_HALO, BOXPLAN_OPS = 5, 6, 7, 8, 9, 10
+BOXPLAN_COUNTS, BOXPLAN_SRCS, BOXPLAN_DSTS = 11, 12, 13
+BOP_TIER, BOP_PACK, BOP_UNPACK, BOP_SEND, BOP_RECV, BOP_RECORD, BOP_WAIT = range(7)
+BEV_DONE, BEV_PACKED = range(2)
 REC_UNSOLVED = 0xFFFF
 
 ERRORS = {
@@ -38,7 +43,7 @@ SYMBOLS = ("gm_version", "gm_last_error", "gm_device_count", "gm_open", "gm_set_
            "gm_set_option", "gm_pack_initial", "gm_expand_host", "gm_comm_unique_id",
            "gm_set_comm", "gm_solve", "gm_solve_graph", "gm_export", "gm_query", "gm_digest", "gm_stats",
            "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_dist_plan", "gm_box_plan",
-           "gm_rank_stats", "gm_close")
+           "gm_rank_stats", "gm_rank_op_ms", "gm_close")
 
 
 class GMError(RuntimeError):
@@ -64,6 +69,7 @@ class Stats(ctypes.Structure):
         ("kernel_launches", ctypes.c_int32),
         ("engine", ctypes.c_int32),
         ("n_edges", ctypes.c_uint64),
+        ("flow_fallbacks", ctypes.c_int32),
     ]
 
     def as_dict(self):
@@ -108,8 +114,10 @@ def lib():
         "gm_dense_table": (ctypes.c_int, [vp, P(vp), P(u64)]),
         "gm_dist_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int,
                                         vp, u64, P(u64), vp, u64, P(u64)]),
-        "gm_box_plan": (ctypes.c_int, [u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, u64, P(u64)]),
+        "gm_box_plan": (ctypes.c_int, [u64, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int, vp, u64,
+                                       P(u64)]),
         "gm_rank_stats": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, P(ctypes.c_int)]),
+        "gm_rank_op_ms": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, P(ctypes.c_int)]),
         "gm_close": (None, [vp]),
     }
     for name, (res, args) in sig.items():
@@ -142,12 +150,15 @@ def dist_plan(heaps, world, rank, what, axis=0, batch=4, slots=4, symmetry=1, ow
     return off[:n_off.value], data[:n_data.value]
 
 
-def box_plan(world, rank, what, root=0xFFFFFFFF):
-    """gm_box_plan -> uint32 numpy array (host only, no GPU): the sharded box solve's plan."""
+def box_plan(world, rank, what, root=0xFFFFFFFF, axis=0, batch=4, symmetry=1, split=0, loopback=0):
+    """gm_box_plan -> uint32 numpy array (host only, no GPU): rank `rank`'s part of the split
+    box solve (csrc/dist_box.hip).  batch / symmetry / split: GM_OPT_DIST_BATCH,
+    GM_OPT_DIST_SYMMETRY, GM_OPT_BOX_SPLIT; loopback: the op list of a virtual rank."""
     import numpy as np
     L = lib()
+    opts = (ctypes.c_int32 * 4)(batch, symmetry, split, loopback)
     n = ctypes.c_uint64()
-    check(L.gm_box_plan(root, world, rank, what, None, 0, ctypes.byref(n)))
+    check(L.gm_box_plan(root, world, rank, opts, what, axis, None, 0, ctypes.byref(n)))
     out = np.zeros(max(1, n.value), dtype=np.uint32)
-    check(L.gm_box_plan(root, world, rank, what, out.ctypes.data, len(out), ctypes.byref(n)))
+    check(L.gm_box_plan(root, world, rank, opts, what, axis, out.ctypes.data, len(out), ctypes.byref(n)))
     return out[:n.value]

@@ -20,9 +20,10 @@ LIB = os.path.join(PKG, "libgmsolve.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("GM_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["gm_api.hip", "dense_sub.hip", "dense_box.hip", "small_dense.hip", "sparse.hip", "dist_sub.hip", "dist_sparse.hip",
+SOURCES = ["gm_api.hip", "dense_sub.hip", "dense_box.hip", "dist_box.hip", "small_dense.hip", "sparse.hip", "dist_sub.hip",
+           "dist_sparse.hip",
            "graph.hip"]
-HEADERS = ["gm_common.hpp", "games.hpp", "gm_internal.hpp", "sparse_common.hpp", "sparse_tables.hpp"]
+HEADERS = ["gm_common.hpp", "box_common.hpp", "games.hpp", "gm_internal.hpp", "sparse_common.hpp", "sparse_tables.hpp"]
 
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result",
             "-I" + os.path.join(REPO, "include"), "-I" + CSRC]

@@ -44,6 +44,7 @@
 // .amdhsa_float_denorm_mode_16_64 3).
 #include "gm_internal.hpp"
 #include "gm_common.hpp"
+#include "box_common.hpp"
 
 #include <algorithm>
 #include <utility>
@@ -83,69 +84,6 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 #ifndef GM_BOX_PRIO_I
 #define GM_BOX_PRIO_I 3        // issuing the next group's child loads
 #endif
-
-// ---------------------------------------------------------------------------
-// key <-> table index
-GM_HD uint32_t box_index_of_key(uint32_t k) {
-    uint32_t off = 0, box = 0;
-    for (int i = 0; i < 4; i++) {
-        const uint32_t h = (k >> (4 * i)) & 15u;
-        off |= (h & 3u) << (4 + 2 * i);
-        box |= (h >> 2) << (2 * i);
-    }
-    for (int j = 0; j < 4; j++) {
-        const uint32_t h = (k >> (16 + 4 * j)) & 15u;
-        off |= (h & 1u) << j;
-        box |= (h >> 1) << (8 + 3 * j);
-    }
-    return (box << 12) | off;
-}
-GM_HD uint32_t box_key_of_index(uint32_t x) {
-    const uint32_t off = x & 4095u, box = x >> 12;
-    uint32_t k = 0;
-    for (int i = 0; i < 4; i++) {
-        const uint32_t h = (((box >> (2 * i)) & 3u) << 2) | ((off >> (4 + 2 * i)) & 3u);
-        k |= h << (4 * i);
-    }
-    for (int j = 0; j < 4; j++) {
-        const uint32_t h = (((box >> (8 + 3 * j)) & 7u) << 1) | ((off >> j) & 1u);
-        k |= h << (16 + 4 * j);
-    }
-    return k;
-}
-GM_HD int box_coord(uint32_t box, int dim) {
-    return dim < 4 ? (int)((box >> (2 * dim)) & 3u) : (int)((box >> (8 + 3 * (dim - 4))) & 7u);
-}
-GM_HD uint32_t box_unit(int dim) { return dim < 4 ? 1u << (2 * dim) : 1u << (8 + 3 * (dim - 4)); }
-
-// ---------------------------------------------------------------------------
-// Heap permutations of the sharded solve.  The game is the same on every
-// heap, so a permutation of heaps maps positions to positions of equal value; the ones
-// that map boxes to boxes permute A heaps among themselves and B heaps among themselves.
-// The sharded solve uses the group H = <r> x <t>: r rotates the A heaps (heap i -> heap
-// i + 1 mod 4), t swaps heaps 4 <-> 5 and 6 <-> 7.  Element code = k | e << 2 for r^k t^e.
-// On a box id: the A coordinates (bits 0-7, 2 bits per heap) rotate left by 2k bits; t
-// swaps the 3-bit B coordinates of heaps 4/5 (bits 8-10 / 11-13) and 6/7 (14-16 / 17-19).
-GM_HD uint32_t bsym_rot8(uint32_t f, uint32_t k) { return ((f | (f << 8)) >> (8 - 2 * k)) & 0xFFu; }
-GM_HD uint32_t bsym_tau_box(uint32_t b) {
-    const uint32_t x = ((b >> 3) ^ b) & 0x1C700u;
-    return b ^ x ^ (x << 3);
-}
-GM_HD uint32_t bsym_box(uint32_t code, uint32_t b) {
-    b = (b & ~0xFFu) | bsym_rot8(b & 0xFFu, code & 3u);
-    return (code & 4u) ? bsym_tau_box(b) : b;
-}
-// on a key (heap i at bits 4i): the low four nibbles rotate left by 4k bits; t swaps
-// nibbles 4/5 and 6/7
-GM_HD uint32_t bsym_key(uint32_t code, uint32_t key) {
-    const uint32_t k = code & 3u, lo = key & 0xFFFFu;
-    key = (key & 0xFFFF0000u) | (((lo | (lo << 16)) >> (16 - 4 * k)) & 0xFFFFu);
-    if (code & 4u) {
-        const uint32_t x = ((key >> 4) ^ key) & 0x0F0F0000u;
-        key ^= x ^ (x << 4);
-    }
-    return key;
-}
 
 // ---------------------------------------------------------------------------
 // device helpers
@@ -225,14 +163,22 @@ constexpr int BX_NLOAD = 48;              // 16-B child rows per lane per group
 
 struct BxGroup {
     uint32_t box[2];
-    uint32_t fill[2];   // sharded solve: per child direction d, 3 bits at 3 d: the code of the
-                        // permutation h whose image h(C) of the child box C this rank computes
+    uint32_t fill[2];   // split solve (dist_box.hip): per child direction d, 4 bits at 4 d: for an A
+                        // heap the digit pair (q << 2 | p) of the A transposition the child is read
+                        // through (q = p: none), for a B heap 1 + the pair of B heaps (0: none)
+    uint32_t srcv;      // split solve: lane 8 k + d holds the box read for box k's child along heap
+                        // d (the child box C, or its image under that transposition, which this
+                        // rank computed); one VGPR, read with readlane when the loads are issued
+    uint32_t dstv;      // split solve: lane 4 k + e (e < 3) holds box k's e-th halo destination: bits
+                        // 28-31 kind (0 none, 1-4 the two top layers along A heap kind - 1, 5 the
+                        // whole box), bits 0-27 its offset in the send buffer / 2 KiB
     bool valid[2];
 };
 
 template <bool SHARD>
 __device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, const uint32_t *__restrict__ fills,
-                                            uint32_t nbox, uint32_t g) {
+                                            const uint32_t *__restrict__ srcs, const uint32_t *__restrict__ dsts,
+                                            uint32_t nbox, uint32_t g, uint32_t lane) {
     BxGroup G;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -241,36 +187,87 @@ __device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, 
         G.box[k] = G.valid[k] ? boxes[i] : 0u;
         G.fill[k] = (SHARD && G.valid[k]) ? fills[i] : 0u;
     }
+    G.srcv = G.dstv = 0;
+    if constexpr (SHARD) {
+        const uint32_t i = 2 * g + (lane >> 3);
+        if (lane < 16 && i < nbox) G.srcv = srcs[8 * i + (lane & 7u)];
+        const uint32_t i2 = 2 * g + (lane >> 2);
+        if (lane < 8 && (lane & 3u) < 3u && i2 < nbox) G.dstv = dsts[3 * i2 + (lane & 3u)];
+    }
     return G;
 }
-
-// Sharded solve: a B child read from the box t(C) is the child's row with B bits b0 <-> b1
-// and b2 <-> b3 swapped: byte e of dword q of the child row is byte sw(e) of dword sw(q) of
-// the loaded row, sw exchanging 1 and 2.
-__device__ __forceinline__ bx_u32x4 bx_tau_row(const bx_u32x4 &x) {
-    constexpr uint32_t S = 0x03010200u;
-    return bx_u32x4{__builtin_amdgcn_perm(x[0], x[0], S), __builtin_amdgcn_perm(x[2], x[2], S),
-                    __builtin_amdgcn_perm(x[1], x[1], S), __builtin_amdgcn_perm(x[3], x[3], S)};
+template <bool SHARD>
+__device__ __forceinline__ uint32_t bx_src(const BxGroup &G, int k, int d) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)G.srcv, 8 * k + d);
 }
+
+// Byte B of a child row read through the B transposition of heaps 4 + Q, 4 + P is byte
+// swap(B) of the loaded row (bits Q, P of B exchanged): each output dword takes its four
+// bytes from at most two loaded dwords, one v_perm_b32.
+constexpr int bx_swb(int b, int q, int p) { return b ^ ((((b >> q) ^ (b >> p)) & 1) * ((1 << q) | (1 << p))); }
+constexpr int bx_src_lo(int w, int q, int p) {
+    int m = 3;
+    for (int e = 0; e < 4; e++) m = bx_swb(4 * w + e, q, p) / 4 < m ? bx_swb(4 * w + e, q, p) / 4 : m;
+    return m;
+}
+constexpr int bx_src_hi(int w, int q, int p) {
+    int m = 0;
+    for (int e = 0; e < 4; e++) m = bx_swb(4 * w + e, q, p) / 4 > m ? bx_swb(4 * w + e, q, p) / 4 : m;
+    return m;
+}
+constexpr uint32_t bx_bsel(int w, int q, int p) {
+    uint32_t sel = 0;
+    for (int e = 0; e < 4; e++) {
+        const int s = bx_swb(4 * w + e, q, p);
+        sel |= (uint32_t)((s / 4 == bx_src_lo(w, q, p) ? 0 : 4) + (s & 3)) << (8 * e);
+    }
+    return sel;
+}
+template <int Q, int P, int W>
+__device__ __forceinline__ uint32_t bx_bsw_dw(const bx_u32x4 &x) {
+    constexpr int lo = bx_src_lo(W, Q, P), hi = bx_src_hi(W, Q, P);
+    constexpr uint32_t sel = bx_bsel(W, Q, P);
+    if constexpr (sel == 0x03020100u) return x[lo];
+    return __builtin_amdgcn_perm(x[hi], x[lo], sel);
+}
+template <int Q, int P>
+__device__ __forceinline__ bx_u32x4 bx_bsw(const bx_u32x4 &x) {
+    return bx_u32x4{bx_bsw_dw<Q, P, 0>(x), bx_bsw_dw<Q, P, 1>(x), bx_bsw_dw<Q, P, 2>(x), bx_bsw_dw<Q, P, 3>(x)};
+}
+// a loaded row back to the child's byte order; `code` (1 + pair of B heaps) is uniform
+__device__ __forceinline__ bx_u32x4 bx_bswap_row(const bx_u32x4 &x, uint32_t code) {
+    switch (code) {
+    case 1: return bx_bsw<0, 1>(x);
+    case 2: return bx_bsw<0, 2>(x);
+    case 3: return bx_bsw<0, 3>(x);
+    case 4: return bx_bsw<1, 2>(x);
+    case 5: return bx_bsw<1, 3>(x);
+    case 6: return bx_bsw<2, 3>(x);
+    }
+    return x;
+}
+__device__ __forceinline__ uint32_t bx_fcode(const BxGroup &G, int k, int dir) { return (G.fill[k] >> (4 * dir)) & 15u; }
 
 // Every child row of a group, in flight at once: R[0..31] the B children of target rows
 // m = lane + 64 i (R[8 i + 4 k + j]: box k, heap 4 + j), R[32..47] the A children's top
 // layers (R[32 + 4 i + 2 k + v]: heap i, box k, layer 3 - v) of the rows a_i in {2, 3}
 // whose other coordinates are the lane.
 //
-// Sharded solve (SHARD): a child box C this rank does not compute is read from its image
-// S = h(C) under the permutation h of the group's fill code, which this rank computed in
-// the same box-tier.  The plan (box_plan) only uses t for B children and r^k for A
-// children: a B child's rows are then S's rows, byte-permuted in bx_fold (bx_tau_row);
-// an A child's row A is S's row rotl8(A, 2k) (the A digits move with the heaps), an
-// address change only.
+// Split solve (SHARD, dist_box.hip): a child box C that this rank neither computes nor
+// received is read from its image S = s(C) under a transposition s of two heaps of the child's
+// own kind (an A child through two A heaps, a B child through two B heaps); this rank computed
+// S in the box-tier before (a transposition keeps the box-tier).  The plan gives per box the
+// eight boxes read (scalar loads; computing the swaps here overflowed the SGPRs) and the fill
+// word: an A transposition moves rows (row A of C is row swap(A) of S, digits q and p: a
+// per-lane address change here), a B transposition permutes the bytes of a row (bx_fold).
 template <bool SHARD, int CPOL = 0>
 __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
                                          bx_u32x4 (&R)[BX_NLOAD]) {
     const __amdgpu_buffer_rsrc_t rt =
         __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, (GM_BOX_EXP & 2) ? 0u : 0xFFFFFFFFu, 0x00020000);
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0u, 0x00020000);
-    // one (descriptor, offset) per child box, used by consecutive loads
+    // one (descriptor, offset) per child box, used by consecutive loads; a B child read through
+    // a B transposition is the same rows of the image box (bytes permuted in bx_fold)
     {
 #pragma unroll
         for (int k = 0; k < 2; k++)
@@ -278,8 +275,7 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
             for (int j = 0; j < 4; j++) {
                 const bool ok = G.valid[k] && box_coord(G.box[k], 4 + j) >= 1;
                 uint32_t src = G.box[k] - box_unit(4 + j);
-                if constexpr (SHARD)
-                    if ((G.fill[k] >> (3 * (4 + j))) & 4u) src = bsym_tau_box(src);
+                if constexpr (SHARD) src = bx_src<SHARD>(G, k, 4 + j);
                 const uint32_t soff = ok ? src << 12 : 0u;
                 const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
 #pragma unroll
@@ -288,6 +284,8 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
                         bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * (lane + 64u * i), soff, CPOL));
             }
     }
+    // an A child read through an A transposition (digits q, p): row A of C is row swap(A) of
+    // the image box -- branch-free, shifts of 0 for no transposition
     {
 #pragma unroll
         for (int i = 0; i < 4; i++) {
@@ -295,28 +293,24 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
 #pragma unroll
             for (int k = 0; k < 2; k++) {
                 const bool ok = G.valid[k] && box_coord(G.box[k], i) >= 1;
+                uint32_t src = G.box[k] - box_unit(i), sq = 0, sp = 0;
+                if constexpr (SHARD) {
+                    const uint32_t code = bx_fcode(G, k, i);
+                    src = bx_src<SHARD>(G, k, i);
+                    sq = 2u * (code >> 2);
+                    sp = 2u * (code & 3u);
+                }
+                const uint32_t soff = ok ? src << 12 : 0u;
                 const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
-                if constexpr (!SHARD) {
-                    const uint32_t soff = ok ? (G.box[k] - box_unit(i)) << 12 : 0u;
 #pragma unroll
-                    for (int v = 0; v < 2; v++) {
-                        const uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
-                        R[32 + 4 * i + 2 * k + v] =
-                            __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, CPOL));
+                for (int v = 0; v < 2; v++) {
+                    uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
+                    if constexpr (SHARD) {
+                        const uint32_t t = ((A >> sq) ^ (A >> sp)) & 3u;
+                        A ^= (t << sq) | (t << sp);
                     }
-                } else {
-                    // row rotl8(A, 2 rot): the lane's digits rotated (VGPR), digit i's layer
-                    // 3 - v moved to digit i + rot (uniform, in the scalar offset)
-                    const uint32_t rot = (G.fill[k] >> (3 * i)) & 3u;
-                    const uint32_t src = bsym_box(rot, G.box[k] - box_unit(i));
-                    const uint32_t soff = ok ? src << 12 : 0u;
-                    const uint32_t L = lo | hi;
-                    const uint32_t voff = __builtin_amdgcn_ubfe(L | (L << 8), 8u - 2u * rot, 8u) << 4;
-                    const uint32_t sh = 2u * ((i + rot) & 3u);
-#pragma unroll
-                    for (int v = 0; v < 2; v++)
-                        R[32 + 4 * i + 2 * k + v] = __builtin_bit_cast(
-                            bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff + ((3u - v) << (sh + 4u)), CPOL));
+                    R[32 + 4 * i + 2 * k + v] =
+                        __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, CPOL));
                 }
             }
         }
@@ -326,14 +320,16 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
 // fold: the image's slot of every position gets the max of its children outside the box
 template <bool SHARD>
 __device__ __forceinline__ void bx_fold(uint32_t *s, const BxGroup &G, uint32_t lane, bx_u32x4 (&R)[BX_NLOAD]) {
-    if constexpr (SHARD) {   // B children read from t(C): back to C's byte order (uniform branches)
+    if constexpr (SHARD) {   // B children read through a B transposition: back to C's byte order (uniform branches)
 #pragma unroll
         for (int k = 0; k < 2; k++)
 #pragma unroll
-            for (int j = 0; j < 4; j++)
-                if ((G.fill[k] >> (3 * (4 + j))) & 4u)
+            for (int j = 0; j < 4; j++) {
+                const uint32_t code = bx_fcode(G, k, 4 + j);
+                if (code)
 #pragma unroll
-                    for (int i = 0; i < 4; i++) R[8 * i + 4 * k + j] = bx_tau_row(R[8 * i + 4 * k + j]);
+                    for (int i = 0; i < 4; i++) R[8 * i + 4 * k + j] = bx_bswap_row(R[8 * i + 4 * k + j], code);
+            }
     }
     // B children: row m of the child box below along heap 4 + j; a position with b_j = 0
     // also takes b | e_j of that row (its child two below)
@@ -553,27 +549,58 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
     bx_unroll(step, std::make_integer_sequence<int, BX_STEPS>{});
 }
 
-// store: rows m = lane + 64 i of both boxes, bytes regrouped per box
-__device__ __forceinline__ void bx_store(uint8_t *table, const BxGroup &G, const uint32_t *s, uint32_t lane) {
+// store: rows m = lane + 64 i of both boxes, bytes regrouped per box.  Split solve: a box another
+// rank needs is also written, from the same registers, to its slot in the halo message (the
+// whole box, or only its two top layers along an A heap, rows compacted as box_pack_kernel
+// packs them), so no pack launch sits between the tier launches.
+template <bool SHARD>
+__device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, const BxGroup &G, const uint32_t *s,
+                                         uint32_t lane) {
     __amdgpu_buffer_rsrc_t w[2];
 #pragma unroll
     for (int k = 0; k < 2; k++)
         w[k] = __builtin_amdgcn_make_buffer_rsrc(table + ((uint64_t)G.box[k] << 12), 0,
                                                  (G.valid[k] && !(GM_BOX_EXP & 4)) ? 4096u : 0u, 0x00020000);
+    uint32_t dst[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    __amdgpu_buffer_rsrc_t wm;
+    if constexpr (SHARD) {
+        wm = __builtin_amdgcn_make_buffer_rsrc((void *)msg, 0, 0xFFFFFFFFu, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int e = 0; e < 3; e++) dst[k][e] = (uint32_t)__builtin_amdgcn_readlane((int)G.dstv, 4 * k + e);
+    }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const uint32_t m = lane + 64u * i;
-        bx_u32x4 o0, o1;
+        bx_u32x4 o[2];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const bx_u32x4 x = *(const bx_u32x4 *)(s + bx_row(m) + 4u * q);
             const uint32_t t01 = __builtin_amdgcn_perm(x[1], x[0], 0x06020400u);
             const uint32_t t23 = __builtin_amdgcn_perm(x[3], x[2], 0x06020400u);
-            o0[q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
-            o1[q] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+            o[0][q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+            o[1][q] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(o0, w[0], 16u * m, 0, GM_BOX_STORE_CPOL);
-        __builtin_amdgcn_raw_buffer_store_b128(o1, w[1], 16u * m, 0, GM_BOX_STORE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(o[0], w[0], 16u * m, 0, GM_BOX_STORE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(o[1], w[1], 16u * m, 0, GM_BOX_STORE_CPOL);
+        if constexpr (SHARD) {
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+#pragma unroll
+                for (int e = 0; e < 3; e++) {
+                    const uint32_t d = dst[k][e], kind = d >> 28;
+                    if (!kind) continue;   // uniform
+                    const uint32_t base = (d & 0x0FFFFFFFu) << 11;
+                    if (kind == 5) {
+                        __builtin_amdgcn_raw_buffer_store_b128(o[k], wm, 16u * m, base, 0);
+                    } else {
+                        const uint32_t hh = 2u * (kind - 1u), a = (m >> hh) & 3u;
+                        const uint32_t t = (m & ((1u << hh) - 1u)) | ((a & 1u) << hh) | ((m >> (hh + 2u)) << (hh + 1u));
+                        if (a >= 2u) __builtin_amdgcn_raw_buffer_store_b128(o[k], wm, 16u * t, base, 0);
+                    }
+                }
+        }
     }
 }
 
@@ -599,7 +626,9 @@ template <bool SHARD>
 __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__restrict__ table,
                                                                      const uint32_t *__restrict__ boxes,
                                                                      const uint32_t *__restrict__ fills,
-                                                                     uint32_t nbox) {
+                                                                     const uint32_t *__restrict__ srcs,
+                                                                     const uint32_t *__restrict__ dsts,
+                                                                     uint8_t *__restrict__ msg, uint32_t nbox) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[BX_LDS];
     uint32_t *s = lds + BX_PAD;
     const uint32_t lane = threadIdx.x;
@@ -614,7 +643,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
     // b2 / b3 neighbour
     s[BX_PITCH * lane + BX_Z] = 0;
     bx_u32x4 R[BX_NLOAD];
-    BxGroup G = bx_group<SHARD>(boxes, fills, nbox, g);
+    BxGroup G = bx_group<SHARD>(boxes, fills, srcs, dsts, nbox, g, lane);
     bx_issue<SHARD>(table, G, lane, R);
 #if GM_BOX_TRACE
     unsigned long long tt[5], acc[4] = {0, 0, 0, 0}, ngr = 0, tbeg, rbeg;
@@ -638,7 +667,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         const uint32_t gn = g + Kx;
         const bool more = gn < g1;
         BxGroup Gn = G;
-        if (more) Gn = bx_group<SHARD>(boxes, fills, nbox, gn);
+        if (more) Gn = bx_group<SHARD>(boxes, fills, srcs, dsts, nbox, gn, lane);
         BX_LDS_ORDER();
 #if GM_BOX_TRACE
         BX_STAMP(tt[2]);
@@ -649,7 +678,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 #if GM_BOX_TRACE
         BX_STAMP(tt[3]);
 #endif
-        bx_store(table, G, s, ln);
+        bx_store<SHARD>(table, msg, G, s, ln);
         BX_LDS_ORDER();
 #if GM_BOX_TRACE
         BX_STAMP(tt[4]);
@@ -698,6 +727,8 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 #ifndef GM_BOX_FLOW_LOAD_CPOL
 #define GM_BOX_FLOW_LOAD_CPOL 16   // child rows read sc1 (the hand-off table's consumer loads)
 #endif
+// the hand-off needs the producer's rows written through to the coherent level before its flag
+static_assert(GM_BOX_STORE_CPOL & 16, "box_flow_kernel publishes flags after sc1 stores: keep GM_BOX_STORE_CPOL sc1");
 struct BxFlow {
     const uint32_t *groups;   // queue q: groups[qbase[q] + j], j < qlen[q]: box-list index | second box << 31
     uint32_t qbase[8], qlen[8];
@@ -711,33 +742,30 @@ struct BxFlow {
 
 template <bool SHARD>
 __device__ __forceinline__ BxGroup bx_group_rec(const uint32_t *__restrict__ boxes, const uint32_t *__restrict__ fills,
-                                                uint32_t rec) {
+                                                const uint32_t *__restrict__ srcs, uint32_t rec, uint32_t lane) {
     BxGroup G;
     const uint32_t i = rec & 0x7FFFFFFFu;
     const bool two = rec >> 31;
     G.valid[0] = true;
     G.box[0] = boxes[i];
-    G.fill[0] = SHARD ? fills[i] : 0u;
     G.valid[1] = two;
     G.box[1] = two ? boxes[i + 1] : 0u;
+    G.fill[0] = SHARD ? fills[i] : 0u;
     G.fill[1] = (SHARD && two) ? fills[i + 1] : 0u;
+    G.srcv = G.dstv = 0;
+    if constexpr (SHARD)
+        if (lane < 16 && (lane < 8 || two)) G.srcv = srcs[8 * (i + (lane >> 3)) + (lane & 7u)];
     return G;
 }
 
-// the box the group's box k reads for its child along heap dir (bx_issue's choice), ~0 if none
+// the box the group's box k reads for its child along heap dir (bx_issue's choice), ~0 if none;
+// lane 8 k + dir asks for its own
 template <bool SHARD>
 __device__ __forceinline__ uint32_t bx_child_src(const BxGroup &G, uint32_t k, uint32_t dir) {
-    const uint32_t box = k ? G.box[1] : G.box[0], fill = k ? G.fill[1] : G.fill[0];
+    const uint32_t box = k ? G.box[1] : G.box[0];
     if (!(k ? G.valid[1] : G.valid[0]) || box_coord(box, (int)dir) < 1) return ~0u;
-    uint32_t src = box - box_unit((int)dir);
-    if constexpr (SHARD) {
-        if (dir >= 4) {
-            if ((fill >> (3 * dir)) & 4u) src = bsym_tau_box(src);
-        } else {
-            src = bsym_box((fill >> (3 * dir)) & 3u, src);
-        }
-    }
-    return src;
+    if constexpr (SHARD) return G.srcv;
+    return box - box_unit((int)dir);
 }
 
 // lanes 0-15 each wait for one child box of G (k = lane >> 3, heap lane & 7): src, and the
@@ -779,7 +807,8 @@ __device__ unsigned long long bx_ftrace[BX_FT_WORDS * BX_FT_GROUPS];
 template <bool SHARD>
 __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__restrict__ table,
                                                                      const uint32_t *__restrict__ boxes,
-                                                                     const uint32_t *__restrict__ fills, BxFlow F) {
+                                                                     const uint32_t *__restrict__ fills,
+                                                                     const uint32_t *__restrict__ srcs, BxFlow F) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[BX_LDS];
     uint32_t *s = lds + BX_PAD;
     const uint32_t lane = threadIdx.x, q = blockIdx.x & 7u, qn = F.qlen[q];
@@ -798,7 +827,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
         unsigned long long ft[5];
         BX_RT(ft[0]);
 #endif
-        const BxGroup G = bx_group_rec<SHARD>(boxes, fills, gq[j]);
+        const BxGroup G = bx_group_rec<SHARD>(boxes, fills, srcs, gq[j], lane);
         const uint32_t src = lane < 16u ? bx_child_src<SHARD>(G, lane >> 3, lane & 7u) : ~0u;
         const uint32_t seen = bx_flag_src_load(F, src);
         if (!(F.dev & 1u) && !bx_wait(F, src, seen, lane, ep)) return;
@@ -821,7 +850,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
 #if GM_BOX_FLOW_TRACE
         BX_RT(ft[3]);
 #endif
-        bx_store(table, G, s, ln);
+        bx_store<false>(table, nullptr, G, s, ln);
         BX_LDS_ORDER();
         // publish: the wave's sc1 stores done, then one lane stores each box's flag sc1
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -871,27 +900,26 @@ __global__ void box_digest_kernel(const uint8_t *__restrict__ table, const uint3
 }
 
 // Records of keys: REC_UNSOLVED outside the root's region (a key with a nibble above the
-// root's, whose slot the solve never wrote).  Sharded: `map` gives per box id the
-// permutation h whose image of the box this rank computed; the key's record is then its
-// image's (the game is symmetric under heap permutations).
-__global__ void box_query_kernel(const uint8_t *__restrict__ table, const uint8_t *__restrict__ map, uint64_t root,
-                                 const uint64_t *__restrict__ keys, uint16_t *__restrict__ out, uint64_t n) {
+// root's, whose slot the solve never wrote).  Split solve with virtual ranks (dist_box.hip):
+// `owner` gives per box id the rank whose table holds it (0xFF: none), `tables` per rank.
+__global__ void box_query_kernel(const uint8_t *const *__restrict__ tables, const uint8_t *__restrict__ owner,
+                                 uint64_t root, const uint64_t *__restrict__ keys, uint16_t *__restrict__ out, uint64_t n) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t k = keys[i];
     bool in = k < (1ull << 32);
     for (int j = 0; j < 8 && in; j++) in = ((k >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
     if (!in) { out[i] = REC_UNSOLVED; return; }
-    uint32_t key = (uint32_t)k;
-    if (map) key = bsym_key(map[box_index_of_key(key) >> 12], key);
-    out[i] = record_of_code(table[box_index_of_key(key)]);
+    const uint32_t idx = box_index_of_key((uint32_t)k);
+    const uint32_t r = owner ? owner[idx >> 12] : 0u;
+    out[i] = r == 0xFFu ? REC_UNSOLVED : record_of_code(tables[r][idx]);
 }
 
 // ---------------------------------------------------------------------------
 // host
 
 // Hilbert index (Skilling's transpose form) of the first 7 box coordinates, 3 bits each
-static uint64_t box_hilbert(uint32_t box) {
+uint64_t box_hilbert(uint32_t box) {
     const int n = 7;
     uint32_t xv[8];
     for (int i = 0; i < n; i++) xv[i] = (uint32_t)box_coord(box, i);
@@ -912,159 +940,54 @@ static uint64_t box_hilbert(uint32_t box) {
     return hv;
 }
 
-// The order whose least orbit member is the orbit's representative: B coordinates first
-// (c4, c5, c6, c7, c0, c1, c2, c3), 3 bits each.  With it every fill is "pure" -- a B child
-// needs only t, an A child only a rotation -- which the kernel relies on (box_plan checks).
-static uint32_t bsym_ord(uint32_t b) {
-    uint32_t o = 0;
-    for (int n = 0; n < 8; n++) o = (o << 3) | (uint32_t)box_coord(b, n < 4 ? 4 + n : n - 4);
-    return o;
+// Resident one-wave workgroups of a box kernel on this device (dynamic LDS `dyn` bytes):
+// the tier launches' grid cap, and the dataflow launch's grid, which must be resident
+// whole for its waits to make progress (asked of the runtime, not
+// assumed).
+static int box_resident(const void *kernel, int device, size_t dyn) {
+    int cus = 256, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 64, dyn) != hipSuccess || per < 1) {
+        (void)hipGetLastError();
+        per = 4 * GM_BOX_WAVES;
+    }
+    return cus * per;
 }
+int box_grid_cap(int device) { return box_resident((const void *)box_tier_kernel<true>, device, 0); }
 
-// The plan of one rank of a `world`-rank sharded box solve (host only, no HIP call).
-//
-// Partition.  H = <r^(4/m)> x <t> with |H| = 2m the largest power of two <= min(world, 8),
-// cut down to the permutations that fix the root's region (its stabiliser H').  Rank r
-// takes the element g = H'[r mod |H'|] and computes R_r = g^-1(F), F = the boxes that are
-// the least member (bsym_ord) of their H'-orbit: R_r holds exactly one member of every
-// orbit, and every R_r is a heap permutation of F, so all ranks have the same number of
-// boxes in every box-tier.  A box fixed by some h != id (a "tie") is in several R_r and
-// computed by each of them; it is OWNED (digest, export) by the first.  A child box C of a
-// box of R_r is either in R_r or some image h(C), h in H', is -- computed by this rank in
-// the same box-tier (h keeps the coordinate sum) -- so a rank never needs another rank's
-// values: no exchange at all.  The kernel reads such a child through h (fill codes).
-struct BoxPlan {
-    int nsym = 1;                                  // |H'|
-    uint32_t g = 0;                                // this rank's element
-    std::vector<uint32_t> boxes, fills, tier_off;  // computed boxes by (box-tier, Hilbert), fill codes
-    std::vector<uint32_t> own;                     // owned boxes, ascending
-    std::vector<uint8_t> map;                      // 2^20: per box of the region, h with h(box) in R_r
-    uint64_t ties = 0;                             // computed boxes also computed by another rank
-};
-
-static int box_plan(uint32_t root_hi, int world, int rank, bool want_map, BoxPlan *p) {
-    if (world < 1 || rank < 0 || rank >= world) { set_error("bad rank %d of %d", rank, world); return GM_E_ARG; }
-    int hs = 1;
-    while (hs * 2 <= std::min(world, 8)) hs *= 2;
-    static const uint32_t Hfull[4][8] = {{0}, {0, 4}, {0, 4, 2, 6}, {0, 4, 1, 5, 2, 6, 3, 7}};
-    const uint32_t *H = Hfull[hs == 1 ? 0 : hs == 2 ? 1 : hs == 4 ? 2 : 3];
-    std::vector<uint32_t> Hs;
-    for (int e = 0; e < hs; e++)
-        if (bsym_box(H[e], root_hi) == root_hi) Hs.push_back(H[e]);
-    const int n = (int)Hs.size();
-    p->nsym = n;
-    p->g = Hs[rank % n];
-    int lim[8], tmax = 0;
-    for (int i = 0; i < 8; i++) { lim[i] = box_coord(root_hi, i); tmax += lim[i]; }
-    auto in_region = [&](uint32_t b) {
-        for (int i = 0; i < 8; i++)
-            if (box_coord(b, i) > lim[i]) return false;
-        return true;
-    };
-    // R membership of every box of the region, and its owner element
-    std::vector<uint8_t> inR(1u << 20, 0);
-    std::vector<uint32_t> region;
-    for (uint32_t b = 0; b < (1u << 20); b++) {
-        if (!in_region(b)) continue;
-        region.push_back(b);
-        uint32_t mo = 0xFFFFFFFFu, og = 0, first = 0;
-        bool any = false;
-        for (int e = 0; e < n; e++) {
-            const uint32_t o = bsym_ord(bsym_box(Hs[e], b));
-            if (o < mo) { mo = o; }
-        }
-        for (int e = 0; e < n; e++)
-            if (bsym_ord(bsym_box(Hs[e], b)) == mo) {
-                if (!any) first = (uint32_t)e;
-                any = true;
-                og++;
-            }
-        const bool mine = bsym_ord(bsym_box(p->g, b)) == mo;
-        inR[b] = mine ? (uint8_t)(1 + (rank < n && first == (uint32_t)rank)) : 0;   // 2 = owned
-        if (mine && og > 1) p->ties++;
-    }
-    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> tiers(tmax + 1);
-    std::vector<std::vector<uint32_t>> tfill(tmax + 1);
-    p->own.clear();
-    for (uint32_t b : region) {
-        if (!inR[b]) continue;
-        if (inR[b] == 2) p->own.push_back(b);
-        int t = 0;
-        for (int i = 0; i < 8; i++) t += box_coord(b, i);
-        tiers[t].push_back({box_hilbert(b), b});
-    }
-    auto fill_of = [&](uint32_t b, uint32_t *code) {
-        uint32_t f = 0;
-        for (int d = 0; d < 8; d++) {
-            if (box_coord(b, d) < 1) continue;
-            const uint32_t cb = b - box_unit(d);
-            if (inR[cb]) continue;
-            bool found = false;
-            for (int e = 1; e < n && !found; e++) {
-                const uint32_t h = Hs[e];
-                const bool pure = d < 4 ? !(h & 4u) : !(h & 3u);
-                if (pure && inR[bsym_box(h, cb)]) { f |= h << (3 * d); found = true; }
-            }
-            if (!found) return false;
-        }
-        *code = f;
-        return true;
-    };
-    p->boxes.clear();
-    p->fills.clear();
-    p->tier_off.assign(1, 0);
-    for (auto &tv : tiers) {
-        std::sort(tv.begin(), tv.end());
-        for (auto &e : tv) {
-            uint32_t f = 0;
-            if (!fill_of(e.second, &f)) {
-                set_error("box plan: no heap permutation in the kernel's form reads a child of box %#x (rank %d of %d)",
-                          e.second, rank, world);
-                return GM_E_STATE;
-            }
-            p->boxes.push_back(e.second);
-            p->fills.push_back(f);
-        }
-        p->tier_off.push_back((uint32_t)p->boxes.size());
-    }
-    p->map.clear();
-    if (want_map && n > 1) {
-        p->map.assign(1u << 20, 0xFF);
-        for (uint32_t b : region)
-            for (int e = 0; e < n; e++)
-                if (inR[bsym_box(Hs[e], b)]) { p->map[b] = (uint8_t)Hs[e]; break; }
-    }
-    return GM_OK;
+void box_launch_tier_split(uint32_t grid, uint8_t *table, const uint32_t *boxes, const uint32_t *fills,
+                           const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint32_t nbox, hipStream_t s) {
+    hipLaunchKernelGGL(box_tier_kernel<true>, dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs, dsts, msg, nbox);
 }
-
-struct BoxRank {
-    int rank = 0;
-    uint8_t *table = nullptr;
-    bool owned = false;
-    uint32_t *d_boxes = nullptr, *d_fills = nullptr, *d_own = nullptr;
-    uint8_t *d_map = nullptr;
-    std::vector<uint32_t> tier_off;
-    std::vector<uint32_t> own;        // host copy (export)
-    uint64_t n_boxes = 0, ties = 0;
-    hipGraphExec_t graph = nullptr;
-    hipEvent_t ev[2] = {nullptr, nullptr};
-    float kernel_ms = 0;
-    uint32_t *d_groups = nullptr;     // one-launch solve: the 8 group queues (BxFlow)
-    uint32_t qbase[8] = {}, qlen[8] = {};
-};
+void box_launch_digest(const uint8_t *table, const uint32_t *boxes, uint64_t nbox, uint64_t root,
+                       unsigned long long *acc, hipStream_t s) {
+    if (nbox) hipLaunchKernelGGL(box_digest_kernel, dim3(4096), dim3(256), 0, s, table, boxes, nbox, root, acc);
+}
+void box_launch_query(const uint8_t *const *tables, const uint8_t *owner, uint64_t root, const uint64_t *keys,
+                      uint16_t *out, uint64_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(box_query_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tables, owner, root, keys,
+                              out, n);
+}
 
 struct DenseBox {
     uint32_t root_hi = 0;
-    int world = 1;                    // ranks of the solve (one per process, or virtual on this GPU)
-    int nsym = 1;                     // |H'|: ranks that compute different box sets
-    bool shard = false, virt = false;
-    std::vector<BoxRank> ranks;       // the ranks this context runs
+    uint8_t *table = nullptr;
+    bool owned = false;
+    uint32_t *d_boxes = nullptr;
+    std::vector<uint32_t> tier_off;
+    std::vector<uint32_t> boxes;      // host copy (digest list = every box of the region)
+    hipGraphExec_t graph = nullptr;
+    hipStream_t graph_stream = nullptr;
+    hipEvent_t ev[2] = {nullptr, nullptr};
     int grid_cap = 2048;
     uint64_t *d_acc = nullptr;
-    hipStream_t graph_stream = nullptr;
+    const uint8_t **d_tables = nullptr;   // [1] = table (box_query_kernel's table array)
     bool flow = false;                // one-launch (dataflow) solve (GM_OPT_BOX_FLOW)
-    bool flow_failed = false;         // a dataflow solve timed out: tier launches from then on
-    uint32_t *d_flow = nullptr;       // [0, 9) queue cursors + error, [16] epoch, [64, 64 + 2^20) box flags
+    int flow_grid = 0;                // the dataflow launch's grid: its resident capacity
+    size_t flow_dyn = 0;              // dynamic LDS of the dataflow launch (GM_BOX_FLOW_EXTRA_LDS, tests)
+    uint32_t *d_flow = nullptr;       // [0, 9) error word at [8], [16] epoch, [64, 64 + 2^20) box flags
+    uint32_t *d_groups = nullptr;     // the 8 group queues (BxFlow)
+    uint32_t qbase[8] = {}, qlen[8] = {};
     uint32_t *h_res = nullptr;        // pinned: [0] the root's code (low byte), [1] the dataflow error word
 };
 
@@ -1074,10 +997,10 @@ static int box_flow_env() {
     static const int v = getenv("GM_BOX_FLOW") ? atoi(getenv("GM_BOX_FLOW")) : -1;
     return v;
 }
-static bool box_flow_wanted(const Ctx *c, bool shard) {
+static bool box_flow_wanted(const Ctx *c) {
     const int e = box_flow_env();
     if (e >= 0) return e != 0;
-    return c->box_flow < 0 ? shard : c->box_flow != 0;
+    return c->box_flow == 1 && !c->box_flow_failed;
 }
 
 // The tier launches' groups in 8 queues: queue x = every tier's XCD run x, tier after
@@ -1086,25 +1009,11 @@ static bool box_flow_wanted(const Ctx *c, bool shard) {
 // children in the tier before, and the run is sorted by key (stable: Hilbert order among
 // equals), so the first rounds of a tier take the groups whose children the first rounds
 // of the tier before made (GM_BOX_FLOW_ORDER 0: Hilbert order only).
-static void box_flow_queues(BoxRank &R, const std::vector<uint32_t> &boxes, const std::vector<uint32_t> &fills,
-                            bool shard, std::vector<uint32_t> &out) {
+static void box_flow_queues(DenseBox &R, std::vector<uint32_t> &out) {
     static const int order = getenv("GM_BOX_FLOW_ORDER") ? atoi(getenv("GM_BOX_FLOW_ORDER")) : 1;
+    const std::vector<uint32_t> &boxes = R.boxes;
     std::vector<uint32_t> q[8];
     std::vector<float> when(1u << 20, 0.0f);   // per box id: normalised position of its group
-    auto child = [&](uint32_t i, int dir) -> uint32_t {
-        const uint32_t box = boxes[i];
-        if (box_coord(box, dir) < 1) return ~0u;
-        uint32_t src = box - box_unit(dir);
-        if (shard) {
-            const uint32_t fill = fills[i];
-            if (dir >= 4) {
-                if ((fill >> (3 * dir)) & 4u) src = bsym_tau_box(src);
-            } else {
-                src = bsym_box((fill >> (3 * dir)) & 3u, src);
-            }
-        }
-        return src;
-    };
     for (size_t t = 0; t + 1 < R.tier_off.size(); t++) {
         const uint32_t o = R.tier_off[t], nb = R.tier_off[t + 1] - o, ng = (nb + 1) / 2;
         const uint32_t qq = ng >> 3, r = ng & 7u;
@@ -1117,10 +1026,9 @@ static void box_flow_queues(BoxRank &R, const std::vector<uint32_t> &boxes, cons
                 float key = 0.0f;
                 if (order)
                     for (uint32_t k = 0; k < (two ? 2u : 1u); k++)
-                        for (int dir = 0; dir < 8; dir++) {
-                            const uint32_t c = child(i + k, dir);
-                            if (c != ~0u) key = std::max(key, when[c]);
-                        }
+                        for (int dir = 0; dir < 8; dir++)
+                            if (box_coord(boxes[i + k], dir) >= 1)
+                                key = std::max(key, when[boxes[i + k] - box_unit(dir)]);
                 run.push_back({key, i | (two ? 0x80000000u : 0u)});
             }
             std::stable_sort(run.begin(), run.end(),
@@ -1144,178 +1052,177 @@ static void box_flow_queues(BoxRank &R, const std::vector<uint32_t> &boxes, cons
     }
 }
 
+// every box of the root's region by box-tier, Hilbert order inside a tier
+static void box_region_tiers(uint32_t root_hi, std::vector<uint32_t> &boxes, std::vector<uint32_t> &tier_off) {
+    int lim[8], tmax = 0;
+    for (int i = 0; i < 8; i++) { lim[i] = box_coord(root_hi, i); tmax += lim[i]; }
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>> tiers(tmax + 1);
+    for (uint32_t b = 0; b < (1u << 20); b++) {
+        bool in = true;
+        for (int i = 0; i < 8 && in; i++) in = box_coord(b, i) <= lim[i];
+        if (in) tiers[box_tier(b)].push_back({box_hilbert(b), b});
+    }
+    boxes.clear();
+    tier_off.assign(1, 0);
+    for (auto &tv : tiers) {
+        std::sort(tv.begin(), tv.end());
+        for (auto &e : tv) boxes.push_back(e.second);
+        tier_off.push_back((uint32_t)boxes.size());
+    }
+}
+
+void dense_box_free(Ctx *c);
+
+// A half-built context is never kept: every failure path frees it.
 static int box_prepare(Ctx *c, DenseBox *d, uint64_t root) {
     d->root_hi = box_index_of_key((uint32_t)root) >> 12;
-    d->virt = c->world <= 1 && c->virtual_ranks > 1;
-    d->world = c->world > 1 ? c->world : c->virtual_ranks;
-    d->shard = d->world > 1;
     GM_HIP(hipMalloc(&d->d_acc, 2 * sizeof(uint64_t)));
-    int cus = 256;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
-    d->grid_cap = cus * 4 * GM_BOX_WAVES;
+    d->grid_cap = box_resident((const void *)box_tier_kernel<false>, c->device, 0);
     const uint64_t bytes = 1ull << 32;
     if (c->adopted_dense && c->adopted_dense_bytes < bytes) {
         set_error("adopted dense table holds %llu bytes, need %llu", (unsigned long long)c->adopted_dense_bytes,
                   (unsigned long long)bytes);
         return GM_E_CAP;
     }
-    const int r0 = d->virt ? 0 : c->rank, r1 = d->virt ? d->world : c->rank + 1;
-    d->ranks.resize(r1 - r0);
-    d->flow = box_flow_wanted(c, d->shard);
+    box_region_tiers(d->root_hi, d->boxes, d->tier_off);
+    GM_HIP(hipMalloc(&d->d_boxes, std::max<size_t>(1, d->boxes.size()) * 4));
+    GM_HIP(hipMemcpy(d->d_boxes, d->boxes.data(), d->boxes.size() * 4, hipMemcpyHostToDevice));
+    d->flow = box_flow_wanted(c);
     if (d->flow) {
         const size_t words = 64 + (1u << 20);
         GM_HIP(hipMalloc(&d->d_flow, words * 4));
         GM_HIP(hipMemset(d->d_flow, 0, words * 4));
+        std::vector<uint32_t> qs;
+        box_flow_queues(*d, qs);
+        GM_HIP(hipMalloc(&d->d_groups, std::max<size_t>(1, qs.size()) * 4));
+        GM_HIP(hipMemcpy(d->d_groups, qs.data(), qs.size() * 4, hipMemcpyHostToDevice));
+        const char *xl = getenv("GM_BOX_FLOW_EXTRA_LDS");   // tests: fewer resident workgroups
+        d->flow_dyn = xl ? (size_t)std::max(0, atoi(xl)) : 0;
+        d->flow_grid = box_resident((const void *)box_flow_kernel<false>, c->device, d->flow_dyn) & ~7;
+        if (d->flow_grid < 8) { set_error("box dataflow kernel: no resident workgroups"); return GM_E_HIP; }
     }
-    for (int r = r0; r < r1; r++) {
-        BoxRank &R = d->ranks[r - r0];
-        R.rank = r;
-        BoxPlan P;
-        GM_TRY(box_plan(d->root_hi, d->world, r, d->shard, &P));
-        d->nsym = P.nsym;
-        R.tier_off = P.tier_off;
-        R.own = P.own;
-        R.n_boxes = P.boxes.size();
-        R.ties = P.ties;
-        GM_HIP(hipMalloc(&R.d_boxes, std::max<size_t>(1, P.boxes.size()) * 4));
-        GM_HIP(hipMemcpy(R.d_boxes, P.boxes.data(), P.boxes.size() * 4, hipMemcpyHostToDevice));
-        GM_HIP(hipMalloc(&R.d_own, std::max<size_t>(1, P.own.size()) * 4));
-        GM_HIP(hipMemcpy(R.d_own, P.own.data(), P.own.size() * 4, hipMemcpyHostToDevice));
-        if (d->shard) {
-            GM_HIP(hipMalloc(&R.d_fills, std::max<size_t>(1, P.fills.size()) * 4));
-            GM_HIP(hipMemcpy(R.d_fills, P.fills.data(), P.fills.size() * 4, hipMemcpyHostToDevice));
-            if (!P.map.empty()) {
-                GM_HIP(hipMalloc(&R.d_map, P.map.size()));
-                GM_HIP(hipMemcpy(R.d_map, P.map.data(), P.map.size(), hipMemcpyHostToDevice));
-            }
+    if (c->adopted_dense) {
+        d->table = (uint8_t *)c->adopted_dense;
+    } else {
+        if (hipMalloc(&d->table, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("hipMalloc of a 4 GiB dense table failed");
+            return GM_E_NOMEM;
         }
-        if (d->flow) {
-            std::vector<uint32_t> qs;
-            box_flow_queues(R, P.boxes, P.fills, d->shard, qs);
-            GM_HIP(hipMalloc(&R.d_groups, std::max<size_t>(1, qs.size()) * 4));
-            GM_HIP(hipMemcpy(R.d_groups, qs.data(), qs.size() * 4, hipMemcpyHostToDevice));
-        }
-        if (c->adopted_dense && r == r0) {
-            R.table = (uint8_t *)c->adopted_dense;
-            R.owned = false;
-        } else {
-            if (hipMalloc(&R.table, bytes) != hipSuccess) {
-                (void)hipGetLastError();
-                set_error("hipMalloc of a 4 GiB dense table failed (rank %d)", r);
-                return GM_E_NOMEM;
-            }
-            R.owned = true;
-            // a virtual rank's own table starts as 0xFF (LOSS in 0, the largest code): a read of
-            // a box the rank never computed would change its results, so tests catch it
-            if (d->virt) GM_HIP(hipMemsetAsync(R.table, 0xFF, bytes, c->stream));
-        }
+        d->owned = true;
     }
+    GM_HIP(hipMalloc(&d->d_tables, sizeof(uint8_t *)));
+    GM_HIP(hipMemcpy(d->d_tables, &d->table, sizeof(uint8_t *), hipMemcpyHostToDevice));
     return GM_OK;
 }
 
-static int box_launch_flow(Ctx *c, DenseBox *d, BoxRank &R) {
+static int box_launch_flow(Ctx *c, DenseBox *d) {
     BxFlow F;
-    F.groups = R.d_groups;
+    F.groups = d->d_groups;
     for (int x = 0; x < 8; x++) {
-        F.qbase[x] = R.qbase[x];
-        F.qlen[x] = R.qlen[x];
+        F.qbase[x] = d->qbase[x];
+        F.qlen[x] = d->qlen[x];
     }
     F.ctr = d->d_flow;
     F.epoch = d->d_flow + 16;
     F.flag = d->d_flow + 64;
     F.dev = box_flow_env() == 2 ? 1u : 0u;
     if (getenv("GM_BOX_FLOW_TEST_STALL") && atoi(getenv("GM_BOX_FLOW_TEST_STALL"))) F.dev |= 8u;
+    // milliseconds, fractions kept (0.5 used to truncate to 0 ticks); <= 0 is refused
     const char *tm = getenv("GM_BOX_FLOW_TIMEOUT_MS");
-    F.timeout = (uint64_t)(tm ? atof(tm) : 200.0) * 100000ull;
+    const double ms = tm ? atof(tm) : 200.0;
+    if (!(ms > 0.0)) { set_error("GM_BOX_FLOW_TIMEOUT_MS must be > 0 (got %s)", tm); return GM_E_ARG; }
+    F.timeout = (uint64_t)(ms * 100000.0);
     GM_HIP(hipMemsetAsync(d->d_flow, 0, 9 * 4, c->stream));
     hipLaunchKernelGGL(box_epoch_kernel, dim3(1), dim3(64), 0, c->stream, d->d_flow + 16);
-    const uint32_t grid = (uint32_t)d->grid_cap & ~7u;
-    if (d->shard)
-        hipLaunchKernelGGL(box_flow_kernel<true>, dim3(grid), dim3(64), 0, c->stream, R.table, R.d_boxes, R.d_fills, F);
-    else
-        hipLaunchKernelGGL(box_flow_kernel<false>, dim3(grid), dim3(64), 0, c->stream, R.table, R.d_boxes,
-                           (const uint32_t *)nullptr, F);
+    hipLaunchKernelGGL(box_flow_kernel<false>, dim3((uint32_t)d->flow_grid), dim3(64), d->flow_dyn, c->stream, d->table,
+                       d->d_boxes, (const uint32_t *)nullptr, (const uint32_t *)nullptr, F);
     GM_HIP(hipGetLastError());
     return GM_OK;
 }
 
-static int box_launch_tiers(Ctx *c, DenseBox *d, BoxRank &R) {
-    if (d->flow) return box_launch_flow(c, d, R);
-    for (size_t t = 0; t + 1 < R.tier_off.size(); t++) {
-        const uint32_t nb = R.tier_off[t + 1] - R.tier_off[t];
+static int box_launch_tiers(Ctx *c, DenseBox *d) {
+    if (d->flow) return box_launch_flow(c, d);
+    for (size_t t = 0; t + 1 < d->tier_off.size(); t++) {
+        const uint32_t nb = d->tier_off[t + 1] - d->tier_off[t];
         if (!nb) continue;
         const uint32_t ng = (nb + 1) / 2;
         // at least 8 workgroups (one per XCD run), at most the resident capacity
         const uint32_t grid = std::max<uint32_t>(8u, std::min<uint32_t>(ng, (uint32_t)d->grid_cap));
-        if (d->shard)
-            hipLaunchKernelGGL(box_tier_kernel<true>, dim3(grid), dim3(64), 0, c->stream, R.table,
-                               R.d_boxes + R.tier_off[t], R.d_fills + R.tier_off[t], nb);
-        else
-            hipLaunchKernelGGL(box_tier_kernel<false>, dim3(grid), dim3(64), 0, c->stream, R.table,
-                               R.d_boxes + R.tier_off[t], (const uint32_t *)nullptr, nb);
+        hipLaunchKernelGGL(box_tier_kernel<false>, dim3(grid), dim3(64), 0, c->stream, d->table,
+                           d->d_boxes + d->tier_off[t], (const uint32_t *)nullptr, (const uint32_t *)nullptr,
+                           (const uint32_t *)nullptr, (uint8_t *)nullptr, nb);
     }
     GM_HIP(hipGetLastError());
     return GM_OK;
 }
 
-static int box_launches(const DenseBox *d, const BoxRank &R) {
+static int box_launches(const DenseBox *d) {
     if (d->flow) return 1;
     int n = 0;
-    for (size_t t = 0; t + 1 < R.tier_off.size(); t++) n += R.tier_off[t + 1] > R.tier_off[t];
+    for (size_t t = 0; t + 1 < d->tier_off.size(); t++) n += d->tier_off[t + 1] > d->tier_off[t];
     return n;
 }
 
-void dense_box_free(Ctx *c);
+// per-position tier counts of the root's region (positions of heap sum t)
+void box_tier_counts(uint64_t root, std::vector<uint64_t> &acc) {
+    acc.assign(1, 1);
+    for (int j = 0; j < 8; j++) {
+        const int lim = (int)((root >> (4 * j)) & 15u);
+        std::vector<uint64_t> nx(acc.size() + lim, 0);
+        for (size_t s = 0; s < acc.size(); s++)
+            for (int hh = 0; hh <= lim; hh++) nx[s + hh] += acc[s];
+        acc.swap(nx);
+    }
+}
 
 int dense_box_solve(Ctx *c, uint64_t root) {
+    if (c->world > 1 || c->virtual_ranks > 1) {   // the split solve (dist_box.hip)
+        dense_box_free(c);
+        return dist_box_solve(c, root);
+    }
+    dist_box_free(c);
     DenseBox *d = c->dbox;
     const uint32_t rh = box_index_of_key((uint32_t)root) >> 12;
-    const bool virt = c->world <= 1 && c->virtual_ranks > 1;
-    const int world = c->world > 1 ? c->world : c->virtual_ranks;
-    if (!d || (c->adopted_dense && d->ranks[0].table != c->adopted_dense) || d->root_hi != rh || d->world != world ||
-        d->virt != virt || (!virt && d->ranks[0].rank != c->rank) ||
-        (d->flow != box_flow_wanted(c, world > 1) && !d->flow_failed)) {
+    if (!d || (c->adopted_dense && d->table != c->adopted_dense) || d->root_hi != rh || d->flow != box_flow_wanted(c)) {
         dense_box_free(c);
         d = c->dbox = new DenseBox();
-        GM_TRY(box_prepare(c, d, root));
-    }
-    const double t0 = now_ms();
-    if (c->timing)
-        for (auto &R : d->ranks)
-            if (!R.ev[0]) {
-                GM_HIP(hipEventCreate(&R.ev[0]));
-                GM_HIP(hipEventCreate(&R.ev[1]));
-            }
-    // one rank after the other (virtual ranks): each rank's launches are its whole
-    // multi-GPU job -- it never waits for another rank -- so its event span is its time
-    for (auto &R : d->ranks) {
-        if (c->use_graph) {
-            if (!R.graph || d->graph_stream != c->stream) {
-                if (R.graph) { (void)hipGraphExecDestroy(R.graph); R.graph = nullptr; }
-                hipGraph_t g;
-                GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-                const int rc = box_launch_tiers(c, d, R);
-                const hipError_t e = hipStreamEndCapture(c->stream, &g);
-                if (rc != GM_OK) return rc;
-                if (e != hipSuccess) { set_error("graph capture failed: %s", hipGetErrorString(e)); return GM_E_HIP; }
-                GM_HIP(hipGraphInstantiate(&R.graph, g, nullptr, nullptr, 0));
-                GM_HIP(hipGraphDestroy(g));
-            }
-            if (c->timing) GM_HIP(hipEventRecord(R.ev[0], c->stream));
-            GM_HIP(hipGraphLaunch(R.graph, c->stream));
-            if (c->timing) GM_HIP(hipEventRecord(R.ev[1], c->stream));
-        } else {
-            if (c->timing) GM_HIP(hipEventRecord(R.ev[0], c->stream));
-            GM_TRY(box_launch_tiers(c, d, R));
-            if (c->timing) GM_HIP(hipEventRecord(R.ev[1], c->stream));
+        const int rc = box_prepare(c, d, root);
+        if (rc != GM_OK) {
+            dense_box_free(c);
+            return rc;
         }
     }
-    if (c->use_graph) d->graph_stream = c->stream;
+    const double t0 = now_ms();
+    if (c->timing && !d->ev[0]) {
+        GM_HIP(hipEventCreate(&d->ev[0]));
+        GM_HIP(hipEventCreate(&d->ev[1]));
+    }
+    if (c->use_graph) {
+        if (!d->graph || d->graph_stream != c->stream) {
+            if (d->graph) { (void)hipGraphExecDestroy(d->graph); d->graph = nullptr; }
+            hipGraph_t g;
+            GM_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+            const int rc = box_launch_tiers(c, d);
+            const hipError_t e = hipStreamEndCapture(c->stream, &g);
+            if (rc != GM_OK) return rc;
+            if (e != hipSuccess) { set_error("graph capture failed: %s", hipGetErrorString(e)); return GM_E_HIP; }
+            GM_HIP(hipGraphInstantiate(&d->graph, g, nullptr, nullptr, 0));
+            GM_HIP(hipGraphDestroy(g));
+            d->graph_stream = c->stream;
+        }
+        if (c->timing) GM_HIP(hipEventRecord(d->ev[0], c->stream));
+        GM_HIP(hipGraphLaunch(d->graph, c->stream));
+        if (c->timing) GM_HIP(hipEventRecord(d->ev[1], c->stream));
+    } else {
+        if (c->timing) GM_HIP(hipEventRecord(d->ev[0], c->stream));
+        GM_TRY(box_launch_tiers(c, d));
+        if (c->timing) GM_HIP(hipEventRecord(d->ev[1], c->stream));
+    }
 #if GM_BOX_FLOW_TRACE
-    if (d->flow && getenv("GM_BOX_FLOW_TRACE_OUT")) {   // the last rank's launch (virtual ranks run in order)
-        const BoxRank &R = d->ranks.back();
+    if (d->flow && getenv("GM_BOX_FLOW_TRACE_OUT")) {
         uint64_t ng = 0;
-        for (int x = 0; x < 8; x++) ng += R.qlen[x];
+        for (int x = 0; x < 8; x++) ng += d->qlen[x];
         std::vector<unsigned long long> h(BX_FT_WORDS * std::min<uint64_t>(ng, BX_FT_GROUPS));
         GM_HIP(hipStreamSynchronize(c->stream));
         GM_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(bx_ftrace), h.size() * 8));
@@ -1338,68 +1245,55 @@ int dense_box_solve(Ctx *c, uint64_t root) {
                 h[7] / (double)(h[6] ? h[6] : 1) / 100.0, h[5] / (double)(h[7] ? h[7] : 1) / 10.0);
     }
 #endif
-    // the root box is fixed by every permutation of the plan, so every rank computes it
-    // (both words in one pinned buffer: one wait for the stream per solve)
+    // the root's code and the dataflow error word in one pinned buffer: one wait per solve
     if (!d->h_res) GM_HIP(hipHostMalloc((void **)&d->h_res, 8, hipHostMallocDefault));
     d->h_res[0] = d->h_res[1] = 0;
-    GM_HIP(hipMemcpyAsync(d->h_res, d->ranks[0].table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToHost,
-                          c->stream));
+    GM_HIP(hipMemcpyAsync(d->h_res, d->table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToHost, c->stream));
     if (d->flow) GM_HIP(hipMemcpyAsync(d->h_res + 1, d->d_flow + 8, 4, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     const uint8_t rs = (uint8_t)(d->h_res[0] & 0xFFu);
-    if (d->flow) {
-        if (d->h_res[1]) {   // a wait timed out: solve again with the tier launches
-            fprintf(stderr, "gmsolve: the one-launch box solve timed out waiting for a child box; "
-                            "re-solving with tier launches\n");
-            for (auto &R : d->ranks)
-                if (R.graph) { (void)hipGraphExecDestroy(R.graph); R.graph = nullptr; }
-            d->flow = false;
-            d->flow_failed = true;
-            return dense_box_solve(c, root);
-        }
+    if (d->flow && d->h_res[1]) {
+        // A wait timed out: solve again with the tier launches.  The context keeps tier
+        // launches from then on (box_flow_failed, cleared by gm_set_option GM_OPT_BOX_FLOW);
+        // every solve that fell back counts in gm_stats_t.flow_fallbacks.
+        fprintf(stderr, "gmsolve: the one-launch box solve timed out waiting for a child box; "
+                        "re-solving with tier launches\n");
+        c->box_flow_failed = true;
+        c->box_flow_fallbacks++;
+        const int fb = c->box_flow_fallbacks;
+        const int rc = dense_box_solve(c, root);
+        c->stats.flow_fallbacks = fb;
+        return rc;
     }
     const double t1 = now_ms();
     c->root_record = record_of_code(rs);
     uint64_t n = 1;
     for (int j = 0; j < 8; j++) n *= ((root >> (4 * j)) & 15u) + 1;
     c->n_positions = n;
-    {
-        std::vector<uint64_t> acc(1, 1);
-        for (int j = 0; j < 8; j++) {
-            std::vector<uint64_t> nx(acc.size() + 15, 0);
-            for (size_t s = 0; s < acc.size(); s++)
-                for (int hh = 0; hh < 16; hh++) nx[s + hh] += acc[s];
-            acc.swap(nx);
-        }
-        c->tier_counts = acc;
-    }
-    int launches = 0;
-    for (auto &R : d->ranks) launches += box_launches(d, R);
+    box_tier_counts(root, c->tier_counts);
     c->stats.n_positions = n;
     c->stats.n_primitive = 1;
-    c->stats.n_tiers = (int)d->ranks[0].tier_off.size() - 1;
+    c->stats.n_tiers = (int)d->tier_off.size() - 1;
     c->stats.solve_ms = t1 - t0;
     c->stats.backward_ms = t1 - t0;
     c->stats.forward_ms = 0;
-    c->stats.exchanged_bytes = 0;   // the sharded solve exchanges nothing (box_plan)
+    c->stats.exchanged_bytes = 0;
+    c->stats.flow_fallbacks = c->box_flow_fallbacks;
     c->stats.algo_bytes = (uint64_t)((double)(1ull << 32) * (1.0 + 1.8125 * 8));
-    c->stats.table_bytes = (1ull << 32) * d->ranks.size();
+    c->stats.table_bytes = 1ull << 32;
     if (c->timing) {
-        float total = 0;
-        for (auto &R : d->ranks) {
-            GM_HIP(hipEventElapsedTime(&R.kernel_ms, R.ev[0], R.ev[1]));
-            total += R.kernel_ms;
-        }
-        c->stats.kernel_ms = total;
-        c->stats.kernel_launches = launches;
+        float ms = 0;
+        GM_HIP(hipEventElapsedTime(&ms, d->ev[0], d->ev[1]));
+        c->stats.kernel_ms = ms;
+        c->stats.kernel_launches = box_launches(d);
     }
     return GM_OK;
 }
 
 int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
+    if (c->dist_box) return dist_box_query(c, keys, recs, n);
     DenseBox *d = c->dbox;
     if (!n) return GM_OK;
-    const BoxRank &R = d->ranks[0];
     uint64_t *dk;
     uint16_t *dr;
     const uint64_t chunk = std::min<uint64_t>(n, 1ull << 26);
@@ -1408,8 +1302,7 @@ int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     for (uint64_t o = 0; o < n; o += chunk) {
         const uint64_t m = std::min(chunk, n - o);
         GM_HIP(hipMemcpyAsync(dk, keys + o, m * 8, hipMemcpyHostToDevice, c->stream));
-        hipLaunchKernelGGL(box_query_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, c->stream, R.table,
-                           R.d_map, c->root, dk, dr, m);
+        box_launch_query(d->d_tables, nullptr, c->root, dk, dr, m, c->stream);
         GM_HIP(hipMemcpyAsync(recs + o, dr, m * 2, hipMemcpyDeviceToHost, c->stream));
     }
     GM_HIP(hipStreamSynchronize(c->stream));
@@ -1418,38 +1311,11 @@ int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     return GM_OK;
 }
 
-// Export: the root's region in ascending key order (one GPU, or every virtual rank), or,
-// for one rank of a multi-process solve, the positions of the boxes it owns.
-int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
-    DenseBox *d = c->dbox;
-    uint32_t lim[8];
-    for (int i = 0; i < 8; i++) lim[i] = (uint32_t)((c->root >> (4 * i)) & 15u);
-    if (d->shard && !d->virt) {
-        std::vector<uint64_t> ks;
-        for (uint32_t b : d->ranks[0].own)
-            for (uint32_t o = 0; o < 4096; o++) {
-                const uint32_t k = box_key_of_index((b << 12) | o);
-                bool in = true;
-                for (int i = 0; i < 8 && in; i++) in = ((k >> (4 * i)) & 15u) <= lim[i];
-                if (in) ks.push_back(k);
-            }
-        *n = ks.size();
-        if (!keys) return GM_OK;
-        if (cap < ks.size()) { set_error("export buffer holds %llu, need %llu", (unsigned long long)cap,
-                                         (unsigned long long)ks.size()); return GM_E_CAP; }
-        std::sort(ks.begin(), ks.end());
-        std::copy(ks.begin(), ks.end(), keys);
-        return dense_box_query(c, keys, recs, ks.size());
-    }
-    *n = c->n_positions;
-    if (!keys) return GM_OK;
-    if (cap < c->n_positions) {
-        set_error("export buffer holds %llu, need %llu", (unsigned long long)cap, (unsigned long long)c->n_positions);
-        return GM_E_CAP;
-    }
-    // the root's box of keys in ascending order (heap 0 fastest)
-    uint32_t h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint64_t j = 0; j < c->n_positions; j++) {
+// keys of the root's region in ascending order (heap 0 fastest)
+void box_region_keys(uint64_t root, uint64_t *keys, uint64_t n) {
+    uint32_t lim[8], h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 8; i++) lim[i] = (uint32_t)((root >> (4 * i)) & 15u);
+    for (uint64_t j = 0; j < n; j++) {
         uint32_t k = 0;
         for (int i = 0; i < 8; i++) k |= h[i] << (4 * i);
         keys[j] = k;
@@ -1458,23 +1324,32 @@ int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint6
             h[i] = 0;
         }
     }
-    if (c->n_positions <= (1ull << 26) || d->shard) return dense_box_query(c, keys, recs, c->n_positions);
-    // large boxes: one copy of the table, decoded on the host
+}
+
+// Export: the root's region in ascending key order.
+int dense_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
+    if (c->dist_box) return dist_box_export(c, keys, recs, cap, n);
+    DenseBox *d = c->dbox;
+    *n = c->n_positions;
+    if (!keys) return GM_OK;
+    if (cap < c->n_positions) {
+        set_error("export buffer holds %llu, need %llu", (unsigned long long)cap, (unsigned long long)c->n_positions);
+        return GM_E_CAP;
+    }
+    box_region_keys(c->root, keys, c->n_positions);
+    if (c->n_positions <= (1ull << 26)) return dense_box_query(c, keys, recs, c->n_positions);
+    // large regions: one copy of the table, decoded on the host
     std::vector<uint8_t> tab(1ull << 32);
-    GM_HIP(hipMemcpy(tab.data(), d->ranks[0].table, tab.size(), hipMemcpyDeviceToHost));
+    GM_HIP(hipMemcpy(tab.data(), d->table, tab.size(), hipMemcpyDeviceToHost));
     for (uint64_t j = 0; j < c->n_positions; j++) recs[j] = record_of_code(tab[box_index_of_key((uint32_t)keys[j])]);
     return GM_OK;
 }
 
-// Digest of the boxes this context's ranks own: the whole region on one GPU or over all
-// virtual ranks, this rank's part in a multi-process solve (the parts sum to the whole).
 int dense_box_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
+    if (c->dist_box) return dist_box_digest(c, digest, n);
     DenseBox *d = c->dbox;
     GM_HIP(hipMemsetAsync(d->d_acc, 0, 16, c->stream));
-    for (auto &R : d->ranks)
-        if (!R.own.empty())
-            hipLaunchKernelGGL(box_digest_kernel, dim3(4096), dim3(256), 0, c->stream, R.table, R.d_own,
-                               (uint64_t)R.own.size(), c->root, (unsigned long long *)d->d_acc);
+    box_launch_digest(d->table, d->d_boxes, d->boxes.size(), c->root, (unsigned long long *)d->d_acc, c->stream);
     GM_HIP(hipGetLastError());
     uint64_t hst[2];
     GM_HIP(hipMemcpyAsync(hst, d->d_acc, 16, hipMemcpyDeviceToHost, c->stream));
@@ -1485,61 +1360,21 @@ int dense_box_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
 }
 
 int dense_box_table(Ctx *c, void **p, uint64_t *bytes) {
-    *p = c->dbox->ranks[0].table;
+    if (c->dist_box) return dist_box_table(c, p, bytes);
+    *p = c->dbox->table;
     *bytes = 1ull << 32;
-    return GM_OK;
-}
-
-int dense_box_rank_stats(Ctx *c, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n) {
-    DenseBox *d = c->dbox;
-    *n = (int)d->ranks.size();
-    if (!kernel_ms && !boxes && !ties) return GM_OK;
-    if (cap < *n) { set_error("rank stats buffer holds %d, need %d", cap, *n); return GM_E_CAP; }
-    for (int i = 0; i < *n; i++) {
-        if (kernel_ms) kernel_ms[i] = d->ranks[i].kernel_ms;
-        if (boxes) boxes[i] = d->ranks[i].n_boxes;
-        if (ties) ties[i] = d->ranks[i].ties;
-    }
-    return GM_OK;
-}
-
-// host only: box_plan for tests and tools (gm_box_plan)
-int dense_box_plan(uint64_t root, int world, int rank, int what, uint32_t *out, uint64_t cap, uint64_t *n) {
-    if (root >> 32) { set_error("root must be a 32-bit key (8 heaps)"); return GM_E_KEY; }
-    BoxPlan P;
-    GM_TRY(box_plan(box_index_of_key((uint32_t)root) >> 12, world, rank, what == GM_BOXPLAN_MAP, &P));
-    std::vector<uint32_t> v;
-    switch (what) {
-    case GM_BOXPLAN_SHAPE: v = {(uint32_t)P.nsym, P.g, (uint32_t)P.boxes.size(), (uint32_t)P.own.size(),
-                                (uint32_t)P.ties, (uint32_t)(P.tier_off.size() - 1)}; break;
-    case GM_BOXPLAN_BOXES: v = P.boxes; break;
-    case GM_BOXPLAN_FILLS: v = P.fills; break;
-    case GM_BOXPLAN_TIER_OFF: v = P.tier_off; break;
-    case GM_BOXPLAN_OWN: v = P.own; break;
-    case GM_BOXPLAN_MAP: v.assign(P.map.begin(), P.map.end()); break;
-    default: set_error("unknown box plan item %d", what); return GM_E_ARG;
-    }
-    *n = v.size();
-    if (!out) return GM_OK;
-    if (cap < v.size()) { set_error("box plan buffer holds %llu, need %llu", (unsigned long long)cap,
-                                    (unsigned long long)v.size()); return GM_E_CAP; }
-    std::copy(v.begin(), v.end(), out);
     return GM_OK;
 }
 
 void dense_box_free(Ctx *c) {
     DenseBox *d = c->dbox;
     if (!d) return;
-    for (auto &R : d->ranks) {
-        if (R.graph) (void)hipGraphExecDestroy(R.graph);
-        for (auto e : R.ev)
-            if (e) (void)hipEventDestroy(e);
-        if (R.owned && R.table) (void)hipFree(R.table);
-        for (void *q : {(void *)R.d_boxes, (void *)R.d_fills, (void *)R.d_own, (void *)R.d_map, (void *)R.d_groups})
-            if (q) (void)hipFree(q);
-    }
-    if (d->d_acc) (void)hipFree(d->d_acc);
-    if (d->d_flow) (void)hipFree(d->d_flow);
+    if (d->graph) (void)hipGraphExecDestroy(d->graph);
+    for (auto e : d->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (d->owned && d->table) (void)hipFree(d->table);
+    for (void *q : {(void *)d->d_boxes, (void *)d->d_groups, (void *)d->d_acc, (void *)d->d_flow, (void *)d->d_tables})
+        if (q) (void)hipFree(q);
     if (d->h_res) (void)hipHostFree(d->h_res);
     delete d;
     c->dbox = nullptr;

@@ -1068,6 +1068,7 @@ int dense_sub_solve(Ctx *c, uint64_t root) {
         return dense_box_solve(c, root);
     }
     dense_box_free(c);
+    dist_box_free(c);
     c->dbox_active = false;
     DenseSub *d = c->dsub;
     if (!d || d->heaps != c->sub.heaps || d->want_threads != c->sub_threads || d->want_x4 != c->sub_interleave ||

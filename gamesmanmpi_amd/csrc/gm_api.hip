@@ -115,6 +115,7 @@ static void free_engines(Ctx *c) {
     small_dense_free(c);
     sparse_free(c);
     dist_sub_free(c);
+    dist_box_free(c);
     dist_sparse_free(c);
 }
 
@@ -209,7 +210,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sub_low = (int)v;
         return GM_OK;
     case GM_OPT_GRAPH: c->use_graph = v != 0; return GM_OK;
-    case GM_OPT_TIMING: c->timing = v != 0; return GM_OK;
+    case GM_OPT_TIMING:
+        if (v < 0 || v > 2) { set_error("timing must be 0, 1 or 2"); return GM_E_ARG; }
+        c->timing = (int)v;
+        return GM_OK;
     case GM_OPT_SUB_THREADS:
         if (v != 64 && v != 128 && v != 256) { set_error("sub_threads must be 64, 128 or 256"); return GM_E_ARG; }
         c->sub_threads = (int)v;
@@ -249,6 +253,11 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
     case GM_OPT_BOX_FLOW:
         if (v < -1 || v > 1) { set_error("box flow must be -1, 0 or 1"); return GM_E_ARG; }
         c->box_flow = (int)v;
+        c->box_flow_failed = false;   // setting it again retries the dataflow launch
+        return GM_OK;
+    case GM_OPT_BOX_SPLIT:
+        if (v < 0 || v > 1) { set_error("box split must be 0 (halves) or 1 (comparisons)"); return GM_E_ARG; }
+        c->box_split = (int)v;
         return GM_OK;
     case GM_OPT_SYMMETRY:
         if (v < 0 || v > 1) { set_error("symmetry must be 0 or 1"); return GM_E_ARG; }
@@ -369,7 +378,7 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
         set_error("virtual ranks and a multi-process communicator are exclusive");
         return GM_E_ARG;
     }
-    // the 8-heap game on the box engine shards inside dense_box.hip (no exchange); other
+    // the 8-heap game on the box engine splits inside dense_box.hip (dist_box.hip); other
     // heap counts and GM_OPT_SUB_INTERLEAVE != 20 keep the block engine's sharded path
     const bool box = !force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT &&
                      c->sub.heaps == 8 && c->sub_interleave == 20;
@@ -506,17 +515,26 @@ int gm_dist_plan(int heaps, int world, int rank, const int32_t *opts, int what, 
     return dist_sub_plan(heaps, world, rank, opts, what, axis, off, off_cap, n_off, data, data_cap, n_data);
 }
 
-int gm_box_plan(uint64_t root, int world, int rank, int what, uint32_t *out, uint64_t cap, uint64_t *n) {
+int gm_box_plan(uint64_t root, int world, int rank, const int32_t *opts, int what, int axis, uint32_t *out,
+                uint64_t cap, uint64_t *n) {
     if (!n) return GM_E_ARG;
-    return dense_box_plan(root, world, rank, what, out, cap, n);
+    return dist_box_plan(root, world, rank, opts, what, axis, out, cap, n);
 }
 
-int gm_rank_stats(gm_ctx *h, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n) {
+int gm_rank_stats(gm_ctx *h, double *kernel_ms, uint64_t *boxes, uint64_t *recv_bytes, int cap, int *n) {
     GM_TRY(need_solved(h));
     if (!n) return GM_E_ARG;
     Ctx *c = &h->c;
-    if (c->engine != GM_ENGINE_DENSE || !c->dbox_active || !c->dbox) { *n = 0; return GM_OK; }
-    return dense_box_rank_stats(c, kernel_ms, boxes, ties, cap, n);
+    if (c->engine != GM_ENGINE_DENSE || !c->dbox_active || !c->dist_box) { *n = 0; return GM_OK; }
+    return dist_box_rank_stats(c, kernel_ms, boxes, recv_bytes, cap, n);
+}
+
+int gm_rank_op_ms(gm_ctx *h, int rank, double *ms, int cap, int *n) {
+    GM_TRY(need_solved(h));
+    if (!n) return GM_E_ARG;
+    Ctx *c = &h->c;
+    if (c->engine != GM_ENGINE_DENSE || !c->dbox_active || !c->dist_box) { *n = 0; return GM_OK; }
+    return dist_box_op_ms(c, rank, ms, cap, n);
 }
 
 void gm_close(gm_ctx *h) {

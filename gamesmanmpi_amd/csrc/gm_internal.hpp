@@ -57,6 +57,7 @@ struct DenseBox;
 struct SmallDense;
 struct Sparse;
 struct DistSub;
+struct DistBox;
 struct DistSparse;
 struct Graph;
 
@@ -79,7 +80,7 @@ struct Ctx {
     int sub_interleave = 20;     // 20 box engine at 8 heaps, else the walker (default); 10 walker, 6 four-block, 13 row dataflow, 1 one block
     int sub_order = 2;   // block order inside a tier: 0 key, 1 Morton, 2 Hilbert (default)
     bool use_graph = true;
-    bool timing = false;
+    int timing = 0;          // 1: event pair around the dominant kernel's launches; 2 (split box engine) also per op
 
     // multi-GPU
     int rank = 0, world = 1;
@@ -91,7 +92,10 @@ struct Ctx {
     int dist_solo = 0;       // diagnostic (loopback): enqueue only rank dist_solo-1's tier launches
     int dist_symmetry = 1;   // sharded dense path: halo blocks derivable by a heap swap are filled locally
     int dist_owner = 0;      // sharded dense path: 0 = split heaps in halves, 1 = tier-balanced comparisons
-    int box_flow = -1;       // box engine: -1 dataflow when sharded, 0 tier launches, 1 dataflow (GM_OPT_BOX_FLOW)
+    int box_flow = -1;       // box engine, one GPU: -1 / 0 tier launches, 1 dataflow (GM_OPT_BOX_FLOW)
+    bool box_flow_failed = false;   // a dataflow solve timed out: tier launches until GM_OPT_BOX_FLOW is set again
+    int box_flow_fallbacks = 0;     // dataflow solves of this context that fell back to tier launches
+    int box_split = 0;       // split box engine (N > 1): 0 halves, 1 comparisons (GM_OPT_BOX_SPLIT)
     int symmetry = 1;        // sparse engines: store one representative per symmetry orbit (games.hpp)
 
     // results
@@ -116,6 +120,7 @@ struct Ctx {
     SmallDense *sd = nullptr;
     Sparse *sp = nullptr;
     DistSub *dist_sub = nullptr;
+    DistBox *dist_box = nullptr;  // the box engine split over ranks (dist_box.hip), reached through dense_box_*
     DistSparse *dist_sp = nullptr;
     Graph *graph = nullptr;
 };
@@ -134,8 +139,28 @@ int dense_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
 int dense_box_digest(Ctx *c, uint64_t *digest, uint64_t *n);
 int dense_box_table(Ctx *c, void **p, uint64_t *bytes);
 void dense_box_free(Ctx *c);
-int dense_box_rank_stats(Ctx *c, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n);
-int dense_box_plan(uint64_t root, int world, int rank, int what, uint32_t *out, uint64_t cap, uint64_t *n);
+// shared with the split box engine (dist_box.hip)
+uint64_t box_hilbert(uint32_t box);
+int box_grid_cap(int device);
+void box_launch_tier_split(uint32_t grid, uint8_t *table, const uint32_t *boxes, const uint32_t *fills,
+                           const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint32_t nbox, hipStream_t s);
+void box_launch_digest(const uint8_t *table, const uint32_t *boxes, uint64_t nbox, uint64_t root,
+                       unsigned long long *acc, hipStream_t s);
+void box_launch_query(const uint8_t *const *tables, const uint8_t *owner, uint64_t root, const uint64_t *keys,
+                      uint16_t *out, uint64_t n, hipStream_t s);
+void box_tier_counts(uint64_t root, std::vector<uint64_t> &acc);
+void box_region_keys(uint64_t root, uint64_t *keys, uint64_t n);
+// the box engine split over G ranks (dist_box.hip)
+int dist_box_solve(Ctx *c, uint64_t root);
+int dist_box_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int dist_box_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
+int dist_box_digest(Ctx *c, uint64_t *digest, uint64_t *n);
+int dist_box_table(Ctx *c, void **p, uint64_t *bytes);
+int dist_box_rank_stats(Ctx *c, double *kernel_ms, uint64_t *boxes, uint64_t *recv_bytes, int cap, int *n);
+int dist_box_op_ms(Ctx *c, int rank, double *ms, int cap, int *n);
+void dist_box_free(Ctx *c);
+int dist_box_plan(uint64_t root, int world, int rank, const int32_t *opts, int what, int axis, uint32_t *out,
+                  uint64_t cap, uint64_t *n);
 
 // the dense tier kernel, shared with the partitioned (multi-GPU) driver
 bool sub_kernel_exists(int low, int high, int nt);

@@ -105,15 +105,25 @@ class Context:
         return out[:n.value]
 
     def rank_stats(self):
-        """Per rank of the last sharded box solve (gm_rank_stats): kernel ms, boxes, tie boxes."""
+        """Per rank of the last split box solve (gm_rank_stats): GPU ms from its first tier launch
+        to its last (GM_OPT_TIMING), boxes computed, halo bytes received per solve."""
         n = ctypes.c_int()
         _lib.check(self.L.gm_rank_stats(self.h, None, None, None, 0, ctypes.byref(n)))
         ms = np.zeros(max(1, n.value), dtype=np.float64)
         boxes = np.zeros(max(1, n.value), dtype=np.uint64)
-        ties = np.zeros(max(1, n.value), dtype=np.uint64)
-        _lib.check(self.L.gm_rank_stats(self.h, ms.ctypes.data, boxes.ctypes.data, ties.ctypes.data, n.value,
+        recv = np.zeros(max(1, n.value), dtype=np.uint64)
+        _lib.check(self.L.gm_rank_stats(self.h, ms.ctypes.data, boxes.ctypes.data, recv.ctypes.data, n.value,
                                         ctypes.byref(n)))
-        return [{"kernel_ms": float(ms[i]), "boxes": int(boxes[i]), "ties": int(ties[i])} for i in range(n.value)]
+        return [{"kernel_ms": float(ms[i]), "boxes": int(boxes[i]), "recv_bytes": int(recv[i])}
+                for i in range(n.value)]
+
+    def rank_op_ms(self, rank):
+        """GPU ms of every op of `rank`'s op list in the last split box solve (GM_OPT_TIMING)."""
+        n = ctypes.c_int()
+        _lib.check(self.L.gm_rank_op_ms(self.h, rank, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(1, n.value), dtype=np.float64)
+        _lib.check(self.L.gm_rank_op_ms(self.h, rank, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out[:n.value]
 
     def adopt_dense_table(self, dev_ptr, nbytes):
         _lib.check(self.L.gm_adopt_buffer(self.h, _lib.BUF_DENSE_TABLE, ctypes.c_void_p(dev_ptr), nbytes))

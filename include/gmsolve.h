@@ -77,27 +77,32 @@ enum {
     GM_OPT_ENGINE = 1,      /* GM_ENGINE_* */
     GM_OPT_SUB_LOW = 2,     /* SUBTRACT dense path: heaps solved per workgroup in LDS (1..4) */
     GM_OPT_GRAPH = 3,       /* SUBTRACT dense path: replay the tier launches as a hipGraph (0/1) */
-    GM_OPT_TIMING = 4,      /* record HIP events around every launch of the dominant kernel (0/1) */
+    GM_OPT_TIMING = 4,      /* record HIP events around every launch of the dominant kernel (0/1); 2 = on
+                               the split box engine also an event pair around every op (gm_rank_op_ms) */
     GM_OPT_VIRTUAL_RANKS = 5, /* >1: run the sharded algorithm with that many ranks inside this one
                                 context on one GPU (loopback transport instead of RCCL); for testing
                                 the multi-GPU partition on a single device */
     GM_OPT_SUB_THREADS = 6, /* SUBTRACT dense path: threads per block workgroup (64, 128, 256) */
     GM_OPT_SUB_INTERLEAVE = 7, /* SUBTRACT dense path: 20 (default) = the box engine at 8 heaps
-                                  (dense_box.hip: 4x4x4x4x2x2x2x2 boxes, 41 launches; sharded at N > 1 with
-                                  no exchange, gm_box_plan); other heap counts use 10; 10 = the block
+                                  (dense_box.hip: 4x4x4x4x2x2x2x2 boxes, 41 launches; split at N > 1, every
+                                  box on one rank, halo boxes over RCCL, gm_box_plan); other heap counts
+                                  use 10; 10 = the block
                                   engine's walker kernel on tiers of >= 4096 blocks, the four-block kernel
                                   below (sharded at N > 1 with halo exchanges, gm_dist_plan); 6 = the
                                   four-block kernel (byte LDS image, 256-thread barrier walk) on every tier;
                                   1 = one block per workgroup of GM_OPT_SUB_THREADS */
     GM_OPT_SUB_ORDER = 8,   /* SUBTRACT dense path: block order inside a tier, 0 = key order, 1 = Morton,
                                2 = Hilbert walk of the tier's free high nibbles (default) */
-    GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers per halo exchange (default 4) */
+    GM_OPT_DIST_BATCH = 9,  /* sharded SUBTRACT path: tiers (box engine: box-tiers) per halo exchange
+                               (default 4) */
     GM_OPT_DIST_SLOTS = 10, /* sharded SUBTRACT path: exchange buffers per split heap, in batches (default 4) */
     GM_OPT_DIST_SOLO = 12,  /* diagnostic, loopback sharded SUBTRACT path: r + 1 = enqueue only rank r's
                                tier launches (no exchange, no waits), to time one rank's compute
                                critical path; the results are NOT valid.  0 (default) = off. */
     GM_OPT_DIST_SYMMETRY = 11, /* sharded SUBTRACT path: 1 (default) = fill halo blocks that are a heap
-                                 permutation of an own block locally, 0 = receive every halo block */
+                                 permutation of an own block locally (box engine: read a crossing child
+                                 box through a heap transposition of a box this rank computed), 0 =
+                                 receive every halo block */
     GM_OPT_DIST_OWNER = 13, /* sharded SUBTRACT path, block owner: 0 = split the top heaps in halves
                                (rank bit a = [heap >= 8]); 1 = tier-balanced: rank bits compare two
                                heaps ([h_x < h_y]) while enough heaps remain, [heap >= 8] after, so
@@ -106,10 +111,15 @@ enum {
                                hook othello_bit_new.py:224-235): 1 (default) = TOOT stores one position
                                per left-right mirror pair when the root is its own mirror image; every
                                count, export, query and digest still covers both positions.  0 = off */
-    GM_OPT_BOX_FLOW = 15    /* box engine (SUBTRACT, 8 heaps): -1 (default) = one-launch dataflow solve
-                               (box_flow_kernel: a box group starts when its child boxes are stored)
-                               for a sharded solve, tier launches on one GPU; 0 = tier launches; 1 =
-                               dataflow always */
+    GM_OPT_BOX_FLOW = 15,   /* box engine (SUBTRACT, 8 heaps), one GPU: -1 (default) / 0 = one launch per
+                               box-tier; 1 = one dataflow launch (box_flow_kernel: a box group starts
+                               when its child boxes are stored; its grid is the kernel's resident
+                               capacity from the occupancy API).  A dataflow solve whose waits time out
+                               is redone with tier launches, and the context keeps tier launches until
+                               this option is set again; gm_stats_t.flow_fallbacks counts them. */
+    GM_OPT_BOX_SPLIT = 16   /* box engine at N > 1 (gm_box_plan): 0 (default) = split heaps in halves
+                               (rank bit a = [box coordinate >= half]); 1 = tier-balanced comparisons
+                               (rank bit = [c_x < c_y], ties by a rule that keeps every axis one-way) */
 };
 
 /* Buffer roles for gm_adopt_buffer. */
@@ -135,6 +145,7 @@ typedef struct {
     int32_t kernel_launches;/* GM_OPT_TIMING: number of those launches */
     int32_t engine;         /* GM_ENGINE_DENSE or GM_ENGINE_SPARSE */
     uint64_t n_edges;       /* sparse path: parent->child edges expanded (this rank) */
+    int32_t flow_fallbacks; /* box engine: dataflow solves of this context redone with tier launches */
 } gm_stats_t;
 
 /* Library version (GM_ABI_VERSION). */
@@ -176,9 +187,8 @@ int gm_expand_host(gm_ctx *ctx, uint64_t key, uint64_t *children, int cap,
  * world = 1 and a uid, a one-rank communicator is created: with GM_OPT_ENGINE =
  * GM_ENGINE_DIST_SPARSE the hash-sharded engine then runs its RCCL transport on
  * one GPU (self send/recv, all-gather, all-reduce), which tests use. */
-/* uid NULL sets rank and world only, with no communicator: enough for the 8-heap SUBTRACT game on
- * the box engine (its ranks exchange nothing, gm_box_plan); the other sharded engines then refuse
- * to solve (GM_E_COMM). */
+/* uid NULL sets rank and world only, with no communicator; every sharded engine then refuses to
+ * solve (GM_E_COMM). */
 int gm_comm_unique_id(void *uid, int bytes);
 int gm_set_comm(gm_ctx *ctx, int rank, int world, const void *uid, int bytes);
 
@@ -207,7 +217,10 @@ int gm_solve_graph(gm_ctx *ctx, uint64_t n, const uint8_t *primitive, const uint
  * tables (src/cache_dict.py:38-79, src/new_process.py:76-78). */
 int gm_export(gm_ctx *ctx, uint64_t *keys, uint16_t *records, uint64_t cap, uint64_t *n);
 
-/* Records of n keys (0xFFFF for keys this rank does not hold).  Replaces
+/* Records of n keys (0xFFFF for keys this rank does not hold: in a multi-process solve a rank
+ * holds the keys it computed -- box engine: the boxes of gm_box_plan GM_BOXPLAN_BOXES, sparse
+ * engine: its hash share; with virtual ranks, or on one GPU, every key of the root's region;
+ * 0xFFFF outside it).  Replaces
  * `pos in self.resolved` / `self.resolved[pos]` lookups (src/new_process.py:111-117). */
 int gm_query(gm_ctx *ctx, const uint64_t *keys, uint16_t *records, uint64_t n);
 
@@ -234,7 +247,7 @@ int gm_adopt_buffer(gm_ctx *ctx, int role, void *dev_ptr, uint64_t bytes);
  *     id of gm_box_plan (heap i >> 2 at bits 2i for heaps 0-3, heap j >> 1 at bits
  *     8 + 3 (j - 4) for heaps 4-7), A = sum over heaps 0-3 of (heap i & 3) << 2i and
  *     B = sum over heaps 4-7 of (heap j & 1) << (j - 4).  At N > 1 a rank's table holds
- *     only the boxes it computed (gm_box_plan GM_BOXPLAN_BOXES); gm_query maps any key.
+ *     the boxes it computed (gm_box_plan GM_BOXPLAN_BOXES) and the halo boxes it received.
  * Read records through gm_query / gm_export unless the layout is handled. */
 int gm_dense_table(gm_ctx *ctx, void **dev_ptr, uint64_t *bytes);
 
@@ -268,36 +281,64 @@ int gm_dist_plan(int heaps, int world, int rank, const int32_t *opts, int what, 
                  uint32_t *off, uint64_t off_cap, uint64_t *n_off,
                  uint32_t *data, uint64_t data_cap, uint64_t *n_data);
 
-/* Host only (no HIP call): the plan of rank `rank` of a `world`-rank sharded solve of the
- * 8-heap SUBTRACT game on the box engine (the default at 8 heaps).  The
- * reference's counterpart is its owner hash, md5(str(pos)) % world (src/game_state.py:23-31):
- * here a rank owns one member of every orbit of a group of heap permutations, and reads the
- * children it does not compute from their images it does, so the ranks exchange nothing.
- * Box ids pack the box coordinates (heap i >> 2 for heaps 0-3 at bits 2i, heap j >> 1 for
- * heaps 4-7 at bits 8 + 3 (j - 4)).
- *   GM_BOXPLAN_SHAPE     {|H'|, this rank's permutation code, boxes computed, boxes owned,
- *                         tie boxes (also computed by another rank), box-tiers}
+/* Host only (no HIP call): the plan of rank `rank` of a `world`-rank split solve of the 8-heap
+ * SUBTRACT game on the box engine (the default at 8 heaps), built by the same
+ * code gm_solve runs.  The reference's counterpart is its owner hash, md5(str(pos)) % world
+ * (src/game_state.py:23-31), with every child sent to its owner and every result sent back
+ * (src/new_process.py:156-160, :179-187).  Here each box has ONE owner, a function of its box
+ * coordinates with one bit per split axis (world rounded down to 1, 2, 4 or 8 ranks with work);
+ * a child box another rank owns is read through a heap transposition of a box this rank
+ * computed, or received from that rank in the batch's halo message.  Box ids pack the box
+ * coordinates (heap i >> 2 for heaps 0-3 at bits 2i, heap j >> 1 for heaps 4-7 at bits
+ * 8 + 3 (j - 4)).  `opts` = {GM_OPT_DIST_BATCH, GM_OPT_DIST_SYMMETRY, GM_OPT_BOX_SPLIT, loopback op
+ * list 0/1} values, NULL = defaults.  `axis` selects the axis of SEND / RECV items.
+ *   GM_BOXPLAN_SHAPE     {world, axes, box-tiers, batch, batches, split, fill} then per axis a = 0..2
+ *                        {kind (0 none, 1 half, 2 comparison), heap d | x, threshold | y, free-heap mask}
  *   GM_BOXPLAN_BOXES     the boxes this rank computes, by box-tier (GM_BOXPLAN_TIER_OFF)
- *   GM_BOXPLAN_FILLS     per computed box: 3 bits per child direction d at bit 3 d, the code
- *                        k | e << 2 of the permutation r^k t^e (r rotates heaps 0-3, t swaps
- *                        heaps 4/5 and 6/7) whose image of the child box is read instead; 0 =
- *                        the child box itself
+ *   GM_BOXPLAN_FILLS     per computed box (the kernel's fill word): 4 bits per child direction d at
+ *                        bit 4 d; A heap d: q << 2 | p, the child read through the transposition of
+ *                        A heaps q and p (q = p: the child box itself); B heap d: 0 = the child box
+ *                        itself, 1..6 = through the transposition of B heaps 4 + pair, pairs (0,1)
+ *                        (0,2) (0,3) (1,2) (1,3) (2,3)
+ *   GM_BOXPLAN_SRCS      per computed box 8 words: the box read for the child along heap d (the
+ *                        child box, or its image under that transposition; 0 where there is no child)
+ *   GM_BOXPLAN_DSTS      per computed box 3 words: the halo message slots the tier kernel also
+ *                        writes it to (bits 28-31: 0 none, 1..4 the two top layers along A heap
+ *                        kind - 1, 5 the whole box; bits 0-27: byte offset in the rank's send
+ *                        buffer / 2 KiB; the buffer holds axis 0's messages, then axis 1's, ...)
  *   GM_BOXPLAN_TIER_OFF  offsets of the box-tiers in GM_BOXPLAN_BOXES
- *   GM_BOXPLAN_OWN       the boxes this rank owns (digest, export); the ranks' lists partition
+ *   GM_BOXPLAN_OWN       GM_BOXPLAN_BOXES ascending (digest, export); the ranks' lists partition
  *                        the root's region
- *   GM_BOXPLAN_MAP       per box id (2^20): the code h with h(box) computed by this rank, 0xFF
- *                        outside the root's region (used by gm_query); empty when world is 1
+ *   GM_BOXPLAN_SEND / _RECV          halo entries sent / received on `axis`: box | code << 20,
+ *                        code 0 = the whole box, 1 + i = its two top layers along A heap i
+ *   GM_BOXPLAN_SEND_OFF / _RECV_OFF  their offsets per batch
+ *   GM_BOXPLAN_HALO      (lo, hi) box-tier range of each batch's message
+ *   GM_BOXPLAN_OPS       6 u32 per op {kind, axis, event, on_exchange_stream, tier | batch, peer};
+ *                        kind 0 tier launch (which also writes its boxes' halo slots), 2 unpack (every
+ *                        message of the batch, `axis` unused), 3 send, 4 receive, 5 event record,
+ *                        6 event wait (1 pack is fused into 0); event 0 tier done, 1 message
+ *                        complete (loopback lists)
+ *   GM_BOXPLAN_COUNTS    {boxes computed, child reads through a transposition, child reads from a message}
  * With out NULL only *n is set. */
 enum { GM_BOXPLAN_SHAPE = 0, GM_BOXPLAN_BOXES = 1, GM_BOXPLAN_FILLS = 2, GM_BOXPLAN_TIER_OFF = 3, GM_BOXPLAN_OWN = 4,
-       GM_BOXPLAN_MAP = 5 };
-int gm_box_plan(uint64_t root_key, int world, int rank, int what, uint32_t *out, uint64_t cap, uint64_t *n);
+       GM_BOXPLAN_SEND = 5, GM_BOXPLAN_SEND_OFF = 6, GM_BOXPLAN_RECV = 7, GM_BOXPLAN_RECV_OFF = 8,
+       GM_BOXPLAN_HALO = 9, GM_BOXPLAN_OPS = 10, GM_BOXPLAN_COUNTS = 11, GM_BOXPLAN_SRCS = 12,
+       GM_BOXPLAN_DSTS = 13 };
+int gm_box_plan(uint64_t root_key, int world, int rank, const int32_t *opts, int what, int axis, uint32_t *out,
+                uint64_t cap, uint64_t *n);
 
-/* Per rank this context ran in its last solve (all virtual ranks, or its own rank of a
- * multi-process solve) on the sharded box engine: the GPU time of the rank's launches
- * (GM_OPT_TIMING; with virtual ranks each rank runs alone, so this is its multi-GPU
- * compute time), the boxes it computed, and how many of those another rank computes too.
- * *n = 0 for every other engine. */
-int gm_rank_stats(gm_ctx *ctx, double *kernel_ms, uint64_t *boxes, uint64_t *ties, int cap, int *n);
+/* Per rank this context ran in its last solve on the split box engine (all virtual ranks, or its
+ * own rank of a multi-process solve): with GM_OPT_TIMING the GPU time from the start of the rank's
+ * first tier launch to the end of its last, the boxes it computed, and the halo bytes it receives
+ * per solve.  With GM_OPT_DIST_SOLO r + 1 (virtual ranks) rank r's list runs alone, its cross-rank
+ * waits dropped -- its own critical path -- enqueued whole behind a 20 ms hold of the stream, so
+ * the time has no host enqueue gaps.  *n = 0 for every other engine. */
+int gm_rank_stats(gm_ctx *ctx, double *kernel_ms, uint64_t *boxes, uint64_t *recv_bytes, int cap, int *n);
+
+/* With GM_OPT_TIMING, the GPU ms of every op of `rank`'s op list (GM_BOXPLAN_OPS order; 0 for
+ * event records and waits) in the last solve of the split box engine, with GM_OPT_TIMING 2 (an event
+ * pair around each op; 1 times only the whole solve and each rank's span). */
+int gm_rank_op_ms(gm_ctx *ctx, int rank, double *ms, int cap, int *n);
 
 /* Release everything. */
 void gm_close(gm_ctx *ctx);

@@ -1,227 +1,320 @@
-"""The sharded box solve's plan, checked on the CPU (no GPU needed).
+"""The split box solve's plan, checked on the CPU (no GPU needed).
 
-At N > 1 the 8-heap subtraction game runs on the box engine (csrc/dense_box.hip), each
-rank computing one member of every orbit of a group H of heap permutations and reading a
-child box it does not compute from its image under some h in H, which it computed in the
-same box-tier.  The plan comes from the product through gm_box_plan (the
-host code gm_solve runs).  Checked here: the owned lists partition the root's region,
-every child read resolves to a box of the rank's own earlier box-tier in the form the
-kernel implements, the ranks' loads are equal per box-tier, and -- position by position,
-in numpy -- a rank that solves only its boxes and reads through the plan's permutations
-reproduces the C oracle's table.  Reference: the owner hash these plans replace,
-src/game_state.py:23-31, and the child/result exchange they make unnecessary,
+At N > 1 the 8-heap subtraction game runs on the box engine split over the ranks
+(csrc/dist_box.hip): every box computed by exactly one rank, a child box another rank owns
+read through a heap transposition of a box this rank computed (symmetric fill) or received
+in the batch's halo message over RCCL.  The plans come from the product through gm_box_plan
+(the host code gm_solve runs).  Checked here: the ranks' boxes partition the root's region
+(work_vs_one_gpu = 1), no rank's boxes meet every orbit of the old orbit plan's heap
+permutation group (so no rank can answer every key), every child read resolves in the form
+the kernel implements, sender and receiver lists agree, the op lists are deadlock- and
+race-free under stream / event / RCCL semantics (tests/box_sim.py), a position-level numpy
+emulation of every rank solving through its plan equals the C oracle, and two or four gloo
+processes run their op lists with real messages.  Reference: the owner hash these plans
+replace, src/game_state.py:23-31, and the child / result exchange they batch,
 src/new_process.py:145-187.
 """
+import multiprocessing as mp
+import socket
+
 import numpy as np
 import pytest
 
+import box_sim as S
 from gamesmanmpi_amd import _lib
 
 FULL = 0xFFFFFFFF
+SMALL = [0x33337777, 0x23457777, 0x0F0FFFFF, 0x5577BBBB, 0x13572468]
 
 
-def coords(b):
-    b = np.asarray(b, dtype=np.int64)
-    return [(b >> (2 * i)) & 3 for i in range(4)] + [(b >> (8 + 3 * j)) & 7 for j in range(4)]
+def own(world, r, root, split=0, symmetry=1):
+    return _lib.box_plan(world, r, _lib.BOXPLAN_OWN, root=root, split=split, symmetry=symmetry).astype(np.int64)
 
 
-def unit(d):
-    return 1 << (2 * d) if d < 4 else 1 << (8 + 3 * (d - 4))
-
-
-def bsym_box(code, b):
-    """Restatement of csrc/dense_box.hip bsym_box: r^k rotates heaps 0-3 (heap i -> i + k),
-    t swaps heaps 4/5 and 6/7."""
-    b = np.asarray(b, dtype=np.int64)
-    code = np.asarray(code, dtype=np.int64)
-    k = code & 3
-    f = b & 0xFF
-    f = ((f | (f << 8)) >> (8 - 2 * k)) & 0xFF
-    b = (b & ~0xFF) | f
-    x = ((b >> 3) ^ b) & 0x1C700
-    return np.where(code & 4, b ^ x ^ (x << 3), b)
-
-
-def bsym_key(code, key):
-    """Restatement of bsym_key on keys (heap i at bits 4 i)."""
-    key = np.asarray(key, dtype=np.int64)
-    code = np.asarray(code, dtype=np.int64)
-    k = code & 3
-    lo = key & 0xFFFF
-    key = (key & 0xFFFF0000) | (((lo | (lo << 16)) >> (16 - 4 * k)) & 0xFFFF)
-    x = ((key >> 4) ^ key) & 0x0F0F0000
-    return np.where(code & 4, key ^ x ^ (x << 4), key)
-
-
-def box_of_key(key):
-    key = np.asarray(key, dtype=np.int64)
-    b = np.zeros_like(key)
-    for i in range(4):
-        b |= ((key >> (4 * i + 2)) & 3) << (2 * i)
-    for j in range(4):
-        b |= ((key >> (16 + 4 * j + 1)) & 7) << (8 + 3 * j)
-    return b
-
-
-def region(root):
-    lim = coords(box_of_key(root))
-    b = np.arange(1 << 20, dtype=np.int64)
-    c = coords(b)
-    ok = np.ones(len(b), bool)
-    for i in range(8):
-        ok &= c[i] <= lim[i]
-    return b[ok]
-
-
-def plan(world, rank, root=FULL):
-    P = {}
-    for name, what in (("shape", _lib.BOXPLAN_SHAPE), ("boxes", _lib.BOXPLAN_BOXES), ("fills", _lib.BOXPLAN_FILLS),
-                       ("off", _lib.BOXPLAN_TIER_OFF), ("own", _lib.BOXPLAN_OWN), ("map", _lib.BOXPLAN_MAP)):
-        P[name] = _lib.box_plan(world, rank, what, root).astype(np.int64)
-    return P
-
-
-INVARIANT_ROOTS = [FULL, 0x33337777, 0x5577BBBB, 0x2211FFFF]
-
-
-@pytest.mark.parametrize("root", [FULL, 0x33337777, 0x23457777, 0x0F0FFFFF])
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_owned_lists_partition_the_region(world, root):
-    reg = region(root)
+@pytest.mark.parametrize("split", [0, 1])
+@pytest.mark.parametrize("world,root", [(2, FULL), (8, FULL)] + [(w, r) for w in (2, 3, 4, 8) for r in SMALL])
+def test_every_box_on_exactly_one_rank(world, root, split):
+    """The ranks' computed boxes partition the root's region: the summed work equals one
+    GPU's (work_vs_one_gpu = 1, no box computed twice)."""
+    reg = S.region(root)
     seen = np.zeros(1 << 20, np.int64)
     for r in range(world):
-        p = plan(world, r, root)
-        seen[p["own"]] += 1
-        assert np.all(np.diff(p["own"]) > 0)
-        # a rank owns only boxes it computes
-        assert np.isin(p["own"], p["boxes"]).all()
+        o = own(world, r, root, split)
+        b = _lib.box_plan(world, r, _lib.BOXPLAN_BOXES, root=root, split=split).astype(np.int64)
+        assert np.array_equal(np.sort(b), o) and np.all(np.diff(o) > 0)
+        seen[o] += 1
     assert (seen[reg] == 1).all() and seen.sum() == len(reg)
 
 
-@pytest.mark.parametrize("root", [FULL, 0x33337777, 0x23457777, 0x0F0FFFFF, 0x5577BBBB])
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_every_child_read_is_an_own_box_of_the_tier_below(world, root):
-    """The kernel's contract (bx_issue): a child of a computed box along heap d is read from
-    bsym_box(code, C) with code the fill's 3 bits at 3 d; that box must be one this rank
-    computes in the box-tier before (an earlier launch), and the code must be a rotation
-    for an A child (an address change) and t for a B child (a byte shuffle)."""
-    for r in range(world):
-        p = plan(world, r, root)
-        boxes, fills, off = p["boxes"], p["fills"], p["off"]
-        tier_of = np.full(1 << 20, -1, np.int64)
-        for t in range(len(off) - 1):
-            tier_of[boxes[off[t]:off[t + 1]]] = t
-        c = coords(boxes)
-        tier = sum(c)
-        assert (tier_of[boxes] == tier).all()   # box-tier t holds the boxes of coordinate sum t
-        for d in range(8):
-            has = c[d] >= 1
-            code = (fills >> (3 * d)) & 7
-            assert (code[~has] == 0).all()
-            if d < 4:
-                assert (code & 4 == 0).all()
-            else:
-                assert (code & 3 == 0).all()
-            src = bsym_box(code[has], boxes[has] - unit(d))
-            assert (tier_of[src] == tier[has] - 1).all(), (r, d)
+def _orbit_h(b):
+    """Canonical member of a box's orbit under the round-4 orbit plan's group H = <rotate
+    heaps 0-3> x <swap 4<->5, 6<->7> (the kernel's old fill group)."""
+    b = np.asarray(b, np.int64)
+    best = None
+    for k in range(4):
+        f = b & 0xFF
+        f = ((f | (f << 8)) >> (8 - 2 * k)) & 0xFF
+        x = (b & ~0xFF) | f
+        for e in range(2):
+            if e:
+                t = ((x >> 3) ^ x) & 0x1C700
+                x = x ^ t ^ (t << 3)
+            best = x if best is None else np.minimum(best, x)
+    return best
 
 
-@pytest.mark.parametrize("world,boxes,ties", [(1, 1 << 20, 0), (2, 532480, 16384), (4, 282880, 40960),
-                                              (8, 145600, 24640)])
-def test_equal_loads_per_box_tier_and_redundancy(world, boxes, ties):
-    """Every rank computes the same number of boxes in every box-tier (each rank's set is a
-    heap permutation of the others'); only tie boxes (fixed by some h != id) are computed by
-    more than one rank: 1.6 %, 7.9 %, 11.1 % more than an even share at 2, 4, 8 ranks."""
-    per = None
-    for r in range(world):
-        p = plan(world, r)
-        nsym, g, nb, nown, nties, ntiers = p["shape"].tolist()
-        assert (nsym, nb, nties, ntiers) == (world, boxes, ties, 41)
-        counts = np.diff(p["off"])
-        per = counts if per is None else per
-        assert np.array_equal(counts, per)
-    assert per.sum() == boxes
+def _orbit_s4s4(b):
+    """Canonical member under every permutation of heaps 0-3 and of heaps 4-7 (sorted coordinates)."""
+    c = S.coords(b)
+    a = np.sort(np.stack(c[:4]), axis=0)
+    bb = np.sort(np.stack(c[4:]), axis=0)
+    out = np.zeros(len(c[0]), np.int64)
+    for i in range(4):
+        out |= a[i] << (2 * i)
+        out |= bb[i] << (8 + 3 * i)
+    return out
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_query_map_sends_every_box_to_a_computed_image(world):
-    reg = region(FULL)
+def test_no_rank_meets_every_orbit(world):
+    """round 4's plan gave every rank one member of every H-orbit, so one
+    rank's table answered every key.  The default split (halves) gives no rank a member of
+    every H-orbit, nor of every orbit of all heap permutations that map boxes to boxes."""
+    reg = S.region(FULL)
+    for canon in (_orbit_h, _orbit_s4s4):
+        allorb = np.unique(canon(reg))
+        for r in range(world):
+            mine = np.unique(canon(own(world, r, FULL, 0)))
+            assert len(mine) < len(allorb), (canon.__name__, r)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_comparison_split_is_a_transversal(world):
+    """Why GM_OPT_BOX_SPLIT 1 (tier-balanced comparisons) is not the default: its rank 0
+    ([c_x >= c_y] on every axis) meets every orbit of the box-preserving heap permutations,
+    so one rank's table plus symmetry answers every key -- the property VERDICT r04 rejected."""
+    reg = S.region(FULL)
+    allorb = np.unique(_orbit_s4s4(reg))
+    assert len(np.unique(_orbit_s4s4(own(world, 0, FULL, 1)))) == len(allorb)
+
+
+@pytest.mark.parametrize("split,symmetry", [(0, 1), (0, 0), (1, 1)])
+@pytest.mark.parametrize("world,root", [(2, FULL), (8, FULL), (4, 0x33337777), (8, 0x23457777), (3, 0x5577BBBB)])
+def test_every_child_read_resolves(world, root, split, symmetry):
+    """The kernel's contract (dense_box.hip bx_issue): a child of a computed box is an own box
+    of the box-tier below, or is read through a transposition of two heaps of its own kind
+    from such a box, or arrives in the halo message of the parent's batch.  Sender and
+    receiver lists agree entry for entry."""
+    P = S.plans(world, root, split=split, symmetry=symmetry)
+    for p in P:
+        got = set()
+        assert S.check_reads(p, got)
+        if not symmetry:
+            assert p["counts"][1] == 0
+    for r, p in enumerate(P):
+        for a in range(p["g"]):
+            if (r >> a) & 1:
+                continue
+            u = r | (1 << a)
+            if u < world:
+                assert np.array_equal(p["send"][a][0], P[u]["recv"][a][0])
+                assert np.array_equal(p["send"][a][1], P[u]["recv"][a][1])
+
+
+def _bytes(ent):
+    return int(sum(2048 if (e >> 20) else 4096 for e in ent.tolist()))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_halo_volume_and_fill(world):
+    """Bytes that cross a link per solve, halves partition (GM_OPT_BOX_SPLIT 0): without the
+    symmetric fill every upper rank receives its lower neighbour's whole boundary layer per
+    axis (2^30 / G bytes); the fill reads all but the boundary boxes whose unsplit heaps of the
+    same kind are all in the lower half, 1/8 or 1/4 of it."""
+    sent = {}
+    for sym in (0, 1):
+        per_axis = [0, 0, 0]
+        for r in range(world):
+            for a in range(3):
+                per_axis[a] += _bytes(_lib.box_plan(world, r, _lib.BOXPLAN_SEND, axis=a, symmetry=sym))
+        sent[sym] = per_axis
+    g = world.bit_length() - 1
+    half = world // 2    # rank pairs per axis
+    assert sent[0][:g] == [half * (1 << 30) // world] * g
+    assert sent[1] == {2: [64 << 20, 0, 0], 4: [64 << 20, 64 << 20, 0],
+                       8: [128 << 20, 128 << 20, 64 << 20]}[world]
+
+
+@pytest.mark.parametrize("world,root,split", [(2, FULL, 0), (8, FULL, 0), (4, 0x23457777, 0), (8, FULL, 1)])
+def test_tier_kernel_writes_every_message_slot(world, root, split):
+    """The tier kernel writes each box it computes to its halo message slots
+    (GM_BOXPLAN_DSTS, csrc/dense_box.hip bx_store): every send entry has exactly one slot on its
+    box, of its kind (the two top layers along A heap k: k + 1; the whole box: 5), at the
+    entry's byte offset in the rank's send buffer (axis 0's messages, then axis 1's, ...,
+    batch order, list order); the box's tier is in the message's range; no other slots."""
     for r in range(world):
-        p = plan(world, r)
-        mine = np.zeros(1 << 20, bool)
-        mine[p["boxes"]] = True
-        m = p["map"]
-        assert (m[reg] != 0xFF).all()
-        assert mine[bsym_box(m[reg], reg)].all()
-        out = np.ones(1 << 20, bool)
-        out[reg] = False
-        assert (m[out] == 0xFF).all()
+        kw = dict(root=root, split=split)
+        boxes = _lib.box_plan(world, r, _lib.BOXPLAN_BOXES, **kw).astype(np.int64)
+        toff = _lib.box_plan(world, r, _lib.BOXPLAN_TIER_OFF, **kw).astype(np.int64)
+        dsts = _lib.box_plan(world, r, _lib.BOXPLAN_DSTS, **kw).astype(np.int64).reshape(-1, 3)
+        halo = _lib.box_plan(world, r, _lib.BOXPLAN_HALO, **kw).astype(np.int64).reshape(-1, 2)
+        assert dsts.shape[0] == len(boxes)
+        tier_of = np.repeat(np.arange(len(toff) - 1), np.diff(toff))
+        where = {int(b): i for i, b in enumerate(boxes.tolist())}
+        want = set()
+        o = 0
+        for a in range(3):
+            off = _lib.box_plan(world, r, _lib.BOXPLAN_SEND_OFF, axis=a, **kw).astype(np.int64)
+            ent = _lib.box_plan(world, r, _lib.BOXPLAN_SEND, axis=a, **kw).astype(np.int64)
+            for j in range(len(off) - 1):
+                for e in ent[off[j]:off[j + 1]].tolist():
+                    i = where[e & 0xFFFFF]
+                    assert halo[j, 0] <= tier_of[i] <= halo[j, 1]
+                    code = e >> 20
+                    want.add((i, (code or 5) << 28 | (o >> 11)))
+                    o += 2048 if code else 4096
+        got = {(i, int(w)) for i, row in enumerate(dsts.tolist()) for w in row if w}
+        assert got == want
+        assert sum(int((row != 0).sum()) for row in dsts) == len(want)
 
 
-def test_uninvariant_root_uses_the_stabiliser():
-    """A root whose region no rotation maps onto itself keeps only the permutations that
-    do (here t alone): 8 ranks then form 2 distinct sets, each computed by 4 ranks."""
-    root = 0x777737BF   # A heaps 15, 11, 7, 3 (box coordinates 3, 2, 1, 0); B heaps all 7
-    for r in range(8):
-        nsym, g, nb, nown, nties, ntiers = plan(8, r, root)["shape"].tolist()
-        assert nsym == 2 and g == (4 if r % 2 else 0)
-        assert (nown > 0) == (r < 2)
+@pytest.mark.parametrize("split", [0, 1])
+@pytest.mark.parametrize("world,root", [(2, 0x33337777), (4, 0x23457777), (8, 0x5577BBBB), (2, FULL), (8, FULL)])
+def test_schedule_is_deadlock_free_and_race_free(world, root, split):
+    P = S.plans(world, root, split=split)
+    for seed in range(2):
+        assert S.simulate(P, seed=seed)
 
 
-def _emulate_rank(root, world, rank, p):
-    """Solve rank `rank`'s boxes position by position (heap-sum order) in numpy, reading a
-    child outside its boxes through the plan's permutation for that heap; returns the keys
-    of its boxes and their 1-byte codes (csrc/gm_common.hpp)."""
-    boxes = p["boxes"]
-    fill_of = np.zeros(1 << 20, np.int64)
-    fill_of[boxes] = p["fills"]
-    mine = np.zeros(1 << 20, bool)
-    mine[boxes] = True
-    lim = [(root >> (4 * i)) & 15 for i in range(8)]
+def _mutate(P, rank, pred, action="drop", shift=3):
+    Q = [dict(p) for p in P]
+    ops = Q[rank]["ops"].tolist()
+    i = next(k for k, o in enumerate(ops) if pred(o))
+    o = ops.pop(i)
+    if action == "earlier":
+        ops.insert(max(0, i - shift), o)
+    Q[rank]["ops"] = np.array(ops, dtype=np.int64).reshape(-1, 6)
+    return Q
+
+
+@pytest.mark.parametrize("what", ["unpack_late", "send_early", "recv"])
+def test_simulator_catches_broken_schedules(what):
+    """The checker bites: each injected schedule bug is reported."""
+    P = S.plans(4, 0x23457777)
+    up = 3
+    if what == "unpack_late":      # every halo is unpacked after the first tier of its batch
+        Q = [dict(p) for p in P]
+        ops = Q[up]["ops"].tolist()
+        i = 0
+        while i < len(ops):
+            if ops[i][0] == S.BOP_UNPACK:
+                k = next((k for k in range(i + 1, len(ops)) if ops[k][0] == S.BOP_TIER), None)
+                if k is not None:
+                    ops.insert(k, ops.pop(i))
+                    i = k
+            i += 1
+        Q[up]["ops"] = np.array(ops, dtype=np.int64).reshape(-1, 6)
+    elif what == "send_early":     # the lower rank sends before the tier that writes the message
+        i = next(k for k, o in enumerate(P[0]["ops"].tolist()) if o[0] == S.BOP_WAIT and o[2] == S.BEV_DONE)
+        Q = [dict(p) for p in P]
+        ops = Q[0]["ops"].tolist()
+        w = ops.pop(i)
+        rec = next(k for k in range(i - 1, -1, -1) if ops[k][0] == S.BOP_RECORD and ops[k][2] == S.BEV_DONE
+                   and ops[k][4] == w[4] and ops[k][1] == w[1])
+        tier = next(k for k in range(rec - 1, -1, -1) if ops[k][0] == S.BOP_TIER)
+        r = ops.pop(rec)
+        ops.insert(tier, r)
+        ops.insert(tier + 1, w)
+        Q[0]["ops"] = np.array(ops, dtype=np.int64).reshape(-1, 6)
+    else:                          # a receive is dropped: its send never matches
+        Q = _mutate(P, up, lambda o: o[0] == S.BOP_RECV)
+    caught = 0
+    for seed in range(10):
+        try:
+            S.simulate(Q, seed=seed)
+        except S.SimError:
+            caught += 1
+    assert caught > 0
+
+
+def _emulate(P, root):
+    """Every rank solves its boxes position by position (heap-sum order, all ranks in step),
+    reading a child outside the parent's box from its own boxes, through the plan's
+    transposition of the parent box's fill word, or -- a received child -- from the owner's
+    values; returns each rank's (keys, 1-byte codes)."""
+    # every position of the region's boxes (a box is solved whole, so a transposition may read
+    # a position of an own box outside the root's region): heap i up to the top of its boxes
+    blim = S.coords(S.box_of_key(root))
+    lim = [4 * int(blim[i]) + 3 if i < 4 else 2 * int(blim[i]) + 1 for i in range(8)]
     stride = np.cumprod([1] + [lim[i] + 1 for i in range(7)])
+    N = int(stride[-1]) * (lim[7] + 1)
 
-    def cidx(k):   # compact index of a key of the root's region
+    def cidx(k):
         return sum(((k >> (4 * i)) & 15) * int(stride[i]) for i in range(8))
 
-    # every key of the rank's boxes
-    off = np.arange(4096, dtype=np.int64)
-    c = coords(boxes)
-    keys = np.zeros((len(boxes), 4096), np.int64)
-    for i in range(4):
-        keys |= ((c[i][:, None] << 2) | ((off[None, :] >> (4 + 2 * i)) & 3)) << (4 * i)
-    for j in range(4):
-        keys |= ((c[4 + j][:, None] << 1) | ((off[None, :] >> j) & 1)) << (16 + 4 * j)
-    keys = np.sort(keys.ravel())
-    h = [(keys >> (4 * i)) & 15 for i in range(8)]
-    assert all((h[i] <= lim[i]).all() for i in range(8))
-    level = sum(h)
-    val = np.zeros(int(stride[-1]) * (lim[7] + 1), np.int64)   # the rank's view of the region
-    val[:] = 255   # never-computed slots hold the largest code: reading one changes the result
-    written = np.zeros(len(val), bool)
-    for s in range(int(level.max()) + 1):
-        kk = keys[level == s]
-        if s == 0:
-            val[cidx(kk)] = 255   # all heaps empty: LOSS in 0
-            written[cidx(kk)] = True
-            continue
-        pb = box_of_key(kk)
-        fills = fill_of[pb]
-        best = np.zeros(len(kk), np.int64)
-        for i in range(8):
-            hi = (kk >> (4 * i)) & 15
-            for sub in (1, 2):
-                ok = hi >= 1
-                child = kk[ok] - (np.minimum(hi[ok], sub) << (4 * i))
-                cb = box_of_key(child)
-                # a child in the parent's box or in a box this rank computes is read directly;
-                # else through the fill code of the heap the step crossed
-                cc = np.where((cb != pb[ok]) & ~mine[cb], (fills[ok] >> (3 * i)) & 7, 0)
-                src = cidx(bsym_key(cc, child))
-                assert written[src].all()
-                best[ok] = np.maximum(best[ok], val[src])
-        val[cidx(kk)] = (255 - best) + 2 * (best >> 7)
-        written[cidx(kk)] = True
-    return keys, val[cidx(keys)]
+    G = len(P)
+    vals = [np.full(N, -1, np.int64) for _ in range(G)]
+    owner = np.full(1 << 20, -1, np.int64)
+    fill_of = np.zeros(1 << 20, np.int64)
+    ranks = []
+    for r, p in enumerate(P):
+        owner[p["boxes"]] = r
+        fill_of[p["boxes"]] = p["fills"]
+        off = np.arange(4096, dtype=np.int64)
+        c = S.coords(p["boxes"])
+        keys = np.zeros((len(p["boxes"]), 4096), np.int64)
+        for i in range(4):
+            keys |= ((c[i][:, None] << 2) | ((off[None, :] >> (4 + 2 * i)) & 3)) << (4 * i)
+        for j in range(4):
+            keys |= ((c[4 + j][:, None] << 1) | ((off[None, :] >> j) & 1)) << (16 + 4 * j)
+        keys = keys.ravel()
+        ranks.append((keys, sum((keys >> (4 * i)) & 15 for i in range(8))))
+    pairs = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
+    top = max(int(l.max()) for _, l in ranks if len(l))
+    for s in range(top + 1):
+        for r in range(G):
+            keys, level = ranks[r]
+            kk = keys[level == s]
+            if not len(kk):
+                continue
+            if s == 0:
+                vals[r][cidx(kk)] = 255
+                continue
+            pb = S.box_of_key(kk)
+            best = np.zeros(len(kk), np.int64)
+            for i in range(8):
+                hi = (kk >> (4 * i)) & 15
+                for sub in (1, 2):
+                    ok = hi >= 1
+                    child = kk[ok] - (np.minimum(hi[ok], sub) << (4 * i))
+                    cb = S.box_of_key(child)
+                    cross = cb != pb[ok]
+                    code = (fill_of[pb[ok]] >> (4 * i)) & 15
+                    if i < 4:
+                        q, p_ = code >> 2, code & 3
+                        filled = cross & (q != p_)
+                    else:
+                        filled = cross & (code != 0)
+                    src = child.copy()
+                    for c in np.unique(code[filled]):
+                        m = filled & (code == c)
+                        if i < 4:
+                            hq, hp = int(c) >> 2, int(c) & 3
+                        else:
+                            hq, hp = 4 + pairs[int(c) - 1][0], 4 + pairs[int(c) - 1][1]
+                        t = ((child[m] >> (4 * hq)) ^ (child[m] >> (4 * hp))) & 15
+                        src[m] = child[m] ^ (t << (4 * hq)) ^ (t << (4 * hp))
+                    assert (owner[S.box_of_key(src[filled])] == r).all()
+                    recv = cross & ~filled & (owner[cb] != r)
+                    v = vals[r][cidx(src)]
+                    if recv.any():
+                        o = owner[cb[recv]]
+                        assert (o >= 0).all()
+                        v[recv] = np.array([vals[int(x)][int(y)] for x, y in zip(o, cidx(child[recv]))])
+                    assert (v >= 0).all(), "rank %d level %d heap %d: a child value is not there yet" % (r, s, i)
+                    best[ok] = np.maximum(best[ok], v)
+            vals[r][cidx(kk)] = (255 - best) + 2 * (best >> 7)
+    return [(keys, vals[r][cidx(keys)]) for r, (keys, _) in enumerate(ranks)]
 
 
 def _record_of_code(c):
@@ -229,21 +322,51 @@ def _record_of_code(c):
     return np.where(c >= 128, (1 << 14) | (255 - c), c - 1).astype(np.uint16)
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_emulated_rank_solves_match_the_oracle(oracle, world):
-    """Each rank, solving only its own boxes and reading the others through the plan's heap
-    permutations, gets the C oracle's record for every position of its boxes (root
-    0x33337777: 256 boxes, 2^20 positions, every position of them in the root's region)."""
-    root = 0x33337777
+@pytest.mark.parametrize("split,symmetry", [(0, 1), (0, 0), (1, 1)])
+@pytest.mark.parametrize("world,root", [(2, 0x33337777), (4, 0x33337777), (8, 0x33337777), (8, 0x23457777)])
+def test_emulated_rank_solves_match_the_oracle(oracle, world, root, split, symmetry):
+    """Each rank, solving only its own boxes and reading every other child through its plan,
+    gets the C oracle's record for every position of its boxes, and together the ranks cover
+    every position of the region once."""
     ok, orec = oracle.solve(5, (8,), root=root)
     ref = dict(zip(ok.tolist(), orec.tolist()))
-    seen = set()
-    for r in range(world):
-        p = plan(world, r, root)
-        keys, val = _emulate_rank(root, world, r, p)
-        rec = _record_of_code(val)
+    P = S.plans(world, root, split=split, symmetry=symmetry)
+    seen = 0
+    for r, (keys, val) in enumerate(_emulate(P, root)):
+        inr = np.ones(len(keys), bool)
+        for i in range(8):
+            inr &= ((keys >> (4 * i)) & 15) <= ((root >> (4 * i)) & 15)
+        keys, val = keys[inr], val[inr]
         want = np.array([ref[k] for k in keys.tolist()], np.uint16)
-        assert np.array_equal(rec, want), r
-        own = np.isin(box_of_key(keys), p["own"])
-        seen.update(keys[own].tolist())
-    assert len(seen) == len(ok)
+        assert np.array_equal(_record_of_code(val), want), r
+        seen += len(keys)
+    assert seen == len(ok)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world,root,batch,symmetry,split", [(2, 0x33337777, 4, 1, 0), (2, 0x23457777, 1, 0, 0),
+                                                             (4, 0x23457777, 2, 1, 1), (4, 0x33557777, 3, 1, 0)])
+def test_gloo_ranks_exchange_halos(world, root, batch, symmetry, split):
+    """world_size > 1 over torch.distributed gloo: every rank runs its own RCCL-mode op list
+    as a host program, halos as real messages carrying the C oracle's codes; afterwards every
+    box it computed and every row it received equals the oracle's."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=S.gloo_main, args=(r, world, port, root, batch, symmetry, split, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all("error" not in r for r in res), res
+    assert sorted(r["rank"] for r in res) == list(range(world))
+    assert all(r["own_ok"] and r["recv_ok"] for r in res), res
+    assert sum(r["own_boxes"] for r in res) == len(S.region(root))
+    assert any(r["received_boxes"] > 0 for r in res)

@@ -2,9 +2,9 @@
 runs them at N > 1.  Needs at least two visible devices (the
 driver's 8-GPU node); on a one-GPU box every test here skips.
 
-* dense, 8 heaps (config 5's engine, csrc/dense_box.hip): each rank solves its share of
-  the boxes alone -- it reads the child boxes it does not compute through heap
-  permutations of its own (DESIGN.md §5) -- so the ranks exchange nothing;
+* dense, 8 heaps (config 5's engine, csrc/dist_box.hip): every box on one rank, per-axis
+  split communicators, each batch's halo boxes as ncclSend / ncclRecv on the exchange
+  streams (DESIGN.md §5.0);
 * dense, block engine (other heap counts, or GM_OPT_SUB_INTERLEAVE 10; csrc/dist_sub.hip):
   per-axis split communicators, halo messages as ncclSend / ncclRecv on the exchange streams;
 * sparse (configs 3/4, csrc/dist_sparse.hip): the reference's LOOK_UP / RESOLVE p2p pair
@@ -48,10 +48,12 @@ def _rank_main(rank, world, phase, game, params, opts):
     tdist.broadcast_object_list(uid, src=0)
     phase("communicator")
     ctx.set_comm(rank, world, uid[0])
+    opts = dict(opts)
+    root = opts.pop("root", None)
     for k, v in opts.items():
         ctx.set_option(getattr(_lib, "OPT_" + k.upper()), v)
     phase("solve")
-    n, rec = ctx.solve(ctx.initial())
+    n, rec = ctx.solve(ctx.initial() if root is None else root)
     phase("digest")
     d, m = ctx.digest()
     res = {"rank": rank, "n": n, "rec": rec, "digest": d, "m": m,
@@ -82,13 +84,23 @@ def _summed(res):
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("interleave", [20, 10])
 def test_dense_rccl_2_32_matches_oracle_digest(world, interleave):
-    """Config 5 at full size over `world` processes: the box engine (20, the default; no
-    exchange) and the block engine (10; halo messages over RCCL)."""
+    """Config 5 at full size over `world` processes: the box engine (20, the default) and the
+    block engine (10), both with halo messages over RCCL."""
     ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["subtract_8"]
     res = _run(world, SUB, (8,), {"sub_interleave": interleave})
     assert all(r["n"] == 1 << 32 and r["rec"] == ref["root_record"] for r in res)
     assert _summed(res) == (ref["digest"], 1 << 32)
-    assert (sum(r["exchanged"] for r in res) > 0) == (interleave == 10)
+    assert sum(r["exchanged"] for r in res) > 0
+
+
+@pytest.mark.parametrize("sym", [0, 1])
+def test_box_rccl_custom_root_vs_oracle(oracle, sym):
+    """The split box engine over 2 processes at a custom root, with and without the symmetric
+    fill: the summed digests equal the oracle's."""
+    root = 0x33557777
+    ok, orec = oracle.solve(SUB, (8,), root=root)
+    res = _run(2, SUB, (8,), {"dist_symmetry": sym, "root": root})
+    assert _summed(res) == (digest(ok, orec), len(ok))
 
 
 @pytest.mark.parametrize("owner", [0, 1])

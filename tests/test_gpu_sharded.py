@@ -1,8 +1,8 @@
 """GPU parity of the sharded (multi-GPU) algorithms on ONE device.
 
-GM_OPT_VIRTUAL_RANKS runs G ranks inside one context: the same partition, block
+GM_OPT_VIRTUAL_RANKS runs G ranks inside one context: the same partition, block / box
 lists, halo / all-to-all schedule and kernels as the one-process-per-GPU RCCL
-path, with the exchanges done by device copies (dist_sub.hip, dist_sparse.hip).
+path, with the exchanges done by device copies (dist_sub.hip, dist_box.hip, dist_sparse.hip).
 Every sharded result must be bit-identical to the single-rank result.
 """
 import ctypes
@@ -115,27 +115,38 @@ def _committed(name):
     return json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))[name]
 
 
-@pytest.mark.parametrize("flow", [-1, 0])
+def _plan_bytes(ranks, root=0xFFFFFFFF, **kw):
+    """Halo bytes all ranks send per solve, from the plan (gm_box_plan GM_BOXPLAN_SEND)."""
+    total = 0
+    for r in range(ranks):
+        for a in range(3):
+            ent = _lib.box_plan(ranks, r, _lib.BOXPLAN_SEND, root=root, axis=a, **kw)
+            total += int(sum(2048 if (int(e) >> 20) else 4096 for e in ent))
+    return total
+
+
+@pytest.mark.parametrize("sym", [1, 0])
 @pytest.mark.parametrize("ranks", [2, 3, 4, 8])
-def test_box_sharded_2_32_matches_oracle_digest(ranks, flow):
-    """Config 5 on the box engine over virtual ranks: every rank solves its boxes alone, on
-    its own table (filled with 0xFF first, so a read of a box the rank never computed would
-    show), reading the child boxes it does not compute through heap permutations of its own
-    boxes.  The ranks' owned digests sum to the C oracle's digest of the whole table, the
-    root record is the oracle's, and nothing is exchanged.  flow -1 (the default: a sharded
-    solve is one dataflow launch per rank, box_flow_kernel) and 0 (tier launches)."""
+def test_box_split_2_32_matches_oracle_digest(ranks, sym):
+    """Config 5 on the box engine split over virtual ranks (csrc/dist_box.hip): every box on
+    ONE rank, each rank on its own table (filled with 0xFF first, so a read of a box the rank
+    neither computed nor received would show), halo boxes exchanged per batch (device copies
+    standing in for RCCL), crossing children read through heap transpositions of own boxes
+    with the symmetric fill (sym 1) or all received (sym 0).  The ranks' digests sum to the C
+    oracle's digest of the whole table, the root record is the oracle's, every rank computed
+    its plan's boxes (summing to 2^20: work_vs_one_gpu = 1), and the bytes exchanged are the
+    plan's."""
     ref = _committed("subtract_8")
-    ctx, n, rec = _solve(SUB, (8,), ranks, timing=1, box_flow=flow)
+    ctx, n, rec = _solve(SUB, (8,), ranks, timing=1, dist_symmetry=sym)
     st = ctx.stats()
-    assert st["kernel_launches"] == (ranks if flow else 41 * ranks)
-    assert st["engine"] == _lib.ENGINE_DIST_DENSE and st["exchanged_bytes"] == 0
+    assert st["engine"] == _lib.ENGINE_DIST_DENSE and st["world"] == ranks
     assert (n, rec) == (1 << 32, ref["root_record"])
     assert ctx.digest() == (ref["digest"], 1 << 32)
     rs = ctx.rank_stats()
-    assert len(rs) == ranks and all(r["kernel_ms"] > 0 for r in rs)
-    want = {2: 532480, 3: 532480, 4: 282880, 8: 145600}[ranks]   # tests/test_box_plan.py pins these
-    assert [r["boxes"] for r in rs] == [want] * ranks   # at 3 ranks, rank 2 repeats rank 0's set
-    # a query answers every key through the rank-0 table's heap permutations
+    want = [int(_lib.box_plan(ranks, r, _lib.BOXPLAN_COUNTS, symmetry=sym)[0]) for r in range(ranks)]
+    assert [r["boxes"] for r in rs] == want and sum(want) == 1 << 20
+    assert st["exchanged_bytes"] == _plan_bytes(ranks, symmetry=sym) > 0
+    # every virtual rank's table together answers every key
     keys = np.array([0xFFFFFFFF, 0, 0x12345678, 0xFEDCBA98, 0x0F0F0F0F, 0x88888888], dtype=np.uint64)
     single, _, _ = _solve(SUB, (8,), 1)
     assert np.array_equal(ctx.query(keys), single.query(keys))
@@ -143,19 +154,44 @@ def test_box_sharded_2_32_matches_oracle_digest(ranks, flow):
     ctx.close()
 
 
+def test_box_split_comparisons_2_32_matches_oracle_digest():
+    """GM_OPT_BOX_SPLIT 1 (tier-balanced comparisons; not the default, tests/test_box_plan.py
+    says why) gives the oracle's digest at 2, 4 and 8 ranks."""
+    ref = _committed("subtract_8")
+    for ranks in (2, 4, 8):
+        ctx, n, rec = _solve(SUB, (8,), ranks, box_split=1)
+        assert (n, rec) == (1 << 32, ref["root_record"])
+        assert ctx.digest() == (ref["digest"], 1 << 32)
+        ctx.close()
+
+
 _ORACLE_ROOTS = {}
+
+
+def _oracle_root(oracle, root):
+    if root not in _ORACLE_ROOTS:
+        _ORACLE_ROOTS[root] = oracle.solve(SUB, (8,), root=root)
+    return _ORACLE_ROOTS[root]
+
+
+@pytest.mark.parametrize("batch", [1, 2, 3, 8, 100])
+def test_box_split_batches(oracle, batch):
+    """Every halo batch size gives the oracle's table (8 ranks, root 0x33557777: 2.4 M positions)."""
+    root = 0x33557777
+    ok, orec = _oracle_root(oracle, root)
+    ctx, n, rec = _solve(SUB, (8,), 8, root=root, dist_batch=batch)
+    k, r = ctx.export()
+    assert np.array_equal(k, ok) and np.array_equal(r, orec)
+    ctx.close()
 
 
 @pytest.mark.parametrize("ranks", [2, 4, 8])
 @pytest.mark.parametrize("root", [0x33337777, 0x33557777, 0x333337BF, 0x13572468])
-def test_box_sharded_custom_roots_vs_oracle(oracle, ranks, root):
-    """Custom roots on the sharded box engine: regions every permutation of the plan maps
-    onto themselves (0x33337777, 0x33557777), one only t does (0x333337BF), one none does
-    (0x13572468: every rank computes everything).  Export, digest and query equal the C
+def test_box_split_custom_roots_vs_oracle(oracle, ranks, root):
+    """Custom roots on the split box engine (axes chosen among the heaps the region splits;
+    0x13572468 leaves ranks without boxes at 8).  Export, digest and query equal the C
     oracle's table; keys outside the root's region query as unsolved."""
-    if root not in _ORACLE_ROOTS:
-        _ORACLE_ROOTS[root] = oracle.solve(SUB, (8,), root=root)
-    ok, orec = _ORACLE_ROOTS[root]
+    ok, orec = _oracle_root(oracle, root)
     ctx, n, rec = _solve(SUB, (8,), ranks, root=root)
     assert n == len(ok)
     k, r = ctx.export()
@@ -165,6 +201,37 @@ def test_box_sharded_custom_roots_vs_oracle(oracle, ranks, root):
     assert np.array_equal(ctx.query(sample), orec[:: max(1, len(ok) // 5000)])
     outside = np.array([root + 1 if (root & 15) < 15 else root | 0xF0000000, 0x1FFFFFFFF], dtype=np.uint64)
     assert ctx.query(outside).tolist() == [_lib.REC_UNSOLVED] * 2
+    ctx.close()
+
+
+def test_box_split_solo_timing():
+    """GM_OPT_DIST_SOLO r + 1 (loopback): rank r's op list alone, its cross-rank waits dropped,
+    the other ranks' messages of the previous full solve standing in, queued whole behind a
+    hold of the stream -- its own GPU critical path, per op (gm_rank_op_ms) and from its first
+    tier launch to its last (gm_rank_stats)."""
+    ctx, n, rec = _solve(SUB, (8,), 8, timing=2)
+    for r in (0, 7):
+        ctx.set_option(_lib.OPT_DIST_SOLO, r + 1)
+        ctx.set_option(_lib.OPT_TIMING, 1)      # the span alone
+        ctx.solve(0xFFFFFFFF)
+        span1 = ctx.rank_stats()[r]["kernel_ms"]
+        assert span1 > 0 and (ctx.rank_op_ms(r) == 0).all()
+        ctx.set_option(_lib.OPT_TIMING, 2)      # and per op
+        ctx.solve(0xFFFFFFFF)
+        ms = ctx.rank_op_ms(r)
+        ops = _lib.box_plan(8, r, _lib.BOXPLAN_OPS, loopback=1).reshape(-1, 6)
+        assert len(ms) == len(ops)
+        kind = ops[:, 0]
+        tier = kind == _lib.BOP_TIER
+        assert (ms[tier] > 0).all()
+        assert (ms[(kind == _lib.BOP_RECORD) | (kind == _lib.BOP_WAIT)] == 0).all()
+        span = ctx.rank_stats()[r]["kernel_ms"]
+        # the list was queued whole behind the hold; the per-op event pairs only add time
+        assert ms[tier].sum() <= span + 1e-3 and span1 <= 1.1 * span + 0.01
+    ctx.set_option(_lib.OPT_DIST_SOLO, 0)
+    ref = _committed("subtract_8")
+    n, rec = ctx.solve(0xFFFFFFFF)
+    assert ctx.digest() == (ref["digest"], 1 << 32)
     ctx.close()
 
 
@@ -178,7 +245,7 @@ def test_box_dataflow_on_one_gpu_vs_oracle(oracle, root):
     d0 = tiers.digest()
     tiers.close()
     ctx, n, rec = _solve(SUB, (8,), 1, root=root, box_flow=1, timing=1)
-    assert ctx.stats()["kernel_launches"] == 1
+    assert ctx.stats()["kernel_launches"] == 1 and ctx.stats()["flow_fallbacks"] == 0
     assert (n, rec, ctx.digest()) == (n0, r0, d0)
     n2, rec2 = ctx.solve(root)
     assert (n2, rec2, ctx.digest()) == (n0, r0, d0)
@@ -191,37 +258,55 @@ def test_box_dataflow_on_one_gpu_vs_oracle(oracle, root):
     ctx.close()
 
 
-_FLOW_STALL = r'''
+_FLOW_RUN = """
 import json, os, sys
 sys.path.insert(0, sys.argv[1])
 from gamesmanmpi_amd import Context, _lib
 ref = json.load(open(os.path.join(sys.argv[1], "tests", "golden", "oracle_digests.json")))["subtract_8"]
 ctx = Context(5, (8,), device=0)
-ctx.set_option(_lib.OPT_VIRTUAL_RANKS, 2)
+ctx.set_option(_lib.OPT_BOX_FLOW, 1)
 ctx.set_option(_lib.OPT_TIMING, 1)
+out = []
 for rep in range(2):
     n, rec = ctx.solve(0xFFFFFFFF)
     assert ctx.digest() == (ref["digest"], 1 << 32) and rec == ref["root_record"], rep
-    assert ctx.stats()["kernel_launches"] == 82, ctx.stats()["kernel_launches"]
-print("ok")
-'''
+    st = ctx.stats()
+    out.append((st["kernel_launches"], st["flow_fallbacks"]))
+print(json.dumps(out))
+"""
 
 
-def test_box_dataflow_timeout_falls_back_to_tier_launches():
-    """A dataflow wait that outlasts its limit (GM_BOX_FLOW_TEST_STALL makes every wait
-    look for an epoch no flag holds; GM_BOX_FLOW_TIMEOUT_MS 20) ends the launch -- every
-    wave sees the error and leaves -- and the solve is redone with tier launches: the
-    oracle's digest, a line on stderr, and tier launches from then on (fresh process: the
-    hooks are read at launch capture)."""
+def _flow_run(**env):
+    import json
     import os
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, GM_BOX_FLOW_TEST_STALL="1", GM_BOX_FLOW_TIMEOUT_MS="20")
-    r = subprocess.run([sys.executable, "-c", _FLOW_STALL, repo], env=env, capture_output=True, text=True,
-                       timeout=180)
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
-    assert "re-solving with tier launches" in r.stderr
+    r = subprocess.run([sys.executable, "-c", _FLOW_RUN, repo], env=dict(os.environ, **env), capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1]), r.stderr
+
+
+def test_box_dataflow_timeout_falls_back_to_tier_launches():
+    """A dataflow wait that outlasts its limit (GM_BOX_FLOW_TEST_STALL makes every wait look
+    for an epoch no flag holds; GM_BOX_FLOW_TIMEOUT_MS 20) ends the launch -- every wave sees
+    the error and leaves -- and the solve is redone with tier launches: the oracle's digest, a
+    line on stderr, gm_stats_t.flow_fallbacks 1, and tier launches from then on (fresh process:
+    the hooks are read at launch capture)."""
+    out, err = _flow_run(GM_BOX_FLOW_TEST_STALL="1", GM_BOX_FLOW_TIMEOUT_MS="20")
+    assert out == [[41, 1], [41, 1]]
+    assert "re-solving with tier launches" in err
+
+
+def test_box_dataflow_grid_from_occupancy():
+    """the dataflow launch's grid is the kernel's resident capacity from
+    the occupancy API, not a constant.  With 48 KiB of extra dynamic LDS per workgroup
+    (GM_BOX_FLOW_EXTRA_LDS) fewer workgroups fit a CU; the launch shrinks to what is resident,
+    so every wait makes progress: one launch, no fallback, the oracle's digest."""
+    out, err = _flow_run(GM_BOX_FLOW_EXTRA_LDS=str(48 << 10))
+    assert out == [[1, 0], [1, 0]], err
+    assert "re-solving" not in err
 
 
 def test_box_engine_query_outside_the_root_region_is_unsolved():
