@@ -212,6 +212,45 @@ def rank_digest_check(heaps, world, root, rank_digests, batch, slots, symmetry, 
     return {"ranks": out, "wrong_ranks": [x["rank"] for x in out if not x["ok"]]}
 
 
+def box_sharding(world, args, root, st, rstats, per_rank, autotune, torch, dist):
+    """The sharding block of the split box engine (csrc/dist_box.hip): the
+    plan's boxes per rank -- one work set divided, work_vs_one_gpu = the boxes all ranks
+    compute / the boxes one GPU computes = 1 -- and the halo bytes each rank received."""
+    from gamesmanmpi_amd import _lib
+    G = world if world > 1 else args.virtual_ranks
+    kw = dict(batch=args.dist_batch, symmetry=args.dist_symmetry)
+    boxes = [int(_lib.box_plan(G, r, _lib.BOXPLAN_COUNTS, root, **kw)[0]) for r in range(G)]
+    one = int(_lib.box_plan(1, 0, _lib.BOXPLAN_COUNTS, root, **kw)[0]) if G > 1 else sum(boxes)
+    sh = _lib.box_plan(G, 0, _lib.BOXPLAN_SHAPE, root, **kw).astype(int).tolist()
+    axes = ["heap %d box coordinate >= %d" % (sh[8 + 4 * a], sh[9 + 4 * a]) for a in range(sh[1])]
+    recv = rstats[0]["recv_bytes"] if (world > 1 and rstats) else None
+    if world > 1:
+        t = torch.tensor([float(st["exchanged_bytes"]), float(recv or 0)], dtype=torch.float64, device=COLL_DEV)
+        allr = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allr, t)
+        sent = [int(a[0].item()) for a in allr]
+        recvd = [int(a[1].item()) for a in allr]
+    else:
+        sent, recvd = [st["exchanged_bytes"]], [r["recv_bytes"] for r in rstats]
+    return {
+        "scheme": ("box engine split: the 2^20 boxes of the 4x4x4x4x2x2x2x2 lattice divided by halves of %d heap "
+                   "coordinate(s) (%s); ranks >= 2^%d idle; each box computed by exactly one rank; a child box "
+                   "of the other half read through a same-kind heap transposition of an own box (symmetric "
+                   "fill) or received: the lower rank's tier kernel writes it to a message slot and an "
+                   "exchange stream per axis sends each batch of %d tiers over RCCL (DESIGN.md §5.0)"
+                   % (sh[1], "; ".join(axes), sh[1], args.dist_batch)),
+        "work_vs_one_gpu": sum(boxes) / max(1, one),
+        "boxes_per_rank": boxes,
+        "halo_batch_tiers": args.dist_batch, "halo_batch_autotune_ms": autotune,
+        "halo_symmetric_fill": bool(args.dist_symmetry),
+        "halo_bytes_sent_per_step_by_rank": sent,
+        "halo_bytes_received_per_step_by_rank": recvd,
+        "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank,
+        "round4_note": ("round 4's N>1 numbers (1.86/3.29/5.17x at 2/4/8 on one GPU's clock) came from each "
+                        "rank computing one member per heap-permutation orbit -- a symmetry reduction of the "
+                        "work, not a division of one work set; this split computes every box once")}
+
+
 def box_rank_digest_check(world, root, rank_digests):
     """N > 1, box engine: each rank's gm_digest covers exactly the boxes it owns
     (csrc/dense_box.hip, gm_box_plan GM_BOXPLAN_OWN); compare every one with the C
@@ -423,8 +462,9 @@ def main():
     ap.add_argument("--no-toot", action="store_true", help="skip the config-3/4 side measurements")
     ap.add_argument("--cpu-heaps", type=int, default=8)
     ap.add_argument("--dist-batch", type=int, default=None,
-                    help="N>1: tiers per halo exchange (default: chosen in warmup from 1, 2, 4, 8 by the "
-                         "max-over-ranks solve time; 4 for virtual ranks)")
+                    help="N>1: tiers per halo exchange (default: chosen in warmup by the max-over-ranks solve "
+                         "time, from 1, 2, 4 on the box engine and 1, 2, 4, 8 on the block engine; %d for "
+                         "virtual ranks)" % 1)
     ap.add_argument("--dist-slots", type=int, default=4, help="N>1: halo buffers per split heap")
     ap.add_argument("--dist-symmetry", type=int, default=1, choices=(0, 1),
                     help="N>1: fill halo blocks that are a heap permutation of an own block locally")
@@ -434,10 +474,6 @@ def main():
     ap.add_argument("--block-engine", action="store_true",
                     help="8 heaps: run the block engine (GM_OPT_SUB_INTERLEAVE 10) instead of the box engine, "
                          "sharded with halo exchanges at N > 1 (the round-3 multi-GPU path, for comparison)")
-    ap.add_argument("--rehearse-one-gpu", action="store_true",
-                    help="N>1 rehearsal on a one-GPU box: every rank on device 0, bench.py's collectives over "
-                         "gloo, no RCCL communicator (the 8-heap box engine needs none), no side configs; the "
-                         "ranks share the GPU, so the time is not a multi-GPU result")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     ap.add_argument("--watchdog", type=float, default=None,
@@ -449,11 +485,6 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    global COLL_DEV
-    if args.rehearse_one_gpu:
-        if args.heaps != 8 or args.block_engine:
-            ap.error("--rehearse-one-gpu runs the 8-heap box engine (no exchange)")
-        local, COLL_DEV, args.no_toot = 0, "cpu", True
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
 
@@ -479,24 +510,18 @@ def main():
     import torch.distributed as dist
     torch.cuda.set_device(local)
     if world > 1:
-        if args.rehearse_one_gpu:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from gamesmanmpi_amd import Context, _lib
 
     ctx = Context(_lib.GAME_SUBTRACT, (args.heaps,), device=local)
-    # the box engine (csrc/dense_box.hip) at 8 heaps: one GPU, and at N > 1 each rank
-    # solving its orbit share of the boxes alone (no exchange); else the block engine
+    # the box engine (csrc/dense_box.hip) at 8 heaps: one GPU, and at N > 1 the boxes split
+    # over the ranks by halves of heap coordinates, halo boxes exchanged per batch of tiers
+    # over the library's own RCCL communicators (csrc/dist_box.hip); else the block engine
     box = args.heaps == 8 and not args.block_engine
     if not box:
         ctx.set_option(_lib.OPT_SUB_INTERLEAVE, 10)
-    if world > 1 and (args.rehearse_one_gpu or box):
-        # the box engine exchanges nothing: rank and world only, no
-        # RCCL communicator of the library's own (torch's process group times the run)
-        ctx.set_comm(rank, world)
-    elif world > 1:
+    if world > 1:
         uid = [None]
         if rank == 0:
             buf = ctypes.create_string_buffer(128)
@@ -514,7 +539,8 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     ctx.set_option(_lib.OPT_TIMING, 1)
-    ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch or 4)
+    default_batch = 1 if box else 4   # box: B = 1 modelled fastest at 2, 4, 8 ranks (profiles/r05d_box_split_time.txt)
+    ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch or default_batch)
     ctx.set_option(_lib.OPT_DIST_SLOTS, args.dist_slots)
     ctx.set_option(_lib.OPT_DIST_SYMMETRY, args.dist_symmetry)
     ctx.set_option(_lib.OPT_DIST_OWNER, args.dist_owner)
@@ -527,12 +553,12 @@ def main():
             dist.barrier()
 
     autotune = None
-    if world > 1 and args.dist_batch is None and not box:
+    if world > 1 and args.dist_batch is None:
         # untimed: the halo batch trades the upper ranks' lag (B - 1 tiers) against the
         # number of RCCL messages; every rank measures the same candidates and takes
         # the same argmin of the max-over-ranks time, so all ranks keep one schedule
         autotune = {}
-        for b in (1, 2, 4, 8):
+        for b in ((1, 2, 4) if box else (1, 2, 4, 8)):
             ctx.set_option(_lib.OPT_DIST_BATCH, b)
             ctx.solve(root)
             barrier()
@@ -547,7 +573,7 @@ def main():
         _, args.dist_batch = min(autotune.values())
         autotune = {k: v[0] for k, v in autotune.items()}
         ctx.set_option(_lib.OPT_DIST_BATCH, args.dist_batch)
-    args.dist_batch = args.dist_batch or 4
+    args.dist_batch = args.dist_batch or default_batch
     for _ in range(args.warmup):
         n, rec = ctx.solve(root)
     barrier()
@@ -644,7 +670,7 @@ def main():
         "data": "synthetic (the game itself: every position of the 2^32-state subtraction game)",
         "config": {"workload": "subtraction game, %d heaps x 4 bits, root %#x (config 5)" % (args.heaps, root),
                    "positions": positions,
-                   "parallelism": "1 GPU" if world == 1 else ("box-orbit-sharded x%d" if box else "block-sharded x%d")
+                   "parallelism": "1 GPU" if world == 1 else ("box-split x%d" if box else "block-sharded x%d")
                    % world},
         "parity": parity,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -653,11 +679,12 @@ def main():
                      "traffic_gbs": traffic_gbs,
                      "traffic_frac": (traffic_gbs / HBM_PEAK_GBS) if traffic_gbs else None,
                      "kernel": (("box_tier_kernel<%s> (csrc/dense_box.hip: 4x4x4x4x2x2x2x2 boxes, one launch "
-                                 "per box-tier)" % ("true" if sharded else "false")
+                                 "per box-tier%s)" % (("true", "; this rank's boxes, its halo message slots written "
+                                                       "by the same kernel") if sharded else ("false", ""))
                                  if launches_per_solve > max(1, args.virtual_ranks) else
                                  "box_flow_kernel<%s> (csrc/dense_box.hip: 4x4x4x4x2x2x2x2 boxes, every box-tier in "
                                  "one launch, a box group starting when its child boxes are stored%s)"
-                                 % (("true", "; this rank's orbit share of the boxes") if sharded else ("false", "")))
+                                 % ("false", ""))
                                 if box else
                                 "sub_tier_kernel_wk<%d> (tiers of >= 4096 blocks), sub_tier_kernel_b4<%d> (smaller)"
                                 % (args.heaps - 3, args.heaps - 3)),
@@ -684,15 +711,8 @@ def main():
                                 if (world == 1 or box) else
                                 "HIP events around this rank's whole sharded solve (includes halo waits)")},
         "exchanged_bytes_per_step_rank0": st["exchanged_bytes"],
-        "rehearsal": ("--rehearse-one-gpu: %d ranks sharing ONE GPU over gloo; not a multi-GPU measurement" % world
-                      if args.rehearse_one_gpu else None),
-        "sharding": None if (world == 1 and args.virtual_ranks == 1) else {
-            "scheme": ("box engine: each rank computes one member of every orbit of heap permutations "
-                       "<rotate heaps 0-3> x <swap heaps 4/5 and 6/7> and reads the child boxes it does not "
-                       "compute through those permutations; no exchange (DESIGN.md §5)"),
-            "boxes_per_rank": rstats[0]["boxes"] if rstats else None,
-            "tie_boxes_per_rank": rstats[0]["ties"] if rstats else None,
-            "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank} if box else {
+        "sharding": None if (world == 1 and args.virtual_ranks == 1) else box_sharding(
+            world, args, root, st, rstats, per_rank, autotune, torch, dist) if box else {
             "halo_batch_tiers": args.dist_batch, "halo_batch_autotune_ms": autotune, "halo_slots": args.dist_slots,
             "halo_symmetric_fill": bool(args.dist_symmetry),
             "block_owner": ("split heaps in halves", "tier-balanced")[args.dist_owner],

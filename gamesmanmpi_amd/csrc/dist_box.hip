@@ -29,9 +29,9 @@
 // [jB-1, jB+B-2] (an A-heap crossing: the child box's two top layers along that heap, 2 KiB;
 // else the whole 4 KiB box).  The tier kernel writes each such box, from the registers that hold
 // it, also to its message slot; after the lower rank's tier jB+B-2 the axis's exchange stream
-// X[a] sends the message; the upper rank receives it -- all axes' messages of the batch in one
-// ncclGroup -- and unpacks them into its table (the boxes' natural slots) in one launch, on its
-// compute stream right before its batch j.  Every rank's work is a precomputed op list (tier
+// X[a] sends the message; the upper rank receives the batch's messages (one per axis on which
+// it is the upper side) and unpacks them all into its table (the boxes' natural slots) in one
+// launch, on its compute stream right before its batch j.  Every rank's work is a precomputed op list (tier
 // launch, unpack, send, receive, event record / wait).  RCCL mode (one
 // process per GPU): the list in order, one communicator per axis.  Loopback mode
 // (GM_OPT_VIRTUAL_RANKS, G ranks inside one context on one GPU, for testing): the same lists on
@@ -638,31 +638,17 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
     return GM_OK;
 }
 
-// Run a rank's ops from R.pc while they do not wait for another rank's unrecorded event.  In
-// RCCL mode a run of receives (one batch's messages, all on S) goes into one ncclGroup: one
-// kernel for all of them.
+// Run a rank's ops from R.pc while they do not wait for another rank's unrecorded event.
+// (RCCL mode: one receive per axis and batch, issued one after another on S -- no ncclGroup
+// across the axes' communicators; the chain of waits runs from higher rank bits to lower ones
+// and rank 0 receives nothing, so no cycle can form.)
 static int bx_advance(Ctx *c, DistBox *d, BxRank &R, bool solo, bool op_events, bool *progress) {
     while (R.pc < R.ops.size()) {
         const BxOp &o = R.ops[R.pc];
         if (d->loopback && !solo && o.kind == BOP_WAIT && o.peer != R.rank && d->ranks[o.peer].recorded[o.ev][o.axis] <= o.arg)
             break;
-        if (!d->loopback && o.kind == BOP_RECV && !op_events) {
-            size_t e = R.pc;
-            while (e < R.ops.size() && R.ops[e].kind == BOP_RECV) e++;
-            GM_NCCL(ncclGroupStart());
-            for (size_t k = R.pc; k < e; k++) {
-                const int rc = bx_exec(c, d, R, k, solo, op_events);
-                if (rc != GM_OK) {
-                    (void)ncclGroupEnd();
-                    return rc;
-                }
-            }
-            GM_NCCL(ncclGroupEnd());
-            R.pc = e;
-        } else {
-            GM_TRY(bx_exec(c, d, R, R.pc, solo, op_events));
-            R.pc++;
-        }
+        GM_TRY(bx_exec(c, d, R, R.pc, solo, op_events));
+        R.pc++;
         *progress = true;
     }
     return GM_OK;
