@@ -1,5 +1,6 @@
 """CPU checks of the C-ABI library: it loads, exports what include/gmsolve.h declares,
-and its host-side descriptor twins agree with the oracle.  No device work here."""
+and its host-side descriptor twins agree with the oracle.  No device work here, except the
+gpu-marked gm_query test (the documented answer of each engine)."""
 import ctypes
 import os
 import re
@@ -170,3 +171,42 @@ def test_reference_plugin_files_route_to_descriptors(rel, name):
     mod = load_plugin(os.path.join(REF, rel))
     c = games.identify(mod)
     assert c is not None and c.name == name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", ["box", "box_virtual_ranks", "block", "sparse"])
+def test_query_semantics_per_engine(oracle, engine):
+    """gm_query as include/gmsolve.h documents it, per engine, on one GPU
+    (a rank of a multi-process split answers only its own boxes' keys:
+    tests/test_gpu_multiproc.py::test_box_rccl_custom_root_vs_oracle).  Every key of the
+    solved set answers the oracle's record; a key outside it answers 0xFFFF."""
+    from gamesmanmpi_amd import Context
+    if engine == "sparse":
+        game, params, root = TOOT, (4, 3), None
+    else:
+        game, params, root = SUB, (8,), 0x33557777
+    ctx = Context(game, params, device=0)
+    if engine == "box_virtual_ranks":
+        ctx.set_option(_lib.OPT_VIRTUAL_RANKS, 4)
+    elif engine == "block":
+        ctx.set_option(_lib.OPT_SUB_INTERLEAVE, 10)
+    if root is None:
+        root = ctx.initial()
+    ctx.solve(root)
+    ok, orec = oracle.solve(game, params, root=root)
+    step = max(1, len(ok) // 5000)
+    assert np.array_equal(ctx.query(ok[::step]), orec[::step])
+    if engine == "sparse":
+        outside = np.setdiff1d(np.arange(int(ok.max()) + 1, int(ok.max()) + 64, dtype=np.uint64), ok)[:8]
+    else:
+        outside = np.array([0x33557778, 0x43557777, 0xFFFFFFFF, 1 << 32], dtype=np.uint64)
+    assert ctx.query(outside).tolist() == [_lib.REC_UNSOLVED] * len(outside)
+    ctx.close()
+
+
+def test_header_documents_query_per_engine():
+    """The header's gm_query comment names the rule for each engine."""
+    text = open(os.path.join(REPO, "include", "gmsolve.h")).read()
+    doc = text[:text.index("int gm_query(")].rsplit("/*", 1)[1]
+    for phrase in ("0xFFFF", "multi-process", "box engine", "sparse", "virtual ranks"):
+        assert phrase in doc, phrase

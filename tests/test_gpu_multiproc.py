@@ -50,6 +50,7 @@ def _rank_main(rank, world, phase, game, params, opts):
     ctx.set_comm(rank, world, uid[0])
     opts = dict(opts)
     root = opts.pop("root", None)
+    qkeys = opts.pop("query_keys", None)
     for k, v in opts.items():
         ctx.set_option(getattr(_lib, "OPT_" + k.upper()), v)
     phase("solve")
@@ -58,6 +59,8 @@ def _rank_main(rank, world, phase, game, params, opts):
     d, m = ctx.digest()
     res = {"rank": rank, "n": n, "rec": rec, "digest": d, "m": m,
            "tiers": [int(x) for x in ctx.tier_counts()], "exchanged": ctx.stats()["exchanged_bytes"]}
+    if qkeys is not None:
+        res["query"] = [int(x) for x in ctx.query(np.array(qkeys, dtype=np.uint64))]
     ctx.close()
     return res
 
@@ -96,11 +99,20 @@ def test_dense_rccl_2_32_matches_oracle_digest(world, interleave):
 @pytest.mark.parametrize("sym", [0, 1])
 def test_box_rccl_custom_root_vs_oracle(oracle, sym):
     """The split box engine over 2 processes at a custom root, with and without the symmetric
-    fill: the summed digests equal the oracle's."""
+    fill: the summed digests equal the oracle's, and gm_query on a rank answers exactly the
+    keys of the boxes it computed (0xFFFF for the others: include/gmsolve.h gm_query), so
+    every sampled key is answered by one rank, with the oracle's record."""
+    from gamesmanmpi_amd import _lib
     root = 0x33557777
     ok, orec = oracle.solve(SUB, (8,), root=root)
-    res = _run(2, SUB, (8,), {"dist_symmetry": sym, "root": root})
+    sample = ok[:: max(1, len(ok) // 4000)]
+    want = orec[:: max(1, len(ok) // 4000)]
+    res = _run(2, SUB, (8,), {"dist_symmetry": sym, "root": root, "query_keys": sample.tolist()})
     assert _summed(res) == (digest(ok, orec), len(ok))
+    q = np.array([r["query"] for r in res])
+    answered = q != _lib.REC_UNSOLVED
+    assert (answered.sum(axis=0) == 1).all()
+    assert np.array_equal(np.where(answered, q, 0).sum(axis=0), want)
 
 
 @pytest.mark.parametrize("owner", [0, 1])
