@@ -915,10 +915,16 @@ __global__ void sub_digest_kernel(const uint8_t *__restrict__ table, uint64_t sl
     }
 }
 
-__global__ void sub_query_kernel(const uint8_t *__restrict__ table, uint64_t slots,
+// a key outside the root's region (a heap above the root's) answers REC_UNSOLVED: the slot
+// may hold an earlier solve's code (include/gmsolve.h gm_query)
+__global__ void sub_query_kernel(const uint8_t *__restrict__ table, uint64_t slots, uint64_t root, int heaps,
                                  const uint64_t *__restrict__ keys, uint16_t *__restrict__ out, uint64_t n) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (i < n) out[i] = keys[i] < slots ? record_of_code(table[keys[i]]) : REC_UNSOLVED;
+    if (i >= n) return;
+    const uint64_t k = keys[i];
+    bool in = k < slots;
+    for (int j = 0; j < heaps && in; j++) in = ((k >> (4 * j)) & 15u) <= ((root >> (4 * j)) & 15u);
+    out[i] = in ? record_of_code(table[k]) : REC_UNSOLVED;
 }
 
 // ---------------------------------------------------------------------------
@@ -1209,7 +1215,7 @@ int dense_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     GM_HIP(hipMalloc(&dr, n * 2));
     GM_HIP(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(sub_query_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, d->table,
-                       d->slots, dk, dr, n);
+                       d->slots, c->root, c->sub.heaps, dk, dr, n);
     GM_HIP(hipMemcpyAsync(recs, dr, n * 2, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     (void)hipFree(dk);

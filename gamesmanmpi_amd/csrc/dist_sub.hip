@@ -791,6 +791,9 @@ int dist_sub_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     for (uint64_t i = 0; i < n; i++) {
         recs[i] = REC_UNSOLVED;
         if (keys[i] >> (4 * d->heaps)) continue;
+        bool in = true;   // outside the root's region: unsolved (include/gmsolve.h gm_query)
+        for (int j = 0; j < d->heaps && in; j++) in = ((keys[i] >> (4 * j)) & 15u) <= ((c->root >> (4 * j)) & 15u);
+        if (!in) continue;
         int own = owner_of(d, keys[i] >> (4 * d->low));
         for (auto &R : d->ranks)
             if (R.rank == own) {

@@ -300,6 +300,16 @@ static int key_bits(const Ctx *c) {
     return 64;
 }
 
+// GM_SPARSE_HOME_W = w > 0 (development): the tier tables' locality home -- a key's group
+// is its top sort_bits() bits (the bits the interior lists are sorted by), each group's keys
+// hashed into 2^w slots from a hashed base (sparse_tables.hpp home_slot); 0 = hash of the key
+static uint32_t home_loc(const Ctx *c) {
+    static const int w = getenv("GM_SPARSE_HOME_W") ? atoi(getenv("GM_SPARSE_HOME_W")) : 0;
+    if (w <= 0 || w > 30) return 0;
+    const int kb = std::min(key_bits(c), 63), b0 = std::max(0, kb - sort_bits());
+    return (uint32_t)b0 | (uint32_t)w << 8;
+}
+
 // Sort a large tier's interior list by the key's top BATCH_SORT_BITS bits into
 // (skeys, sslot) for the batch kernels; the scratch is kept for the replay's sorts.
 static int batch_sort(Ctx *c, Sparse *sp, SpTier &T, bool alloc) {
@@ -355,7 +365,7 @@ static int ensure_counts(Sparse *sp, size_t n) {
 
 static FrontRef front_ref(Sparse *sp, size_t t) {
     SpTier &T = sp->tiers[t];
-    return FrontRef{T.slots, T.cap, sp->d_counts + t};
+    return FrontRef{T.slots, T.cap, sp->d_counts + t, eff_loc(T.loc, T.cap)};
 }
 
 static ResRef res_ref(Sparse *sp, size_t t) { return res_ref_of(sp->tiers[t]); }
@@ -409,7 +419,7 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
         unsigned long long *cnt = sp->d_replay, *tscr = sp->d_replay + NC, *rootw = sp->d_replay + NC + 16 * T + 1;
         uint32_t *err = (uint32_t *)(sp->d_replay + NC + 16 * T);
         auto fref = [&](size_t u) { return FrontRef{u < T ? sp->tiers[u].slots : nullptr, u < T ? sp->tiers[u].cap : 0,
-                                                    cnt + u}; };
+                                                    cnt + u, u < T ? eff_loc(sp->tiers[u].loc, sp->tiers[u].cap) : 0u}; };
         std::vector<ResRef> tabs(T);
         uint64_t maxcap = 1;
         for (size_t t = 0; t < T; t++) {
@@ -511,6 +521,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     double t0 = now_ms();
 
     sp->tiers.resize(1);
+    sp->tiers[0].loc = home_loc(c);
     GM_TRY(tier_alloc(c, &sp->tiers[0].slots, 1024));
     sp->tiers[0].cap = 1024;
     hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, front_ref(sp, 0), root, sp->d_err);
@@ -539,7 +550,10 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         if (sp->tiers[t].ni >= split_max() && batch_enabled()) GM_TRY(batch_sort(c, sp, sp->tiers[t], true));
         // 2. size the tables of the tiers the children land in: load <= 0.7 for the
         //    predicted distinct children; a misprediction costs one re-run
-        if (sp->tiers.size() < t + S + 1) sp->tiers.resize(t + S + 1);
+        if (sp->tiers.size() < t + S + 1) {
+            sp->tiers.resize(t + S + 1);
+            for (auto &U : sp->tiers) U.loc = home_loc(c);
+        }
         GM_TRY(ensure_counts(sp, sp->tiers.size()));
         uint64_t offered = 0, before = 0;
         for (int s = 0; s < S; s++) {

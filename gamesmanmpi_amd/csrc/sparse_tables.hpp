@@ -26,15 +26,25 @@ struct alignas(16) RSlot {
     uint64_t score;   // u16 preference score in the low bits
 };
 
+// loc: the table's home function (home_slot): 0 = a hash of the whole key; else
+// gshift | wlog << 8 = the key's group (key >> gshift) picks a base slot and a hash of the
+// key one of the 2^wlog slots from it (GM_SPARSE_HOME_W, sparse.hip)
 struct FrontRef {           // inserting into a tier table
     RSlot *s;
     uint64_t cap;
     unsigned long long *count;
+    uint32_t loc = 0;
 };
 struct ResRef {             // looking up in a tier table
     RSlot *s;
     uint64_t cap;
+    uint32_t loc = 0;
 };
+// the home function a table of `cap` slots uses: a locality home only when the table
+// holds at least two windows (the same rule for inserts, lookups and rehashes)
+inline GM_HD uint32_t eff_loc(uint32_t loc, uint64_t cap) {
+    return (loc >> 8) && cap >= (2ull << (loc >> 8)) ? loc : 0u;
+}
 
 constexpr uint64_t MAX_PROBE = 2048;   // an insert probing further marks the table full
 constexpr double TABLE_LOAD = 0.7;     // planned load of a tier table
@@ -62,19 +72,25 @@ struct SpTier {
     uint64_t *skeys = nullptr;
     uint32_t *sslot = nullptr;
     int64_t tier = 0;            // the descriptor tier of the positions (root tier + index)
+    uint32_t loc = 0;            // home function (FrontRef::loc) requested for this tier's table
 };
 
 namespace {
 
 // home slot: the low half of mix64 scaled to cap (the high half picks the owner
-// rank in the sharded engine, so the two stay independent)
-__device__ __forceinline__ uint64_t home_slot(uint64_t key, uint64_t cap) {
+// rank in the sharded engine, so the two stay independent).  With a locality home
+// (loc != 0) the keys of one group -- one value of the key's top bits, which the sorted
+// interior lists walk together -- share a window of 2^wlog slots at a hashed base.
+__device__ __forceinline__ uint64_t home_slot(uint64_t key, uint64_t cap, uint32_t loc) {
     const uint64_t m = mix64(key);
-    return __umul64hi((m << 32) | (m >> 32), cap);
+    if (!loc) return __umul64hi((m << 32) | (m >> 32), cap);
+    const uint64_t g = mix64((key >> (loc & 63u)) ^ 0x5851F42D4C957F2Dull);
+    const uint64_t h = __umul64hi(g, cap) + (m & ((1ull << (loc >> 8)) - 1ull));
+    return h >= cap ? h - cap : h;
 }
 
 __device__ __forceinline__ bool front_insert(const FrontRef &t, uint64_t key, uint32_t *err) {
-    uint64_t h = home_slot(key, t.cap);
+    uint64_t h = home_slot(key, t.cap, t.loc);
     const uint64_t lim = t.cap < MAX_PROBE ? t.cap : MAX_PROBE;
     for (uint64_t probe = 0; probe < lim; probe++) {
         const uint64_t cur = t.s[h].key;
@@ -94,7 +110,7 @@ __device__ __forceinline__ bool front_insert(const FrontRef &t, uint64_t key, ui
 // score of key, or -1 when absent; each probe is one 16-byte load
 __device__ __forceinline__ int res_find(const ResRef &t, uint64_t key) {
     if (!t.s) return -1;
-    uint64_t h = home_slot(key, t.cap);
+    uint64_t h = home_slot(key, t.cap, t.loc);
     for (uint64_t probe = 0; probe < t.cap; probe++) {
         const u64x2 v = *(const u64x2 *)&t.s[h];
         if (v[0] == key) return (int)(v[1] & 0xFFFFu);
@@ -283,7 +299,7 @@ inline int tier_grow(Ctx *c, SpTier &T, uint64_t cap, uint32_t *d_err) {
     RSlot *ns;
     GM_TRY(tier_alloc(c, &ns, cap));
     if (T.cap) {
-        FrontRef dst{ns, cap, nullptr};
+        FrontRef dst{ns, cap, nullptr, eff_loc(T.loc, cap)};
         hipLaunchKernelGGL(front_rehash_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap, dst,
                            d_err);
         dev_free(c, T.slots);
@@ -293,7 +309,7 @@ inline int tier_grow(Ctx *c, SpTier &T, uint64_t cap, uint32_t *d_err) {
     return GM_OK;
 }
 
-inline ResRef res_ref_of(const SpTier &T) { return ResRef{T.slots, T.cap}; }
+inline ResRef res_ref_of(const SpTier &T) { return ResRef{T.slots, T.cap, eff_loc(T.loc, T.cap)}; }
 
 // capacity for `n` keys at the planned load (multiple of 1024)
 inline uint64_t table_cap_for(uint64_t n) {
