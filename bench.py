@@ -361,6 +361,8 @@ def sparse_config(name, game, params, rank, world, dist, torch):
         out["ok"] = n == 1187212827 and out["per_ply_counts_match_appendix_d"] and out["digest_matches_oracle"]
         out["edges"] = st["n_edges"]
         out["algo_bytes_per_position"] = st["algo_bytes"] / n
+        if world == 1:
+            out["roofline"] = toot_roofline(st["algo_bytes"], med)
         if world == 1:   # the CPU leg's bounded sample, solved here too: the same workload on both
             sub = toot_sample_root(params)
             sn, srec, sts = timed_solves(ctx, sub, rank, world, dist, torch, warmup=1, repeats=3)
@@ -373,6 +375,49 @@ def sparse_config(name, game, params, rank, world, dist, torch):
         out["ok"] = n == 54089 and (rec >> 14) == 1 and (rec & 0x3FFF) == 12 and out["digest_matches_oracle"]
     ctx.close()
     return out
+
+
+RANDOM_LOAD_PEAK = 47e9   # random 16-B loads/s from an 8 GiB table (tools/randbench.hip, profiles/r01_randbench.txt)
+RANDOM_CAS_PEAK = 17e9    # random 8-B CAS/s from an 8 GiB table (same)
+TOOT_PROFILE = os.path.join(REPO, "profiles", "traffic_toot6x4.json")
+
+
+def toot_roofline(algo_bytes, solve_s):
+    """Config 3's roofline.  The sparse engine is bound by the random-
+    access rate, not by bytes: every insert and lookup moves a 64-B line.
+    So the block grades the two kernels that make 80 % of a solve, expand (one probe per edge,
+    a CAS per new key) and retro (one lookup per undecided child), by their memory-side
+    request rates from the committed profile (profiles/traffic_toot6x4.json: rocprofv3
+    kernel trace of replayed solves + one-solve PMC passes, tools/sparse_replay_profile.py)
+    against the measured random-access peaks; and it sets the counted HBM-side bytes of a
+    solve beside the SURVEY §8d algorithmic bytes (10 + 18 d per position)."""
+    try:
+        prof = json.load(open(TOOT_PROFILE))
+    except (OSError, ValueError):
+        return None
+    ks = prof["kernels"]
+    per = {}
+    for k in ("expand_kernel", "retro_kernel"):
+        x = ks[k]
+        sec = x["ms"] / 1e3
+        per[k] = {"ms": x["ms"], "ea_read_req": x["ea_read_req"], "ea_write_req": x["ea_write_req"],
+                  "read_req_per_s": x["ea_read_req"] / sec, "write_req_per_s": x["ea_write_req"] / sec,
+                  "frac_of_random_load_peak": x["ea_read_req"] / sec / RANDOM_LOAD_PEAK, "l2_hit": x["l2_hit"]}
+    rd = sum(per[k]["ea_read_req"] for k in per)
+    sec = sum(per[k]["ms"] for k in per) / 1e3
+    counted = sum(x["fetch_bytes"] + x["write_bytes"] for x in ks.values())
+    return {"bound": "random access", "unit": "requests/s",
+            "achieved": rd / sec, "peak": RANDOM_LOAD_PEAK, "frac": rd / sec / RANDOM_LOAD_PEAK,
+            "achieved_note": "memory-side read requests of expand + retro per second of their kernel time",
+            "peak_cas_per_s": RANDOM_CAS_PEAK,
+            "peak_source": "tools/randbench.hip (profiles/r01_randbench.txt): random 16-B loads 47 G/s, "
+                           "random 8-B CAS 17 G/s, 8 GiB table",
+            "kernels": per,
+            "algo_bytes_per_solve": algo_bytes, "algo_gbs": algo_bytes / solve_s / 1e9,
+            "algo_frac_of_hbm_peak": algo_bytes / solve_s / 1e9 / HBM_PEAK_GBS,
+            "counted_bytes_per_solve": counted, "counted_over_algo_bytes": counted / algo_bytes,
+            "profile": "profiles/traffic_toot6x4.json",
+            "profile_kernel_sum_ms": min(prof["kernel_sum_ms_per_replay"])}
 
 
 SPARSE_CPU_SAMPLE = {"othello_4x4": (4, (4, 4)),    # the whole config-4 workload

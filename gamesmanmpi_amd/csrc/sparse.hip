@@ -507,6 +507,46 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
     return GM_OK;   // positions, tiers, edges, bytes: unchanged from the recorded solve
 }
 
+// GM_SPARSE_PROBE_STATS (development): per tier table, the mean number of probes a lookup
+// of a stored key takes (its slot's distance from its home + 1) and the longest, on stderr
+__global__ void probe_stats_kernel(const RSlot *__restrict__ s, uint64_t cap, uint32_t loc,
+                                   unsigned long long *acc) {
+    uint64_t sum = 0, cnt = 0, mx = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = s[i].key;
+        if (k == EMPTY_KEY) continue;
+        const uint64_t h = home_slot(k, cap, loc);
+        const uint64_t dist = i >= h ? i - h : i + cap - h;
+        sum += dist + 1;
+        cnt++;
+        mx = dist + 1 > mx ? dist + 1 : mx;
+    }
+    wave_add(acc, sum);
+    wave_add(acc + 1, cnt);
+    atomicMax(acc + 2, (unsigned long long)mx);
+}
+
+static int probe_stats(Ctx *c, Sparse *sp) {
+    unsigned long long *acc = sp->d_scratch + 32, h[3];
+    uint64_t tsum = 0, tcnt = 0;
+    for (size_t t = 0; t < sp->tiers.size(); t++) {
+        const SpTier &T = sp->tiers[t];
+        if (!T.cap) continue;
+        GM_HIP(hipMemsetAsync(acc, 0, 24, c->stream));
+        hipLaunchKernelGGL(probe_stats_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap,
+                           eff_loc(T.loc, T.cap), acc);
+        GM_HIP(hipMemcpyAsync(h, acc, 24, hipMemcpyDeviceToHost, c->stream));
+        GM_HIP(hipStreamSynchronize(c->stream));
+        tsum += h[0];
+        tcnt += h[1];
+        fprintf(stderr, "[gm] probe stats tier %zu: %llu keys in %llu slots, mean probes %.3f, longest %llu\n", t,
+                h[1], (unsigned long long)T.cap, h[1] ? (double)h[0] / h[1] : 0.0, h[2]);
+    }
+    fprintf(stderr, "[gm] probe stats all tiers: %llu keys, mean probes %.3f (loc %#x)\n", (unsigned long long)tcnt,
+            tcnt ? (double)tsum / tcnt : 0.0, sp->tiers.empty() ? 0u : sp->tiers[0].loc);
+    return GM_OK;
+}
+
 template <class D>
 static int solve_with(Ctx *c, const D &d, uint64_t root) {
     constexpr int S = D::MAX_SKIP;
@@ -629,6 +669,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         c->tier_counts.push_back(T.count_all);
         tb += T.cap * sizeof(RSlot) + T.ni * 13;
     }
+    if (getenv("GM_SPARSE_PROBE_STATS")) GM_TRY(probe_stats(c, sp));
     c->n_positions = n;
     c->stats.n_positions = n;
     c->stats.n_tiers = (int32_t)sp->tiers.size();
