@@ -141,6 +141,9 @@ class _Level:
 CHUNK = 64    # positions expanded between two looks at the incoming pipes (GM_GRAPH_CHUNK)
 
 
+HANDSHAKE_S = 5.0   # a connection's HMAC challenge and peer number must arrive within this
+
+
 def _mesh(me, nw, tag, key, timeout_s=120.0):
     """Pipes to every other worker: worker w listens on an abstract unix socket named by
     the walk's tag and w, connects to every lower-numbered worker's and accepts every
@@ -149,33 +152,68 @@ def _mesh(me, nw, tag, key, timeout_s=120.0):
     is authenticated with the walk's random key (multiprocessing's HMAC challenge); one
     that fails it is dropped.  The workers build the mesh themselves so the parent never holds
     the n(n-1) descriptors (growing a threaded process's descriptor table waits for an RCU
-    grace period, ~0.1 s a doubling on a busy host)."""
+    grace period, ~0.1 s a doubling on a busy host).  Everything is bounded by timeout_s
+    (ADVICE r04): the accept loop polls, and a connection's challenge and its first message
+    must arrive within HANDSHAKE_S (a socket receive timeout, cleared once it is a peer),
+    so a local process that connects and never answers, or a peer that died before
+    connecting, ends the mesh with TimeoutError -- worker_main reports it to the parent."""
+    import socket
+    import struct
     from multiprocessing import AuthenticationError
-    from multiprocessing.connection import Client, Listener
+    from multiprocessing.connection import Client, Connection, answer_challenge, deliver_challenge
     name = "\0" + tag + "-%d"
-    lst = Listener(name % me, family="AF_UNIX", backlog=max(1, nw), authkey=key)
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    srv.bind(name % me)
+    srv.listen(max(1, nw))
+    srv.settimeout(0.25)
     peers = [None] * nw
     deadline = time.time() + timeout_s
-    for p in range(me):
-        while True:
-            try:
-                c = Client(name % p, family="AF_UNIX", authkey=key)
-                break
-            except (FileNotFoundError, ConnectionRefusedError):
-                if time.time() > deadline:
-                    raise
-                time.sleep(0.002)
-        c.send_bytes(b"%d" % me)
-        peers[p] = c
-    left = nw - 1 - me
-    while left:
+
+    def rcvtimeo(c, secs):   # SO_RCVTIMEO on the connection's descriptor (0 = none)
+        so = socket.socket(fileno=c.fileno())
         try:
-            c = lst.accept()
-        except (AuthenticationError, EOFError, OSError):
-            continue
-        peers[int(c.recv_bytes())] = c
-        left -= 1
-    lst.close()
+            so.setsockopt(socket.SOL_SOCKET, socket.SO_RCVTIMEO, struct.pack("ll", int(secs), 0))
+        finally:
+            so.detach()
+
+    try:
+        for p in range(me):
+            while True:
+                try:
+                    c = Client(name % p, family="AF_UNIX", authkey=key)
+                    break
+                except (FileNotFoundError, ConnectionRefusedError):
+                    if time.time() > deadline:
+                        raise
+                    time.sleep(0.002)
+            c.send_bytes(b"%d" % me)
+            peers[p] = c
+        left = nw - 1 - me
+        while left:
+            if time.time() > deadline:
+                raise TimeoutError("walk worker %d: %d higher-numbered peers did not connect within %.0f s"
+                                   % (me, left, timeout_s))
+            try:
+                s, _ = srv.accept()
+            except socket.timeout:
+                continue
+            s.settimeout(None)
+            c = Connection(s.detach())
+            try:
+                rcvtimeo(c, max(1.0, min(HANDSHAKE_S, deadline - time.time())))
+                deliver_challenge(c, key)
+                answer_challenge(c, key)
+                w = int(c.recv_bytes())
+                if not (me < w < nw) or peers[w] is not None:
+                    raise ValueError("bad peer number %d" % w)
+                rcvtimeo(c, 0)
+            except (AuthenticationError, EOFError, OSError, ValueError):
+                c.close()
+                continue
+            peers[w] = c
+            left -= 1
+    finally:
+        srv.close()
     return peers
 
 

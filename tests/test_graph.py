@@ -3,6 +3,7 @@ device descriptor reproduces are enumerated on the host with their own functions
 and resolved on the device.  CPU tests check the enumeration; GPU tests check the
 solve against the golden tables and the canonical oracle (oracle/canonical.py)."""
 import os
+import time
 
 import numpy as np
 import pytest
@@ -314,3 +315,57 @@ def test_worker_mesh_drops_unauthenticated_connections():
         for p in range(nw):
             if p != w:
                 assert out[w][p].recv_bytes() == b"%d>%d" % (p, w)
+
+
+def _silent_stranger(tag, me):
+    import socket
+    s = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    for _ in range(500):
+        try:
+            s.connect("\0" + tag + "-%d" % me)
+            return s
+        except (FileNotFoundError, ConnectionRefusedError):
+            time.sleep(0.01)
+    raise AssertionError("worker socket never appeared")
+
+
+def test_walk_mesh_survives_a_silent_connection_and_times_out():
+    """a local process that connects to a walk worker's socket and never answers
+    the HMAC challenge is dropped after the handshake limit (the mesh still forms with the
+    real peer), and a peer that never connects ends the mesh with TimeoutError instead of a
+    hang (walk_worker._mesh)."""
+    import os
+    import threading
+    from gamesmanmpi_amd import walk_worker
+    old = walk_worker.HANDSHAKE_S
+    walk_worker.HANDSHAKE_S = 1.0
+    try:
+        key, tag = os.urandom(32), "gmtest-%d" % os.getpid()
+        got = {}
+        t0 = threading.Thread(target=lambda: got.update(w0=walk_worker._mesh(0, 2, tag, key, timeout_s=20)))
+        t0.start()
+        stranger = _silent_stranger(tag, 0)
+        time.sleep(0.1)
+        peers1 = walk_worker._mesh(1, 2, tag, key, timeout_s=20)
+        t0.join(30)
+        assert not t0.is_alive() and got["w0"][1] is not None and peers1[0] is not None
+        got["w0"][1].send_bytes(b"ping")
+        assert peers1[0].recv_bytes() == b"ping"
+        stranger.close()
+        tag2 = tag + "b"
+        err = {}
+
+        def lone():
+            try:
+                walk_worker._mesh(0, 2, tag2, key, timeout_s=2.5)
+            except Exception as e:   # noqa: BLE001 -- the test inspects it
+                err["e"] = e
+        t = time.time()
+        th = threading.Thread(target=lone)
+        th.start()
+        s2 = _silent_stranger(tag2, 0)
+        th.join(30)
+        assert isinstance(err.get("e"), TimeoutError) and time.time() - t < 10
+        s2.close()
+    finally:
+        walk_worker.HANDSHAKE_S = old
