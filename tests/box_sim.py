@@ -136,51 +136,87 @@ class SimError(AssertionError):
     pass
 
 
-def check_reads(P, received):
-    """Every child read of every computed box resolves (the kernel's contract): returns the
-    per-box set of (child box, direction) pairs read from a message."""
-    tier_of = np.full(1 << 20, -1, np.int64)
-    off = P["off"]
-    for t in range(len(off) - 1):
-        tier_of[P["boxes"][off[t]:off[t + 1]]] = t
-    mine = tier_of >= 0
-    got = defaultdict(set)    # (axis, batch) -> {(box, code)}
+PAIRS = np.array([(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)], np.int64)
+
+
+def swap_boxes(b, q, p):
+    """Boxes b with the coordinates of heaps q and p exchanged (elementwise; q, p of one kind)."""
+    b, q, p = (np.asarray(x, np.int64) for x in (b, q, p))
+    sq = np.where(q < 4, 2 * q, 8 + 3 * (q - 4))
+    sp = np.where(p < 4, 2 * p, 8 + 3 * (p - 4))
+    m = np.where(q < 4, 3, 7)
+    fq, fp = (b >> sq) & m, (b >> sp) & m
+    return (b & ~(m << sq) & ~(m << sp)) | (fq << sp) | (fp << sq)
+
+
+def direction_reads(P, d):
+    """For every computed box with a child along heap d: (box index, child C, source read,
+    swapped?) -- the kernel's read of that child (dense_box.hip bx_issue), vectorised."""
+    boxes = P["boxes"]
+    c = coords(boxes)
+    idx = np.nonzero(c[d] >= 1)[0]
+    C = boxes[idx] - unit(d)
+    src = P["srcs"][idx, d]
+    code = (P["fills"][idx] >> (4 * d)) & 15
+    if d < 4:
+        q, p = code >> 2, code & 3
+        sw = q != p
+    else:
+        sw = code != 0
+        pr = PAIRS[np.maximum(code - 1, 0)]
+        q, p = 4 + pr[:, 0], 4 + pr[:, 1]
+    return idx, C, src, sw, q, p
+
+
+def received_keys(P):
+    """batch << 28 | code << 20 | box of every entry the rank receives."""
+    ks = []
     for a in range(3):
         offs, ent = P["recv"][a]
         for j in range(len(offs) - 1):
-            for e in ent[offs[j]:offs[j + 1]].tolist():
-                got[(a, j)].add((e & 0xFFFFF, e >> 20))
-    for i, b in enumerate(P["boxes"].tolist()):
-        t = int(tier_of[b])
-        c = coords(b)
-        for d in range(8):
-            if c[d] < 1:
-                continue
-            C = b - unit(d)
-            src = int(P["srcs"][i, d])
-            sw = transposed_heaps(P["fills"][i], d)
-            if sw is not None:
-                if src != swap_box(C, *sw) or src == C:
-                    raise SimError("rank %d box %#x dir %d: source %#x is not the transposition %s of %#x" %
-                                   (P["rank"], b, d, src, sw, C))
-                if (sw[0] < 4) != (d < 4):
-                    raise SimError("rank %d: a child along heap %d read through heaps %s" % (P["rank"], d, sw))
-                if not mine[src] or tier_of[src] != t - 1:
-                    raise SimError("rank %d box %#x dir %d: fill source %#x not an own box of tier %d" %
-                                   (P["rank"], b, d, src, t - 1))
-                continue
-            if src != C:
-                raise SimError("rank %d box %#x dir %d: source %#x without a transposition" % (P["rank"], b, d, src))
-            if mine[C]:
-                if tier_of[C] != t - 1:
-                    raise SimError("rank %d: child %#x of %#x not in the tier below" % (P["rank"], C, b))
-                continue
-            j = t // P["batch"]
-            ok = any((C, 0) in got[(a, j)] or (d < 4 and (C, 1 + d) in got[(a, j)]) for a in range(3))
-            if not ok:
-                raise SimError("rank %d box %#x dir %d: child %#x neither own, filled nor in message %d" %
-                               (P["rank"], b, d, C, j))
-            received.add((C, d))
+            ks.append((np.int64(j) << 28) | ent[offs[j]:offs[j + 1]].astype(np.int64))
+    return np.unique(np.concatenate(ks)) if ks else np.zeros(0, np.int64)
+
+
+def check_reads(P, received=None):
+    """Every child read of every computed box resolves (the kernel's contract): an own box of
+    the tier below, a same-kind heap transposition of one (the fill), or an entry of the
+    parent's batch's halo message (a whole box, or for an A-heap child its two top layers)."""
+    boxes, off = P["boxes"], P["off"]
+    tier_of = np.full(1 << 20, -1, np.int64)
+    tier_of[boxes] = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    T = tier_of[boxes]
+    rk = received_keys(P)
+    for d in range(8):
+        idx, C, src, sw, q, p = direction_reads(P, d)
+        t = T[idx]
+        if sw.any():
+            exp = swap_boxes(C[sw], q[sw], p[sw])
+            bad = (src[sw] != exp) | (exp == C[sw]) | (tier_of[exp] != t[sw] - 1)
+            if bad.any():
+                i = np.nonzero(bad)[0][0]
+                raise SimError("rank %d box %#x dir %d: fill source %#x is not an own box of the tier below, "
+                               "or not the transposition (%d %d) of %#x" % (P["rank"], boxes[idx[sw][i]], d,
+                                                                          src[sw][i], q[sw][i], p[sw][i], C[sw][i]))
+            if ((q[sw] < 4) != (d < 4)).any():
+                raise SimError("rank %d: a child along heap %d read through heaps of the other kind" % (P["rank"], d))
+        ns = ~sw
+        Cn, tn = C[ns], t[ns]
+        if (src[ns] != Cn).any():
+            raise SimError("rank %d dir %d: a source without a transposition is not the child" % (P["rank"], d))
+        own = tier_of[Cn] >= 0
+        if (tier_of[Cn[own]] != tn[own] - 1).any():
+            raise SimError("rank %d dir %d: an own child not in the tier below" % (P["rank"], d))
+        rest, j = Cn[~own], tn[~own] // P["batch"]
+        ok = np.isin((j << 28) | rest, rk)
+        if d < 4:
+            ok |= np.isin((j << 28) | ((1 + d) << 20) | rest, rk)
+        if not ok.all():
+            i = np.nonzero(~ok)[0][0]
+            raise SimError("rank %d dir %d: child %#x neither own, filled nor in message %d" % (P["rank"], d, rest[i],
+                                                                                          j[i]))
+        if received is not None:
+            received.update(zip(rest.tolist(), [d] * len(rest)))
     return True
 
 
@@ -192,7 +228,14 @@ def simulate(P, seed=0):
     mine = [np.zeros(1 << 20, bool) for _ in range(G)]
     for r, p in enumerate(P):
         mine[r][p["boxes"]] = True
-    have = [set() for _ in range(G)]           # (box, code) unpacked
+    have = [np.zeros((5, 1 << 20), bool) for _ in range(G)]   # [code][box] unpacked (code 0 whole box)
+    reads = []
+    for p in P:
+        rd = []
+        for d in range(8):
+            idx, C, src, sw, q, pp = direction_reads(p, d)
+            rd.append((idx, C, src))
+        reads.append(rd)
     tier_boxes = []
     for p in P:
         off = p["off"]
@@ -248,19 +291,18 @@ def simulate(P, seed=0):
         kind, axis, ev, on_x, arg, peer = op(r, i)
         if kind == BOP_TIER:
             own = tier_boxes[r][arg]
-            for k, b in enumerate(own.tolist()):
-                idx = p["off"][arg] + k
-                c = coords(b)
-                for d in range(8):
-                    if c[d] < 1:
-                        continue
-                    C = b - unit(d)
-                    src = int(p["srcs"][idx, d])
-                    if src != C or mine[r][C]:
-                        if not final[r][src]:
-                            raise SimError("rank %d tier %d: source %#x of %#x not computed yet" % (r, arg, src, b))
-                    elif not ((C, 0) in have[r] or (d < 4 and (C, 1 + d) in have[r])):
-                        raise SimError("rank %d tier %d: child %#x of %#x not arrived" % (r, arg, C, b))
+            lo, hi = p["off"][arg], p["off"][arg + 1]
+            for d in range(8):
+                idx, C, src = reads[r][d]
+                k = (idx >= lo) & (idx < hi)
+                Ck, sk = C[k], src[k]
+                local = (sk != Ck) | mine[r][Ck]
+                if not final[r][sk[local]].all():
+                    raise SimError("rank %d tier %d: a source of direction %d not computed yet" % (r, arg, d))
+                far = Ck[~local]
+                ok = have[r][0][far] | (have[r][1 + d][far] if d < 4 else False)
+                if not np.all(ok):
+                    raise SimError("rank %d tier %d: child %#x not arrived" % (r, arg, far[~ok][0]))
             if final[r][own].any():
                 raise SimError("rank %d computes a box twice" % r)
             final[r][own] = True
@@ -287,7 +329,7 @@ def simulate(P, seed=0):
                 ent = arrived[r].get((a, arg))
                 if ent is None:
                     raise SimError("rank %d unpacks message %d on axis %d before it arrived" % (r, arg, a))
-                have[r].update((int(e) & 0xFFFFF, int(e) >> 20) for e in ent)
+                have[r][ent >> 20, ent & 0xFFFFF] = True
         done.add((r, i))
 
     remaining = sum(len(q) for q in streams.values())

@@ -107,8 +107,7 @@ def test_every_child_read_resolves(world, root, split, symmetry):
     receiver lists agree entry for entry."""
     P = S.plans(world, root, split=split, symmetry=symmetry)
     for p in P:
-        got = set()
-        assert S.check_reads(p, got)
+        assert S.check_reads(p)
         if not symmetry:
             assert p["counts"][1] == 0
     for r, p in enumerate(P):
@@ -145,7 +144,7 @@ def test_halo_volume_and_fill(world):
                        8: [128 << 20, 128 << 20, 64 << 20]}[world]
 
 
-@pytest.mark.parametrize("world,root,split", [(2, FULL, 0), (8, FULL, 0), (4, 0x23457777, 0), (8, FULL, 1)])
+@pytest.mark.parametrize("world,root,split", [(8, FULL, 0), (4, 0x23457777, 0), (8, 0x5577BBBB, 1)])
 def test_tier_kernel_writes_every_message_slot(world, root, split):
     """The tier kernel writes each box it computes to its halo message slots
     (GM_BOXPLAN_DSTS, csrc/dense_box.hip bx_store): every send entry has exactly one slot on its
@@ -322,8 +321,9 @@ def _record_of_code(c):
     return np.where(c >= 128, (1 << 14) | (255 - c), c - 1).astype(np.uint16)
 
 
-@pytest.mark.parametrize("split,symmetry", [(0, 1), (0, 0), (1, 1)])
-@pytest.mark.parametrize("world,root", [(2, 0x33337777), (4, 0x33337777), (8, 0x33337777), (8, 0x23457777)])
+@pytest.mark.parametrize("world,root,split,symmetry", [(2, 0x33337777, 0, 1), (4, 0x33337777, 0, 0),
+                                                       (8, 0x33337777, 1, 1), (8, 0x23457777, 0, 1),
+                                                       (8, 0x23457777, 0, 0)])
 def test_emulated_rank_solves_match_the_oracle(oracle, world, root, split, symmetry):
     """Each rank, solving only its own boxes and reading every other child through its plan,
     gets the C oracle's record for every position of its boxes, and together the ranks cover
@@ -350,7 +350,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("world,root,batch,symmetry,split", [(2, 0x33337777, 4, 1, 0), (2, 0x23457777, 1, 0, 0),
-                                                             (4, 0x23457777, 2, 1, 1), (4, 0x33557777, 3, 1, 0)])
+                                                             (4, 0x23457777, 2, 1, 1)])
 def test_gloo_ranks_exchange_halos(world, root, batch, symmetry, split):
     """world_size > 1 over torch.distributed gloo: every rank runs its own RCCL-mode op list
     as a host program, halos as real messages carrying the C oracle's codes; afterwards every

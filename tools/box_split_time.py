@@ -23,8 +23,10 @@ sys.path.insert(0, REPO)
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")   # as bench.py: a hardware queue per stream
 
 
-def dag(ops_by_rank, ms_by_rank, bytes_of, lat_us, link_gbs):
-    """Critical path (ms) of every rank's op list: streams in order, events, sends -> receives."""
+def dag(ops_by_rank, ms_by_rank, bytes_of, lat_us, link_gbs, waits=None):
+    """Critical path (ms) of every rank's op list: streams in order, events, sends -> receives.
+    waits (a list, one float per rank): the time each rank's compute stream sat idle waiting
+    for a message."""
     BOP_TIER, BOP_PACK, BOP_UNPACK, BOP_SEND, BOP_RECV, BOP_RECORD, BOP_WAIT = range(7)
     G = len(ops_by_rank)
     ev = {}          # (rank, kind, axis, batch) -> time recorded
@@ -58,6 +60,8 @@ def dag(ops_by_rank, ms_by_rank, bytes_of, lat_us, link_gbs):
                     k = (axis, arg, peer)
                     if k not in sent:
                         break
+                    if waits is not None:
+                        waits[r] += max(0.0, sent[k] - t0)
                     free[r][st] = max(t0, sent[k])
                 else:
                     free[r][st] = t0 + ms[pc[r]]
@@ -78,6 +82,7 @@ def main():
     ap.add_argument("--sym", type=int, default=1)
     ap.add_argument("--lat-us", type=float, default=15.0)
     ap.add_argument("--link-gbs", type=float, default=64.0)
+    ap.add_argument("--dump", default=None, help="directory for per-G JSON dumps of the op lists and op times")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -129,7 +134,8 @@ def main():
                 offs[(r, axis)] = (off, np.where((ent >> 20) != 0, 2048, 4096))
             off, by = offs[(r, axis)]
             return int(by[off[j]:off[j + 1]].sum())
-        end = dag(ops, ms, bytes_of, a.lat_us, a.link_gbs)
+        waits = [0.0] * G
+        end = dag(ops, ms, bytes_of, a.lat_us, a.link_gbs, waits)
         end0 = dag(ops, ms, bytes_of, 0.0, 1e9)
         # the DAG with every op scaled so a rank's ops sum to its span (gaps between ops spread)
         scaled = []
@@ -148,10 +154,20 @@ def main():
                 "modelled_speedup_scaled": round(base / max(end_s), 3),
                 "tier_ms_sum": [round(float(m[o[:, 0] == 0].sum()), 4) for m, o in zip(ms, ops)],
                 "modelled_ms": round(max(end), 4), "modelled_speedup": round(base / max(end), 3),
+                "modelled_end_ms_by_rank": [round(x, 4) for x in end],
+                "modelled_message_wait_ms_by_rank": [round(x, 4) for x in waits],
                 "modelled_ms_free_links": round(max(end0), 4),
                 "link_model": {"lat_us": a.lat_us, "gbs": a.link_gbs},
                 "loopback_all_ranks_one_gpu_ms": round(loop_ms, 4), "halo_bytes_per_solve": sent}
         print(json.dumps(line), flush=True)
+        if a.dump:   # the op lists and per-op ms, for replaying schedule variants offline
+            os.makedirs(a.dump, exist_ok=True)
+            with open(os.path.join(a.dump, "split_ops_G%d_B%d_s%d.json" % (G, a.batch, a.split)), "w") as f:
+                json.dump({"G": G, "batch": a.batch, "split": a.split, "base_ms": base, "spans": spans,
+                           "ops": [o.tolist() for o in ops], "ms": [m.tolist() for m in ms],
+                           "send_bytes": {"%d,%d,%d" % (r, ax, j): bytes_of(r, ax, j) for r in range(G)
+                                          for ax in range(3) for j in range(len(_lib.box_plan(G, r,
+                                          _lib.BOXPLAN_SEND_OFF, axis=ax, **kw)) - 1)}}, f)
         ctx.close()
         torch.cuda.empty_cache()
     return 0
