@@ -243,6 +243,9 @@ def box_sharding(world, args, root, st, rstats, per_rank, autotune, torch, dist)
         "boxes_per_rank": boxes,
         "halo_batch_tiers": args.dist_batch, "halo_batch_autotune_ms": autotune,
         "halo_symmetric_fill": bool(args.dist_symmetry),
+        "halo_transport": ("peer copies through HIP IPC, device flags (GM_OPT_BOX_TRANSPORT 1)"
+                           if args.box_transport == "ipc" else "RCCL send / recv, one communicator per axis")
+                          if world > 1 else "loopback (device copies between virtual ranks)",
         "halo_bytes_sent_per_step_by_rank": sent,
         "halo_bytes_received_per_step_by_rank": recvd,
         "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank,
@@ -519,6 +522,9 @@ def main():
     ap.add_argument("--block-engine", action="store_true",
                     help="8 heaps: run the block engine (GM_OPT_SUB_INTERLEAVE 10) instead of the box engine, "
                          "sharded with halo exchanges at N > 1 (the round-3 multi-GPU path, for comparison)")
+    ap.add_argument("--box-transport", choices=("rccl", "ipc"), default="rccl",
+                    help="N>1, 8 heaps: halo messages over RCCL (default) or peer copies through HIP IPC "
+                         "(GM_OPT_BOX_TRANSPORT 1; also runs with several ranks on one GPU)")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     ap.add_argument("--watchdog", type=float, default=None,
@@ -566,6 +572,8 @@ def main():
     box = args.heaps == 8 and not args.block_engine
     if not box:
         ctx.set_option(_lib.OPT_SUB_INTERLEAVE, 10)
+    if box and args.box_transport == "ipc":
+        ctx.set_option(_lib.OPT_BOX_TRANSPORT, 1)
     if world > 1:
         uid = [None]
         if rank == 0:

@@ -24,6 +24,7 @@ OPT_DIST_OWNER = 13
 OPT_SYMMETRY = 14
 OPT_BOX_FLOW = 15
 OPT_BOX_SPLIT = 16
+OPT_BOX_TRANSPORT = 17
 BUF_DENSE_TABLE = 1
 PLAN_SHAPE, PLAN_OWN, PLAN_FILL, PLAN_SEND, PLAN_RECV, PLAN_OPS, PLAN_XDEST = 0, 1, 2, 3, 4, 5, 6
 BOXPLAN_SHAPE, BOXPLAN_BOXES, BOXPLAN_FILLS, BOXPLAN_TIER_OFF, BOXPLAN_OWN = 0, 1, 2, 3, 4

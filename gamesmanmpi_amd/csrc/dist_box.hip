@@ -45,6 +45,11 @@
 #include <algorithm>
 #include <mutex>
 
+#include <cstring>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 namespace gm {
 
 enum { BXA_NULL = 0, BXA_HALF = 1, BXA_CMP = 2 };
@@ -165,6 +170,7 @@ struct BxPlan {
     std::vector<uint32_t> srcs;                     // per box, 8 per child direction: the box read
     std::vector<uint32_t> dsts;                     // per box, 3: its halo message slots (dense_box.hip BxGroup)
     std::vector<uint32_t> send_off[3], send[3], recv_off[3], recv[3];   // per axis: per-batch offsets, entries
+    std::vector<uint64_t> peer_rmoff[3];            // per axis where this rank sends: the receiver's message offsets
     uint64_t filled = 0, received = 0;              // child reads through a transposition / from a message
 };
 
@@ -303,6 +309,14 @@ static int bx_plan(const BxShape &S, int r, BxPlan &P) {
         GM_TRY(bx_rank_reads(S, U, ub, nullptr, nullptr, roff, rent, nullptr, nullptr));
         P.send_off[a] = roff[a];
         P.send[a] = rent[a];
+        {   // where each message lands in the receiver's buffer (the IPC transport copies it there)
+            for (int b = 0; b < 3; b++)
+                if (roff[b].size() != (size_t)S.nbatch + 1) roff[b].assign(S.nbatch + 1, 0);
+            std::vector<uint64_t> eoff[3], moff[3];
+            uint64_t total;
+            bx_layout(S, roff, rent, eoff, moff, &total);
+            P.peer_rmoff[a] = moff[a];
+        }
         for (uint32_t e : P.send[a])
             if (bx_owner(S, e & 0xFFFFFu) != r) { set_error("box split: send list holds a box of another rank"); return GM_E_STATE; }
     }
@@ -412,6 +426,39 @@ __global__ void bx_hold_kernel(uint64_t ticks) {
     while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
+// IPC transport (GM_OPT_BOX_TRANSPORT 1): completion flags in device memory, monotone per
+// solve (the solve's sequence number), set by one lane with a system-scope release after the
+// stream's earlier work, and polled by one lane with system-scope acquire loads.  A wait that
+// outlasts its limit (s_memrealtime, 100 MHz) sets *err and ends, so a peer that never
+// delivers ends the solve with GM_E_COMM instead of holding the stream.
+__global__ void bx_flag_set_kernel(uint64_t *flag, uint64_t v) {
+    if (threadIdx.x) return;
+    __threadfence_system();
+    __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void bx_flag_wait_kernel(const uint64_t *flag, uint64_t want, uint64_t ticks, uint32_t *err) {
+    if (threadIdx.x) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+            atomicOr(err, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+
+// the root's code, tagged with the solve's sequence number, into every rank's flag block
+__global__ void bx_root_post_kernel(const uint8_t *slot, uint64_t *const *words, int n, uint64_t seq) {
+    if (threadIdx.x) return;
+    const uint64_t v = seq << 8 | *slot;
+    __threadfence_system();
+    for (int i = 0; i < n; i++) __hip_atomic_store(words[i], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+constexpr uint64_t BX_IPC_WAIT_TICKS = 30ull * 100000000ull;   // 30 s
+
 // ---------------------------------------------------------------------------- context
 struct BxRank {
     int rank = 0;
@@ -440,6 +487,14 @@ struct BxRank {
     std::vector<hipEvent_t> tev;
     std::vector<double> op_ms;
     float span_ms = 0;
+    // IPC transport: own flag block {arrived[3][nbatch], consumed[3], root}, error word, and the
+    // mapped buffers and flag blocks of the ranks this one sends to
+    uint64_t *flags = nullptr;
+    uint32_t *d_err = nullptr;
+    uint8_t *peer_rbuf[3] = {};
+    uint64_t *peer_flags[3] = {};
+    std::vector<uint64_t> peer_rmoff[3];
+    bool waited_consumed[3] = {};
 };
 
 struct DistBox {
@@ -456,7 +511,124 @@ struct DistBox {
     ncclComm_t comm[3] = {};
     bool own_comm[3] = {};
     uint64_t sent = 0;
+    // IPC transport
+    bool ipc = false;
+    uint64_t seq = 0;                     // solves run on this context (the flags' values)
+    std::vector<void *> opened;           // peer mappings (hipIpcCloseMemHandle on free)
+    uint64_t **d_root_words = nullptr;    // every rank's root word (the root's owner posts to all)
+    int n_root_words = 0;
 };
+
+// flag block layout: arrived[a][j] at a * nbatch + j, consumed[a] at 3 * nbatch + a, root word after
+static size_t bx_flag_words(const BxShape &S) { return 3 * (size_t)S.nbatch + 4; }
+static size_t bx_flag_consumed(const BxShape &S, int a) { return 3 * (size_t)S.nbatch + a; }
+static size_t bx_flag_root(const BxShape &S) { return 3 * (size_t)S.nbatch + 3; }
+
+// Rendezvous of the IPC transport: every rank publishes handles of its receive buffer and flag
+// block in a POSIX shared-memory segment named by the unique id and this context's prepare
+// count (identical on every rank: prepares are collective), maps the handles of the ranks it
+// needs, and rank 0 unlinks the segment once every rank has mapped.
+struct BxShmSlot {
+    hipIpcMemHandle_t rbuf, flags;
+    uint64_t ready, mapped;
+};
+
+static int bx_ipc_rendezvous(Ctx *c, DistBox *d, BxRank &R) {
+    const BxShape &S = d->S;
+    char name[96];
+    uint64_t k0, k1;
+    std::memcpy(&k0, c->uid, 8);
+    std::memcpy(&k1, c->uid + 8, 8);
+    snprintf(name, sizeof name, "/gmbx-%016llx%016llx-%d", (unsigned long long)k0, (unsigned long long)k1,
+             c->box_prepares);
+    const size_t bytes = sizeof(BxShmSlot) * (size_t)S.G;
+    const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) { set_error("shm_open(%s) failed", name); return GM_E_COMM; }
+    if (ftruncate(fd, (off_t)bytes) != 0) {
+        close(fd);
+        set_error("ftruncate of %s failed", name);
+        return GM_E_COMM;
+    }
+    void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) { set_error("mmap of %s failed", name); return GM_E_COMM; }
+    BxShmSlot *slot = (BxShmSlot *)m;
+    int rc = GM_OK;
+    auto wait_all = [&](uint64_t BxShmSlot::*field) {
+        const double t0 = now_ms();
+        for (int r = 0; r < S.G; r++)
+            while (__atomic_load_n(&(slot[r].*field), __ATOMIC_ACQUIRE) == 0) {
+                if (now_ms() - t0 > 120e3) return false;
+                usleep(200);
+            }
+        return true;
+    };
+    if (hipIpcGetMemHandle(&slot[R.rank].rbuf, R.rbuf) != hipSuccess ||
+        hipIpcGetMemHandle(&slot[R.rank].flags, R.flags) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("hipIpcGetMemHandle failed (rank %d)", R.rank);
+        rc = GM_E_COMM;
+    }
+    __atomic_store_n(&slot[R.rank].ready, rc == GM_OK ? 1 : 2, __ATOMIC_RELEASE);
+    if (rc == GM_OK && !wait_all(&BxShmSlot::ready)) {
+        set_error("IPC rendezvous %s: not every rank published its handles within 120 s", name);
+        rc = GM_E_COMM;
+    }
+    for (int r = 0; r < S.G && rc == GM_OK; r++)
+        if (__atomic_load_n(&slot[r].ready, __ATOMIC_ACQUIRE) != 1) {
+            set_error("IPC rendezvous %s: rank %d failed to publish", name, r);
+            rc = GM_E_COMM;
+        }
+    auto open = [&](const hipIpcMemHandle_t &h, void **p) {
+        if (hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        d->opened.push_back(*p);
+        return true;
+    };
+    std::vector<uint64_t *> words(S.G, nullptr);
+    for (int r = 0; r < S.G && rc == GM_OK; r++) {
+        if (r == R.rank) {
+            words[r] = R.flags + bx_flag_root(S);
+            continue;
+        }
+        void *f = nullptr;
+        if (!open(slot[r].flags, &f)) {
+            set_error("hipIpcOpenMemHandle of rank %d's flags failed", r);
+            rc = GM_E_COMM;
+            break;
+        }
+        words[r] = (uint64_t *)f + bx_flag_root(S);
+        for (int a = 0; a < S.g; a++)
+            if (!((R.rank >> a) & 1) && r == (R.rank | (1 << a))) {
+                void *b = nullptr;
+                if (!open(slot[r].rbuf, &b)) {
+                    set_error("hipIpcOpenMemHandle of rank %d's receive buffer failed", r);
+                    rc = GM_E_COMM;
+                    break;
+                }
+                R.peer_rbuf[a] = (uint8_t *)b;
+                R.peer_flags[a] = (uint64_t *)f;
+            }
+    }
+    if (rc == GM_OK) {
+        if (hipMalloc(&d->d_root_words, S.G * sizeof(uint64_t *)) != hipSuccess ||
+            hipMemcpy(d->d_root_words, words.data(), S.G * sizeof(uint64_t *), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("root word table");
+            rc = GM_E_HIP;
+        }
+        d->n_root_words = S.G;
+    }
+    __atomic_store_n(&slot[R.rank].mapped, 1, __ATOMIC_RELEASE);
+    if (R.rank == 0) {
+        (void)wait_all(&BxShmSlot::mapped);
+        shm_unlink(name);
+    }
+    munmap(m, bytes);
+    return rc;
+}
 
 static int bx_upload(const std::vector<uint32_t> &v, uint32_t **d) {
     GM_HIP(hipMalloc(d, std::max<size_t>(1, v.size()) * 4));
@@ -474,12 +646,14 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
     GM_TRY(bx_shape(box_index_of_key((uint32_t)root) >> 12, G, c->dist_batch, c->dist_symmetry, c->box_split, &d->S));
     const BxShape &S = d->S;
     d->grid_cap = box_grid_cap(c->device);
+    d->ipc = !loopback && c->box_transport == 1;
+    c->box_prepares++;
     GM_HIP(hipMalloc(&d->d_acc, 16));
     GM_HIP(hipMalloc(&d->d_root, 4));
     GM_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
     GM_HIP(hipEventCreate(&d->ev_t0));
     GM_HIP(hipEventCreate(&d->ev_t1));
-    if (!loopback) {
+    if (!loopback && !d->ipc) {
         // one communicator per axis; every rank makes the same calls in the same order
         d->comm[0] = c->comm;
         for (int a = 1; a < S.g; a++) {
@@ -527,6 +701,13 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
         for (int a = 0; a < 3; a++) {
             R.send_off[a] = P.send_off[a];
             R.recv_off[a] = P.recv_off[a];
+            R.peer_rmoff[a] = P.peer_rmoff[a];
+        }
+        if (d->ipc) {
+            GM_HIP(hipMalloc(&R.flags, bx_flag_words(S) * 8));
+            GM_HIP(hipMemset(R.flags, 0, bx_flag_words(S) * 8));
+            GM_HIP(hipMalloc(&R.d_err, 4));
+            GM_HIP(hipMemset(R.d_err, 0, 4));
         }
         for (int a = 0; a < S.g; a++)
             for (int k = 0; k < BEV_KINDS; k++) {
@@ -560,6 +741,10 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
             R.own_S = true;
         }
         for (int a = 0; a < S.g; a++) GM_HIP(hipStreamCreateWithFlags(&R.X[a], hipStreamNonBlocking));
+    }
+    if (d->ipc) {
+        GM_HIP(hipDeviceSynchronize());   // buffers zeroed before any peer can write into them
+        GM_TRY(bx_ipc_rendezvous(c, d, d->ranks[0]));
     }
     GM_HIP(hipMalloc(&d->d_owner, 1u << 20));
     GM_HIP(hipMemcpy(d->d_owner, owner.data(), 1u << 20, hipMemcpyHostToDevice));
@@ -599,9 +784,27 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
         return GM_E_STATE;
     case BOP_SEND: {
         const uint64_t o0 = R.smoff[a][j], n = R.smoff[a][j + 1] - o0;
-        // pieces of <= 1 GiB (one ncclSend above 2 GiB arrived corrupted, csrc/dist_sparse.hip)
-        for (uint64_t p = 0; p < n; p += 1ull << 30)
-            GM_NCCL(ncclSend(R.sbuf + o0 + p, std::min<uint64_t>(n - p, 1ull << 30), ncclUint8, o.peer, d->comm[a], st));
+        if (d->ipc) {
+            // the receiver's buffer must be free: it finished the previous solve's unpacks
+            if (!R.waited_consumed[a]) {
+                hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, R.peer_flags[a] + bx_flag_consumed(d->S, a),
+                                   d->seq - 1, BX_IPC_WAIT_TICKS, R.d_err);
+                R.waited_consumed[a] = true;
+            }
+            if (R.peer_rmoff[a].size() <= (size_t)j + 1 || R.peer_rmoff[a][j + 1] - R.peer_rmoff[a][j] != n) {
+                set_error("box split: message %d on axis %d has %llu bytes, the receiver expects otherwise", j, a,
+                          (unsigned long long)n);
+                return GM_E_STATE;
+            }
+            GM_HIP(hipMemcpyAsync(R.peer_rbuf[a] + R.peer_rmoff[a][j], R.sbuf + o0, n, hipMemcpyDeviceToDevice, st));
+            hipLaunchKernelGGL(bx_flag_set_kernel, dim3(1), dim3(64), 0, st, R.peer_flags[a] + (size_t)a * d->S.nbatch + j,
+                               d->seq);
+        } else {
+            // pieces of <= 1 GiB (one ncclSend above 2 GiB arrived corrupted, csrc/dist_sparse.hip)
+            for (uint64_t p = 0; p < n; p += 1ull << 30)
+                GM_NCCL(ncclSend(R.sbuf + o0 + p, std::min<uint64_t>(n - p, 1ull << 30), ncclUint8, o.peer, d->comm[a],
+                                 st));
+        }
         R.sent_bytes += n;
         d->sent += n;
         break;
@@ -617,6 +820,9 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
             }
             GM_HIP(hipMemcpyAsync(R.rbuf + o0, L.sbuf + l0, n, hipMemcpyDeviceToDevice, st));
             d->sent += n;
+        } else if (d->ipc) {   // the sender copies the message in and sets the flag
+            hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, R.flags + (size_t)a * d->S.nbatch + j, d->seq,
+                               BX_IPC_WAIT_TICKS, R.d_err);
         } else {
             for (uint64_t p = 0; p < n; p += 1ull << 30)
                 GM_NCCL(ncclRecv(R.rbuf + o0 + p, std::min<uint64_t>(n - p, 1ull << 30), ncclUint8, o.peer, d->comm[a], st));
@@ -705,6 +911,12 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
         for (int a = 0; a < d->S.g; a++) GM_HIP(hipStreamWaitEvent(R.X[a], d->ev_fork, 0));
     }
     GM_TRY(bx_enqueue(c, d, c->dist_solo, op_events));
+    if (d->ipc)   // this solve's messages are unpacked: the senders may write the next solve's
+        for (auto &R : d->ranks)
+            for (int a = 0; a < d->S.g; a++)
+                if ((R.rank >> a) & 1)
+                    hipLaunchKernelGGL(bx_flag_set_kernel, dim3(1), dim3(64), 0, R.S, R.flags + bx_flag_consumed(d->S, a),
+                                       d->seq);
     for (auto &R : d->ranks) {
         for (int a = 0; a < d->S.g; a++) {
             GM_HIP(hipEventRecord(R.ev_join[a], R.X[a]));
@@ -722,8 +934,13 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
 int dist_box_solve(Ctx *c, uint64_t root) {
     const bool loopback = c->world <= 1 && c->virtual_ranks > 1;
     const int G = loopback ? c->virtual_ranks : c->world;
-    if (!loopback && !c->comm) {
+    const bool ipc = !loopback && c->box_transport == 1;
+    if (!loopback && !ipc && !c->comm) {
         set_error("a %d-rank solve needs an RCCL communicator (gm_set_comm with a unique id)", G);
+        return GM_E_COMM;
+    }
+    if (ipc && !c->have_uid) {
+        set_error("the IPC transport needs gm_set_comm with a unique id (it names the rendezvous)");
         return GM_E_COMM;
     }
     DistBox *d = c->dist_box;
@@ -731,7 +948,7 @@ int dist_box_solve(Ctx *c, uint64_t root) {
     if (!d || d->S.G != G || d->loopback != loopback || d->S.root_hi != rh || d->want_batch != c->dist_batch ||
         d->want_sym != c->dist_symmetry || d->want_split != c->box_split ||
         (!loopback && c->adopted_dense && d->ranks[0].table != c->adopted_dense) ||
-        (!loopback && d->ranks[0].rank != c->rank)) {
+        (!loopback && d->ranks[0].rank != c->rank) || d->ipc != ipc) {
         dist_box_free(c);
         d = c->dist_box = new DistBox();
         const int rc = bx_prepare(c, d, root, G, loopback);
@@ -748,20 +965,48 @@ int dist_box_solve(Ctx *c, uint64_t root) {
     const bool solo = loopback && c->dist_solo > 0;
     const bool op_events = c->timing >= 2;
     if (solo && c->timing) hipLaunchKernelGGL(bx_hold_kernel, dim3(1), dim3(64), 0, H, (uint64_t)(20000 * 100));
+    if (ipc) {
+        d->seq++;
+        for (auto &R : d->ranks)
+            for (bool &w : R.waited_consumed) w = false;
+    }
     GM_HIP(hipEventRecord(d->ev_t0, H));
     GM_TRY(bx_run(c, d, op_events));
     GM_HIP(hipEventRecord(d->ev_t1, H));
     const double t_enq = now_ms();
-    // root record: the max over ranks of the owner's code (the others contribute 0)
+    // root record: the max over ranks of the owner's code (the others contribute 0); with the
+    // IPC transport the owner posts it, tagged with the solve's number, to every rank
     const int ro = bx_owner(d->S, rh);
-    GM_HIP(hipMemsetAsync(d->d_root, 0, 4, H));
-    for (auto &R : d->ranks)
-        if (R.rank == ro && R.table)
-            GM_HIP(hipMemcpyAsync(d->d_root, R.table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToDevice, H));
-    if (!loopback) GM_NCCL(ncclAllReduce(d->d_root, d->d_root, 1, ncclUint32, ncclMax, c->comm, H));
     uint32_t rs = 0;
-    GM_HIP(hipMemcpyAsync(&rs, d->d_root, 4, hipMemcpyDeviceToHost, H));
-    GM_HIP(hipStreamSynchronize(H));
+    if (ipc) {
+        BxRank &R = d->ranks[0];
+        if (R.rank == ro)
+            hipLaunchKernelGGL(bx_root_post_kernel, dim3(1), dim3(64), 0, H, R.table + box_index_of_key((uint32_t)root),
+                               d->d_root_words, d->n_root_words, d->seq);
+        hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, H, R.flags + bx_flag_root(d->S), d->seq << 8,
+                           BX_IPC_WAIT_TICKS, R.d_err);
+        uint64_t w = 0;
+        uint32_t err = 0;
+        GM_HIP(hipMemcpyAsync(&w, R.flags + bx_flag_root(d->S), 8, hipMemcpyDeviceToHost, H));
+        GM_HIP(hipMemcpyAsync(&err, R.d_err, 4, hipMemcpyDeviceToHost, H));
+        GM_HIP(hipStreamSynchronize(H));
+        if (err) {
+            GM_HIP(hipMemset(R.d_err, 0, 4));
+            set_error("IPC transport: a peer rank did not deliver within %llu s (solve %llu)",
+                      (unsigned long long)(BX_IPC_WAIT_TICKS / 100000000ull), (unsigned long long)d->seq);
+            return GM_E_COMM;
+        }
+        rs = (uint32_t)(w & 0xFF);
+    } else {
+        GM_HIP(hipMemsetAsync(d->d_root, 0, 4, H));
+        for (auto &R : d->ranks)
+            if (R.rank == ro && R.table)
+                GM_HIP(hipMemcpyAsync(d->d_root, R.table + box_index_of_key((uint32_t)root), 1, hipMemcpyDeviceToDevice,
+                                      H));
+        if (!loopback) GM_NCCL(ncclAllReduce(d->d_root, d->d_root, 1, ncclUint32, ncclMax, c->comm, H));
+        GM_HIP(hipMemcpyAsync(&rs, d->d_root, 4, hipMemcpyDeviceToHost, H));
+        GM_HIP(hipStreamSynchronize(H));
+    }
     const double t1 = now_ms();
     c->root_record = record_of_code((uint8_t)rs);
     uint64_t n = 1;
@@ -947,6 +1192,11 @@ void dist_box_free(Ctx *c) {
     }
     for (hipEvent_t e : {d->ev_fork, d->ev_t0, d->ev_t1})
         if (e) (void)hipEventDestroy(e);
+    for (void *q : d->opened) (void)hipIpcCloseMemHandle(q);
+    for (auto &R : d->ranks)
+        for (void *q : {(void *)R.flags, (void *)R.d_err})
+            if (q) (void)hipFree(q);
+    if (d->d_root_words) (void)hipFree(d->d_root_words);
     for (int a = 0; a < 3; a++)
         if (d->own_comm[a] && d->comm[a]) (void)ncclCommDestroy(d->comm[a]);
     for (void *q : {(void *)d->d_acc, (void *)d->d_root, (void *)d->d_owner, (void *)d->d_tables})

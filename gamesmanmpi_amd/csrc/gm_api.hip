@@ -39,6 +39,23 @@ bool trace_on() {
     return on;
 }
 
+// The communicator is made when a solve first needs it -- every rank's first sharded solve,
+// so the call is collective as RCCL requires -- and not at all for a transport that needs none
+// (the split box engine's IPC peer copies, which also run when the ranks share one GPU, where
+// RCCL refuses to make a communicator).
+int ensure_comm(Ctx *c) {
+    if (c->comm) return GM_OK;
+    if (!c->have_uid) {
+        set_error("a %d-rank solve needs gm_set_comm with a unique id", c->world);
+        return GM_E_COMM;
+    }
+    ncclUniqueId id;
+    memcpy(&id, c->uid, sizeof id);
+    GM_HIP(hipSetDevice(c->device));
+    GM_NCCL(ncclCommInitRank(&c->comm, c->world, id, c->rank));
+    return GM_OK;
+}
+
 // Best fit from the context's cache of released buffers (no more than 2x the
 // request), else hipMalloc; if that fails, release the cache and retry once.
 int dev_alloc(Ctx *c, void **p, uint64_t bytes) {
@@ -255,6 +272,10 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->box_flow = (int)v;
         c->box_flow_failed = false;   // setting it again retries the dataflow launch
         return GM_OK;
+    case GM_OPT_BOX_TRANSPORT:
+        if (v < 0 || v > 1) { set_error("GM_OPT_BOX_TRANSPORT must be 0 (RCCL) or 1 (IPC peer copies)"); return GM_E_ARG; }
+        c->box_transport = (int)v;
+        return GM_OK;
     case GM_OPT_BOX_SPLIT:
         if (v < 0 || v > 1) { set_error("box split must be 0 (halves) or 1 (comparisons)"); return GM_E_ARG; }
         c->box_split = (int)v;
@@ -339,17 +360,17 @@ int gm_set_comm(gm_ctx *h, int rank, int world, const void *uid, int bytes) {
     if (!h || world < 1 || rank < 0 || rank >= world) { set_error("bad rank/world"); return GM_E_ARG; }
     Ctx *c = &h->c;
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    if (c->dist_box) dist_box_free(c);   // its transport belongs to the previous communicator
     c->rank = rank;
     c->world = world;
-    // no uid: rank and world only.  Enough for the 8-heap box engine, whose ranks exchange
-    // nothing; the RCCL engines refuse to solve without a communicator (gm_solve)
+    c->have_uid = false;
+    // no uid: rank and world only; the sharded engines refuse to solve without one (gm_solve)
     if (!uid || bytes <= 0) return GM_OK;
     if (bytes < (int)sizeof(ncclUniqueId)) { set_error("uid must hold %d bytes", (int)sizeof(ncclUniqueId)); return GM_E_ARG; }
     if (c->device < 0) { set_error("no HIP device"); return GM_E_HIP; }
-    ncclUniqueId id;
-    memcpy(&id, uid, sizeof id);
-    GM_HIP(hipSetDevice(c->device));
-    GM_NCCL(ncclCommInitRank(&c->comm, world, id, rank));
+    static_assert(sizeof(ncclUniqueId) <= sizeof(c->uid), "unique id size");
+    memcpy(c->uid, uid, sizeof(ncclUniqueId));
+    c->have_uid = true;
     return GM_OK;
 }
 
@@ -382,9 +403,12 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     // heap counts and GM_OPT_SUB_INTERLEAVE != 20 keep the block engine's sharded path
     const bool box = !force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT &&
                      c->sub.heaps == 8 && c->sub_interleave == 20;
-    if (sharded && !box && c->world > 1 && !c->comm) {
-        set_error("a %d-rank solve of this game needs an RCCL communicator (gm_set_comm with a unique id)", c->world);
-        return GM_E_COMM;
+    if (sharded && c->virtual_ranks <= 1 && (c->world > 1 || force_dist_sparse) && !(box && c->box_transport == 1)) {
+        if (!c->have_uid) {
+            set_error("a %d-rank solve of this game needs an RCCL communicator (gm_set_comm with a unique id)", c->world);
+            return GM_E_COMM;
+        }
+        GM_TRY(ensure_comm(c));
     }
     if (sharded && !box) eng = (!force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT)
                                    ? GM_ENGINE_DIST_DENSE

@@ -84,7 +84,11 @@ struct Ctx {
 
     // multi-GPU
     int rank = 0, world = 1;
-    ncclComm_t comm = nullptr;
+    ncclComm_t comm = nullptr;   // made on first use from uid (ensure_comm): a transport that needs none never makes it
+    bool have_uid = false;
+    unsigned char uid[128] = {};
+    int box_transport = 0;       // split box engine across processes: 0 RCCL, 1 peer copies over IPC (GM_OPT_BOX_TRANSPORT)
+    int box_prepares = 0;        // split box contexts built so far (names the IPC rendezvous of each)
     int virtual_ranks = 1;   // >1: run that many ranks inside this context (loopback transport)
     hipStream_t comm_stream = nullptr;
     int dist_batch = 4;      // sharded dense path: tiers per halo exchange
@@ -215,6 +219,7 @@ double now_ms();
 int dev_alloc(Ctx *c, void **p, uint64_t bytes);
 void dev_free(Ctx *c, void *p);
 bool trace_on();
+int ensure_comm(Ctx *c);   // the RCCL communicator of gm_set_comm's unique id (collective on first use)
 
 }  // namespace gm
 

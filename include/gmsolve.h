@@ -117,9 +117,17 @@ enum {
                                capacity from the occupancy API).  A dataflow solve whose waits time out
                                is redone with tier launches, and the context keeps tier launches until
                                this option is set again; gm_stats_t.flow_fallbacks counts them. */
-    GM_OPT_BOX_SPLIT = 16   /* box engine at N > 1 (gm_box_plan): 0 (default) = split heaps in halves
+    GM_OPT_BOX_SPLIT = 16,  /* box engine at N > 1 (gm_box_plan): 0 (default) = split heaps in halves
                                (rank bit a = [box coordinate >= half]); 1 = tier-balanced comparisons
                                (rank bit = [c_x < c_y], ties by a rule that keeps every axis one-way) */
+    GM_OPT_BOX_TRANSPORT = 17  /* box engine at N > 1, one process per rank: how a halo message
+                               travels.  0 (default) = ncclSend / ncclRecv on per-axis communicators;
+                               1 = peer copies into the receiver's buffer, mapped through HIP IPC
+                               (hipIpcGetMemHandle, exchanged through a POSIX shared-memory segment
+                               named by the unique id), with completion flags in device memory that
+                               stream-ordered kernels set and poll (30 s limit, then GM_E_COMM).  1
+                               also runs when the ranks share one GPU, where RCCL refuses; all the
+                               ranks of one node.  Set on every rank before the first solve. */
 };
 
 /* Buffer roles for gm_adopt_buffer. */
@@ -186,8 +194,11 @@ int gm_expand_host(gm_ctx *ctx, uint64_t key, uint64_t *children, int cap,
  * reference passes to Process (solver_launcher.py:47-52, :132-140).  With
  * world = 1 and a uid, a one-rank communicator is created: with GM_OPT_ENGINE =
  * GM_ENGINE_DIST_SPARSE the hash-sharded engine then runs its RCCL transport on
- * one GPU (self send/recv, all-gather, all-reduce), which tests use. */
-/* uid NULL sets rank and world only, with no communicator; every sharded engine then refuses to
+ * one GPU (self send/recv, all-gather, all-reduce), which tests use.
+ * The communicator itself is made by the first solve that needs one (collective: every rank's
+ * first sharded solve), not by this call, so ranks whose transport needs none -- the split box
+ * engine with GM_OPT_BOX_TRANSPORT 1, possibly several ranks on one GPU -- never make it.
+ * uid NULL sets rank and world only, with no communicator; every sharded engine then refuses to
  * solve (GM_E_COMM). */
 int gm_comm_unique_id(void *uid, int bytes);
 int gm_set_comm(gm_ctx *ctx, int rank, int world, const void *uid, int bytes);

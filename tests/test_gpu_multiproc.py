@@ -1,6 +1,7 @@
-"""Multi-process RCCL runs of the sharded engines: one process per GPU, as bench.py
-runs them at N > 1.  Needs at least two visible devices (the
-driver's 8-GPU node); on a one-GPU box every test here skips.
+"""Multi-process runs of the sharded engines: one process per rank, as bench.py runs them at
+N > 1.  The RCCL tests need one visible device per rank (the driver's
+8-GPU node) and skip on a one-GPU box; the box engine's IPC-transport tests run there too,
+their ranks sharing the GPU (RCCL refuses two ranks on one device).
 
 * dense, 8 heaps (config 5's engine, csrc/dist_box.hip): every box on one rank, per-axis
   split communicators, each batch's halo boxes as ncclSend / ncclRecv on the exchange
@@ -38,7 +39,9 @@ def _rank_main(rank, world, phase, game, params, opts):
     import torch.distributed as tdist
     from gamesmanmpi_amd import Context, _lib
     tdist.init_process_group("gloo", rank=rank, world_size=world)   # MASTER_* from the parent
-    ctx = Context(game, params, device=rank)
+    opts = dict(opts)
+    shared = opts.pop("share_gpus", False)   # ranks round-robin over the visible GPUs (IPC transport)
+    ctx = Context(game, params, device=rank % _lib.lib().gm_device_count() if shared else rank)
     phase("unique id")
     uid = [None]
     if rank == 0:
@@ -48,16 +51,19 @@ def _rank_main(rank, world, phase, game, params, opts):
     tdist.broadcast_object_list(uid, src=0)
     phase("communicator")
     ctx.set_comm(rank, world, uid[0])
-    opts = dict(opts)
     root = opts.pop("root", None)
     qkeys = opts.pop("query_keys", None)
+    solves = opts.pop("solves", 1)
     for k, v in opts.items():
         ctx.set_option(getattr(_lib, "OPT_" + k.upper()), v)
-    phase("solve")
-    n, rec = ctx.solve(ctx.initial() if root is None else root)
-    phase("digest")
-    d, m = ctx.digest()
-    res = {"rank": rank, "n": n, "rec": rec, "digest": d, "m": m,
+    digests = []
+    for i in range(solves):
+        phase("solve %d" % i)
+        n, rec = ctx.solve(ctx.initial() if root is None else root)
+        phase("digest %d" % i)
+        digests.append(ctx.digest())
+    d, m = digests[-1]
+    res = {"rank": rank, "n": n, "rec": rec, "digest": d, "m": m, "digests": digests,
            "tiers": [int(x) for x in ctx.tier_counts()], "exchanged": ctx.stats()["exchanged_bytes"]}
     if qkeys is not None:
         res["query"] = [int(x) for x in ctx.query(np.array(qkeys, dtype=np.uint64))]
@@ -65,11 +71,15 @@ def _rank_main(rank, world, phase, game, params, opts):
     return res
 
 
-def _run(world, game, params, opts=None):
+def _run(world, game, params, opts=None, shared=False):
     """Every rank in its own process; on a timeout, an error or a dead rank, every
     rank is terminated then killed and the failure names each rank's last phase
-    (tests/mp_ranks.py)."""
-    if _devices() < world:
+    (tests/mp_ranks.py).  shared: the ranks may share GPUs (the box engine's IPC transport)."""
+    if shared:
+        if _devices() < 1:
+            pytest.skip("needs a GPU")
+        opts = dict(opts or {}, share_gpus=True)
+    elif _devices() < world:
         pytest.skip("needs %d GPUs (one process per GPU over RCCL)" % world)
     import socket
     from mp_ranks import run_ranks
@@ -132,3 +142,45 @@ def test_sparse_rccl_matches_oracle_digest(world, name, game, params):
     assert _summed(res) == (ref["digest"], ref["positions"])
     if "per_ply" in ref:
         assert all(r["tiers"] == ref["per_ply"] for r in res)
+
+
+def _oracle_box(oracle, root):
+    ok, orec = oracle.solve(SUB, (8,), root=root)
+    return ok, orec, (digest(ok, orec), len(ok))
+
+
+@pytest.mark.parametrize("world,root,batch,sym", [(2, 0x33557777, 1, 1), (3, 0x33557777, 2, 0),
+                                                  (4, 0x23457777, 1, 1)])
+def test_box_ipc_ranks_vs_oracle(oracle, world, root, batch, sym):
+    """The split box engine across PROCESSES with the IPC transport (GM_OPT_BOX_TRANSPORT 1):
+    each process one rank, the halo messages peer-copied into the receiver's buffer mapped
+    through hipIpcOpenMemHandle, completion flags set and polled by stream-ordered kernels --
+    runs on a one-GPU box, the ranks sharing the GPU (RCCL refuses that).  Three solves in a
+    row (the flags' sequence numbers and the back-pressure on reused buffers): the summed
+    digests equal the C oracle's every time, every rank reports the root record, and every
+    sampled key is answered by exactly one rank (gm_query)."""
+    from gamesmanmpi_amd import _lib
+    ok, orec, want = _oracle_box(oracle, root)
+    sample = ok[:: max(1, len(ok) // 3000)]
+    res = _run(world, SUB, (8,), {"box_transport": 1, "root": root, "dist_batch": batch, "dist_symmetry": sym,
+                                  "solves": 3, "query_keys": sample.tolist()}, shared=True)
+    for i in range(3):
+        assert (sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1), sum(r["digests"][i][1] for r in res)) == want
+    rec = orec[np.searchsorted(ok, root)]
+    assert all(r["rec"] == rec for r in res)
+    q = np.array([r["query"] for r in res])
+    answered = q != _lib.REC_UNSOLVED
+    assert (answered.sum(axis=0) == 1).all()
+    assert np.array_equal(np.where(answered, q, 0).sum(axis=0), orec[:: max(1, len(ok) // 3000)])
+    assert sum(r["exchanged"] for r in res) > 0
+
+
+def test_box_ipc_ranks_2_32_matches_oracle_digest():
+    """Config 5 at full size over 4 processes with the IPC transport (sharing one GPU on a
+    one-GPU box): the summed digests equal the committed oracle digest, twice."""
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["subtract_8"]
+    res = _run(4, SUB, (8,), {"box_transport": 1, "dist_batch": 1, "solves": 2}, shared=True)
+    for i in range(2):
+        assert (sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1),
+                sum(r["digests"][i][1] for r in res)) == (ref["digest"], 1 << 32)
+    assert all(r["n"] == 1 << 32 and r["rec"] == ref["root_record"] for r in res)
