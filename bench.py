@@ -525,6 +525,10 @@ def main():
     ap.add_argument("--box-transport", choices=("rccl", "ipc"), default="rccl",
                     help="N>1, 8 heaps: halo messages over RCCL (default) or peer copies through HIP IPC "
                          "(GM_OPT_BOX_TRANSPORT 1; also runs with several ranks on one GPU)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N>1 rehearsal on a one-GPU box: every rank on device 0, bench.py's collectives over "
+                         "gloo, the box engine's halos over the IPC transport (RCCL refuses two ranks on one "
+                         "GPU), no side configs; the ranks share the GPU, so the time is not a multi-GPU result")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     ap.add_argument("--watchdog", type=float, default=None,
@@ -536,6 +540,11 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    global COLL_DEV
+    if args.rehearse_one_gpu:
+        if args.heaps != 8 or args.block_engine:
+            ap.error("--rehearse-one-gpu runs the 8-heap box engine")
+        local, COLL_DEV, args.no_toot, args.box_transport = 0, "cpu", True, "ipc"
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
 
@@ -561,7 +570,10 @@ def main():
     import torch.distributed as dist
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from gamesmanmpi_amd import Context, _lib
 
@@ -772,6 +784,8 @@ def main():
             "host_enqueue_ms_per_step_rank0": enqueue_ms / max(1, args.steps),
             "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank},
         "cpu_baseline": None,
+        "rehearsal": ("--rehearse-one-gpu: %d ranks sharing ONE GPU (gloo for bench.py's collectives, IPC transport "
+                      "for the halos); not a multi-GPU measurement" % world if args.rehearse_one_gpu else None),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], live = cpu_baseline(args.cpu_heaps)
