@@ -151,13 +151,14 @@ def dist_plan(heaps, world, rank, what, axis=0, batch=4, slots=4, symmetry=1, ow
     return off[:n_off.value], data[:n_data.value]
 
 
-def box_plan(world, rank, what, root=0xFFFFFFFF, axis=0, batch=4, symmetry=1, split=0, loopback=0):
+def box_plan(world, rank, what, root=0xFFFFFFFF, axis=0, batch=4, symmetry=1, split=0, loopback=0, transport=0):
     """gm_box_plan -> uint32 numpy array (host only, no GPU): rank `rank`'s part of the split
-    box solve (csrc/dist_box.hip).  batch / symmetry / split: GM_OPT_DIST_BATCH,
-    GM_OPT_DIST_SYMMETRY, GM_OPT_BOX_SPLIT; loopback: the op list of a virtual rank."""
+    box solve (csrc/dist_box.hip).  batch / symmetry / split / transport: GM_OPT_DIST_BATCH,
+    GM_OPT_DIST_SYMMETRY, GM_OPT_BOX_SPLIT, GM_OPT_BOX_TRANSPORT; loopback: the op list of a
+    virtual rank."""
     import numpy as np
     L = lib()
-    opts = (ctypes.c_int32 * 4)(batch, symmetry, split, loopback)
+    opts = (ctypes.c_int32 * 5)(batch, symmetry, split, loopback, transport)
     n = ctypes.c_uint64()
     check(L.gm_box_plan(root, world, rank, opts, what, axis, None, 0, ctypes.byref(n)))
     out = np.zeros(max(1, n.value), dtype=np.uint32)

@@ -553,9 +553,12 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
 // rank needs is also written, from the same registers, to its slot in the halo message (the
 // whole box, or only its two top layers along an A heap, rows compacted as box_pack_kernel
 // packs them), so no pack launch sits between the tier launches.
-template <bool SHARD>
-__device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, const BxGroup &G, const uint32_t *s,
-                                         uint32_t lane) {
+// DIRECT (loopback and IPC transports): the box goes straight to its slot in the receiving
+// rank's own table (peer p0..p2 by axis, slot kind << 28 | axis << 26), rows where they lie,
+// so the receiver needs no unpack.
+template <bool SHARD, bool DIRECT = false>
+__device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, uint8_t *p0, uint8_t *p1, uint8_t *p2,
+                                         const BxGroup &G, const uint32_t *s, uint32_t lane) {
     __amdgpu_buffer_rsrc_t w[2];
 #pragma unroll
     for (int k = 0; k < 2; k++)
@@ -584,7 +587,21 @@ __device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, const BxG
         }
         __builtin_amdgcn_raw_buffer_store_b128(o[0], w[0], 16u * m, 0, GM_BOX_STORE_CPOL);
         __builtin_amdgcn_raw_buffer_store_b128(o[1], w[1], 16u * m, 0, GM_BOX_STORE_CPOL);
-        if constexpr (SHARD) {
+        if constexpr (SHARD && DIRECT) {
+#pragma unroll
+            for (int k = 0; k < 2; k++)
+#pragma unroll
+                for (int e = 0; e < 3; e++) {
+                    const uint32_t d = dst[k][e], kind = d >> 28, ax = (d >> 26) & 3u;
+                    if (!kind) continue;   // uniform
+                    uint8_t *pb = ax == 0 ? p0 : (ax == 1 ? p1 : p2);
+                    const __amdgpu_buffer_rsrc_t wp =
+                        __builtin_amdgcn_make_buffer_rsrc(pb + ((uint64_t)G.box[k] << 12), 0, 4096u, 0x00020000);
+                    const uint32_t a = (m >> (2u * ((kind - 1u) & 3u))) & 3u;
+                    if (kind == 5 || a >= 2u)
+                        __builtin_amdgcn_raw_buffer_store_b128(o[k], wp, 16u * m, 0, GM_BOX_STORE_CPOL);
+                }
+        } else if constexpr (SHARD) {
 #pragma unroll
             for (int k = 0; k < 2; k++)
 #pragma unroll
@@ -622,13 +639,14 @@ __device__ unsigned long long bx_trace_acc[8];
 // workgroups of an XCD side by side, so neighbouring groups share child boxes in its L2.
 // SHARD: one rank of the sharded solve: its own box list, with a fill code
 // per box saying where each child box is read from.
-template <bool SHARD>
+template <bool SHARD, bool DIRECT = false>
 __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__restrict__ table,
                                                                      const uint32_t *__restrict__ boxes,
                                                                      const uint32_t *__restrict__ fills,
                                                                      const uint32_t *__restrict__ srcs,
                                                                      const uint32_t *__restrict__ dsts,
-                                                                     uint8_t *__restrict__ msg, uint32_t nbox) {
+                                                                     uint8_t *__restrict__ msg, uint8_t *p0, uint8_t *p1,
+                                                                     uint8_t *p2, uint32_t nbox) {
     __shared__ __attribute__((aligned(16))) uint32_t lds[BX_LDS];
     uint32_t *s = lds + BX_PAD;
     const uint32_t lane = threadIdx.x;
@@ -678,7 +696,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 #if GM_BOX_TRACE
         BX_STAMP(tt[3]);
 #endif
-        bx_store<SHARD>(table, msg, G, s, ln);
+        bx_store<SHARD, DIRECT>(table, msg, p0, p1, p2, G, s, ln);
         BX_LDS_ORDER();
 #if GM_BOX_TRACE
         BX_STAMP(tt[4]);
@@ -850,7 +868,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
 #if GM_BOX_FLOW_TRACE
         BX_RT(ft[3]);
 #endif
-        bx_store<false>(table, nullptr, G, s, ln);
+        bx_store<false>(table, nullptr, nullptr, nullptr, nullptr, G, s, ln);
         BX_LDS_ORDER();
         // publish: the wave's sc1 stores done, then one lane stores each box's flag sc1
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -866,6 +884,118 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_flow_kernel(uint8_t *__r
             o[5] = G.box[0] | ((unsigned long long)blockIdx.x << 32);
         }
 #endif
+        j += K;
+        if (j >= qn) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Split solve as dataflow (dist_box.hip, GM_OPT_BOX_FLOW 1 with virtual ranks or the IPC
+// transport): each rank's whole box-tier chain in one launch, as box_flow_kernel, and the
+// exchange folded into the same hand-off -- a group stores its halo boxes straight into the
+// receiving rank's table (bx_store DIRECT), drains, and then stores those boxes' flags in the
+// RECEIVER's flag array with a system-scope release; the receiver's groups wait on their child
+// boxes' flags in their own array whoever stored them.  So a box starts when its own children
+// are in, across ranks as within one.  One launch may carry several ranks (virtual ranks on
+// one GPU: workgroup w runs rank w % n, all of them resident together, which the waits need);
+// every rank's epoch is the solve's sequence number.
+// per rank (gm_internal.hpp BxSplitFlowDesc): table, box list, fill words, sources, halo
+// slots, group queues (as BxFlow::groups), its flag array (per box id: the epoch of the solve
+// that stored it -- own boxes and the halo boxes other ranks store into its table), and per
+// axis the receiving rank's table and flag array (null where this rank sends nothing)
+typedef BxSplitFlowDesc BxSplitFlow;
+
+// SYS: some rank stores into this one's flags from another GPU (IPC transport across devices):
+// system-scope polls, which bypass the L2; else agent scope, as box_flow_kernel
+template <bool SYS>
+__device__ __forceinline__ bool bx_split_wait(const uint32_t *flag, uint32_t src, uint32_t ep, uint32_t *err,
+                                              uint64_t timeout, uint32_t lane) {
+    auto ld = [&](uint32_t b) {
+        if (b == ~0u) return ep;
+        return SYS ? __hip_atomic_load(&flag[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                   : __hip_atomic_load(&flag[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (__all(ld(src) == ep)) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (__all(ld(src) == ep)) return true;
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+            if (lane == 0) atomicOr(err, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(GM_BOX_FLOW_SLEEP);
+    }
+}
+
+template <bool SYS>
+__global__ __launch_bounds__(64, GM_BOX_WAVES) void box_split_flow_kernel(const BxSplitFlow *__restrict__ ranks,
+                                                                           uint32_t nranks, uint32_t ep, uint32_t *err,
+                                                                           uint64_t timeout) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BX_LDS];
+    uint32_t *s = lds + BX_PAD;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t r = blockIdx.x % nranks, k = blockIdx.x / nranks;
+    const uint32_t nk = (gridDim.x - r + nranks - 1u) / nranks;   // workgroups of rank r
+    const uint32_t q = k & 7u, K = (nk - q + 7u) >> 3;
+    // the descriptor is re-read (scalar loads) where each field is used instead of held in
+    // SGPRs across the group: held, its pointers overflow the SGPR budget of the fold and walk
+    auto fd = [&]() {
+        const BxSplitFlow *p = ranks + r;
+        asm volatile("" : "+s"(p));
+        return p;
+    };
+    const uint32_t qn = fd()->qlen[q];
+    uint32_t j = k >> 3;
+    if (j >= qn) return;
+    const BxLaneC L = bx_lane_consts(lane);
+    s[BX_PITCH * lane + BX_Z] = 0;
+    bx_u32x4 R[BX_NLOAD];
+    for (;;) {
+        BxGroup G;
+        uint32_t rec;
+        {
+            const BxSplitFlow *F = fd();
+            rec = F->groups[F->qbase[q] + j];
+            G = bx_group_rec<true>(F->boxes, F->fills, F->srcs, rec, lane);
+            const uint32_t src = lane < 16u ? bx_child_src<true>(G, lane >> 3, lane & 7u) : ~0u;
+            if (!bx_split_wait<SYS>(F->flag, src, ep, err, timeout, lane)) return;
+        }
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_I);
+        bx_issue<true, GM_BOX_FLOW_LOAD_CPOL>(fd()->table, G, lane, R);
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_F);
+        bx_fold<true>(s, G, ln, R);
+        BX_LDS_ORDER();
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_W);
+        bx_walk(s, ln, L);
+        __builtin_amdgcn_s_setprio(GM_BOX_PRIO_S);
+        {
+            const BxSplitFlow *F = fd();
+            const uint32_t i = (rec & 0x7FFFFFFFu) + (lane >> 2);   // the halo slots, needed from here on
+            if (lane < 8 && (lane & 3u) < 3u && (lane < 4 || (rec >> 31))) G.dstv = F->dsts[3 * i + (lane & 3u)];
+            bx_store<true, true>(F->table, nullptr, F->ptab[0], F->ptab[1], F->ptab[2], G, s, ln);
+        }
+        BX_LDS_ORDER();
+        // publish (the hand-off of box_flow_kernel): the wave's stores are written through
+        // (GM_BOX_STORE_CPOL, own and halo rows alike) and done, then the flags -- own boxes in
+        // this rank's array, halo boxes also in the receiver's.  No release fence: on this chip
+        // it would write back the XCD's whole L2 per group (measured: 4x slower solves)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        {
+            const BxSplitFlow *F = fd();
+            if (lane == 0) {
+                __hip_atomic_store(&F->flag[G.box[0]], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (G.valid[1]) __hip_atomic_store(&F->flag[G.box[1]], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane < 8 && (lane & 3u) < 3u && (G.dstv >> 28)) {
+                const uint32_t ax = (G.dstv >> 26) & 3u, b = (lane >> 2) ? G.box[1] : G.box[0];
+                uint32_t *pf = ax == 0 ? F->pflag[0] : (ax == 1 ? F->pflag[1] : F->pflag[2]);
+                if (SYS) __hip_atomic_store(&pf[b], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                else __hip_atomic_store(&pf[b], ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         j += K;
         if (j >= qn) break;
     }
@@ -956,8 +1086,27 @@ static int box_resident(const void *kernel, int device, size_t dyn) {
 int box_grid_cap(int device) { return box_resident((const void *)box_tier_kernel<true>, device, 0); }
 
 void box_launch_tier_split(uint32_t grid, uint8_t *table, const uint32_t *boxes, const uint32_t *fills,
-                           const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint32_t nbox, hipStream_t s) {
-    hipLaunchKernelGGL(box_tier_kernel<true>, dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs, dsts, msg, nbox);
+                           const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint8_t *const *peers,
+                           uint32_t nbox, hipStream_t s) {
+    if (peers)
+        hipLaunchKernelGGL((box_tier_kernel<true, true>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs, dsts,
+                           nullptr, peers[0], peers[1], peers[2], nbox);
+    else
+        hipLaunchKernelGGL((box_tier_kernel<true, false>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs, dsts,
+                           msg, nullptr, nullptr, nullptr, nbox);
+}
+void box_launch_split_flow(uint32_t grid, const void *ranks, uint32_t nranks, uint32_t ep, uint32_t *err,
+                           uint64_t timeout_ticks, bool sys, hipStream_t s) {
+    if (sys)
+        hipLaunchKernelGGL(box_split_flow_kernel<true>, dim3(grid), dim3(64), 0, s, (const BxSplitFlow *)ranks, nranks,
+                           ep, err, timeout_ticks);
+    else
+        hipLaunchKernelGGL(box_split_flow_kernel<false>, dim3(grid), dim3(64), 0, s, (const BxSplitFlow *)ranks, nranks,
+                           ep, err, timeout_ticks);
+}
+int box_split_flow_resident(int device) {
+    return std::min(box_resident((const void *)box_split_flow_kernel<true>, device, 0),
+                    box_resident((const void *)box_split_flow_kernel<false>, device, 0));
 }
 void box_launch_digest(const uint8_t *table, const uint32_t *boxes, uint64_t nbox, uint64_t root,
                        unsigned long long *acc, hipStream_t s) {
@@ -1151,7 +1300,8 @@ static int box_launch_tiers(Ctx *c, DenseBox *d) {
         const uint32_t grid = std::max<uint32_t>(8u, std::min<uint32_t>(ng, (uint32_t)d->grid_cap));
         hipLaunchKernelGGL(box_tier_kernel<false>, dim3(grid), dim3(64), 0, c->stream, d->table,
                            d->d_boxes + d->tier_off[t], (const uint32_t *)nullptr, (const uint32_t *)nullptr,
-                           (const uint32_t *)nullptr, (uint8_t *)nullptr, nb);
+                           (const uint32_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr,
+                           (uint8_t *)nullptr, nb);
     }
     GM_HIP(hipGetLastError());
     return GM_OK;

@@ -169,8 +169,8 @@ struct BxPlan {
     std::vector<uint32_t> boxes, fills, tier_off;   // computed boxes by box-tier (Hilbert order), fill words
     std::vector<uint32_t> srcs;                     // per box, 8 per child direction: the box read
     std::vector<uint32_t> dsts;                     // per box, 3: its halo message slots (dense_box.hip BxGroup)
+    std::vector<uint32_t> dsts_direct;              // the same slots as kind << 28 | axis << 26 (direct writes)
     std::vector<uint32_t> send_off[3], send[3], recv_off[3], recv[3];   // per axis: per-batch offsets, entries
-    std::vector<uint64_t> peer_rmoff[3];            // per axis where this rank sends: the receiver's message offsets
     uint64_t filled = 0, received = 0;              // child reads through a transposition / from a message
 };
 
@@ -309,14 +309,6 @@ static int bx_plan(const BxShape &S, int r, BxPlan &P) {
         GM_TRY(bx_rank_reads(S, U, ub, nullptr, nullptr, roff, rent, nullptr, nullptr));
         P.send_off[a] = roff[a];
         P.send[a] = rent[a];
-        {   // where each message lands in the receiver's buffer (the IPC transport copies it there)
-            for (int b = 0; b < 3; b++)
-                if (roff[b].size() != (size_t)S.nbatch + 1) roff[b].assign(S.nbatch + 1, 0);
-            std::vector<uint64_t> eoff[3], moff[3];
-            uint64_t total;
-            bx_layout(S, roff, rent, eoff, moff, &total);
-            P.peer_rmoff[a] = moff[a];
-        }
         for (uint32_t e : P.send[a])
             if (bx_owner(S, e & 0xFFFFFu) != r) { set_error("box split: send list holds a box of another rank"); return GM_E_STATE; }
     }
@@ -332,6 +324,7 @@ static int bx_plan(const BxShape &S, int r, BxPlan &P) {
     std::vector<uint32_t> idx(1u << 20, ~0u);
     for (size_t i = 0; i < P.boxes.size(); i++) idx[P.boxes[i]] = (uint32_t)i;
     P.dsts.assign(3 * P.boxes.size(), 0);
+    P.dsts_direct.assign(3 * P.boxes.size(), 0);
     for (int a = 0; a < S.g; a++)
         for (size_t k = 0; k < P.send[a].size(); k++) {
             const uint32_t e = P.send[a][k], i = idx[e & 0xFFFFFu], code = e >> 20;
@@ -343,6 +336,7 @@ static int bx_plan(const BxShape &S, int r, BxPlan &P) {
                 return GM_E_STATE;
             }
             d[slot] = (code ? code : 5u) << 28 | (uint32_t)(eoff[a][k] >> 11);
+            P.dsts_direct[3 * (size_t)i + slot] = (code ? code : 5u) << 28 | (uint32_t)a << 26;
         }
     return GM_OK;
 }
@@ -365,7 +359,8 @@ static uint32_t bx_cnt(const std::vector<uint32_t> &off, int j) {
 // the ops: profiles/r05b_*), then its tiers; after the tier that ends message jj's range, on
 // each axis where it is the lower side, the exchange stream X[a] waits for that tier and sends
 // (the tier kernel wrote the message itself: no pack op).
-static void bx_build_ops(const BxShape &S, int r, const BxPlan &P, bool loopback, std::vector<BxOp> &ops) {
+static void bx_build_ops(const BxShape &S, int r, const BxPlan &P, bool loopback, bool direct, std::vector<BxOp> &ops) {
+    (void)loopback;
     auto op = [&](int kind, int axis, int ev, bool on_x, int arg, int peer) {
         ops.push_back(BxOp{(uint8_t)kind, (uint8_t)axis, (uint8_t)ev, (uint8_t)on_x, arg, peer});
     };
@@ -375,24 +370,25 @@ static void bx_build_ops(const BxShape &S, int r, const BxPlan &P, bool loopback
         bool any = false;
         for (int a = 0; a < S.g; a++) {
             if (!((r >> a) & 1) || !bx_cnt(P.recv_off[a], j)) continue;
-            const int lower = r ^ (1 << a);
-            if (loopback) op(BOP_WAIT, a, BEV_PACKED, false, j, lower);
-            op(BOP_RECV, a, 0, false, j, lower);
+            op(BOP_RECV, a, 0, false, j, r ^ (1 << a));
             any = true;
         }
-        if (any) op(BOP_UNPACK, 0, 0, false, j, r);
+        if (any && !direct) op(BOP_UNPACK, 0, 0, false, j, r);   // direct: the sender wrote the table
         for (int t = j * B; t < std::min(T, j * B + B); t++) {
             op(BOP_TIER, 0, 0, false, t, r);
             for (int jj = 0; jj < S.nbatch; jj++) {
                 if (S.hi[jj] != t || S.lo[jj] > S.hi[jj]) continue;
+                bool recorded = false;
                 for (int a = 0; a < S.g; a++) {
                     if (((r >> a) & 1) || !bx_cnt(P.send_off[a], jj)) continue;
-                    op(BOP_RECORD, a, BEV_DONE, false, jj, r);
+                    if (direct) {   // the boxes are in the receiver's table: signal it, from S
+                        op(BOP_SEND, a, 0, false, jj, r | (1 << a));
+                        continue;
+                    }
+                    if (!recorded) op(BOP_RECORD, 0, BEV_DONE, false, jj, r);   // one event per tier
+                    recorded = true;
                     op(BOP_WAIT, a, BEV_DONE, true, jj, r);
-                    if (loopback)
-                        op(BOP_RECORD, a, BEV_PACKED, true, jj, r);
-                    else
-                        op(BOP_SEND, a, 0, true, jj, r | (1 << a));
+                    op(BOP_SEND, a, 0, true, jj, r | (1 << a));
                 }
             }
         }
@@ -449,6 +445,19 @@ __global__ void bx_flag_wait_kernel(const uint64_t *flag, uint64_t want, uint64_
     }
 }
 
+__global__ void bx_flags_set_kernel(uint64_t *f0, uint64_t *f1, uint64_t *f2, uint64_t v) {
+    if (threadIdx.x) return;
+    __threadfence_system();
+    if (f0) __hip_atomic_store(f0, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (f1) __hip_atomic_store(f1, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (f2) __hip_atomic_store(f2, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void bx_mark_kernel(uint32_t *flag, const uint32_t *boxes, uint32_t n, uint32_t ep) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flag[boxes[i]] = ep;
+}
+
 // the root's code, tagged with the solve's sequence number, into every rank's flag block
 __global__ void bx_root_post_kernel(const uint8_t *slot, uint64_t *const *words, int n, uint64_t seq) {
     if (threadIdx.x) return;
@@ -488,13 +497,18 @@ struct BxRank {
     std::vector<double> op_ms;
     float span_ms = 0;
     // IPC transport: own flag block {arrived[3][nbatch], consumed[3], root}, error word, and the
-    // mapped buffers and flag blocks of the ranks this one sends to
+    // mapped flag blocks of the ranks this one sends to (their tables: peer_table)
     uint64_t *flags = nullptr;
     uint32_t *d_err = nullptr;
-    uint8_t *peer_rbuf[3] = {};
     uint64_t *peer_flags[3] = {};
-    std::vector<uint64_t> peer_rmoff[3];
-    bool waited_consumed[3] = {};
+    uint8_t *peer_table[3] = {};          // direct writes: the table of the rank this one sends to, per axis
+    // GM_OPT_BOX_FLOW 1 (split dataflow): group queues, per-box flags (own and received boxes),
+    // the receivers' flag arrays, the boxes it receives (solo timing marks them stored)
+    uint32_t *d_groups = nullptr, *boxflag = nullptr, *d_recv_boxes = nullptr;
+    uint32_t qbase[8] = {}, qlen[8] = {};
+    uint32_t *peer_boxflag[3] = {};
+    uint32_t n_recv_boxes = 0;
+    int sig_done = 0;                     // direct: batches signalled so far in this solve (+1)
 };
 
 struct DistBox {
@@ -513,6 +527,13 @@ struct DistBox {
     uint64_t sent = 0;
     // IPC transport
     bool ipc = false;
+    bool direct = false;                  // halo boxes written straight into the receiver's table (loopback, IPC)
+    bool flow = false;                    // GM_OPT_BOX_FLOW 1: each rank's chain one dataflow launch
+    BxSplitFlowDesc *d_desc = nullptr;    // per rank (index = position in `ranks`)
+    uint32_t *d_flow_err = nullptr;
+    int flow_grid = 0;
+    uint64_t flow_ticks = 0;
+    bool flow_sys = false;                // a peer on another GPU: system-scope flag polls and stores
     uint64_t seq = 0;                     // solves run on this context (the flags' values)
     std::vector<void *> opened;           // peer mappings (hipIpcCloseMemHandle on free)
     uint64_t **d_root_words = nullptr;    // every rank's root word (the root's owner posts to all)
@@ -524,13 +545,14 @@ static size_t bx_flag_words(const BxShape &S) { return 3 * (size_t)S.nbatch + 4;
 static size_t bx_flag_consumed(const BxShape &S, int a) { return 3 * (size_t)S.nbatch + a; }
 static size_t bx_flag_root(const BxShape &S) { return 3 * (size_t)S.nbatch + 3; }
 
-// Rendezvous of the IPC transport: every rank publishes handles of its receive buffer and flag
-// block in a POSIX shared-memory segment named by the unique id and this context's prepare
+// Rendezvous of the IPC transport: every rank publishes handles of its table (the allocation
+// holding it and the table's offset there: an adopted torch tensor may sit inside a larger
+// block) and its flag block in a POSIX shared-memory segment named by the unique id and this context's prepare
 // count (identical on every rank: prepares are collective), maps the handles of the ranks it
 // needs, and rank 0 unlinks the segment once every rank has mapped.
 struct BxShmSlot {
-    hipIpcMemHandle_t rbuf, flags;
-    uint64_t ready, mapped;
+    hipIpcMemHandle_t table, flags, boxflag;
+    uint64_t table_off, has_table, has_boxflag, pci, ready, mapped;
 };
 
 static int bx_ipc_rendezvous(Ctx *c, DistBox *d, BxRank &R) {
@@ -563,11 +585,35 @@ static int bx_ipc_rendezvous(Ctx *c, DistBox *d, BxRank &R) {
             }
         return true;
     };
-    if (hipIpcGetMemHandle(&slot[R.rank].rbuf, R.rbuf) != hipSuccess ||
-        hipIpcGetMemHandle(&slot[R.rank].flags, R.flags) != hipSuccess) {
+    slot[R.rank].has_table = R.table ? 1 : 0;
+    if (R.table) {
+        hipDeviceptr_t base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)R.table) != hipSuccess ||
+            hipIpcGetMemHandle(&slot[R.rank].table, (void *)base) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("hipIpcGetMemHandle of rank %d's table failed", R.rank);
+            rc = GM_E_COMM;
+        }
+        slot[R.rank].table_off = (uint64_t)((uint8_t *)R.table - (uint8_t *)base);
+    }
+    if (rc == GM_OK && hipIpcGetMemHandle(&slot[R.rank].flags, R.flags) != hipSuccess) {
         (void)hipGetLastError();
-        set_error("hipIpcGetMemHandle failed (rank %d)", R.rank);
+        set_error("hipIpcGetMemHandle of rank %d's flags failed", R.rank);
         rc = GM_E_COMM;
+    }
+    slot[R.rank].has_boxflag = R.boxflag ? 1 : 0;
+    if (rc == GM_OK && R.boxflag && hipIpcGetMemHandle(&slot[R.rank].boxflag, R.boxflag) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("hipIpcGetMemHandle of rank %d's box flags failed", R.rank);
+        rc = GM_E_COMM;
+    }
+    {
+        int bus = 0, dev = 0, dom = 0;
+        (void)hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, c->device);
+        (void)hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, c->device);
+        (void)hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, c->device);
+        slot[R.rank].pci = (uint64_t)(uint32_t)dom << 32 | (uint64_t)(uint32_t)bus << 8 | (uint64_t)(uint32_t)dev;
     }
     __atomic_store_n(&slot[R.rank].ready, rc == GM_OK ? 1 : 2, __ATOMIC_RELEASE);
     if (rc == GM_OK && !wait_all(&BxShmSlot::ready)) {
@@ -602,15 +648,33 @@ static int bx_ipc_rendezvous(Ctx *c, DistBox *d, BxRank &R) {
         words[r] = (uint64_t *)f + bx_flag_root(S);
         for (int a = 0; a < S.g; a++)
             if (!((R.rank >> a) & 1) && r == (R.rank | (1 << a))) {
+                R.peer_flags[a] = (uint64_t *)f;
+                if (!slot[r].has_table) continue;   // a rank without boxes receives nothing
                 void *b = nullptr;
-                if (!open(slot[r].rbuf, &b)) {
-                    set_error("hipIpcOpenMemHandle of rank %d's receive buffer failed", r);
+                if (!open(slot[r].table, &b)) {
+                    set_error("hipIpcOpenMemHandle of rank %d's table failed", r);
                     rc = GM_E_COMM;
                     break;
                 }
-                R.peer_rbuf[a] = (uint8_t *)b;
-                R.peer_flags[a] = (uint64_t *)f;
+                R.peer_table[a] = (uint8_t *)b + slot[r].table_off;
+                if (slot[r].has_boxflag) {
+                    void *bf = nullptr;
+                    if (!open(slot[r].boxflag, &bf)) {
+                        set_error("hipIpcOpenMemHandle of rank %d's box flags failed", r);
+                        rc = GM_E_COMM;
+                        break;
+                    }
+                    R.peer_boxflag[a] = (uint32_t *)bf;
+                }
             }
+    }
+    if (rc == GM_OK && d->flow) {   // ranks sharing this GPU run their dataflow launches side by side
+        int share = 0;
+        for (int r = 0; r < S.G; r++) {
+            share += slot[r].pci == slot[R.rank].pci;
+            d->flow_sys = d->flow_sys || slot[r].pci != slot[R.rank].pci;
+        }
+        d->flow_grid = std::max(8, (d->flow_grid / std::max(1, share)) & ~7);
     }
     if (rc == GM_OK) {
         if (hipMalloc(&d->d_root_words, S.G * sizeof(uint64_t *)) != hipSuccess ||
@@ -647,6 +711,18 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
     const BxShape &S = d->S;
     d->grid_cap = box_grid_cap(c->device);
     d->ipc = !loopback && c->box_transport == 1;
+    d->direct = loopback || d->ipc;
+    d->flow = d->direct && c->box_flow == 1;
+    if (d->flow) {
+        d->flow_grid = box_split_flow_resident(c->device) & ~7;
+        if (d->flow_grid < 8) { set_error("split dataflow kernel: no resident workgroups"); return GM_E_HIP; }
+        // 200 ms of s_memrealtime (100 MHz) for virtual ranks, which start together; 30 s across
+        // processes, which reach their launches at their own pace
+        d->flow_ticks = d->ipc ? BX_IPC_WAIT_TICKS : (uint64_t)(200.0 * 1e5);
+        if (const char *tm = getenv("GM_BOX_FLOW_TIMEOUT_MS")) d->flow_ticks = (uint64_t)(std::max(0.001, atof(tm)) * 1e5);
+        GM_HIP(hipMalloc(&d->d_flow_err, 4));
+        GM_HIP(hipMemset(d->d_flow_err, 0, 4));
+    }
     c->box_prepares++;
     GM_HIP(hipMalloc(&d->d_acc, 16));
     GM_HIP(hipMalloc(&d->d_root, 4));
@@ -678,30 +754,31 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
         GM_TRY(bx_upload(P.boxes, &R.d_boxes));
         GM_TRY(bx_upload(P.fills, &R.d_fills));
         GM_TRY(bx_upload(P.srcs, &R.d_srcs));
-        GM_TRY(bx_upload(P.dsts, &R.d_dsts));
+        GM_TRY(bx_upload(d->direct ? P.dsts_direct : P.dsts, &R.d_dsts));
         std::vector<uint64_t> seoff[3], reoff[3];
         bx_layout(S, P.send_off, P.send, seoff, R.smoff, &R.sbytes);
         bx_layout(S, P.recv_off, P.recv, reoff, R.rmoff, &R.rbytes);
         for (uint64_t bytes : {R.sbytes, R.rbytes})
             if ((bytes >> 11) >= (1u << 28)) { set_error("halo buffer of %llu bytes", (unsigned long long)bytes); return GM_E_STATE; }
-        GM_HIP(hipMalloc(&R.sbuf, std::max<uint64_t>(16, R.sbytes)));
-        GM_HIP(hipMalloc(&R.rbuf, std::max<uint64_t>(16, R.rbytes)));
-        std::vector<uint32_t> ue, uo;
-        R.unp_off.assign(1, 0);
-        for (int j = 0; j < S.nbatch; j++) {
-            for (int a = 0; a < S.g; a++)
-                for (uint32_t k = P.recv_off[a][j]; k < P.recv_off[a][j + 1]; k++) {
-                    ue.push_back(P.recv[a][k]);
-                    uo.push_back((uint32_t)(reoff[a][k] >> 11));
-                }
-            R.unp_off.push_back((uint32_t)ue.size());
+        if (!d->direct) {   // messages: a send buffer the tier kernel fills, a receive buffer to unpack
+            GM_HIP(hipMalloc(&R.sbuf, std::max<uint64_t>(16, R.sbytes)));
+            GM_HIP(hipMalloc(&R.rbuf, std::max<uint64_t>(16, R.rbytes)));
+            std::vector<uint32_t> ue, uo;
+            R.unp_off.assign(1, 0);
+            for (int j = 0; j < S.nbatch; j++) {
+                for (int a = 0; a < S.g; a++)
+                    for (uint32_t k = P.recv_off[a][j]; k < P.recv_off[a][j + 1]; k++) {
+                        ue.push_back(P.recv[a][k]);
+                        uo.push_back((uint32_t)(reoff[a][k] >> 11));
+                    }
+                R.unp_off.push_back((uint32_t)ue.size());
+            }
+            GM_TRY(bx_upload(ue, &R.d_unp_ent));
+            GM_TRY(bx_upload(uo, &R.d_unp_eoff));
         }
-        GM_TRY(bx_upload(ue, &R.d_unp_ent));
-        GM_TRY(bx_upload(uo, &R.d_unp_eoff));
         for (int a = 0; a < 3; a++) {
             R.send_off[a] = P.send_off[a];
             R.recv_off[a] = P.recv_off[a];
-            R.peer_rmoff[a] = P.peer_rmoff[a];
         }
         if (d->ipc) {
             GM_HIP(hipMalloc(&R.flags, bx_flag_words(S) * 8));
@@ -709,13 +786,40 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
             GM_HIP(hipMalloc(&R.d_err, 4));
             GM_HIP(hipMemset(R.d_err, 0, 4));
         }
-        for (int a = 0; a < S.g; a++)
-            for (int k = 0; k < BEV_KINDS; k++) {
-                R.ev[k][a].assign(S.nbatch, nullptr);
-                for (int j = 0; j < S.nbatch; j++)
-                    if (bx_cnt(P.send_off[a], j)) GM_HIP(hipEventCreateWithFlags(&R.ev[k][a][j], hipEventDisableTiming));
+        // one completion event per batch the rank sends (slot 0: all axes share it)
+        R.ev[BEV_DONE][0].assign(S.nbatch, nullptr);
+        for (int j = 0; j < S.nbatch; j++) {
+            bool any = false;
+            for (int a = 0; a < S.g; a++) any |= bx_cnt(P.send_off[a], j) != 0;
+            if (any) GM_HIP(hipEventCreateWithFlags(&R.ev[BEV_DONE][0][j], hipEventDisableTiming));
+        }
+        bx_build_ops(S, R.rank, P, loopback, d->direct, R.ops);
+        if (d->flow) {   // queues as the one-GPU dataflow launch's: per XCD run x, tier after tier
+            std::vector<uint32_t> q[8];
+            for (size_t t = 0; t + 1 < R.tier_off.size(); t++) {
+                const uint32_t o0 = R.tier_off[t], nb = R.tier_off[t + 1] - o0, ng = (nb + 1) / 2;
+                const uint32_t qq = ng >> 3, rr = ng & 7u;
+                for (uint32_t x = 0; x < 8; x++) {
+                    const uint32_t g0 = x * qq + std::min(x, rr), g1 = g0 + qq + (x < rr ? 1u : 0u);
+                    for (uint32_t g = g0; g < g1; g++)
+                        q[x].push_back((o0 + 2 * g) | ((2 * g + 1 < nb) ? 1u << 31 : 0u));
+                }
             }
-        bx_build_ops(S, R.rank, P, loopback, R.ops);
+            std::vector<uint32_t> all;
+            for (int x = 0; x < 8; x++) {
+                R.qbase[x] = (uint32_t)all.size();
+                R.qlen[x] = (uint32_t)q[x].size();
+                all.insert(all.end(), q[x].begin(), q[x].end());
+            }
+            GM_TRY(bx_upload(all, &R.d_groups));
+            GM_HIP(hipMalloc(&R.boxflag, (1u << 20) * 4));
+            GM_HIP(hipMemset(R.boxflag, 0, (1u << 20) * 4));
+            std::vector<uint32_t> rb;
+            for (int a = 0; a < S.g; a++)
+                for (uint32_t e : P.recv[a]) rb.push_back(e & 0xFFFFFu);
+            R.n_recv_boxes = (uint32_t)rb.size();
+            GM_TRY(bx_upload(rb, &R.d_recv_boxes));
+        }
         for (auto &e : R.ev_join) GM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         // the table: a rank without boxes holds none
         if (!loopback && c->adopted_dense) {
@@ -742,9 +846,40 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
         }
         for (int a = 0; a < S.g; a++) GM_HIP(hipStreamCreateWithFlags(&R.X[a], hipStreamNonBlocking));
     }
+    if (loopback)   // direct writes: a lower rank's tier kernel stores its halo boxes into the upper's table
+        for (auto &R : d->ranks)
+            for (int a = 0; a < S.g; a++)
+                if (!((R.rank >> a) & 1) && (R.rank | (1 << a)) < G) {
+                    R.peer_table[a] = d->ranks[R.rank | (1 << a)].table;
+                    R.peer_boxflag[a] = d->ranks[R.rank | (1 << a)].boxflag;
+                }
     if (d->ipc) {
         GM_HIP(hipDeviceSynchronize());   // buffers zeroed before any peer can write into them
         GM_TRY(bx_ipc_rendezvous(c, d, d->ranks[0]));
+    }
+    if (d->flow) {
+        std::vector<BxSplitFlowDesc> desc(d->ranks.size());
+        for (size_t i = 0; i < d->ranks.size(); i++) {
+            const BxRank &R = d->ranks[i];
+            BxSplitFlowDesc &D = desc[i];
+            D.table = R.table;
+            D.boxes = R.d_boxes;
+            D.fills = R.d_fills;
+            D.srcs = R.d_srcs;
+            D.dsts = R.d_dsts;
+            D.groups = R.d_groups;
+            for (int x = 0; x < 8; x++) {
+                D.qbase[x] = R.qbase[x];
+                D.qlen[x] = R.qlen[x];
+            }
+            D.flag = R.boxflag;
+            for (int a = 0; a < 3; a++) {
+                D.ptab[a] = R.peer_table[a];
+                D.pflag[a] = R.peer_boxflag[a];
+            }
+        }
+        GM_HIP(hipMalloc(&d->d_desc, desc.size() * sizeof(BxSplitFlowDesc)));
+        GM_HIP(hipMemcpy(d->d_desc, desc.data(), desc.size() * sizeof(BxSplitFlowDesc), hipMemcpyHostToDevice));
     }
     GM_HIP(hipMalloc(&d->d_owner, 1u << 20));
     GM_HIP(hipMemcpy(d->d_owner, owner.data(), 1u << 20, hipMemcpyHostToDevice));
@@ -768,7 +903,7 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
             const uint32_t grid = std::max<uint32_t>(8u, std::min<uint32_t>(ng, (uint32_t)d->grid_cap));
             const size_t o0 = R.tier_off[j];
             box_launch_tier_split(grid, R.table, R.d_boxes + o0, R.d_fills + o0, R.d_srcs + 8 * o0, R.d_dsts + 3 * o0,
-                                  R.sbuf, nb, st);
+                                  R.sbuf, d->direct ? R.peer_table : nullptr, nb, st);
         }
         break;
     }
@@ -784,21 +919,19 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
         return GM_E_STATE;
     case BOP_SEND: {
         const uint64_t o0 = R.smoff[a][j], n = R.smoff[a][j + 1] - o0;
-        if (d->ipc) {
-            // the receiver's buffer must be free: it finished the previous solve's unpacks
-            if (!R.waited_consumed[a]) {
-                hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, R.peer_flags[a] + bx_flag_consumed(d->S, a),
-                                   d->seq - 1, BX_IPC_WAIT_TICKS, R.d_err);
-                R.waited_consumed[a] = true;
+        if (d->direct) {   // the tier kernels wrote the boxes into the receiver's table: tell it
+            if (R.sig_done != j + 1) {   // one signal per batch for every axis (bx_advance groups them)
+                R.sig_done = j + 1;
+                if (d->ipc) {
+                    uint64_t *f[3] = {nullptr, nullptr, nullptr};
+                    for (size_t k = i; k < R.ops.size() && R.ops[k].kind == BOP_SEND && R.ops[k].arg == j; k++)
+                        f[R.ops[k].axis] = R.peer_flags[R.ops[k].axis] + (size_t)R.ops[k].axis * d->S.nbatch + j;
+                    hipLaunchKernelGGL(bx_flags_set_kernel, dim3(1), dim3(64), 0, st, f[0], f[1], f[2], d->seq);
+                } else {
+                    GM_HIP(hipEventRecord(R.ev[BEV_DONE][0][j], st));
+                    R.recorded[BEV_DONE][0] = j + 1;
+                }
             }
-            if (R.peer_rmoff[a].size() <= (size_t)j + 1 || R.peer_rmoff[a][j + 1] - R.peer_rmoff[a][j] != n) {
-                set_error("box split: message %d on axis %d has %llu bytes, the receiver expects otherwise", j, a,
-                          (unsigned long long)n);
-                return GM_E_STATE;
-            }
-            GM_HIP(hipMemcpyAsync(R.peer_rbuf[a] + R.peer_rmoff[a][j], R.sbuf + o0, n, hipMemcpyDeviceToDevice, st));
-            hipLaunchKernelGGL(bx_flag_set_kernel, dim3(1), dim3(64), 0, st, R.peer_flags[a] + (size_t)a * d->S.nbatch + j,
-                               d->seq);
         } else {
             // pieces of <= 1 GiB (one ncclSend above 2 GiB arrived corrupted, csrc/dist_sparse.hip)
             for (uint64_t p = 0; p < n; p += 1ull << 30)
@@ -806,19 +939,19 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
                                  st));
         }
         R.sent_bytes += n;
-        d->sent += n;
+        if (!d->loopback) d->sent += n;   // loopback counts each message once, at its receive
         break;
     }
     case BOP_RECV: {
         const uint64_t o0 = R.rmoff[a][j], n = R.rmoff[a][j + 1] - o0;
-        if (d->loopback) {
+        if (d->loopback) {   // direct writes: the boxes are in place once the sender's tier passed
             const BxRank &L = d->ranks[o.peer];
-            const uint64_t l0 = L.smoff[a][j];
-            if (L.smoff[a][j + 1] - l0 != n || bx_cnt(L.send_off[a], j) != bx_cnt(R.recv_off[a], j)) {
+            if (L.smoff[a][j + 1] - L.smoff[a][j] != n || bx_cnt(L.send_off[a], j) != bx_cnt(R.recv_off[a], j)) {
                 set_error("box split: rank %d's message %d on axis %d disagrees with rank %d's", o.peer, j, a, R.rank);
                 return GM_E_STATE;
             }
-            GM_HIP(hipMemcpyAsync(R.rbuf + o0, L.sbuf + l0, n, hipMemcpyDeviceToDevice, st));
+            // solo timing: the other ranks' boxes are taken as written (the previous full solve's)
+            if (!solo) GM_HIP(hipStreamWaitEvent(st, L.ev[BEV_DONE][0][j], 0));
             d->sent += n;
         } else if (d->ipc) {   // the sender copies the message in and sets the flag
             hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, R.flags + (size_t)a * d->S.nbatch + j, d->seq,
@@ -829,16 +962,12 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
         }
         break;
     }
-    case BOP_RECORD:
-        GM_HIP(hipEventRecord(R.ev[o.ev][a][j], st));
-        R.recorded[o.ev][a] = j + 1;
+    case BOP_RECORD:   // a tier's completion (one event per rank and batch: slot 0)
+        GM_HIP(hipEventRecord(R.ev[BEV_DONE][0][j], st));
         break;
-    case BOP_WAIT: {
-        if (solo && o.peer != R.rank) break;   // solo timing: the other ranks' messages are taken as arrived
-        const BxRank &P = d->loopback ? d->ranks[o.peer] : R;
-        GM_HIP(hipStreamWaitEvent(st, P.ev[o.ev][a][j], 0));
+    case BOP_WAIT:
+        GM_HIP(hipStreamWaitEvent(st, R.ev[BEV_DONE][0][j], 0));
         break;
-    }
     }
     if (timed) GM_HIP(hipEventRecord(R.tev[2 * i + 1], st));
     return GM_OK;
@@ -851,8 +980,7 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
 static int bx_advance(Ctx *c, DistBox *d, BxRank &R, bool solo, bool op_events, bool *progress) {
     while (R.pc < R.ops.size()) {
         const BxOp &o = R.ops[R.pc];
-        if (d->loopback && !solo && o.kind == BOP_WAIT && o.peer != R.rank && d->ranks[o.peer].recorded[o.ev][o.axis] <= o.arg)
-            break;
+        if (d->loopback && !solo && o.kind == BOP_RECV && d->ranks[o.peer].recorded[BEV_DONE][0] <= o.arg) break;
         GM_TRY(bx_exec(c, d, R, R.pc, solo, op_events));
         R.pc++;
         *progress = true;
@@ -868,6 +996,7 @@ static int bx_advance(Ctx *c, DistBox *d, BxRank &R, bool solo, bool op_events, 
 static int bx_enqueue(Ctx *c, DistBox *d, int solo, bool op_events) {
     for (auto &R : d->ranks) {
         R.pc = 0;
+        R.sig_done = 0;
         for (auto &k : R.recorded)
             for (int &x : k) x = 0;
         if (op_events && R.tev.size() != 2 * R.ops.size()) {
@@ -910,7 +1039,41 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
         if (R.S != H) GM_HIP(hipStreamWaitEvent(R.S, d->ev_fork, 0));
         for (int a = 0; a < d->S.g; a++) GM_HIP(hipStreamWaitEvent(R.X[a], d->ev_fork, 0));
     }
-    GM_TRY(bx_enqueue(c, d, c->dist_solo, op_events));
+    if (d->ipc)   // the ranks this one writes into finished reading the previous solve's halos
+        for (auto &R : d->ranks)
+            for (int a = 0; a < d->S.g; a++)
+                if (R.peer_flags[a])
+                    hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, R.S,
+                                       R.peer_flags[a] + bx_flag_consumed(d->S, a), d->seq - 1, BX_IPC_WAIT_TICKS, R.d_err);
+    if (d->flow) {
+        // one launch: every virtual rank together (co-resident), a solo rank alone (its received
+        // boxes marked stored: the previous full solve's stand in), or this process's rank
+        const uint32_t ep = (uint32_t)d->seq;
+        if (d->loopback && c->dist_solo > 0) {
+            const int r = c->dist_solo - 1;
+            if (r >= (int)d->ranks.size()) { set_error("dist_solo out of range"); return GM_E_ARG; }
+            BxRank &R = d->ranks[r];
+            if (R.n_recv_boxes)
+                hipLaunchKernelGGL(bx_mark_kernel, dim3((R.n_recv_boxes + 255) / 256), dim3(256), 0, R.S, R.boxflag,
+                                   (const uint32_t *)R.d_recv_boxes, R.n_recv_boxes, ep);
+            box_launch_split_flow((uint32_t)d->flow_grid, d->d_desc + r, 1, ep, d->d_flow_err, d->flow_ticks, false, R.S);
+        } else if (d->loopback) {
+            const uint32_t n = (uint32_t)d->ranks.size();
+            box_launch_split_flow(std::max<uint32_t>(8 * n, (uint32_t)d->flow_grid / n * n), d->d_desc, n, ep,
+                                  d->d_flow_err, d->flow_ticks, false, d->ranks[0].S);
+        } else {
+            box_launch_split_flow((uint32_t)d->flow_grid, d->d_desc, 1, ep, d->d_flow_err, d->flow_ticks, d->flow_sys,
+                                  d->ranks[0].S);
+        }
+        for (auto &R : d->ranks) R.sent_bytes = 0;
+        d->sent = 0;
+        for (auto &R : d->ranks)
+            for (int a = 0; a < d->S.g; a++)
+                for (int j = 0; j < d->S.nbatch; j++)
+                    if (!d->loopback || !c->dist_solo) d->sent += R.smoff[a][j + 1] - R.smoff[a][j];
+    } else {
+        GM_TRY(bx_enqueue(c, d, c->dist_solo, op_events));
+    }
     if (d->ipc)   // this solve's messages are unpacked: the senders may write the next solve's
         for (auto &R : d->ranks)
             for (int a = 0; a < d->S.g; a++)
@@ -948,7 +1111,7 @@ int dist_box_solve(Ctx *c, uint64_t root) {
     if (!d || d->S.G != G || d->loopback != loopback || d->S.root_hi != rh || d->want_batch != c->dist_batch ||
         d->want_sym != c->dist_symmetry || d->want_split != c->box_split ||
         (!loopback && c->adopted_dense && d->ranks[0].table != c->adopted_dense) ||
-        (!loopback && d->ranks[0].rank != c->rank) || d->ipc != ipc) {
+        (!loopback && d->ranks[0].rank != c->rank) || d->ipc != ipc || d->flow != ((loopback || ipc) && c->box_flow == 1)) {
         dist_box_free(c);
         d = c->dist_box = new DistBox();
         const int rc = bx_prepare(c, d, root, G, loopback);
@@ -963,13 +1126,9 @@ int dist_box_solve(Ctx *c, uint64_t root) {
     // caller's stream (bx_hold_kernel), so every op is queued before the GPU reaches it and the
     // rank's span and per-op times hold no host enqueue gaps
     const bool solo = loopback && c->dist_solo > 0;
-    const bool op_events = c->timing >= 2;
+    const bool op_events = c->timing >= 2 && !(d->flow);   // a dataflow solve is one op
     if (solo && c->timing) hipLaunchKernelGGL(bx_hold_kernel, dim3(1), dim3(64), 0, H, (uint64_t)(20000 * 100));
-    if (ipc) {
-        d->seq++;
-        for (auto &R : d->ranks)
-            for (bool &w : R.waited_consumed) w = false;
-    }
+    if (ipc || d->flow) d->seq++;   // the flags' value of this solve (IPC transport, dataflow epochs)
     GM_HIP(hipEventRecord(d->ev_t0, H));
     GM_TRY(bx_run(c, d, op_events));
     GM_HIP(hipEventRecord(d->ev_t1, H));
@@ -1006,6 +1165,16 @@ int dist_box_solve(Ctx *c, uint64_t root) {
         if (!loopback) GM_NCCL(ncclAllReduce(d->d_root, d->d_root, 1, ncclUint32, ncclMax, c->comm, H));
         GM_HIP(hipMemcpyAsync(&rs, d->d_root, 4, hipMemcpyDeviceToHost, H));
         GM_HIP(hipStreamSynchronize(H));
+    }
+    if (d->flow) {
+        uint32_t ferr = 0;
+        GM_HIP(hipMemcpy(&ferr, d->d_flow_err, 4, hipMemcpyDeviceToHost));
+        if (ferr) {
+            GM_HIP(hipMemset(d->d_flow_err, 0, 4));
+            set_error("split dataflow: a box waited longer than %.0f ms for its child boxes (solve %llu)",
+                      d->flow_ticks / 1e5, (unsigned long long)d->seq);
+            return GM_E_STATE;
+        }
     }
     const double t1 = now_ms();
     c->root_record = record_of_code((uint8_t)rs);
@@ -1061,7 +1230,7 @@ int dist_box_solve(Ctx *c, uint64_t root) {
                 }
             if (ran && first < R.ops.size()) GM_HIP(hipEventElapsedTime(&R.span_ms, R.tev[2 * first], R.tev[2 * last + 1]));
         }
-        c->stats.kernel_launches = launches;
+        c->stats.kernel_launches = d->flow ? 1 : launches;
     }
     return GM_OK;
 }
@@ -1197,6 +1366,11 @@ void dist_box_free(Ctx *c) {
         for (void *q : {(void *)R.flags, (void *)R.d_err})
             if (q) (void)hipFree(q);
     if (d->d_root_words) (void)hipFree(d->d_root_words);
+    for (auto &R : d->ranks)
+        for (void *q : {(void *)R.d_groups, (void *)R.boxflag, (void *)R.d_recv_boxes})
+            if (q) (void)hipFree(q);
+    for (void *q : {(void *)d->d_desc, (void *)d->d_flow_err})
+        if (q) (void)hipFree(q);
     for (int a = 0; a < 3; a++)
         if (d->own_comm[a] && d->comm[a]) (void)ncclCommDestroy(d->comm[a]);
     for (void *q : {(void *)d->d_acc, (void *)d->d_root, (void *)d->d_owner, (void *)d->d_tables})
@@ -1217,6 +1391,7 @@ int dist_box_plan(uint64_t root, int world, int rank, const int32_t *opts, int w
     const int fill = opts ? (int)opts[1] : dflt.dist_symmetry;
     const int split = opts ? (int)opts[2] : dflt.box_split;
     const int loopback = opts ? (int)opts[3] : 0;
+    const int transport = opts ? (int)opts[4] : 0;
     BxShape S;
     GM_TRY(bx_shape(box_index_of_key((uint32_t)root) >> 12, world, batch, fill, split, &S));
     if (rank < 0 || rank >= world) { set_error("bad rank %d of %d", rank, world); return GM_E_ARG; }
@@ -1266,7 +1441,7 @@ int dist_box_plan(uint64_t root, int world, int rank, const int32_t *opts, int w
         case GM_BOXPLAN_RECV_OFF: v = P.recv_off[axis]; break;
         case GM_BOXPLAN_OPS: {
             std::vector<BxOp> ops;
-            bx_build_ops(S, rank, P, loopback != 0, ops);
+            bx_build_ops(S, rank, P, loopback != 0, loopback != 0 || transport == 1, ops);
             for (const BxOp &o : ops) {
                 v.push_back(o.kind);
                 v.push_back(o.axis);

@@ -146,8 +146,21 @@ void dense_box_free(Ctx *c);
 // shared with the split box engine (dist_box.hip)
 uint64_t box_hilbert(uint32_t box);
 int box_grid_cap(int device);
+void box_launch_split_flow(uint32_t grid, const void *ranks, uint32_t nranks, uint32_t ep, uint32_t *err,
+                           uint64_t timeout_ticks, bool sys, hipStream_t s);
+int box_split_flow_resident(int device);
+// the split dataflow launch's per-rank descriptor (dense_box.hip BxSplitFlow), filled by dist_box.hip
+struct BxSplitFlowDesc {
+    uint8_t *table;
+    const uint32_t *boxes, *fills, *srcs, *dsts, *groups;
+    uint32_t qbase[8], qlen[8];
+    uint32_t *flag;
+    uint8_t *ptab[3];
+    uint32_t *pflag[3];
+};
 void box_launch_tier_split(uint32_t grid, uint8_t *table, const uint32_t *boxes, const uint32_t *fills,
-                           const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint32_t nbox, hipStream_t s);
+                           const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint8_t *const *peers,
+                           uint32_t nbox, hipStream_t s);
 void box_launch_digest(const uint8_t *table, const uint32_t *boxes, uint64_t nbox, uint64_t root,
                        unsigned long long *acc, hipStream_t s);
 void box_launch_query(const uint8_t *const *tables, const uint8_t *owner, uint64_t root, const uint64_t *keys,

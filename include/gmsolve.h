@@ -302,7 +302,7 @@ int gm_dist_plan(int heaps, int world, int rank, const int32_t *opts, int what, 
  * computed, or received from that rank in the batch's halo message.  Box ids pack the box
  * coordinates (heap i >> 2 for heaps 0-3 at bits 2i, heap j >> 1 for heaps 4-7 at bits
  * 8 + 3 (j - 4)).  `opts` = {GM_OPT_DIST_BATCH, GM_OPT_DIST_SYMMETRY, GM_OPT_BOX_SPLIT, loopback op
- * list 0/1} values, NULL = defaults.  `axis` selects the axis of SEND / RECV items.
+ * list 0/1, GM_OPT_BOX_TRANSPORT} values (5 int32), NULL = defaults.  `axis` selects the axis of SEND / RECV items.
  *   GM_BOXPLAN_SHAPE     {world, axes, box-tiers, batch, batches, split, fill} then per axis a = 0..2
  *                        {kind (0 none, 1 half, 2 comparison), heap d | x, threshold | y, free-heap mask}
  *   GM_BOXPLAN_BOXES     the boxes this rank computes, by box-tier (GM_BOXPLAN_TIER_OFF)

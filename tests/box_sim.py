@@ -62,7 +62,7 @@ def tier(b):
     return sum(coords(b))
 
 
-def load_plan(world, rank, root=FULL, batch=4, symmetry=1, split=0):
+def load_plan(world, rank, root=FULL, batch=4, symmetry=1, split=0, transport=0):
     kw = dict(root=root, batch=batch, symmetry=symmetry, split=split)
     P = {"rank": rank}
     sh = _lib.box_plan(world, rank, _lib.BOXPLAN_SHAPE, **kw).astype(np.int64)
@@ -79,7 +79,8 @@ def load_plan(world, rank, root=FULL, batch=4, symmetry=1, split=0):
                           _lib.box_plan(world, rank, _lib.BOXPLAN_SEND, axis=a, **kw).astype(np.int64)))
         P["recv"].append((_lib.box_plan(world, rank, _lib.BOXPLAN_RECV_OFF, axis=a, **kw).astype(np.int64),
                           _lib.box_plan(world, rank, _lib.BOXPLAN_RECV, axis=a, **kw).astype(np.int64)))
-    P["ops"] = _lib.box_plan(world, rank, _lib.BOXPLAN_OPS, **kw).astype(np.int64).reshape(-1, 6)
+    P["ops"] = _lib.box_plan(world, rank, _lib.BOXPLAN_OPS, transport=transport, **kw).astype(np.int64).reshape(-1, 6)
+    P["direct"] = transport == 1   # the IPC transport: the sender's tier kernel writes the receiver's table
     return P
 
 
@@ -246,12 +247,15 @@ def simulate(P, seed=0):
         last = {}
         for i, (kind, axis, ev, on_x, arg, peer) in enumerate(p["ops"].tolist()):
             streams.setdefault((r, axis) if on_x else (r, "S"), deque()).append(i)
+            # one completion event per rank and batch, shared by the axes (dist_box.hip: slot 0)
             if kind == BOP_RECORD:
-                last[(ev, axis, arg)] = (r, i)
+                last[(ev, arg)] = (r, i)
             elif kind == BOP_WAIT:
                 if peer != r:
                     raise SimError("RCCL mode waits on another rank's event")
-                bound[(r, i)] = last.get((ev, axis, arg))
+                if (ev, arg) not in last:
+                    raise SimError("rank %d waits on batch %d's event before any record of it" % (r, arg))
+                bound[(r, i)] = last[(ev, arg)]
     p2p = {}
     cnt = defaultdict(int)
     for r, p in enumerate(P):
@@ -321,6 +325,8 @@ def simulate(P, seed=0):
                 raise SimError("axis %d message %d: rank %d expects other entries than rank %d sends" %
                                (axis, arg, r, peer))
             arrived[r][(axis, arg)] = ent
+            if p["direct"]:   # no unpack: the boxes are in the table once the flag is seen
+                have[r][ent >> 20, ent & 0xFFFFF] = True
         elif kind == BOP_UNPACK:
             # one launch for every message of the batch
             for a in range(3):

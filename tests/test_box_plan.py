@@ -185,6 +185,17 @@ def test_schedule_is_deadlock_free_and_race_free(world, root, split):
         assert S.simulate(P, seed=seed)
 
 
+@pytest.mark.parametrize("world,root", [(2, 0x33337777), (4, 0x23457777), (8, FULL)])
+def test_ipc_schedule_is_deadlock_free_and_race_free(world, root):
+    """The IPC transport's lists (GM_OPT_BOX_TRANSPORT 1): no pack or unpack -- the lower rank's
+    tier kernel writes each halo box into the upper rank's table, the send is the completion
+    flag after that tier, the receive the wait for it -- under the same simulator."""
+    P = S.plans(world, root, transport=1)
+    assert not any((p["ops"][:, 0] == S.BOP_UNPACK).any() for p in P)
+    for seed in range(2):
+        assert S.simulate(P, seed=seed)
+
+
 def _mutate(P, rank, pred, action="drop", shift=3):
     Q = [dict(p) for p in P]
     ops = Q[rank]["ops"].tolist()

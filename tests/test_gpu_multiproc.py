@@ -184,3 +184,17 @@ def test_box_ipc_ranks_2_32_matches_oracle_digest():
         assert (sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1),
                 sum(r["digests"][i][1] for r in res)) == (ref["digest"], 1 << 32)
     assert all(r["n"] == 1 << 32 and r["rec"] == ref["root_record"] for r in res)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_box_ipc_dataflow_ranks_vs_oracle(oracle, world):
+    """The split dataflow across processes (GM_OPT_BOX_FLOW 1 + GM_OPT_BOX_TRANSPORT 1): each
+    process's chain one launch, its halo boxes and their flags stored into the receiving
+    process's table and flag array through the IPC mappings -- a box of one process waits on a
+    flag another process stores.  The ranks share the GPU here, so each launch takes its share
+    of the resident workgroups.  Three solves: the summed digests equal the oracle's."""
+    root = 0x33557777
+    ok, orec, want = _oracle_box(oracle, root)
+    res = _run(world, SUB, (8,), {"box_transport": 1, "box_flow": 1, "root": root, "solves": 3}, shared=True)
+    for i in range(3):
+        assert (sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1), sum(r["digests"][i][1] for r in res)) == want

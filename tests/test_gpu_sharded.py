@@ -390,3 +390,49 @@ def test_sparse_rccl_transport_one_rank_toot_6x4():
     assert ctx.tier_counts().tolist() == c1
     assert ctx.digest() == d1
     ctx.close()
+
+
+@pytest.mark.parametrize("ranks", [2, 4, 8])
+def test_box_split_dataflow_2_32_matches_oracle_digest(ranks):
+    """GM_OPT_BOX_FLOW 1 on the split box engine (csrc/dense_box.hip box_split_flow_kernel):
+    every virtual rank's whole chain in ONE launch with the others' (workgroup w runs rank
+    w % G), the halo boxes stored straight into the receiving rank's table and their flags
+    into its flag array, a box starting when its child boxes' flags -- own or received -- hold
+    the solve's epoch.  Twice in a row (epochs): the committed 2^32 oracle digest, the root
+    record, one launch per solve, the plan's halo bytes."""
+    ref = _committed("subtract_8")
+    ctx, n, rec = _solve(SUB, (8,), ranks, timing=1, box_flow=1)
+    for _ in range(2):
+        assert (n, rec) == (1 << 32, ref["root_record"])
+        assert ctx.digest() == (ref["digest"], 1 << 32)
+        st = ctx.stats()
+        assert st["kernel_launches"] == 1 and st["exchanged_bytes"] == _plan_bytes(ranks) > 0
+        n, rec = ctx.solve(0xFFFFFFFF)
+    ctx.close()
+
+
+@pytest.mark.parametrize("root", [0x33557777, 0x13572468])
+def test_box_split_dataflow_custom_roots_vs_oracle(oracle, root):
+    """The split dataflow at 8 virtual ranks on custom roots (0x13572468 leaves ranks idle):
+    export equals the C oracle's table."""
+    ok, orec = _oracle_root(oracle, root)
+    ctx, n, rec = _solve(SUB, (8,), 8, root=root, box_flow=1)
+    k, r = ctx.export()
+    assert np.array_equal(k, ok) and np.array_equal(r, orec)
+    ctx.close()
+
+
+def test_box_split_dataflow_solo_rank():
+    """GM_OPT_DIST_SOLO with the split dataflow: one rank's launch alone, the boxes it
+    receives marked stored for the solve's epoch (the previous full solve wrote them) -- its
+    own dataflow critical path; the full solve after it still equals the oracle."""
+    ref = _committed("subtract_8")
+    ctx, n, rec = _solve(SUB, (8,), 8, timing=1, box_flow=1)
+    for r in (0, 7):
+        ctx.set_option(_lib.OPT_DIST_SOLO, r + 1)
+        ctx.solve(0xFFFFFFFF)
+        assert ctx.rank_stats()[r]["kernel_ms"] > 0
+    ctx.set_option(_lib.OPT_DIST_SOLO, 0)
+    ctx.solve(0xFFFFFFFF)
+    assert ctx.digest() == (ref["digest"], 1 << 32)
+    ctx.close()

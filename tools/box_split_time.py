@@ -19,6 +19,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BOP_TIER_, BOP_UNPACK_ = 0, 2
 sys.path.insert(0, REPO)
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")   # as bench.py: a hardware queue per stream
 
@@ -56,6 +57,14 @@ def dag(ops_by_rank, ms_by_rank, bytes_of, lat_us, link_gbs, waits=None):
                         go = max(t0, link.get((r, axis), 0.0))    # one message at a time per link
                         link[(r, axis)] = go + nb / (link_gbs * 1e6)
                         sent[(axis, arg, r)] = link[(r, axis)] + lat_us / 1000.0
+                elif kind == BOP_SEND and not on_x:
+                    # direct (loopback) lists: the tier wrote the boxes; the signal leaves from S
+                    t1 = t0 + ms[pc[r]]
+                    free[r][st] = t1
+                    nb = bytes_of(r, axis, arg)
+                    go = max(t1, link.get((r, axis), 0.0))
+                    link[(r, axis)] = go + nb / (link_gbs * 1e6)
+                    sent[(axis, arg, r)] = link[(r, axis)] + lat_us / 1000.0
                 elif kind == BOP_RECV:
                     k = (axis, arg, peer)
                     if k not in sent:
@@ -73,6 +82,61 @@ def dag(ops_by_rank, ms_by_rank, bytes_of, lat_us, link_gbs, waits=None):
     return end
 
 
+def flow_main(a):
+    """The split dataflow: every rank's chain is one launch, cross-rank waits are per box.  Per
+    G: the loopback solve with all ranks in ONE launch (workgroup w runs rank w % G, so at G = 8
+    each rank runs on one XCD: G ranks on 1/G of the chip each, with the real box-level waits
+    between them) and each rank's solo launch on the whole chip with its received boxes
+    marked stored (its own critical path).  Printed per G: the concurrent time over the one-GPU
+    time (the stagger and wait overhead of the split, at equal total compute), the slowest
+    solo span, and their product -- the multi-GPU estimate that applies the measured
+    overhead to a rank running alone on its own GPU."""
+    import numpy as np
+    import torch
+    from gamesmanmpi_amd import Context, _lib
+    ref = json.load(open(os.path.join(REPO, "tests", "golden", "oracle_digests.json")))["subtract_8"]
+    stream = torch.cuda.Stream()
+
+    def timed(ctx, reps):
+        t = []
+        for _ in range(reps + 1):
+            ctx.solve(0xFFFFFFFF)
+            t.append(ctx.stats()["kernel_ms"])
+        return float(np.median(t[1:]))
+    one = Context(_lib.GAME_SUBTRACT, (8,), device=0)
+    one.set_stream(stream.cuda_stream)
+    one.set_option(_lib.OPT_TIMING, 1)
+    base = timed(one, a.reps)
+    one.close()
+    print(json.dumps({"ranks": 1, "ms": round(base, 4)}), flush=True)
+    for G in a.ranks:
+        ctx = Context(_lib.GAME_SUBTRACT, (8,), device=0)
+        ctx.set_stream(stream.cuda_stream)
+        for k, v in ((_lib.OPT_VIRTUAL_RANKS, G), (_lib.OPT_BOX_FLOW, 1), (_lib.OPT_DIST_SYMMETRY, a.sym),
+                     (_lib.OPT_TIMING, 1)):
+            ctx.set_option(k, v)
+        conc = timed(ctx, a.reps)
+        ok = ctx.digest() == (ref["digest"], 1 << 32)
+        spans = []
+        for r in range(G):
+            ctx.set_option(_lib.OPT_DIST_SOLO, r + 1)
+            sp = []
+            for _ in range(a.reps + 1):
+                ctx.solve(0xFFFFFFFF)
+                sp.append(ctx.rank_stats()[r]["kernel_ms"])
+            spans.append(float(np.median(sp[1:])))
+        ctx.set_option(_lib.OPT_DIST_SOLO, 0)
+        over = conc / base
+        est = max(spans) * over
+        print(json.dumps({"ranks": G, "flow": True, "digest_ok": ok, "concurrent_loopback_ms": round(conc, 4),
+                          "overhead_vs_one_gpu": round(over, 3), "solo_span_ms": [round(x, 4) for x in spans],
+                          "estimate_ms": round(est, 4), "estimate_speedup": round(base / est, 3),
+                          "ideal_speedup_from_solo": round(base / max(spans), 3)}), flush=True)
+        ctx.close()
+        torch.cuda.empty_cache()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, nargs="+", default=[2, 4, 8])
@@ -83,7 +147,11 @@ def main():
     ap.add_argument("--lat-us", type=float, default=15.0)
     ap.add_argument("--link-gbs", type=float, default=64.0)
     ap.add_argument("--dump", default=None, help="directory for per-G JSON dumps of the op lists and op times")
+    ap.add_argument("--flow", action="store_true",
+                    help="the split dataflow (GM_OPT_BOX_FLOW 1): per-rank solo spans and the concurrent loopback")
     a = ap.parse_args()
+    if a.flow:
+        return flow_main(a)
     import numpy as np
     import torch
     from gamesmanmpi_amd import Context, _lib
@@ -137,11 +205,13 @@ def main():
         waits = [0.0] * G
         end = dag(ops, ms, bytes_of, a.lat_us, a.link_gbs, waits)
         end0 = dag(ops, ms, bytes_of, 0.0, 1e9)
-        # the DAG with every op scaled so a rank's ops sum to its span (gaps between ops spread)
+        # the DAG with the tier (and unpack) launches scaled so they sum to the rank's solo span --
+        # the gaps between launches and the signal / event costs spread over them -- and the
+        # other ops at zero: their per-op event pairs (GM_OPT_TIMING 2) time mostly themselves
         scaled = []
         for m, o, sp in zip(ms, ops, spans):
-            f = sp / max(1e-9, float(m.sum()))
-            scaled.append(m * f)
+            mc = np.where(np.isin(o[:, 0], [BOP_TIER_, BOP_UNPACK_]), m, 0.0)
+            scaled.append(mc * (sp / max(1e-9, float(mc.sum()))))
         end_s = dag(ops, scaled, bytes_of, a.lat_us, a.link_gbs)
         names = ["tier", "pack", "unpack", "send", "recv", "record", "wait"]   # pack: fused into tier
         worst = int(np.argmax(spans))
