@@ -116,16 +116,21 @@ enum {
                                when its child boxes are stored; its grid is the kernel's resident
                                capacity from the occupancy API).  A dataflow solve whose waits time out
                                is redone with tier launches, and the context keeps tier launches until
-                               this option is set again; gm_stats_t.flow_fallbacks counts them. */
+                               this option is set again; gm_stats_t.flow_fallbacks counts them.
+                               Split solve (virtual ranks or GM_OPT_BOX_TRANSPORT 1): 1 = each rank's
+                               chain one launch, halo boxes and their flags stored into the receiving
+                               rank's table and flag array (box_split_flow_kernel); a wait past 200 ms
+                               (30 s across processes) fails the solve with GM_E_STATE. */
     GM_OPT_BOX_SPLIT = 16,  /* box engine at N > 1 (gm_box_plan): 0 (default) = split heaps in halves
                                (rank bit a = [box coordinate >= half]); 1 = tier-balanced comparisons
                                (rank bit = [c_x < c_y], ties by a rule that keeps every axis one-way) */
     GM_OPT_BOX_TRANSPORT = 17  /* box engine at N > 1, one process per rank: how a halo message
                                travels.  0 (default) = ncclSend / ncclRecv on per-axis communicators;
-                               1 = peer copies into the receiver's buffer, mapped through HIP IPC
-                               (hipIpcGetMemHandle, exchanged through a POSIX shared-memory segment
-                               named by the unique id), with completion flags in device memory that
-                               stream-ordered kernels set and poll (30 s limit, then GM_E_COMM).  1
+                               1 = the sender's tier kernel stores its halo boxes straight into the
+                               receiver's table, mapped through HIP IPC (hipIpcGetMemHandle, exchanged
+                               through a POSIX shared-memory segment named by the unique id), with
+                               completion flags in device memory that stream-ordered kernels set and
+                               poll (30 s limit, then GM_E_COMM).  1
                                also runs when the ranks share one GPU, where RCCL refuses; all the
                                ranks of one node.  Set on every rank before the first solve. */
 };
