@@ -144,10 +144,18 @@ static int bx_shape(uint32_t root_hi, int world, int batch, int fill, int split,
     }
     static const int pref[3][3] = {{3, -1, -1}, {3, 7, -1}, {2, 3, 7}};
     static const int order[8] = {3, 7, 2, 6, 1, 5, 0, 4};
+    // GM_BOX_SPLIT_HEAPS (development): the half-split heaps, e.g. "1,2,3"
+    int envh[3] = {-1, -1, -1};
+    if (const char *e = getenv("GM_BOX_SPLIT_HEAPS"))
+        for (int k = 0; k < 3 && *e; k++) {
+            envh[k] = atoi(e);
+            while (*e && *e != ',') e++;
+            if (*e == ',') e++;
+        }
     if (S->g > 0)
         for (int k = 0; k < 3 && n < S->g; k++) {
-            const int d = pref[S->g - 1][k];
-            if (d >= 0 && !used[d] && S->lim[d] >= 1) S->ax[n++] = half(d);
+            const int d = envh[0] >= 0 ? envh[k] : pref[S->g - 1][k];
+            if (d >= 0 && d < 8 && !used[d] && S->lim[d] >= 1) S->ax[n++] = half(d);
         }
     for (int k = 0; k < 8 && n < S->g; k++)
         if (!used[order[k]] && S->lim[order[k]] >= 1) S->ax[n++] = half(order[k]);
