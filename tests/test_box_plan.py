@@ -381,3 +381,37 @@ def test_gloo_ranks_exchange_halos(world, root, batch, symmetry, split):
     assert all(r["own_ok"] and r["recv_ok"] for r in res), res
     assert sum(r["own_boxes"] for r in res) == len(S.region(root))
     assert any(r["received_boxes"] > 0 for r in res)
+
+
+_HEAPS_CHECK = """
+import os, sys
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, os.path.join(sys.argv[1], "tests"))
+import numpy as np
+import box_sim as S
+from gamesmanmpi_amd import _lib
+G = int(sys.argv[2])
+sh = _lib.box_plan(G, 0, _lib.BOXPLAN_SHAPE).astype(int).tolist()
+heaps = [sh[8 + 4 * a] for a in range(sh[1])]
+seen = np.zeros(1 << 20, np.int64)
+P = S.plans(G, batch=1)
+for p in P:
+    seen[p["own"]] += 1
+    assert S.check_reads(p)
+assert (seen == 1).all()
+print(heaps)
+"""
+
+
+@pytest.mark.parametrize("world,heaps", [(4, "2,3"), (8, "1,2,3")])
+def test_split_heaps_knob_keeps_the_plan_valid(world, heaps):
+    """GM_BOX_SPLIT_HEAPS (development knob: which heaps the halves split; measured and not
+    kept): the axes follow it, the ranks still partition the boxes, and every
+    child read resolves (fresh process: the knob is read by the plan)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _HEAPS_CHECK, repo, str(world)], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, GM_BOX_SPLIT_HEAPS=heaps))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().splitlines()[-1] == "[%s]" % heaps.replace(",", ", ")

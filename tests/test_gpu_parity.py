@@ -287,6 +287,21 @@ def test_sparse_sorted_lists_everywhere_vs_golden(split_max, mode):
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("home_w", ["16", "20"])
+def test_sparse_locality_home_vs_golden(home_w):
+    """GM_SPARSE_HOME_W (development knob, DESIGN.md §4.2: measured and not kept): the tier
+    tables' locality home -- a key's group picks a base, a hash of the key one of 2^w slots
+    from it -- gives the same tables: the golden tables and the Toot 4x4 oracle digest,
+    synced solve and replay (fresh process: the knob is read once)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GM_SPARSE_HOME_W=home_w, GM_SPARSE_SPLIT_MAX="4096")
+    r = subprocess.run([sys.executable, "-c", _SPARSE_BATCH_EVERYWHERE, repo], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
 def test_subtract_graph_replay_is_identical(oracle):
     ref = oracle.subtract_dense(5)
     for graph in (0, 1, 1):
