@@ -961,7 +961,7 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
             // solo timing: the other ranks' boxes are taken as written (the previous full solve's)
             if (!solo) GM_HIP(hipStreamWaitEvent(st, L.ev[BEV_DONE][0][j], 0));
             d->sent += n;
-        } else if (d->ipc) {   // the sender copies the message in and sets the flag
+        } else if (d->ipc) {   // the sender's tier kernels stored the boxes here; wait for its flag
             hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, R.flags + (size_t)a * d->S.nbatch + j, d->seq,
                                BX_IPC_WAIT_TICKS, R.d_err);
         } else {
