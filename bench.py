@@ -236,16 +236,21 @@ def box_sharding(world, args, root, st, rstats, per_rank, autotune, torch, dist)
         "scheme": ("box engine split: the 2^20 boxes of the 4x4x4x4x2x2x2x2 lattice divided by halves of %d heap "
                    "coordinate(s) (%s); ranks >= 2^%d idle; each box computed by exactly one rank; a child box "
                    "of the other half read through a same-kind heap transposition of an own box (symmetric "
-                   "fill) or received: the lower rank's tier kernel writes it to a message slot and an "
-                   "exchange stream per axis sends each batch of %d tiers over RCCL (DESIGN.md §5.0)"
-                   % (sh[1], "; ".join(axes), sh[1], args.dist_batch)),
+                   "fill) or received: %s (DESIGN.md §5.0)"
+                   % (sh[1], "; ".join(axes), sh[1],
+                      ("the lower rank's tier kernel writes it to a message slot and an exchange stream per axis "
+                       "sends each batch of %d tiers over RCCL" % args.dist_batch)
+                      if (world > 1 and args.box_transport != "ipc") else
+                      ("the lower rank's tier kernel stores it straight into the receiver's table, one signal "
+                       "per batch of %d tiers" % args.dist_batch))),
         "work_vs_one_gpu": sum(boxes) / max(1, one),
         "boxes_per_rank": boxes,
         "halo_batch_tiers": args.dist_batch, "halo_batch_autotune_ms": autotune,
         "halo_symmetric_fill": bool(args.dist_symmetry),
-        "halo_transport": ("peer copies through HIP IPC, device flags (GM_OPT_BOX_TRANSPORT 1)"
+        "halo_transport": ("direct stores into the peer's table mapped through HIP IPC, device flags "
+                           "(GM_OPT_BOX_TRANSPORT 1)"
                            if args.box_transport == "ipc" else "RCCL send / recv, one communicator per axis")
-                          if world > 1 else "loopback (device copies between virtual ranks)",
+                          if world > 1 else "loopback (direct stores between the virtual ranks' tables, event per batch)",
         "halo_bytes_sent_per_step_by_rank": sent,
         "halo_bytes_received_per_step_by_rank": recvd,
         "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank,
@@ -523,7 +528,7 @@ def main():
                     help="8 heaps: run the block engine (GM_OPT_SUB_INTERLEAVE 10) instead of the box engine, "
                          "sharded with halo exchanges at N > 1 (the round-3 multi-GPU path, for comparison)")
     ap.add_argument("--box-transport", choices=("rccl", "ipc"), default="rccl",
-                    help="N>1, 8 heaps: halo messages over RCCL (default) or peer copies through HIP IPC "
+                    help="N>1, 8 heaps: halo messages over RCCL (default) or direct stores into the peer's table through HIP IPC "
                          "(GM_OPT_BOX_TRANSPORT 1; also runs with several ranks on one GPU)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 rehearsal on a one-GPU box: every rank on device 0, bench.py's collectives over "

@@ -64,7 +64,8 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 #ifndef GM_BOX_WAVES
 #define GM_BOX_WAVES 2         // waves per SIMD the register budget must allow
 #endif
-// development ablations (results invalid): bit 1 no walk, 2 no child loads, 4 no stores, 8 no fold
+// development ablations (results invalid): bit 1 no walk, 2 no child loads, 4 no stores, 8 no fold;
+// split solve: 16 children read as at N = 1 (no fills: exact for rank 0), 32 no halo stores
 #ifndef GM_BOX_EXP
 #define GM_BOX_EXP 0
 #endif
@@ -260,9 +261,10 @@ __device__ __forceinline__ uint32_t bx_fcode(const BxGroup &G, int k, int dir) {
 // eight boxes read (scalar loads; computing the swaps here overflowed the SGPRs) and the fill
 // word: an A transposition moves rows (row A of C is row swap(A) of S, digits q and p: a
 // per-lane address change here), a B transposition permutes the bytes of a row (bx_fold).
-template <bool SHARD, int CPOL = 0>
+template <bool SHARD_, int CPOL = 0>
 __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
                                          bx_u32x4 (&R)[BX_NLOAD]) {
+    constexpr bool SHARD = SHARD_ && !(GM_BOX_EXP & 16);
     const __amdgpu_buffer_rsrc_t rt =
         __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, (GM_BOX_EXP & 2) ? 0u : 0xFFFFFFFFu, 0x00020000);
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0u, 0x00020000);
@@ -318,8 +320,9 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
 }
 
 // fold: the image's slot of every position gets the max of its children outside the box
-template <bool SHARD>
+template <bool SHARD_>
 __device__ __forceinline__ void bx_fold(uint32_t *s, const BxGroup &G, uint32_t lane, bx_u32x4 (&R)[BX_NLOAD]) {
+    constexpr bool SHARD = SHARD_ && !(GM_BOX_EXP & 16);
     if constexpr (SHARD) {   // B children read through a B transposition: back to C's byte order (uniform branches)
 #pragma unroll
         for (int k = 0; k < 2; k++)
@@ -556,9 +559,10 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
 // DIRECT (loopback and IPC transports): the box goes straight to its slot in the receiving
 // rank's own table (peer p0..p2 by axis, slot kind << 28 | axis << 26), rows where they lie,
 // so the receiver needs no unpack.
-template <bool SHARD, bool DIRECT = false>
+template <bool SHARD_, bool DIRECT = false>
 __device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, uint8_t *p0, uint8_t *p1, uint8_t *p2,
                                          const BxGroup &G, const uint32_t *s, uint32_t lane) {
+    constexpr bool SHARD = SHARD_ && !(GM_BOX_EXP & 32);
     __amdgpu_buffer_rsrc_t w[2];
 #pragma unroll
     for (int k = 0; k < 2; k++)
