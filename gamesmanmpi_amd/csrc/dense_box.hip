@@ -64,6 +64,9 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 #ifndef GM_BOX_WAVES
 #define GM_BOX_WAVES 2         // waves per SIMD the register budget must allow
 #endif
+#ifndef GM_BOX_SPLIT_PLAIN
+#define GM_BOX_SPLIT_PLAIN 1   // split tier kernel: a group without fills issues its loads as at N = 1
+#endif
 // development ablations (results invalid): bit 1 no walk, 2 no child loads, 4 no stores, 8 no fold;
 // split solve: 16 children read as at N = 1 (no fills: exact for rank 0), 32 no halo stores
 #ifndef GM_BOX_EXP
@@ -176,7 +179,7 @@ struct BxGroup {
     bool valid[2];
 };
 
-template <bool SHARD>
+template <bool SHARD, bool FILL = true>
 __device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, const uint32_t *__restrict__ fills,
                                             const uint32_t *__restrict__ srcs, const uint32_t *__restrict__ dsts,
                                             uint32_t nbox, uint32_t g, uint32_t lane) {
@@ -186,12 +189,12 @@ __device__ __forceinline__ BxGroup bx_group(const uint32_t *__restrict__ boxes, 
         const uint32_t i = 2 * g + k;
         G.valid[k] = i < nbox;
         G.box[k] = G.valid[k] ? boxes[i] : 0u;
-        G.fill[k] = (SHARD && G.valid[k]) ? fills[i] : 0u;
+        G.fill[k] = (SHARD && FILL && G.valid[k]) ? fills[i] : 0u;
     }
     G.srcv = G.dstv = 0;
     if constexpr (SHARD) {
         const uint32_t i = 2 * g + (lane >> 3);
-        if (lane < 16 && i < nbox) G.srcv = srcs[8 * i + (lane & 7u)];
+        if (FILL && lane < 16 && i < nbox) G.srcv = srcs[8 * i + (lane & 7u)];
         const uint32_t i2 = 2 * g + (lane >> 2);
         if (lane < 8 && (lane & 3u) < 3u && i2 < nbox) G.dstv = dsts[3 * i2 + (lane & 3u)];
     }
@@ -261,10 +264,15 @@ __device__ __forceinline__ uint32_t bx_fcode(const BxGroup &G, int k, int dir) {
 // eight boxes read (scalar loads; computing the swaps here overflowed the SGPRs) and the fill
 // word: an A transposition moves rows (row A of C is row swap(A) of S, digits q and p: a
 // per-lane address change here), a B transposition permutes the bytes of a row (bx_fold).
-template <bool SHARD_, int CPOL = 0>
+template <bool SHARD_, int CPOL = 0, bool PLAIN = false>
 __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G, uint32_t lane,
                                          bx_u32x4 (&R)[BX_NLOAD]) {
     constexpr bool SHARD = SHARD_ && !(GM_BOX_EXP & 16);
+    if constexpr (SHARD && PLAIN)   // a group without fills reads every child where it lies (uniform)
+        if (!(G.fill[0] | G.fill[1])) {
+            bx_issue<false, CPOL>(table, G, lane, R);
+            return;
+        }
     const __amdgpu_buffer_rsrc_t rt =
         __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, (GM_BOX_EXP & 2) ? 0u : 0xFFFFFFFFu, 0x00020000);
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0u, 0x00020000);
@@ -304,16 +312,20 @@ __device__ __forceinline__ void bx_issue(const uint8_t *table, const BxGroup &G,
                 }
                 const uint32_t soff = ok ? src << 12 : 0u;
                 const __amdgpu_buffer_rsrc_t r = ok ? rt : rz;
+                uint32_t A[2];
 #pragma unroll
-                for (int v = 0; v < 2; v++) {
-                    uint32_t A = lo | ((3u - v) << (2 * i)) | hi;
-                    if constexpr (SHARD) {
-                        const uint32_t t = ((A >> sq) ^ (A >> sp)) & 3u;
-                        A ^= (t << sq) | (t << sp);
+                for (int v = 0; v < 2; v++) A[v] = lo | ((3u - v) << (2 * i)) | hi;
+                if constexpr (SHARD) {   // branch-free: shifts of 0 for no transposition
+#pragma unroll
+                    for (int v = 0; v < 2; v++) {
+                        const uint32_t t = ((A[v] >> sq) ^ (A[v] >> sp)) & 3u;
+                        A[v] ^= (t << sq) | (t << sp);
                     }
-                    R[32 + 4 * i + 2 * k + v] =
-                        __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A, soff, CPOL));
                 }
+#pragma unroll
+                for (int v = 0; v < 2; v++)
+                    R[32 + 4 * i + 2 * k + v] =
+                        __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, 16u * A[v], soff, CPOL));
             }
         }
     }
@@ -643,7 +655,9 @@ __device__ unsigned long long bx_trace_acc[8];
 // workgroups of an XCD side by side, so neighbouring groups share child boxes in its L2.
 // SHARD: one rank of the sharded solve: its own box list, with a fill code
 // per box saying where each child box is read from.
-template <bool SHARD, bool DIRECT = false>
+// FILL (split solve): some box of the launch reads a child through a transposition; a launch
+// without (every tier of rank 0, most of the others' first tiers) reads its children as at N = 1.
+template <bool SHARD, bool DIRECT = false, bool FILL = true>
 __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__restrict__ table,
                                                                      const uint32_t *__restrict__ boxes,
                                                                      const uint32_t *__restrict__ fills,
@@ -665,8 +679,9 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
     // b2 / b3 neighbour
     s[BX_PITCH * lane + BX_Z] = 0;
     bx_u32x4 R[BX_NLOAD];
-    BxGroup G = bx_group<SHARD>(boxes, fills, srcs, dsts, nbox, g, lane);
-    bx_issue<SHARD>(table, G, lane, R);
+    constexpr bool SF = SHARD && FILL;
+    BxGroup G = bx_group<SHARD, FILL>(boxes, fills, srcs, dsts, nbox, g, lane);
+    bx_issue<SF, 0, GM_BOX_SPLIT_PLAIN>(table, G, lane, R);
 #if GM_BOX_TRACE
     unsigned long long tt[5], acc[4] = {0, 0, 0, 0}, ngr = 0, tbeg, rbeg;
     BX_STAMP(tbeg);
@@ -683,13 +698,13 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         BX_STAMP(tt[1]);
 #endif
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_F);
-        if (!(GM_BOX_EXP & 8)) bx_fold<SHARD>(s, G, ln, R);
+        if (!(GM_BOX_EXP & 8)) bx_fold<SF>(s, G, ln, R);
         else   // keep the loads live: one xor per row into the image
             for (int q = 0; q < BX_NLOAD; q++) s[ln + 64 * (q & 7)] ^= R[q][0] ^ R[q][3];
         const uint32_t gn = g + Kx;
         const bool more = gn < g1;
         BxGroup Gn = G;
-        if (more) Gn = bx_group<SHARD>(boxes, fills, srcs, dsts, nbox, gn, lane);
+        if (more) Gn = bx_group<SHARD, FILL>(boxes, fills, srcs, dsts, nbox, gn, lane);
         BX_LDS_ORDER();
 #if GM_BOX_TRACE
         BX_STAMP(tt[2]);
@@ -711,7 +726,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
         g = gn;
         G = Gn;
         __builtin_amdgcn_s_setprio(GM_BOX_PRIO_I);   // the next group's loads out first
-        bx_issue<SHARD>(table, G, lane, R);
+        bx_issue<SF, 0, GM_BOX_SPLIT_PLAIN>(table, G, lane, R);
     }
 #if GM_BOX_TRACE
     unsigned long long tend, rend;
@@ -1091,13 +1106,19 @@ int box_grid_cap(int device) { return box_resident((const void *)box_tier_kernel
 
 void box_launch_tier_split(uint32_t grid, uint8_t *table, const uint32_t *boxes, const uint32_t *fills,
                            const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint8_t *const *peers,
-                           uint32_t nbox, hipStream_t s) {
-    if (peers)
-        hipLaunchKernelGGL((box_tier_kernel<true, true>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs, dsts,
-                           nullptr, peers[0], peers[1], peers[2], nbox);
+                           uint32_t nbox, bool fill, hipStream_t s) {
+    if (peers && fill)
+        hipLaunchKernelGGL((box_tier_kernel<true, true, true>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs,
+                           dsts, nullptr, peers[0], peers[1], peers[2], nbox);
+    else if (peers)
+        hipLaunchKernelGGL((box_tier_kernel<true, true, false>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs,
+                           dsts, nullptr, peers[0], peers[1], peers[2], nbox);
+    else if (fill)
+        hipLaunchKernelGGL((box_tier_kernel<true, false, true>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs,
+                           dsts, msg, nullptr, nullptr, nullptr, nbox);
     else
-        hipLaunchKernelGGL((box_tier_kernel<true, false>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs, dsts,
-                           msg, nullptr, nullptr, nullptr, nbox);
+        hipLaunchKernelGGL((box_tier_kernel<true, false, false>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs,
+                           dsts, msg, nullptr, nullptr, nullptr, nbox);
 }
 void box_launch_split_flow(uint32_t grid, const void *ranks, uint32_t nranks, uint32_t ep, uint32_t *err,
                            uint64_t timeout_ticks, bool sys, hipStream_t s) {

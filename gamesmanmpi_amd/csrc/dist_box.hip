@@ -482,6 +482,7 @@ struct BxRank {
     uint8_t *table = nullptr;
     bool owned = false;
     std::vector<uint32_t> tier_off;
+    std::vector<uint8_t> tier_fill;       // per tier: some box reads a child through a transposition
     std::vector<uint32_t> boxes;          // host copy
     uint32_t *d_boxes = nullptr, *d_fills = nullptr, *d_srcs = nullptr, *d_dsts = nullptr;
     // one send and one receive buffer; per axis the byte offset of each batch's message
@@ -756,6 +757,9 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
         BxPlan P;
         GM_TRY(bx_plan(S, R.rank, P));
         R.tier_off = P.tier_off;
+        R.tier_fill.assign(P.tier_off.size(), 0);
+        for (size_t t = 0; t + 1 < P.tier_off.size(); t++)
+            for (uint32_t k = P.tier_off[t]; k < P.tier_off[t + 1] && !R.tier_fill[t]; k++) R.tier_fill[t] = P.fills[k] != 0;
         R.boxes = P.boxes;
         R.filled = P.filled;
         R.received = P.received;
@@ -911,7 +915,7 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
             const uint32_t grid = std::max<uint32_t>(8u, std::min<uint32_t>(ng, (uint32_t)d->grid_cap));
             const size_t o0 = R.tier_off[j];
             box_launch_tier_split(grid, R.table, R.d_boxes + o0, R.d_fills + o0, R.d_srcs + 8 * o0, R.d_dsts + 3 * o0,
-                                  R.sbuf, d->direct ? R.peer_table : nullptr, nb, st);
+                                  R.sbuf, d->direct ? R.peer_table : nullptr, nb, R.tier_fill[j] != 0, st);
         }
         break;
     }

@@ -160,7 +160,7 @@ struct BxSplitFlowDesc {
 };
 void box_launch_tier_split(uint32_t grid, uint8_t *table, const uint32_t *boxes, const uint32_t *fills,
                            const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint8_t *const *peers,
-                           uint32_t nbox, hipStream_t s);
+                           uint32_t nbox, bool fill, hipStream_t s);
 void box_launch_digest(const uint8_t *table, const uint32_t *boxes, uint64_t nbox, uint64_t root,
                        unsigned long long *acc, hipStream_t s);
 void box_launch_query(const uint8_t *const *tables, const uint8_t *owner, uint64_t root, const uint64_t *keys,
