@@ -527,9 +527,11 @@ def main():
     ap.add_argument("--block-engine", action="store_true",
                     help="8 heaps: run the block engine (GM_OPT_SUB_INTERLEAVE 10) instead of the box engine, "
                          "sharded with halo exchanges at N > 1 (the round-3 multi-GPU path, for comparison)")
-    ap.add_argument("--box-transport", choices=("rccl", "ipc"), default="rccl",
-                    help="N>1, 8 heaps: halo messages over RCCL (default) or direct stores into the peer's table through HIP IPC "
-                         "(GM_OPT_BOX_TRANSPORT 1; also runs with several ranks on one GPU)")
+    ap.add_argument("--box-transport", choices=("rccl", "ipc"), default="ipc",
+                    help="N>1, 8 heaps: the tier kernel stores halo boxes straight into the peer's table mapped "
+                         "through HIP IPC, over xGMI, and each rank's solve replays as one captured graph "
+                         "(GM_OPT_BOX_TRANSPORT 1, default: one node; also runs with several ranks on one GPU), or "
+                         "halo messages over RCCL send / recv, launched eagerly (the library's default transport)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 rehearsal on a one-GPU box: every rank on device 0, bench.py's collectives over "
                          "gloo, the box engine's halos over the IPC transport (RCCL refuses two ranks on one "
@@ -584,8 +586,9 @@ def main():
 
     ctx = Context(_lib.GAME_SUBTRACT, (args.heaps,), device=local)
     # the box engine (csrc/dense_box.hip) at 8 heaps: one GPU, and at N > 1 the boxes split
-    # over the ranks by halves of heap coordinates, halo boxes exchanged per batch of tiers
-    # over the library's own RCCL communicators (csrc/dist_box.hip); else the block engine
+    # over the ranks by halves of heap coordinates, halo boxes stored into the receiving rank's
+    # table (IPC transport) or exchanged over the library's RCCL communicators per batch of
+    # tiers (csrc/dist_box.hip); else the block engine
     box = args.heaps == 8 and not args.block_engine
     if not box:
         ctx.set_option(_lib.OPT_SUB_INTERLEAVE, 10)

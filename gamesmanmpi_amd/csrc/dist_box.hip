@@ -434,15 +434,26 @@ __global__ void bx_hold_kernel(uint64_t ticks) {
 // solve (the solve's sequence number), set by one lane with a system-scope release after the
 // stream's earlier work, and polled by one lane with system-scope acquire loads.  A wait that
 // outlasts its limit (s_memrealtime, 100 MHz) sets *err and ends, so a peer that never
-// delivers ends the solve with GM_E_COMM instead of holding the stream.
-__global__ void bx_flag_set_kernel(uint64_t *flag, uint64_t v) {
+// delivers ends the solve with GM_E_COMM instead of holding the stream.  The sequence number
+// lives in device memory (*seqp, advanced by bx_seq_kernel at the start of every solve), so
+// a solve replays as one captured graph.
+__global__ void bx_seq_kernel(uint64_t *seqp) {
+    if (!threadIdx.x) *seqp += 1;
+}
+
+__global__ void bx_flag_set_kernel(uint64_t *flag, const uint64_t *seqp) {
     if (threadIdx.x) return;
+    const uint64_t v = *seqp;
     __threadfence_system();
     __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void bx_flag_wait_kernel(const uint64_t *flag, uint64_t want, uint64_t ticks, uint32_t *err) {
+// waits until *flag >= (*seqp + add) << shift
+__global__ void bx_flag_wait_kernel(const uint64_t *flag, const uint64_t *seqp, int add, uint32_t shift, uint64_t ticks,
+                                    uint32_t *err) {
     if (threadIdx.x) return;
+    const int64_t w = (int64_t)*seqp + add;
+    const uint64_t want = w > 0 ? (uint64_t)w << shift : 0u;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
@@ -453,8 +464,9 @@ __global__ void bx_flag_wait_kernel(const uint64_t *flag, uint64_t want, uint64_
     }
 }
 
-__global__ void bx_flags_set_kernel(uint64_t *f0, uint64_t *f1, uint64_t *f2, uint64_t v) {
+__global__ void bx_flags_set_kernel(uint64_t *f0, uint64_t *f1, uint64_t *f2, const uint64_t *seqp) {
     if (threadIdx.x) return;
+    const uint64_t v = *seqp;
     __threadfence_system();
     if (f0) __hip_atomic_store(f0, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (f1) __hip_atomic_store(f1, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -467,9 +479,9 @@ __global__ void bx_mark_kernel(uint32_t *flag, const uint32_t *boxes, uint32_t n
 }
 
 // the root's code, tagged with the solve's sequence number, into every rank's flag block
-__global__ void bx_root_post_kernel(const uint8_t *slot, uint64_t *const *words, int n, uint64_t seq) {
+__global__ void bx_root_post_kernel(const uint8_t *slot, uint64_t *const *words, int n, const uint64_t *seqp) {
     if (threadIdx.x) return;
-    const uint64_t v = seq << 8 | *slot;
+    const uint64_t v = *seqp << 8 | *slot;
     __threadfence_system();
     for (int i = 0; i < n; i++) __hip_atomic_store(words[i], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -544,6 +556,19 @@ struct DistBox {
     uint64_t flow_ticks = 0;
     bool flow_sys = false;                // a peer on another GPU: system-scope flag polls and stores
     uint64_t seq = 0;                     // solves run on this context (the flags' values)
+    uint64_t *d_seq = nullptr;            // IPC: the same count in device memory (the kernels read it)
+    // GM_BOX_SIGNAL_KERNELS=1 (development, virtual ranks): each signal and each receive also
+    // launches the IPC transport's one-lane flag kernel (on a scratch flag), so a solo span
+    // carries the launches an IPC rank's list holds
+    uint64_t *d_scratch = nullptr;
+    // virtual ranks and the IPC transport: a solve's launches captured once and replayed as one
+    // graph (the op lists are fixed per plan); key = the solo rank it was captured for
+    hipGraphExec_t gexec = nullptr;
+    hipStream_t graph_stream = nullptr;
+    int graph_key = -1;
+    bool graph_bad = false;               // capture refused: launch eagerly from then on
+    uint64_t graph_sent = 0;
+    std::vector<uint64_t> graph_rank_sent;
     std::vector<void *> opened;           // peer mappings (hipIpcCloseMemHandle on free)
     uint64_t **d_root_words = nullptr;    // every rank's root word (the root's owner posts to all)
     int n_root_words = 0;
@@ -733,6 +758,14 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
         GM_HIP(hipMemset(d->d_flow_err, 0, 4));
     }
     c->box_prepares++;
+    if (d->ipc || (loopback && getenv("GM_BOX_SIGNAL_KERNELS") && atoi(getenv("GM_BOX_SIGNAL_KERNELS")) == 1)) {
+        GM_HIP(hipMalloc(&d->d_seq, 8));
+        GM_HIP(hipMemset(d->d_seq, 0, 8));
+        if (!d->ipc) {
+            GM_HIP(hipMalloc(&d->d_scratch, 16));   // flag, error word
+            GM_HIP(hipMemset(d->d_scratch, 0, 16));
+        }
+    }
     GM_HIP(hipMalloc(&d->d_acc, 16));
     GM_HIP(hipMalloc(&d->d_root, 4));
     GM_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
@@ -938,8 +971,12 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
                     uint64_t *f[3] = {nullptr, nullptr, nullptr};
                     for (size_t k = i; k < R.ops.size() && R.ops[k].kind == BOP_SEND && R.ops[k].arg == j; k++)
                         f[R.ops[k].axis] = R.peer_flags[R.ops[k].axis] + (size_t)R.ops[k].axis * d->S.nbatch + j;
-                    hipLaunchKernelGGL(bx_flags_set_kernel, dim3(1), dim3(64), 0, st, f[0], f[1], f[2], d->seq);
+                    hipLaunchKernelGGL(bx_flags_set_kernel, dim3(1), dim3(64), 0, st, f[0], f[1], f[2],
+                                       (const uint64_t *)d->d_seq);
                 } else {
+                    if (d->d_scratch)
+                        hipLaunchKernelGGL(bx_flags_set_kernel, dim3(1), dim3(64), 0, st, d->d_scratch, (uint64_t *)nullptr,
+                                           (uint64_t *)nullptr, (const uint64_t *)d->d_seq);
                     GM_HIP(hipEventRecord(R.ev[BEV_DONE][0][j], st));
                     R.recorded[BEV_DONE][0] = j + 1;
                 }
@@ -964,10 +1001,13 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
             }
             // solo timing: the other ranks' boxes are taken as written (the previous full solve's)
             if (!solo) GM_HIP(hipStreamWaitEvent(st, L.ev[BEV_DONE][0][j], 0));
+            if (d->d_scratch)   // (the flag holds at least 0: returns at once)
+                hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, (const uint64_t *)d->d_scratch,
+                                   (const uint64_t *)d->d_seq, -(1 << 30), 0u, BX_IPC_WAIT_TICKS, (uint32_t *)(d->d_scratch + 1));
             d->sent += n;
         } else if (d->ipc) {   // the sender's tier kernels stored the boxes here; wait for its flag
-            hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, R.flags + (size_t)a * d->S.nbatch + j, d->seq,
-                               BX_IPC_WAIT_TICKS, R.d_err);
+            hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, R.flags + (size_t)a * d->S.nbatch + j,
+                               (const uint64_t *)d->d_seq, 0, 0u, BX_IPC_WAIT_TICKS, R.d_err);
         } else {
             for (uint64_t p = 0; p < n; p += 1ull << 30)
                 GM_NCCL(ncclRecv(R.rbuf + o0 + p, std::min<uint64_t>(n - p, 1ull << 30), ncclUint8, o.peer, d->comm[a], st));
@@ -1051,12 +1091,16 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
         if (R.S != H) GM_HIP(hipStreamWaitEvent(R.S, d->ev_fork, 0));
         for (int a = 0; a < d->S.g; a++) GM_HIP(hipStreamWaitEvent(R.X[a], d->ev_fork, 0));
     }
-    if (d->ipc)   // the ranks this one writes into finished reading the previous solve's halos
+    if (d->ipc) {
+        hipLaunchKernelGGL(bx_seq_kernel, dim3(1), dim3(64), 0, d->ranks[0].S, d->d_seq);   // this solve's number
+        // the ranks this one writes into finished reading the previous solve's halos
         for (auto &R : d->ranks)
             for (int a = 0; a < d->S.g; a++)
                 if (R.peer_flags[a])
                     hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, R.S,
-                                       R.peer_flags[a] + bx_flag_consumed(d->S, a), d->seq - 1, BX_IPC_WAIT_TICKS, R.d_err);
+                                       R.peer_flags[a] + bx_flag_consumed(d->S, a), (const uint64_t *)d->d_seq, -1, 0u,
+                                       BX_IPC_WAIT_TICKS, R.d_err);
+    }
     if (d->flow) {
         // one launch: every virtual rank together (co-resident), a solo rank alone (its received
         // boxes marked stored: the previous full solve's stand in), or this process's rank
@@ -1091,7 +1135,7 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
             for (int a = 0; a < d->S.g; a++)
                 if ((R.rank >> a) & 1)
                     hipLaunchKernelGGL(bx_flag_set_kernel, dim3(1), dim3(64), 0, R.S, R.flags + bx_flag_consumed(d->S, a),
-                                       d->seq);
+                                       (const uint64_t *)d->d_seq);
     for (auto &R : d->ranks) {
         for (int a = 0; a < d->S.g; a++) {
             GM_HIP(hipEventRecord(R.ev_join[a], R.X[a]));
@@ -1103,6 +1147,49 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
         }
     }
     GM_HIP(hipGetLastError());
+    return GM_OK;
+}
+
+// A solve's launches.  Virtual ranks and the IPC transport (every op a kernel launch, an event
+// record / wait or a flag kernel reading the device-side sequence number) capture them once
+// per plan and solo rank and replay the graph: the tier launches then follow each other with
+// no per-launch gap.  RCCL mode launches eagerly (a capture refused half-way would leave the
+// ranks' point-to-point sequence numbers out of step); so do per-op timing (GM_OPT_TIMING 2)
+// and the dataflow launch, and GM_OPT_GRAPH 0.
+static int bx_launch(Ctx *c, DistBox *d, bool op_events) {
+    hipStream_t H = c->stream;
+    if (!c->use_graph || op_events || d->flow || !(d->loopback || d->ipc) || d->graph_bad) return bx_run(c, d, op_events);
+    const int key = d->loopback ? c->dist_solo : 0;
+    if (!d->gexec || d->graph_key != key || d->graph_stream != H) {
+        if (d->gexec) {
+            (void)hipGraphExecDestroy(d->gexec);
+            d->gexec = nullptr;
+        }
+        hipGraph_t g = nullptr;
+        GM_HIP(hipStreamBeginCapture(H, hipStreamCaptureModeThreadLocal));
+        const int rc = bx_run(c, d, false);
+        const hipError_t e = hipStreamEndCapture(H, &g);
+        if (rc != GM_OK) {
+            if (g) (void)hipGraphDestroy(g);
+            return rc;
+        }
+        if (e != hipSuccess || !g || hipGraphInstantiate(&d->gexec, g, nullptr, nullptr, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            if (g) (void)hipGraphDestroy(g);
+            d->gexec = nullptr;
+            d->graph_bad = true;   // nothing of the capture ran: launch the same ops eagerly
+            return bx_run(c, d, false);
+        }
+        (void)hipGraphDestroy(g);
+        d->graph_key = key;
+        d->graph_stream = H;
+        d->graph_sent = d->sent;
+        d->graph_rank_sent.clear();
+        for (auto &R : d->ranks) d->graph_rank_sent.push_back(R.sent_bytes);
+    }
+    d->sent = d->graph_sent;   // the host counts of the captured enqueue
+    for (size_t i = 0; i < d->ranks.size(); i++) d->ranks[i].sent_bytes = d->graph_rank_sent[i];
+    GM_HIP(hipGraphLaunch(d->gexec, H));
     return GM_OK;
 }
 
@@ -1142,7 +1229,7 @@ int dist_box_solve(Ctx *c, uint64_t root) {
     if (solo && c->timing) hipLaunchKernelGGL(bx_hold_kernel, dim3(1), dim3(64), 0, H, (uint64_t)(20000 * 100));
     if (ipc || d->flow) d->seq++;   // the flags' value of this solve (IPC transport, dataflow epochs)
     GM_HIP(hipEventRecord(d->ev_t0, H));
-    GM_TRY(bx_run(c, d, op_events));
+    GM_TRY(bx_launch(c, d, op_events));
     GM_HIP(hipEventRecord(d->ev_t1, H));
     const double t_enq = now_ms();
     // root record: the max over ranks of the owner's code (the others contribute 0); with the
@@ -1153,9 +1240,9 @@ int dist_box_solve(Ctx *c, uint64_t root) {
         BxRank &R = d->ranks[0];
         if (R.rank == ro)
             hipLaunchKernelGGL(bx_root_post_kernel, dim3(1), dim3(64), 0, H, R.table + box_index_of_key((uint32_t)root),
-                               d->d_root_words, d->n_root_words, d->seq);
-        hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, H, R.flags + bx_flag_root(d->S), d->seq << 8,
-                           BX_IPC_WAIT_TICKS, R.d_err);
+                               d->d_root_words, d->n_root_words, (const uint64_t *)d->d_seq);
+        hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, H, R.flags + bx_flag_root(d->S),
+                           (const uint64_t *)d->d_seq, 0, 8u, BX_IPC_WAIT_TICKS, R.d_err);
         uint64_t w = 0;
         uint32_t err = 0;
         GM_HIP(hipMemcpyAsync(&w, R.flags + bx_flag_root(d->S), 8, hipMemcpyDeviceToHost, H));
@@ -1354,6 +1441,7 @@ void dist_box_free(Ctx *c) {
     DistBox *d = c->dist_box;
     if (!d) return;
     (void)hipDeviceSynchronize();
+    if (d->gexec) (void)hipGraphExecDestroy(d->gexec);
     for (auto &R : d->ranks) {
         if (R.owned && R.table) (void)hipFree(R.table);
         for (void *q : {(void *)R.d_boxes, (void *)R.d_fills, (void *)R.d_srcs, (void *)R.d_dsts, (void *)R.sbuf,
@@ -1385,7 +1473,8 @@ void dist_box_free(Ctx *c) {
         if (q) (void)hipFree(q);
     for (int a = 0; a < 3; a++)
         if (d->own_comm[a] && d->comm[a]) (void)ncclCommDestroy(d->comm[a]);
-    for (void *q : {(void *)d->d_acc, (void *)d->d_root, (void *)d->d_owner, (void *)d->d_tables})
+    for (void *q : {(void *)d->d_acc, (void *)d->d_root, (void *)d->d_owner, (void *)d->d_tables, (void *)d->d_seq,
+                    (void *)d->d_scratch})
         if (q) (void)hipFree(q);
     delete d;
     c->dist_box = nullptr;

@@ -76,7 +76,10 @@ enum {
 enum {
     GM_OPT_ENGINE = 1,      /* GM_ENGINE_* */
     GM_OPT_SUB_LOW = 2,     /* SUBTRACT dense path: heaps solved per workgroup in LDS (1..4) */
-    GM_OPT_GRAPH = 3,       /* SUBTRACT dense path: replay the tier launches as a hipGraph (0/1) */
+    GM_OPT_GRAPH = 3,       /* SUBTRACT dense path: replay the tier launches as a hipGraph (0/1, default
+                               1); the split box engine with virtual ranks or GM_OPT_BOX_TRANSPORT 1
+                               captures each solve's launches once and replays them too (RCCL
+                               transport: always eager) */
     GM_OPT_TIMING = 4,      /* record HIP events around every launch of the dominant kernel (0/1); 2 = on
                                the split box engine also an event pair around every op (gm_rank_op_ms) */
     GM_OPT_VIRTUAL_RANKS = 5, /* >1: run the sharded algorithm with that many ranks inside this one

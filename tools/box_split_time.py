@@ -147,6 +147,8 @@ def main():
     ap.add_argument("--lat-us", type=float, default=15.0)
     ap.add_argument("--link-gbs", type=float, default=64.0)
     ap.add_argument("--dump", default=None, help="directory for per-G JSON dumps of the op lists and op times")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="GM_OPT_GRAPH 0: the split solves' launches eager instead of one captured graph")
     ap.add_argument("--flow", action="store_true",
                     help="the split dataflow (GM_OPT_BOX_FLOW 1): per-rank solo spans and the concurrent loopback")
     a = ap.parse_args()
@@ -171,7 +173,7 @@ def main():
         ctx = Context(_lib.GAME_SUBTRACT, (8,), device=0)
         ctx.set_stream(stream.cuda_stream)
         for k, v in ((_lib.OPT_VIRTUAL_RANKS, G), (_lib.OPT_DIST_BATCH, a.batch), (_lib.OPT_BOX_SPLIT, a.split),
-                     (_lib.OPT_DIST_SYMMETRY, a.sym), (_lib.OPT_TIMING, 1)):
+                     (_lib.OPT_DIST_SYMMETRY, a.sym), (_lib.OPT_TIMING, 1), (_lib.OPT_GRAPH, 0 if a.no_graph else 1)):
             ctx.set_option(k, v)
         ctx.solve(0xFFFFFFFF)
         ok = ctx.digest() == (ref["digest"], 1 << 32)
@@ -217,7 +219,7 @@ def main():
         worst = int(np.argmax(spans))
         by_kind = {names[k]: round(float(ms[worst][ops[worst][:, 0] == k].sum()), 4) for k in range(5)}
         counts = {names[k]: int((ops[worst][:, 0] == k).sum()) for k in range(7)}
-        line = {"ranks": G, "batch": a.batch, "split": a.split, "sym": a.sym, "digest_ok": ok,
+        line = {"ranks": G, "batch": a.batch, "split": a.split, "sym": a.sym, "graph": not a.no_graph, "digest_ok": ok,
                 "slowest_rank": worst, "slowest_ms_by_op_kind": by_kind, "slowest_op_counts": counts,
                 "solo_span_ms": [round(x, 4) for x in spans],
                 "modelled_ms_scaled_to_spans": round(max(end_s), 4),
