@@ -1166,7 +1166,11 @@ static int bx_launch(Ctx *c, DistBox *d, bool op_events) {
             d->gexec = nullptr;
         }
         hipGraph_t g = nullptr;
-        GM_HIP(hipStreamBeginCapture(H, hipStreamCaptureModeThreadLocal));
+        if (hipStreamBeginCapture(H, hipStreamCaptureModeThreadLocal) != hipSuccess) {   // e.g. a legacy stream
+            (void)hipGetLastError();
+            d->graph_bad = true;
+            return bx_run(c, d, false);
+        }
         const int rc = bx_run(c, d, false);
         const hipError_t e = hipStreamEndCapture(H, &g);
         if (rc != GM_OK) {

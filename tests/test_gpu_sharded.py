@@ -2,7 +2,8 @@
 
 GM_OPT_VIRTUAL_RANKS runs G ranks inside one context: the same partition, block / box
 lists, halo / all-to-all schedule and kernels as the one-process-per-GPU RCCL
-path, with the exchanges done by device copies (dist_sub.hip, dist_box.hip, dist_sparse.hip).
+path, with the exchanges done by device copies (dist_sub.hip, dist_sparse.hip) or by the tier
+kernel's direct stores into the receiving rank's table (dist_box.hip).
 Every sharded result must be bit-identical to the single-rank result.
 """
 import ctypes
@@ -130,8 +131,9 @@ def _plan_bytes(ranks, root=0xFFFFFFFF, **kw):
 def test_box_split_2_32_matches_oracle_digest(ranks, sym):
     """Config 5 on the box engine split over virtual ranks (csrc/dist_box.hip): every box on
     ONE rank, each rank on its own table (filled with 0xFF first, so a read of a box the rank
-    neither computed nor received would show), halo boxes exchanged per batch (device copies
-    standing in for RCCL), crossing children read through heap transpositions of own boxes
+    neither computed nor received would show), halo boxes stored by the lower rank's tier kernel
+    into the upper rank's table (an event per batch standing in for the signal; the solve
+    replayed as one captured graph), crossing children read through heap transpositions of own boxes
     with the symmetric fill (sym 1) or all received (sym 0).  The ranks' digests sum to the C
     oracle's digest of the whole table, the root record is the oracle's, every rank computed
     its plan's boxes (summing to 2^20: work_vs_one_gpu = 1), and the bytes exchanged are the
@@ -152,6 +154,38 @@ def test_box_split_2_32_matches_oracle_digest(ranks, sym):
     assert np.array_equal(ctx.query(keys), single.query(keys))
     single.close()
     ctx.close()
+
+
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_box_split_graph_and_eager_launches(ranks, monkeypatch):
+    """The split solve's launches captured once and replayed as a graph (GM_OPT_GRAPH 1, the
+    default), launched eagerly (0), and replayed with the IPC transport's flag kernels in the
+    lists (GM_BOX_SIGNAL_KERNELS=1, read when the plan is prepared): three solves each, every one
+    the oracle's digest and the plan's halo bytes; a solo rank's replay (its own graph) too."""
+    ref = _committed("subtract_8")
+    want = _plan_bytes(ranks)
+    for graph, sigk in ((1, None), (0, None), (1, "1")):
+        if sigk:
+            monkeypatch.setenv("GM_BOX_SIGNAL_KERNELS", sigk)
+        else:
+            monkeypatch.delenv("GM_BOX_SIGNAL_KERNELS", raising=False)
+        ctx = Context(SUB, (8,), device=0)
+        ctx.set_option(_lib.OPT_GRAPH, graph)
+        ctx.set_option(_lib.OPT_VIRTUAL_RANKS, ranks)
+        for _ in range(3):
+            n, rec = ctx.solve(0xFFFFFFFF)
+            assert (n, rec) == (1 << 32, ref["root_record"])
+            assert ctx.digest() == (ref["digest"], 1 << 32), (graph, sigk)
+            assert ctx.stats()["exchanged_bytes"] == want
+        ctx.set_option(_lib.OPT_DIST_SOLO, ranks)   # the top rank alone: the others' boxes stand in
+        ctx.set_option(_lib.OPT_TIMING, 1)
+        for _ in range(2):
+            ctx.solve(0xFFFFFFFF)
+            assert ctx.rank_stats()[ranks - 1]["kernel_ms"] > 0
+        ctx.set_option(_lib.OPT_DIST_SOLO, 0)
+        ctx.solve(0xFFFFFFFF)
+        assert ctx.digest() == (ref["digest"], 1 << 32)
+        ctx.close()
 
 
 def test_box_split_comparisons_2_32_matches_oracle_digest():
