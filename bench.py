@@ -625,6 +625,38 @@ def main():
         if world > 1:
             dist.barrier()
 
+    transport_fallback = None
+    if world > 1 and box and args.box_transport == "ipc":
+        # untimed probe: the IPC transport's cross-process schedule has run on hardware with the
+        # ranks sharing one GPU only.  If its first solve fails on any rank, or the summed
+        # digest is not the committed oracle digest, every rank falls back to RCCL together.
+        err = ""
+        try:
+            ctx.solve(root)
+        except _lib.GMError as e:
+            err = str(e)
+        ref = committed_digest("subtract_%d" % args.heaps) if root == (1 << (4 * args.heaps)) - 1 else None
+        if os.environ.get("GM_BENCH_PROBE_FAIL") == "1":   # test hook: report a failed probe
+            err = err or "probe failure forced (GM_BENCH_PROBE_FAIL)"
+        bad = 1.0 if err else 0.0
+        if not err and ref is not None:
+            d, nd = summed_digest(ctx, world, dist, torch)
+            bad = 0.0 if (d, nd) == (ref["digest"], ref["positions"]) else 1.0
+            err = err or ("" if not bad else "summed digest %#x differs from the committed oracle digest" % d)
+        flag = torch.tensor([bad], dtype=torch.float64, device=COLL_DEV)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item() > 0:
+            msgs = [None] * world
+            dist.all_gather_object(msgs, err)
+            transport_fallback = "IPC transport probe failed (%s)" % "; ".join(
+                "rank %d: %s" % (r, m) for r, m in enumerate(msgs) if m)
+            if not args.rehearse_one_gpu:   # (ranks sharing one GPU: RCCL refuses, nothing to fall back to)
+                transport_fallback += "; halos over RCCL instead"
+                args.box_transport = "rccl"
+                ctx.set_option(_lib.OPT_BOX_TRANSPORT, 0)
+            sys.stderr.write("bench.py rank %d: %s\n" % (rank, transport_fallback))
+            barrier()
+
     autotune = None
     if world > 1 and args.dist_batch is None:
         # untimed: the halo batch trades the upper ranks' lag (B - 1 tiers) against the
@@ -792,6 +824,7 @@ def main():
             "host_enqueue_ms_per_step_rank0": enqueue_ms / max(1, args.steps),
             "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank},
         "cpu_baseline": None,
+        "halo_transport_fallback": transport_fallback,
         "rehearsal": ("--rehearse-one-gpu: %d ranks sharing ONE GPU (gloo for bench.py's collectives, IPC transport "
                       "for the halos); not a multi-GPU measurement" % world if args.rehearse_one_gpu else None),
     }

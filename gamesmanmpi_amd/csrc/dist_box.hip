@@ -452,6 +452,9 @@ __global__ void bx_flag_set_kernel(uint64_t *flag, const uint64_t *seqp) {
 __global__ void bx_flag_wait_kernel(const uint64_t *flag, const uint64_t *seqp, int add, uint32_t shift, uint64_t ticks,
                                     uint32_t *err) {
     if (threadIdx.x) return;
+    // a wait of this solve already timed out: the rest return at once (one 30 s wait per solve
+    // at most, not one per batch)
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const int64_t w = (int64_t)*seqp + add;
     const uint64_t want = w > 0 ? (uint64_t)w << shift : 0u;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
