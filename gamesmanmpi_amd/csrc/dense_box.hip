@@ -61,6 +61,9 @@ typedef uint16_t bx_u16x2 __attribute__((ext_vector_type(2)));
 #ifndef GM_BOX_STORE_CPOL
 #define GM_BOX_STORE_CPOL 16   // sc1 write-through: a stored box is next read a launch later
 #endif
+#ifndef GM_BOX_TIER_STORE_CPOL
+#define GM_BOX_TIER_STORE_CPOL GM_BOX_STORE_CPOL   // the tier launches' own (the dataflow kernels keep sc1)
+#endif
 #ifndef GM_BOX_WAVES
 #define GM_BOX_WAVES 2         // waves per SIMD the register budget must allow
 #endif
@@ -571,7 +574,7 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
 // DIRECT (loopback and IPC transports): the box goes straight to its slot in the receiving
 // rank's own table (peer p0..p2 by axis, slot kind << 28 | axis << 26), rows where they lie,
 // so the receiver needs no unpack.
-template <bool SHARD_, bool DIRECT = false>
+template <bool SHARD_, bool DIRECT = false, int CP = GM_BOX_STORE_CPOL>
 __device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, uint8_t *p0, uint8_t *p1, uint8_t *p2,
                                          const BxGroup &G, const uint32_t *s, uint32_t lane) {
     constexpr bool SHARD = SHARD_ && !(GM_BOX_EXP & 32);
@@ -601,8 +604,8 @@ __device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, uint8_t *
             o[0][q] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
             o[1][q] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
         }
-        __builtin_amdgcn_raw_buffer_store_b128(o[0], w[0], 16u * m, 0, GM_BOX_STORE_CPOL);
-        __builtin_amdgcn_raw_buffer_store_b128(o[1], w[1], 16u * m, 0, GM_BOX_STORE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(o[0], w[0], 16u * m, 0, CP);
+        __builtin_amdgcn_raw_buffer_store_b128(o[1], w[1], 16u * m, 0, CP);
         if constexpr (SHARD && DIRECT) {
 #pragma unroll
             for (int k = 0; k < 2; k++)
@@ -615,7 +618,7 @@ __device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, uint8_t *
                         __builtin_amdgcn_make_buffer_rsrc(pb + ((uint64_t)G.box[k] << 12), 0, 4096u, 0x00020000);
                     const uint32_t a = (m >> (2u * ((kind - 1u) & 3u))) & 3u;
                     if (kind == 5 || a >= 2u)
-                        __builtin_amdgcn_raw_buffer_store_b128(o[k], wp, 16u * m, 0, GM_BOX_STORE_CPOL);
+                        __builtin_amdgcn_raw_buffer_store_b128(o[k], wp, 16u * m, 0, CP);
                 }
         } else if constexpr (SHARD) {
 #pragma unroll
@@ -715,7 +718,7 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 #if GM_BOX_TRACE
         BX_STAMP(tt[3]);
 #endif
-        bx_store<SHARD, DIRECT>(table, msg, p0, p1, p2, G, s, ln);
+        bx_store<SHARD, DIRECT, GM_BOX_TIER_STORE_CPOL>(table, msg, p0, p1, p2, G, s, ln);
         BX_LDS_ORDER();
 #if GM_BOX_TRACE
         BX_STAMP(tt[4]);
