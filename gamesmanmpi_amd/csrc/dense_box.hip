@@ -437,8 +437,11 @@ __device__ __forceinline__ void bx_unroll(F &f, std::integer_sequence<int, I...>
 // before it takes by DPP (row_shr 1, 2, 4, 8 inside a 16-lane row), and two steps after
 // the lanes one b2 / b3 step below (the rows 16 and 32 lanes down), whose codes it reads
 // from the image, fetched two steps ahead.
+#ifndef GM_BOX_WALK_B01
+#define GM_BOX_WALK_B01 0   // 1: the b0 / b1 neighbours from the image too (no DPP; d = S2 popc(b) + a0)
+#endif
 constexpr int BX_S2 = 2;
-constexpr int BX_DMAX = 2 + 2 * BX_S2 + 3;   // latest start
+constexpr int BX_DMAX = GM_BOX_WALK_B01 ? 4 * BX_S2 + 3 : 2 + 2 * BX_S2 + 3;   // latest start
 constexpr int BX_STEPS = 64 + BX_DMAX;
 #ifndef GM_BOX_FAHEAD
 #define GM_BOX_FAHEAD 4   // the fold value of a step is read from LDS this many steps ahead
@@ -464,7 +467,8 @@ struct BxLaneC {
 __device__ __forceinline__ BxLaneC bx_lane_consts(uint32_t lane) {
     BxLaneC L;
     const uint32_t a0 = lane & 3u, b = (lane >> 2) & 15u;
-    const int d = (int)__popc(b & 3u) + BX_S2 * (int)__popc(b & 12u) + (int)a0;
+    const int d = GM_BOX_WALK_B01 ? BX_S2 * (int)__popc(b) + (int)a0
+                                  : (int)__popc(b & 3u) + BX_S2 * (int)__popc(b & 12u) + (int)a0;
     L.d = d;
     L.m01 = a0 >= 1 ? ~0u : 0u;
     L.m02 = a0 >= 2 ? ~0u : 0u;
@@ -503,6 +507,7 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
     const uint32_t a0 = ln & 3u, b = (ln >> 2) & 15u;
     const int base = (int)((uint32_t)BX_AS * a0 + b) - BX_PITCH * d, zb = BX_Z - BX_PITCH * d;
     const int base2 = (b & 4u) ? base - 4 : zb, base3 = (b & 8u) ? base - 8 : zb;
+    const int base0 = (b & 1u) ? base - 1 : zb, base1 = (b & 2u) ? base - 2 : zb;
     const int dummy = BX_IMG + (int)ln;   // idle steps (before d, after d + 63) use a slot of their own
     // this lane's codes as (a1 - 1, a1 - 2, a2 - 1, a2 - 2) children of the positions 1, 2,
     // 4 and 8 steps later, masked when they are made (0 where the digit wraps): rings by step
@@ -519,8 +524,15 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
     };
     // LDS inputs: the fold (nothing in the walk writes it before its step), FA steps
     // ahead; the b2 / b3 neighbours' codes, made S2 steps before they are needed
+#if GM_BOX_WALK_B01
+    struct In { uint32_t C2, C3, C0, C1; };
+    auto fetchc = [&](auto TT) { return In{s[slot(TT, base2)], s[slot(TT, base3)], s[slot(TT, base0)], s[slot(TT, base1)]}; };
+#else
     struct In { uint32_t C2, C3; };
     auto fetchc = [&](auto TT) { return In{s[slot(TT, base2)], s[slot(TT, base3)]}; };
+    (void)base0;
+    (void)base1;
+#endif
     auto fetchf = [&](auto TT) { return s[slot(TT, base)]; };
     uint32_t pff[BX_FA];
     In pfc[BX_S2];
@@ -538,9 +550,15 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
         // the step-to-step chain: the a0 - 1, b0 and b1 neighbours' codes of the step
         // before (DPP), this lane's own (the a1 - 1 child), the b2 / b3 neighbours (LDS)
         const uint32_t hb = hk[(T + 31) & 31];
-        const uint32_t y1 = bx_dpp_shr<0x111>(hb) & m01, c0 = bx_dpp_shr<0x114>(hb) & mb0, c1 = bx_dpp_shr<0x118>(hb);
+        const uint32_t y1 = bx_dpp_shr<0x111>(hb) & m01;
         const In cn = pfc[T % BX_S2];
+#if GM_BOX_WALK_B01
+        const uint32_t m = bx_max3(bx_max3(bx_max3(pre, cn.C2, cn.C3), y1, cn.C0), cn.C1, g1);
+        (void)mb0;
+#else
+        const uint32_t c0 = bx_dpp_shr<0x114>(hb) & mb0, c1 = bx_dpp_shr<0x118>(hb);
         const uint32_t m = bx_max3(bx_max3(bx_max3(pre, cn.C2, cn.C3), y1, c0), c1, g1);
+#endif
         if constexpr (T + 1 < BX_STEPS) {
             constexpr int U = T + 1;
             const uint32_t y2 = bx_dpp_shr<0x112>(hb) & m02;   // the a0 - 2 neighbour of step U: its code of step U - 2
