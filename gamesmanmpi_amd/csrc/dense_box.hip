@@ -464,11 +464,11 @@ struct BxLaneC {
     uint32_t m01, m02, mb0;                  // a0 - 1 / a0 - 2 / b0 neighbour validity
     uint32_t v11, v12, v21[4], v22[4];       // (a1, a2) child validity bytes by step phase
 };
-__device__ __forceinline__ BxLaneC bx_lane_consts(uint32_t lane) {
+__device__ __forceinline__ BxLaneC bx_lane_consts(uint32_t lane, int dadd = 0) {
     BxLaneC L;
     const uint32_t a0 = lane & 3u, b = (lane >> 2) & 15u;
-    const int d = GM_BOX_WALK_B01 ? BX_S2 * (int)__popc(b) + (int)a0
-                                  : (int)__popc(b & 3u) + BX_S2 * (int)__popc(b & 12u) + (int)a0;
+    const int d = dadd + (GM_BOX_WALK_B01 ? BX_S2 * (int)__popc(b) + (int)a0
+                                          : (int)__popc(b & 3u) + BX_S2 * (int)__popc(b & 12u) + (int)a0);
     L.d = d;
     L.m01 = a0 >= 1 ? ~0u : 0u;
     L.m02 = a0 >= 2 ? ~0u : 0u;
@@ -592,9 +592,11 @@ __device__ __forceinline__ void bx_walk(uint32_t *s, uint32_t ln, const BxLaneC 
 // DIRECT (loopback and IPC transports): the box goes straight to its slot in the receiving
 // rank's own table (peer p0..p2 by axis, slot kind << 28 | axis << 26), rows where they lie,
 // so the receiver needs no unpack.
-template <bool SHARD_, bool DIRECT = false, int CP = GM_BOX_STORE_CPOL>
+// (NI rows per lane from row set i0: the one-wave kernel stores all four, a wave of the
+// four-wave kernel its own.)
+template <bool SHARD_, bool DIRECT = false, int CP = GM_BOX_STORE_CPOL, int NI = 4>
 __device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, uint8_t *p0, uint8_t *p1, uint8_t *p2,
-                                         const BxGroup &G, const uint32_t *s, uint32_t lane) {
+                                         const BxGroup &G, const uint32_t *s, uint32_t lane, uint32_t i0 = 0) {
     constexpr bool SHARD = SHARD_ && !(GM_BOX_EXP & 32);
     __amdgpu_buffer_rsrc_t w[2];
 #pragma unroll
@@ -611,8 +613,8 @@ __device__ __forceinline__ void bx_store(uint8_t *table, uint8_t *msg, uint8_t *
             for (int e = 0; e < 3; e++) dst[k][e] = (uint32_t)__builtin_amdgcn_readlane((int)G.dstv, 4 * k + e);
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint32_t m = lane + 64u * i;
+    for (int ii = 0; ii < NI; ii++) {
+        const uint32_t m = lane + 64u * (i0 + (uint32_t)ii);
         bx_u32x4 o[2];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -763,6 +765,213 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 #endif
 }
 
+
+// ---------------------------------------------------------------------------
+// Thin box-tiers (round 5): one group per workgroup of FOUR waves.  A lone group of the
+// one-wave kernel is a latency chain of ~8.5 µs (48 child loads, the fold of all 256 rows,
+// 73 walk steps, the store), and a box-tier with fewer groups than the chip has SIMDs pays
+// it whole (§9.1: 12 of the 41 box-tiers at N = 1, 14 of a rank's 33 at G = 8).  Here wave w
+// owns the rows with a3 = w (A = lane + 64 w): it loads only its rows' children (8 B-child
+// rows, the top layers of the boxes below along heaps 0-2 -- a row takes them by its own
+// digit, the others are zeroed in the pairing -- and along heap 3 when w < 2), folds them,
+// walks p' = 0..15 of its quarter (p = 16 w + p') and stores it.  Its a3 - 1 / a3 - 2
+// children are the codes waves w - 1 / w - 2 made BX4_L / 2 BX4_L steps before: the waves run
+// BX4_L steps apart and a workgroup barrier ends every step, so a step's codes are visible
+// to the other waves' prefetches that follow it (read from the image like the b2 / b3
+// neighbours).  31 walk steps instead of 73.
+constexpr int BX4_L = BX_S2;   // lag between consecutive waves, >= the prefetch distance
+constexpr int BX4_STEPS = 16 + BX_DMAX + 3 * BX4_L;
+constexpr int BX4_NLOAD = 24;
+
+// 16 u16 pairs of two rows, or zeros where the lane does not take them (per-lane selectors)
+__device__ __forceinline__ void bx_pairs_if(const bx_u32x4 &x0, const bx_u32x4 &x1, bool take, uint32_t (&p)[16]) {
+    uint32_t sel[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+        sel[r] = take ? ((uint32_t)r | 0x0c00u | ((4u + (uint32_t)r) << 16) | 0x0c000000u) : 0x0c0c0c0cu;
+#pragma unroll
+    for (int b = 0; b < 16; b++) p[b] = __builtin_amdgcn_perm(x1[b >> 2], x0[b >> 2], sel[b & 3]);
+}
+
+// R[4 k + j]: row m of box k's child along heap 4 + j; R[8 + 4 i + 2 k + v]: row m with digit i
+// set to 3 - v of box k's child along heap i (i < 3); R[20 + 2 k + v]: heap 3's (w < 2)
+template <bool SHARD>
+__device__ __forceinline__ void bx4_issue(const uint8_t *table, const BxGroup &G, uint32_t lane, uint32_t w,
+                                          bx_u32x4 (&R)[BX4_NLOAD]) {
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0xFFFFFFFFu, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc((void *)table, 0, 0u, 0x00020000);
+    const uint32_t m = lane + 64u * w;
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const bool ok = G.valid[k] && box_coord(G.box[k], 4 + j) >= 1;
+            uint32_t src = G.box[k] - box_unit(4 + j);
+            if constexpr (SHARD) src = bx_src<SHARD>(G, k, 4 + j);
+            R[4 * k + j] = __builtin_bit_cast(bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(ok ? rt : rz, 16u * m,
+                                                                                              ok ? src << 12 : 0u, 0));
+        }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            // heap 3: only the rows a3 = 0 (layers 3, 2) and a3 = 1 (layer 3) take children (uniform)
+            const bool ok = G.valid[k] && box_coord(G.box[k], i) >= 1 && (i < 3 || w < 2u);
+            uint32_t src = G.box[k] - box_unit(i), sq = 0, sp = 0;
+            if constexpr (SHARD) {
+                const uint32_t code = bx_fcode(G, k, i);
+                src = bx_src<SHARD>(G, k, i);
+                sq = 2u * (code >> 2);
+                sp = 2u * (code & 3u);
+            }
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                uint32_t A = (m & ~(3u << (2 * i))) | ((3u - v) << (2 * i));
+                if constexpr (SHARD) {
+                    const uint32_t t = ((A >> sq) ^ (A >> sp)) & 3u;
+                    A ^= (t << sq) | (t << sp);
+                }
+                R[8 + 4 * i + 2 * k + v] = __builtin_bit_cast(
+                    bx_u32x4, __builtin_amdgcn_raw_buffer_load_b128(ok ? rt : rz, 16u * A, ok ? src << 12 : 0u, 0));
+            }
+        }
+}
+
+template <bool SHARD>
+__device__ __forceinline__ void bx4_fold(uint32_t *s, const BxGroup &G, uint32_t lane, uint32_t w,
+                                         bx_u32x4 (&R)[BX4_NLOAD]) {
+    if constexpr (SHARD) {   // B children read through a B transposition: back to C's byte order
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t code = bx_fcode(G, k, 4 + j);
+                if (code) R[4 * k + j] = bx_bswap_row(R[4 * k + j], code);
+            }
+    }
+    uint32_t F[16];
+#pragma unroll
+    for (int jp = 0; jp < 4; jp += 2) {   // as bx_fold: two B heaps at a time
+        uint32_t P[16], Q[16];
+        bx_pairs(R[jp], R[4 + jp], P);
+        bx_pairs(R[jp + 1], R[4 + jp + 1], Q);
+#pragma unroll
+        for (int b = 0; b < 16; b++) {
+            uint32_t in[5];
+            int n = 0;
+            if (jp) in[n++] = F[b];
+            in[n++] = P[b];
+            in[n++] = Q[b];
+            if (!((b >> jp) & 1)) in[n++] = P[b | (1 << jp)];
+            if (!((b >> (jp + 1)) & 1)) in[n++] = Q[b | (2 << jp)];
+            uint32_t f = n >= 3 ? bx_max3(in[0], in[1], in[2]) : bx_max2(in[0], in[1]);
+            if (n == 4) f = bx_max2(f, in[3]);
+            if (n == 5) f = bx_max3(f, in[3], in[4]);
+            F[b] = f;
+        }
+    }
+    const uint32_t m = lane + 64u * w;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        // the row's digit a_i: 0 takes layers 3 and 2 of the box below, 1 layer 3, else none
+        const uint32_t a = (m >> (2 * i)) & 3u;
+        uint32_t L3[16], L2[16];
+        bx_pairs_if(R[8 + 4 * i + 0], R[8 + 4 * i + 2], a <= 1u, L3);
+        bx_pairs_if(R[8 + 4 * i + 1], R[8 + 4 * i + 3], a == 0u, L2);
+#pragma unroll
+        for (int b = 0; b < 16; b++) F[b] = bx_max3(F[b], L3[b], L2[b]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        *(bx_u32x4 *)(s + bx_row(m) + 4u * q) = bx_u32x4{F[4 * q], F[4 * q + 1], F[4 * q + 2], F[4 * q + 3]};
+}
+
+// bx_walk for wave w's quarter (p' = 0..15, p = 16 w + p'), a barrier per step
+__device__ __forceinline__ void bx4_walk(uint32_t *s, uint32_t ln, uint32_t w, const BxLaneC &L) {
+    const int d = L.d;   // this lane's start, BX4_L w later than in wave 0
+    const uint32_t m01 = L.m01, m02 = L.m02, mb0 = L.mb0;
+    const uint32_t v11 = L.v11, v12 = L.v12;
+    const uint32_t v21[4] = {L.v21[0], L.v21[1], L.v21[2], L.v21[3]};
+    const uint32_t v22[4] = {L.v22[0], L.v22[1], L.v22[2], L.v22[3]};
+    const uint32_t a0 = ln & 3u, b = (ln >> 2) & 15u;
+    // position (A = a0 + 4 p, B = b), p = 16 w + T - d, at dword base + PITCH T
+    const int base = (int)((uint32_t)BX_AS * a0 + b) + BX_PITCH * (16 * (int)w - d);
+    const int zb = BX_Z + BX_PITCH * (16 * (int)w - d);
+    const int base2 = (b & 4u) ? base - 4 : zb, base3 = (b & 8u) ? base - 8 : zb;
+    const int base31 = w >= 1u ? base - 16 * BX_PITCH : zb, base32 = w >= 2u ? base - 32 * BX_PITCH : zb;
+    const int dummy = BX_IMG + (int)ln;
+    uint32_t g1 = 0, g2[2] = {0, 0}, g4[4] = {0, 0, 0, 0}, g8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t hb = 0;   // this lane's code of the step before (the DPP source)
+    auto slot = [&](auto TT, int bs) {
+        constexpr int T = decltype(TT)::v;
+        const int idx = bs + BX_PITCH * T;
+        return (uint32_t)(T - d) < 16u ? idx : dummy;
+    };
+    struct In { uint32_t C2, C3, A1, A2; };
+    auto fetchc = [&](auto TT) {
+        return In{s[slot(TT, base2)], s[slot(TT, base3)], s[slot(TT, base31)], s[slot(TT, base32)]};
+    };
+    auto fetchf = [&](auto TT) { return s[slot(TT, base)]; };
+    uint32_t pff[BX_FA];
+    In pfc[BX_S2];
+    auto firstf = [&](auto TT) { pff[decltype(TT)::v] = fetchf(TT); };
+    bx_unroll(firstf, std::make_integer_sequence<int, BX_FA>{});
+    auto firstc = [&](auto TT) { pfc[decltype(TT)::v] = fetchc(TT); };
+    bx_unroll(firstc, std::make_integer_sequence<int, BX_S2>{});
+    uint32_t pre = bx_max3(pff[0], pfc[0].A1, pfc[0].A2);
+    auto step = [&](auto TT) {
+        constexpr int T = decltype(TT)::v;
+        const uint32_t y1 = bx_dpp_shr<0x111>(hb) & m01, c0 = bx_dpp_shr<0x114>(hb) & mb0, c1 = bx_dpp_shr<0x118>(hb);
+        const In cn = pfc[T % BX_S2];
+        const uint32_t mx = bx_max3(bx_max3(bx_max3(pre, cn.C2, cn.C3), y1, c0), c1, g1);
+        if constexpr (T + 1 < BX4_STEPS) {
+            constexpr int U = T + 1;
+            const uint32_t y2 = bx_dpp_shr<0x112>(hb) & m02;
+            const In cu = pfc[U % BX_S2];
+            const uint32_t q = bx_max3(pff[U % BX_FA], g2[U & 1], g4[U & 3]);
+            pre = bx_max3(bx_max3(q, g8[U & 7], y2), cu.A1, cu.A2);
+        }
+        uint32_t c = bx_code2(mx);
+        c = (uint32_t)(T - d) < 16u ? c : 0u;
+        hb = c;
+        g1 = bx_and_byte<(T + 1) & 3>(c, v11);
+        g2[T & 1] = bx_and_byte<(T + 2) & 3>(c, v12);
+        g4[T & 3] = bx_and_byte<(T + 4) & 3>(c, v21[((T + 4) >> 2) & 3]);
+        g8[T & 7] = bx_and_byte<(T + 8) & 3>(c, v22[((T + 8) >> 2) & 3]);
+        s[slot(TT, base)] = c;
+        __syncthreads();   // this step's codes, for the other waves' prefetches below
+        if constexpr (T + BX_FA < BX4_STEPS) pff[T % BX_FA] = fetchf(BxT<T + BX_FA>{});
+        if constexpr (T + BX_S2 < BX4_STEPS) pfc[T % BX_S2] = fetchc(BxT<T + BX_S2>{});
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    bx_unroll(step, std::make_integer_sequence<int, BX4_STEPS>{});
+}
+
+template <bool SHARD, bool DIRECT = false, bool FILL = true>
+__global__ __launch_bounds__(256) void box_tier4_kernel(uint8_t *__restrict__ table, const uint32_t *__restrict__ boxes,
+                                                        const uint32_t *__restrict__ fills,
+                                                        const uint32_t *__restrict__ srcs,
+                                                        const uint32_t *__restrict__ dsts, uint8_t *__restrict__ msg,
+                                                        uint8_t *p0, uint8_t *p1, uint8_t *p2, uint32_t nbox) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[BX_LDS];
+    uint32_t *s = lds + BX_PAD;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint32_t ng = (nbox + 1) / 2;
+    constexpr bool SF = SHARD && FILL;
+    const BxLaneC L = bx_lane_consts(lane, BX4_L * (int)w);
+    if (lane < 16u) s[BX_PITCH * (16u * w + lane) + BX_Z] = 0;   // this wave's rows' zero slots
+    for (uint32_t g = blockIdx.x; g < ng; g += gridDim.x) {
+        const BxGroup G = bx_group<SHARD, FILL>(boxes, fills, srcs, dsts, nbox, g, lane);
+        bx_u32x4 R[BX4_NLOAD];
+        bx4_issue<SF>(table, G, lane, w, R);
+        bx4_fold<SF>(s, G, lane, w, R);
+        BX_LDS_ORDER();
+        bx4_walk(s, lane, w, L);
+        bx_store<SHARD, DIRECT, GM_BOX_TIER_STORE_CPOL, 1>(table, msg, p0, p1, p2, G, s, lane, w);
+        BX_LDS_ORDER();
+    }
+}
 
 // ---------------------------------------------------------------------------
 // One-launch (dataflow) solve, GM_BOX_FLOW: the box-tier launches' groups, tier after
@@ -1125,9 +1334,34 @@ static int box_resident(const void *kernel, int device, size_t dyn) {
 }
 int box_grid_cap(int device) { return box_resident((const void *)box_tier_kernel<true>, device, 0); }
 
+// Box-tiers of at most this many groups run the four-wave kernel (GM_BOX_THIN_GROUPS, development;
+// default 0 = never: measured no faster -- a thin launch's ~9 µs is not its walk, §9.1)
+uint32_t box_thin_groups() {
+    static const uint32_t v = getenv("GM_BOX_THIN_GROUPS") ? (uint32_t)strtoul(getenv("GM_BOX_THIN_GROUPS"), nullptr, 10)
+                                                           : 0u;
+    return v;
+}
+
 void box_launch_tier_split(uint32_t grid, uint8_t *table, const uint32_t *boxes, const uint32_t *fills,
                            const uint32_t *srcs, const uint32_t *dsts, uint8_t *msg, uint8_t *const *peers,
                            uint32_t nbox, bool fill, hipStream_t s) {
+    const uint32_t ng = (nbox + 1) / 2;
+    if (ng <= box_thin_groups()) {   // a thin box-tier: the four-wave kernel, one group per workgroup
+        uint8_t *q0 = peers ? peers[0] : nullptr, *q1 = peers ? peers[1] : nullptr, *q2 = peers ? peers[2] : nullptr;
+        if (peers && fill)
+            hipLaunchKernelGGL((box_tier4_kernel<true, true, true>), dim3(ng), dim3(256), 0, s, table, boxes, fills, srcs,
+                               dsts, nullptr, q0, q1, q2, nbox);
+        else if (peers)
+            hipLaunchKernelGGL((box_tier4_kernel<true, true, false>), dim3(ng), dim3(256), 0, s, table, boxes, fills, srcs,
+                               dsts, nullptr, q0, q1, q2, nbox);
+        else if (fill)
+            hipLaunchKernelGGL((box_tier4_kernel<true, false, true>), dim3(ng), dim3(256), 0, s, table, boxes, fills, srcs,
+                               dsts, msg, nullptr, nullptr, nullptr, nbox);
+        else
+            hipLaunchKernelGGL((box_tier4_kernel<true, false, false>), dim3(ng), dim3(256), 0, s, table, boxes, fills, srcs,
+                               dsts, msg, nullptr, nullptr, nullptr, nbox);
+        return;
+    }
     if (peers && fill)
         hipLaunchKernelGGL((box_tier_kernel<true, true, true>), dim3(grid), dim3(64), 0, s, table, boxes, fills, srcs,
                            dsts, nullptr, peers[0], peers[1], peers[2], nbox);
@@ -1342,6 +1576,13 @@ static int box_launch_tiers(Ctx *c, DenseBox *d) {
         const uint32_t nb = d->tier_off[t + 1] - d->tier_off[t];
         if (!nb) continue;
         const uint32_t ng = (nb + 1) / 2;
+        if (ng <= box_thin_groups()) {   // a thin box-tier: the four-wave kernel, one group per workgroup
+            hipLaunchKernelGGL(box_tier4_kernel<false>, dim3(ng), dim3(256), 0, c->stream, d->table,
+                               d->d_boxes + d->tier_off[t], (const uint32_t *)nullptr, (const uint32_t *)nullptr,
+                               (const uint32_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr, (uint8_t *)nullptr,
+                               (uint8_t *)nullptr, nb);
+            continue;
+        }
         // at least 8 workgroups (one per XCD run), at most the resident capacity
         const uint32_t grid = std::max<uint32_t>(8u, std::min<uint32_t>(ng, (uint32_t)d->grid_cap));
         hipLaunchKernelGGL(box_tier_kernel<false>, dim3(grid), dim3(64), 0, c->stream, d->table,

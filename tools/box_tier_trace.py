@@ -35,7 +35,7 @@ def main():
     rows = []
     for f in glob.glob(a.trace + "/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "box_tier_kernel<false>" in r["Kernel_Name"]:
+            if "box_tier_kernel<false" in r["Kernel_Name"] or "box_tier4_kernel<false" in r["Kernel_Name"]:
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     rows.sort()
     n = len(rows) // 41
