@@ -1336,10 +1336,9 @@ int box_grid_cap(int device) { return box_resident((const void *)box_tier_kernel
 
 // Box-tiers of at most this many groups run the four-wave kernel (GM_BOX_THIN_GROUPS, development;
 // default 0 = never: measured no faster -- a thin launch's ~9 µs is not its walk, §9.1)
-uint32_t box_thin_groups() {
-    static const uint32_t v = getenv("GM_BOX_THIN_GROUPS") ? (uint32_t)strtoul(getenv("GM_BOX_THIN_GROUPS"), nullptr, 10)
-                                                           : 0u;
-    return v;
+uint32_t box_thin_groups() {   // (read per launch: the launches are enqueued once per captured graph)
+    const char *e = getenv("GM_BOX_THIN_GROUPS");
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
 }
 
 void box_launch_tier_split(uint32_t grid, uint8_t *table, const uint32_t *boxes, const uint32_t *fills,

@@ -188,6 +188,19 @@ def test_box_split_graph_and_eager_launches(ranks, monkeypatch):
         ctx.close()
 
 
+def test_box_four_wave_thin_tiers(monkeypatch):
+    """GM_BOX_THIN_GROUPS (development): box-tiers of at most that many groups run the four-wave
+    kernel (box_tier4_kernel) -- at N = 1 and on every split variant (messages, direct stores,
+    with and without fills) -- and every table is still the oracle's."""
+    ref = _committed("subtract_8")
+    monkeypatch.setenv("GM_BOX_THIN_GROUPS", "1000")
+    for ranks, sym in ((1, 1), (2, 1), (8, 1), (8, 0)):
+        ctx, n, rec = _solve(SUB, (8,), ranks, dist_symmetry=sym)
+        assert (n, rec) == (1 << 32, ref["root_record"])
+        assert ctx.digest() == (ref["digest"], 1 << 32), (ranks, sym)
+        ctx.close()
+
+
 def test_box_split_comparisons_2_32_matches_oracle_digest():
     """GM_OPT_BOX_SPLIT 1 (tier-balanced comparisons; not the default, tests/test_box_plan.py
     says why) gives the oracle's digest at 2, 4 and 8 ranks."""
