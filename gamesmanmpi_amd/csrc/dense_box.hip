@@ -779,7 +779,11 @@ __global__ __launch_bounds__(64, GM_BOX_WAVES) void box_tier_kernel(uint8_t *__r
 // BX4_L steps apart and a workgroup barrier ends every step, so a step's codes are visible
 // to the other waves' prefetches that follow it (read from the image like the b2 / b3
 // neighbours).  31 walk steps instead of 73.
-constexpr int BX4_L = BX_S2;   // lag between consecutive waves, >= the prefetch distance
+#ifndef GM_BOX4_K
+#define GM_BOX4_K 1   // a workgroup barrier every K steps
+#endif
+constexpr int BX4_K = GM_BOX4_K;
+constexpr int BX4_L = BX_S2 + BX4_K - 1;   // lag between consecutive waves: a prefetch sees the code
 constexpr int BX4_STEPS = 16 + BX_DMAX + 3 * BX4_L;
 constexpr int BX4_NLOAD = 24;
 
@@ -939,7 +943,10 @@ __device__ __forceinline__ void bx4_walk(uint32_t *s, uint32_t ln, uint32_t w, c
         g4[T & 3] = bx_and_byte<(T + 4) & 3>(c, v21[((T + 4) >> 2) & 3]);
         g8[T & 7] = bx_and_byte<(T + 8) & 3>(c, v22[((T + 8) >> 2) & 3]);
         s[slot(TT, base)] = c;
-        __syncthreads();   // this step's codes, for the other waves' prefetches below
+        if constexpr ((T + 1) % BX4_K == 0)
+            __syncthreads();   // the codes so far, for the other waves' prefetches below
+        else
+            BX_LDS_ORDER();
         if constexpr (T + BX_FA < BX4_STEPS) pff[T % BX_FA] = fetchf(BxT<T + BX_FA>{});
         if constexpr (T + BX_S2 < BX4_STEPS) pfc[T % BX_S2] = fetchc(BxT<T + BX_S2>{});
         __builtin_amdgcn_sched_barrier(0);
