@@ -27,7 +27,12 @@ Keys:
   four_to_one: the pile as a signed int64 (stored two's complement in u64);
   ttt:         sum of c * 3**(x + 3y), c = 0 blank, 1 X / player 1, 2 O / player 2;
   toot:        the first 2A+16 bits of the position string (planes + hands), MSB-first;
-  othello:     all 2A+16 bits of the position string, MSB-first.
+  othello:     all 2A+16 bits of the position string, MSB-first;
+  othello 8x8: the first 8 bytes of blake2b(position string bytes), big-endian (2A+16 = 144
+               bits do not fit a u64; tests/plugins/othello8_endgame.py).
+
+``--only othello8`` writes just the 8x8 endgame fixture (othello_8x8_endgame.npz) and its
+entry in roots.json.
 """
 import argparse
 import importlib.util
@@ -95,6 +100,30 @@ def key_bits(nkeep):
     return k
 
 
+def key_blake8(pos):
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(pos.encode("ISO-8859-1"), digest_size=8).digest(), "big")
+
+
+# tests/plugins/othello8_endgame.py's root: the reference's default 8x8 board after a fixed
+# random playout from the start (seed 5), 10 empty squares left
+OTHELLO8_ENDGAME_HEX = "303800204018057a4646bfdebfe6fa800200"
+
+
+def othello8_endgame(canonical, ref_utils, roots):
+    oth = _load("game_module", os.path.join(REF, "test_games/othello_bit_new.py"))   # 8x8 as shipped
+    ref_utils.game_module = oth
+    assert (oth.length, oth.height) == (8, 8)
+    root = bytes.fromhex(OTHELLO8_ENDGAME_HEX).decode("latin-1")
+    t0 = time.time()
+    table, positions = canonical.solve(oth, root)
+    save_table("othello_8x8_endgame", table, positions, key_blake8,
+               {"game": "othello_bit_new", "dims": [8, 8], "root_hex": OTHELLO8_ENDGAME_HEX, "key": "blake2b-8"})
+    v, r = table[canonical.default_key(root)]
+    roots["othello_8x8_endgame"] = {"root_hex": OTHELLO8_ENDGAME_HEX, "canonical": canonical.root_line(v, r),
+                                    "positions": len(table), "seconds": round(time.time() - t0, 1)}
+
+
 def save_table(name, table, positions, keyfn, meta):
     keys = np.empty(len(table), dtype=np.uint64)
     recs = np.empty(len(table), dtype=np.uint16)
@@ -117,12 +146,21 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--live", action="store_true")
     ap.add_argument("--skip-big", action="store_true")
+    ap.add_argument("--only", choices=("othello8",), default=None)
     args = ap.parse_args()
     _install_stubs()
     import canonical
     import src.utils as ref_utils
 
     roots = {}
+    if args.only == "othello8":
+        path = os.path.join(HERE, "roots.json")
+        roots = json.load(open(path))
+        othello8_endgame(canonical, ref_utils, roots)
+        with open(path, "w") as f:
+            json.dump(roots, f, indent=1, sort_keys=True)
+        print(json.dumps(roots["othello_8x8_endgame"], indent=1))
+        return
 
     def root_line(table, positions, root, keyfn=None):
         v, r = table[canonical.default_key(root)]
@@ -203,6 +241,8 @@ def main():
         roots[name] = {"root_hex": root.encode("latin-1").hex(),
                        "canonical": root_line(table, positions, root),
                        "positions": len(table), "seconds": round(time.time() - t0, 1)}
+
+    othello8_endgame(canonical, ref_utils, roots)
 
     with open(os.path.join(HERE, "roots.json"), "w") as f:
         json.dump(roots, f, indent=1, sort_keys=True)

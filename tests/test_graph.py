@@ -80,6 +80,30 @@ def test_graph_engine_matches_canonical_oracle_on_new_plugins(rel):
 
 
 @pytest.mark.gpu
+def test_graph_engine_othello_8x8_endgame_matches_golden():
+    """Othello on the reference's default 8x8 board from an endgame root (10 empty squares,
+    56,552 positions; 144-bit positions no device descriptor holds): the solver takes the
+    explicit-graph path on its own (host walk with the plugin's functions, GPU resolve), and
+    every record equals the golden table of the REFERENCE's plugin from the same root."""
+    import hashlib
+    import json
+    from conftest import GOLDEN
+    from gamesmanmpi_amd import Solver
+    mod = load_plugin("tests/plugins/othello8_endgame.py")
+    s = Solver(mod, device=0)
+    n, rec = s.solve()
+    keys, recs = golden("othello_8x8_endgame")
+    assert s.ctx.stats()["engine"] == 5 and n == len(keys)
+    idx, r = s.table()
+    blake = [int.from_bytes(hashlib.blake2b(s.codec.pos(i).encode("ISO-8859-1"), digest_size=8).digest(), "big")
+             for i in idx.tolist()]
+    assert dict(zip(blake, r.tolist())) == dict(zip(keys.tolist(), recs.tolist()))
+    roots = json.load(open(os.path.join(GOLDEN, "roots.json")))
+    assert s.root_line() == roots["othello_8x8_endgame"]["canonical"]
+    s.close()
+
+
+@pytest.mark.gpu
 def test_graph_engine_rejects_a_cycle():
     from gamesmanmpi_amd import Context, GMError, _lib
     ctx = Context(_lib.GAME_GRAPH, (), device=0)

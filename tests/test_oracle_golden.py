@@ -118,6 +118,26 @@ def test_python_canonical_on_our_bitboard_plugins(plugin, dims, name, nkeep):
     assert [g[1] for g in got] == recs.tolist()
 
 
+def _blake8(pos):
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(pos.encode("ISO-8859-1"), digest_size=8).digest(), "big")
+
+
+def test_python_canonical_on_our_othello_8x8_endgame():
+    """§8f.3 at the reference's own 8x8 board: our plugin (test_games/othello_bit_new.py at its
+    default 8x8) from the endgame root of tests/plugins/othello8_endgame.py gives, under the
+    canonical oracle, exactly the golden table made from the REFERENCE's plugin (positions
+    keyed by an 8-byte blake2b of their 144-bit string); no device descriptor claims it."""
+    from gamesmanmpi_amd import games
+    mod = load_plugin("tests/plugins/othello8_endgame.py")
+    assert games.identify(mod) is None
+    table, positions = canonical.solve(mod)
+    keys, recs = golden("othello_8x8_endgame")
+    got = sorted((_blake8(positions[k]), (v << 14) | r) for k, (v, r) in table.items())
+    assert [g[0] for g in got] == keys.tolist()
+    assert [g[1] for g in got] == recs.tolist()
+
+
 def test_subtract_oracle_closed_form_and_f2o(oracle):
     # values: LOSS iff xor_i (h_i mod 3) == 0; one heap == Four-To-One (golden) for piles >= 0
     rec = oracle.subtract_dense(4)
