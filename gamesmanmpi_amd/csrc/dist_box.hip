@@ -467,6 +467,26 @@ __global__ void bx_flag_wait_kernel(const uint64_t *flag, const uint64_t *seqp, 
     }
 }
 
+// the receives of one batch on every axis in one launch: waits until each given flag holds the
+// solve's number
+__global__ void bx_flags_wait_kernel(const uint64_t *f0, const uint64_t *f1, const uint64_t *f2, const uint64_t *seqp,
+                                     uint64_t ticks, uint32_t *err) {
+    if (threadIdx.x) return;
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;   // as bx_flag_wait_kernel
+    const uint64_t want = *seqp;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (const uint64_t *f : {f0, f1, f2}) {
+        if (!f) continue;
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                atomicOr(err, 1u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(4);
+        }
+    }
+}
+
 __global__ void bx_flags_set_kernel(uint64_t *f0, uint64_t *f1, uint64_t *f2, const uint64_t *seqp) {
     if (threadIdx.x) return;
     const uint64_t v = *seqp;
@@ -533,6 +553,7 @@ struct BxRank {
     uint32_t *peer_boxflag[3] = {};
     uint32_t n_recv_boxes = 0;
     int sig_done = 0;                     // direct: batches signalled so far in this solve (+1)
+    int rcv_done = 0;                     // IPC: batches whose receives are waited for (+1)
 };
 
 struct DistBox {
@@ -1004,13 +1025,21 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
             }
             // solo timing: the other ranks' boxes are taken as written (the previous full solve's)
             if (!solo) GM_HIP(hipStreamWaitEvent(st, L.ev[BEV_DONE][0][j], 0));
-            if (d->d_scratch)   // (the flag holds at least 0: returns at once)
+            if (d->d_scratch && R.rcv_done != j + 1) {   // one wait per batch, as IPC (the flag holds 0: at once)
+                R.rcv_done = j + 1;
                 hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, (const uint64_t *)d->d_scratch,
                                    (const uint64_t *)d->d_seq, -(1 << 30), 0u, BX_IPC_WAIT_TICKS, (uint32_t *)(d->d_scratch + 1));
+            }
             d->sent += n;
-        } else if (d->ipc) {   // the sender's tier kernels stored the boxes here; wait for its flag
-            hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, st, R.flags + (size_t)a * d->S.nbatch + j,
-                               (const uint64_t *)d->d_seq, 0, 0u, BX_IPC_WAIT_TICKS, R.d_err);
+        } else if (d->ipc) {   // the sender's tier kernels stored the boxes here; wait for its flags
+            if (R.rcv_done != j + 1) {   // one wait for the batch's receives on every axis
+                R.rcv_done = j + 1;
+                const uint64_t *f[3] = {nullptr, nullptr, nullptr};
+                for (size_t k = i; k < R.ops.size() && R.ops[k].kind == BOP_RECV && R.ops[k].arg == j; k++)
+                    f[R.ops[k].axis] = R.flags + (size_t)R.ops[k].axis * d->S.nbatch + j;
+                hipLaunchKernelGGL(bx_flags_wait_kernel, dim3(1), dim3(64), 0, st, f[0], f[1], f[2],
+                                   (const uint64_t *)d->d_seq, BX_IPC_WAIT_TICKS, R.d_err);
+            }
         } else {
             for (uint64_t p = 0; p < n; p += 1ull << 30)
                 GM_NCCL(ncclRecv(R.rbuf + o0 + p, std::min<uint64_t>(n - p, 1ull << 30), ncclUint8, o.peer, d->comm[a], st));
@@ -1052,6 +1081,7 @@ static int bx_enqueue(Ctx *c, DistBox *d, int solo, bool op_events) {
     for (auto &R : d->ranks) {
         R.pc = 0;
         R.sig_done = 0;
+        R.rcv_done = 0;
         for (auto &k : R.recorded)
             for (int &x : k) x = 0;
         if (op_events && R.tev.size() != 2 * R.ops.size()) {
