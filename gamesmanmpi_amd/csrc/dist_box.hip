@@ -441,13 +441,6 @@ __global__ void bx_seq_kernel(uint64_t *seqp) {
     if (!threadIdx.x) *seqp += 1;
 }
 
-__global__ void bx_flag_set_kernel(uint64_t *flag, const uint64_t *seqp) {
-    if (threadIdx.x) return;
-    const uint64_t v = *seqp;
-    __threadfence_system();
-    __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // waits until *flag >= (*seqp + add) << shift
 __global__ void bx_flag_wait_kernel(const uint64_t *flag, const uint64_t *seqp, int add, uint32_t shift, uint64_t ticks,
                                     uint32_t *err) {
@@ -470,10 +463,11 @@ __global__ void bx_flag_wait_kernel(const uint64_t *flag, const uint64_t *seqp, 
 // the receives of one batch on every axis in one launch: waits until each given flag holds the
 // solve's number
 __global__ void bx_flags_wait_kernel(const uint64_t *f0, const uint64_t *f1, const uint64_t *f2, const uint64_t *seqp,
-                                     uint64_t ticks, uint32_t *err) {
+                                     int add, uint64_t ticks, uint32_t *err) {
     if (threadIdx.x) return;
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;   // as bx_flag_wait_kernel
-    const uint64_t want = *seqp;
+    const int64_t w = (int64_t)*seqp + add;
+    const uint64_t want = w > 0 ? (uint64_t)w : 0u;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (const uint64_t *f : {f0, f1, f2}) {
         if (!f) continue;
@@ -1038,7 +1032,7 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
                 for (size_t k = i; k < R.ops.size() && R.ops[k].kind == BOP_RECV && R.ops[k].arg == j; k++)
                     f[R.ops[k].axis] = R.flags + (size_t)R.ops[k].axis * d->S.nbatch + j;
                 hipLaunchKernelGGL(bx_flags_wait_kernel, dim3(1), dim3(64), 0, st, f[0], f[1], f[2],
-                                   (const uint64_t *)d->d_seq, BX_IPC_WAIT_TICKS, R.d_err);
+                                   (const uint64_t *)d->d_seq, 0, BX_IPC_WAIT_TICKS, R.d_err);
             }
         } else {
             for (uint64_t p = 0; p < n; p += 1ull << 30)
@@ -1126,13 +1120,19 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
     }
     if (d->ipc) {
         hipLaunchKernelGGL(bx_seq_kernel, dim3(1), dim3(64), 0, d->ranks[0].S, d->d_seq);   // this solve's number
-        // the ranks this one writes into finished reading the previous solve's halos
-        for (auto &R : d->ranks)
+        // the ranks this one writes into finished reading the previous solve's halos (one launch)
+        for (auto &R : d->ranks) {
+            const uint64_t *f[3] = {nullptr, nullptr, nullptr};
+            bool any = false;
             for (int a = 0; a < d->S.g; a++)
-                if (R.peer_flags[a])
-                    hipLaunchKernelGGL(bx_flag_wait_kernel, dim3(1), dim3(64), 0, R.S,
-                                       R.peer_flags[a] + bx_flag_consumed(d->S, a), (const uint64_t *)d->d_seq, -1, 0u,
-                                       BX_IPC_WAIT_TICKS, R.d_err);
+                if (R.peer_flags[a]) {
+                    f[a] = R.peer_flags[a] + bx_flag_consumed(d->S, a);
+                    any = true;
+                }
+            if (any)
+                hipLaunchKernelGGL(bx_flags_wait_kernel, dim3(1), dim3(64), 0, R.S, f[0], f[1], f[2],
+                                   (const uint64_t *)d->d_seq, -1, BX_IPC_WAIT_TICKS, R.d_err);
+        }
     }
     if (d->flow) {
         // one launch: every virtual rank together (co-resident), a solo rank alone (its received
@@ -1163,12 +1163,19 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
     } else {
         GM_TRY(bx_enqueue(c, d, c->dist_solo, op_events));
     }
-    if (d->ipc)   // this solve's messages are unpacked: the senders may write the next solve's
-        for (auto &R : d->ranks)
+    if (d->ipc)   // this solve's halos are read: the senders may write the next solve's (one launch)
+        for (auto &R : d->ranks) {
+            uint64_t *f[3] = {nullptr, nullptr, nullptr};
+            bool any = false;
             for (int a = 0; a < d->S.g; a++)
-                if ((R.rank >> a) & 1)
-                    hipLaunchKernelGGL(bx_flag_set_kernel, dim3(1), dim3(64), 0, R.S, R.flags + bx_flag_consumed(d->S, a),
-                                       (const uint64_t *)d->d_seq);
+                if ((R.rank >> a) & 1) {
+                    f[a] = R.flags + bx_flag_consumed(d->S, a);
+                    any = true;
+                }
+            if (any)
+                hipLaunchKernelGGL(bx_flags_set_kernel, dim3(1), dim3(64), 0, R.S, f[0], f[1], f[2],
+                                   (const uint64_t *)d->d_seq);
+        }
     for (auto &R : d->ranks) {
         for (int a = 0; a < d->S.g; a++) {
             GM_HIP(hipEventRecord(R.ev_join[a], R.X[a]));
