@@ -196,6 +196,22 @@ def test_ipc_schedule_is_deadlock_free_and_race_free(world, root):
         assert S.simulate(P, seed=seed)
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ipc_lists_group_a_batch_per_kind(world):
+    """dist_box.hip's IPC executor signals a batch's sends with one flag kernel and waits for a
+    batch's receives with one (the first op of the run takes the others' flags): so in every
+    rank's list the SEND ops of one batch, and its RECV ops, must be one unbroken run."""
+    P = S.plans(world, FULL, transport=1)
+    for p in P:
+        ops = p["ops"]
+        for kind in (S.BOP_SEND, S.BOP_RECV):
+            idx = np.nonzero(ops[:, 0] == kind)[0]
+            for j in np.unique(ops[idx, 4]):
+                run = idx[ops[idx, 4] == j]
+                assert (np.diff(run) == 1).all(), (p["rank"] if "rank" in p else None, kind, j, run)
+                assert len(np.unique(ops[run, 1])) == len(run)   # one op per axis
+
+
 def _mutate(P, rank, pred, action="drop", shift=3):
     Q = [dict(p) for p in P]
     ops = Q[rank]["ops"].tolist()
