@@ -1,6 +1,6 @@
 // dist_box.hip -- the 8-heap synthetic game (config 5) on the box engine, split over G ranks:
-// every box computed by exactly ONE rank, cross-rank child boxes exchanged per batch of
-// box-tiers over RCCL.
+// every box computed by exactly ONE rank, cross-rank child boxes handed over per batch of
+// box-tiers.
 //
 // The reference shards positions by an owner hash, md5(str(pos)) % world
 // (src/game_state.py:23-31), sends every child to its owner (src/new_process.py:156-160) and
@@ -25,19 +25,23 @@
 // is still computed by exactly one rank; only the transfer is avoided.
 //
 // Schedule.  Box-tiers are grouped in batches of B (GM_OPT_DIST_BATCH): batch j = tiers
-// [jB, jB+B).  Its message on axis a, X_j, holds the lower rank's crossing boxes of tiers
-// [jB-1, jB+B-2] (an A-heap crossing: the child box's two top layers along that heap, 2 KiB;
-// else the whole 4 KiB box).  The tier kernel writes each such box, from the registers that hold
-// it, also to its message slot; after the lower rank's tier jB+B-2 the axis's exchange stream
-// X[a] sends the message; the upper rank receives the batch's messages (one per axis on which
-// it is the upper side) and unpacks them all into its table (the boxes' natural slots) in one
-// launch, on its compute stream right before its batch j.  Every rank's work is a precomputed op list (tier
-// launch, unpack, send, receive, event record / wait).  RCCL mode (one
-// process per GPU): the list in order, one communicator per axis.  Loopback mode
-// (GM_OPT_VIRTUAL_RANKS, G ranks inside one context on one GPU, for testing): the same lists on
-// per-rank streams and tables, a receive being a device copy of the sender's packed message,
-// enqueued by a host scheduler that interleaves the lists so that every cross-rank wait comes
-// after the record it waits for.
+// [jB, jB+B).  The lower rank's crossing boxes of tiers [jB-1, jB+B-2] (an A-heap crossing: the
+// child box's two top layers along that heap, 2 KiB; else the whole 4 KiB box) reach the upper
+// rank before its batch j.  The tier kernel writes each such box a second time, from the
+// registers that hold it:
+//   RCCL transport (GM_OPT_BOX_TRANSPORT 0, any number of nodes): into its slot of the batch's
+//     message; after tier jB+B-2 the axis's exchange stream X[a] ncclSends it on the axis's
+//     communicator, and the upper rank ncclRecvs and unpacks the batch's messages on its compute
+//     stream right before its batch j.  Launched eagerly.
+//   IPC transport (1, one node) and virtual ranks (GM_OPT_VIRTUAL_RANKS, testing): straight into
+//     the upper rank's table (mapped through hipIpcOpenMemHandle, or the other virtual rank's),
+//     the slot the box has there; after the tier one signal per batch -- a one-lane flag kernel
+//     (IPC) or an event record (virtual ranks) -- and the upper rank's compute stream waits for
+//     it before its batch.  A solve's launches are captured once and replayed as one hipGraph.
+// Every rank's work is a precomputed op list (tier launch, unpack, send, receive, event record /
+// wait; gm_box_plan shows it on the host); virtual ranks run theirs on per-rank streams and
+// tables, enqueued by a host scheduler that interleaves the lists so that every cross-rank wait
+// comes after the record it waits for.
 #include "gm_internal.hpp"
 #include "gm_common.hpp"
 #include "box_common.hpp"
