@@ -42,3 +42,21 @@ def test_bench_line_virtual_ranks_split():
     rf = d["roofline"]
     assert rf["launches_per_solve"] > 4 * 30 and rf["kernel"].startswith("box_tier_kernel<true>")
     assert rf["traffic"] is None   # the committed PMC summary is the one-GPU solve's
+
+
+def test_bench_rehearsal_two_processes_one_gpu():
+    """bench.py at N = 2 as the driver launches it (torch.distributed.run, one process per
+    rank), both ranks on this one GPU (--rehearse-one-gpu: gloo for the bench's collectives,
+    the IPC transport for the halos): the IPC probe passes (no fallback), every rank's owned
+    digest equals the oracle's, and the line says it is a rehearsal."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--rehearse-one-gpu", "--dist-batch", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["parity"]["ok"] and d["halo_transport_fallback"] is None
+    assert d["rehearsal"] and d["sharding"]["work_vs_one_gpu"] == 1.0
+    assert d["parity"]["per_rank_vs_oracle"]["wrong_ranks"] == []
