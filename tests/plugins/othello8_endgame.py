@@ -9,10 +9,15 @@ host with these functions and resolved on the GPU (gm_solve_graph).  The golden 
 (tests/golden/othello_8x8_endgame.npz) is the canonical solution of the REFERENCE's plugin
 from the same root (tests/golden/make_golden.py --only othello8).
 """
+import os
+
 from test_games.othello_bit_new import *  # noqa: F401,F403  (the game: moves, rules, encoding)
 from test_games.othello_bit_new import do_move, gen_moves, primitive  # noqa: F401
 
-ROOT_HEX = "303800204018057a4646bfdebfe6fa800200"
+# GM_OTHELLO8_ROOT (a position string in hex) replaces the root for scale runs: the same
+# playout stopped earlier, 12 empties "30380028503841784646bfd6afc6be000200", 13
+# "30381c2c503841784646a1d2afc6be000100" (DESIGN §7)
+ROOT_HEX = os.environ.get("GM_OTHELLO8_ROOT", "303800204018057a4646bfdebfe6fa800200")
 
 
 def initial_position():
