@@ -628,13 +628,16 @@ def main():
     transport_fallback = None
     if world > 1 and box and args.box_transport == "ipc":
         # untimed probe: the IPC transport's cross-process schedule has run on hardware with the
-        # ranks sharing one GPU only.  If its first solve fails on any rank, or the summed
-        # digest is not the committed oracle digest, every rank falls back to RCCL together.
-        # Two solves: the second reads halo rows the first one's reads may have left in the
-        # receiver's caches, so a stale line would show there.
+        # ranks sharing one GPU only.  If a probe solve fails on any rank, or the summed digest
+        # is not the committed oracle digest, every rank falls back to RCCL together.  Received
+        # boxes are poisoned (GM_OPT_POISON 1): every rank's table starts as 0xFF, and each
+        # halo box goes back to 0xFF once read, so solve 2 reads nothing solve 1 left -- a halo
+        # that lands late, or is read from a stale line, changes that solve's digest
+        # (tests/test_gpu_multiproc.py::test_box_ipc_early_read_caught_by_poison injects one).
         err = ""
         ref = committed_digest("subtract_%d" % args.heaps) if root == (1 << (4 * args.heaps)) - 1 else None
         bad = 0.0
+        ctx.set_option(_lib.OPT_POISON, 1)
         for k in range(2):
             try:
                 ctx.solve(root)
@@ -652,6 +655,7 @@ def main():
                 if (d, nd) != (ref["digest"], ref["positions"]):
                     bad, err = 1.0, "solve %d: summed digest %#x differs from the committed oracle digest" % (k + 1, d)
                     break
+        ctx.set_option(_lib.OPT_POISON, 0)   # the timed solves run the plain schedule
         flag = torch.tensor([bad], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
         if flag.item() > 0:
@@ -665,6 +669,13 @@ def main():
                 ctx.set_option(_lib.OPT_BOX_TRANSPORT, 0)
             sys.stderr.write("bench.py rank %d: %s\n" % (rank, transport_fallback))
             barrier()
+            if args.rehearse_one_gpu:   # nothing to fall back to: one clean non-zero exit
+                if rank == 0:
+                    print(json.dumps({"metric": METRIC, "value": None, "error": transport_fallback}), flush=True)
+                watchdog.cancel()
+                ctx.close()
+                dist.destroy_process_group()
+                sys.exit(4)
 
     autotune = None
     if world > 1 and args.dist_batch is None:

@@ -25,6 +25,9 @@ OPT_SYMMETRY = 14
 OPT_BOX_FLOW = 15
 OPT_BOX_SPLIT = 16
 OPT_BOX_TRANSPORT = 17
+OPT_SPARSE_TRANSPORT = 18
+OPT_POISON = 19
+ABI_VERSION = 2
 BUF_DENSE_TABLE = 1
 PLAN_SHAPE, PLAN_OWN, PLAN_FILL, PLAN_SEND, PLAN_RECV, PLAN_OPS, PLAN_XDEST = 0, 1, 2, 3, 4, 5, 6
 BOXPLAN_SHAPE, BOXPLAN_BOXES, BOXPLAN_FILLS, BOXPLAN_TIER_OFF, BOXPLAN_OWN = 0, 1, 2, 3, 4
@@ -71,6 +74,7 @@ class Stats(ctypes.Structure):
         ("engine", ctypes.c_int32),
         ("n_edges", ctypes.c_uint64),
         ("flow_fallbacks", ctypes.c_int32),
+        ("n_stored", ctypes.c_uint64),
     ]
 
     def as_dict(self):

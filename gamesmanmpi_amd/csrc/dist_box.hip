@@ -445,6 +445,21 @@ __global__ void bx_seq_kernel(uint64_t *seqp) {
     if (!threadIdx.x) *seqp += 1;
 }
 
+// GM_OPT_POISON (test hook): every box this rank receives reads 0xFF until its sender stores it
+// again; one workgroup per box, 16 B a lane
+__global__ void bx_poison_kernel(uint8_t *table, const uint32_t *boxes) {
+    uint4 *b = (uint4 *)(table + ((uint64_t)boxes[blockIdx.x] << 12));
+    b[threadIdx.x] = make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+
+// GM_OPT_POISON 2 / 3 (test hook): from solve `from` on, hold this stream for `ticks` (a sender
+// made late)
+__global__ void bx_hold_from_kernel(const uint64_t *seqp, uint64_t from, uint64_t ticks) {
+    if (threadIdx.x || *seqp < from) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 // waits until *flag >= (*seqp + add) << shift
 __global__ void bx_flag_wait_kernel(const uint64_t *flag, const uint64_t *seqp, int add, uint32_t shift, uint64_t ticks,
                                     uint32_t *err) {
@@ -466,10 +481,13 @@ __global__ void bx_flag_wait_kernel(const uint64_t *flag, const uint64_t *seqp, 
 
 // the receives of one batch on every axis in one launch: waits until each given flag holds the
 // solve's number
+// (skip_from > 0, GM_OPT_POISON 2 / 3 test hook: from solve skip_from on, return at once -- a
+// receiver that reads its halo as if the flag had been set early)
 __global__ void bx_flags_wait_kernel(const uint64_t *f0, const uint64_t *f1, const uint64_t *f2, const uint64_t *seqp,
-                                     int add, uint64_t ticks, uint32_t *err) {
+                                     int add, uint64_t ticks, uint32_t *err, uint64_t skip_from = 0) {
     if (threadIdx.x) return;
     if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;   // as bx_flag_wait_kernel
+    if (skip_from && *seqp >= skip_from) return;
     const int64_t w = (int64_t)*seqp + add;
     const uint64_t want = w > 0 ? (uint64_t)w : 0u;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -550,6 +568,8 @@ struct BxRank {
     uint32_t qbase[8] = {}, qlen[8] = {};
     uint32_t *peer_boxflag[3] = {};
     uint32_t n_recv_boxes = 0;
+    uint32_t *d_poison_boxes = nullptr;   // GM_OPT_POISON: every box this rank receives
+    uint32_t n_poison_boxes = 0;
     int sig_done = 0;                     // direct: batches signalled so far in this solve (+1)
     int rcv_done = 0;                     // IPC: batches whose receives are waited for (+1)
 };
@@ -557,7 +577,7 @@ struct BxRank {
 struct DistBox {
     BxShape S;
     bool loopback = false;
-    int want_batch = 0, want_sym = 0, want_split = 0;
+    int want_batch = 0, want_sym = 0, want_split = 0, want_poison = 0;
     std::vector<BxRank> ranks;            // the ranks this context runs
     int grid_cap = 2048;
     unsigned long long *d_acc = nullptr;
@@ -763,6 +783,7 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
     d->want_batch = c->dist_batch;
     d->want_sym = c->dist_symmetry;
     d->want_split = c->box_split;
+    d->want_poison = c->poison;
     GM_TRY(bx_shape(box_index_of_key((uint32_t)root) >> 12, G, c->dist_batch, c->dist_symmetry, c->box_split, &d->S));
     const BxShape &S = d->S;
     d->grid_cap = box_grid_cap(c->device);
@@ -847,6 +868,15 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
             R.send_off[a] = P.send_off[a];
             R.recv_off[a] = P.recv_off[a];
         }
+        if (c->poison) {
+            std::vector<uint32_t> pb;
+            for (int a = 0; a < S.g; a++)
+                for (uint32_t e : P.recv[a]) pb.push_back(e & 0xFFFFFu);
+            std::sort(pb.begin(), pb.end());
+            pb.erase(std::unique(pb.begin(), pb.end()), pb.end());
+            R.n_poison_boxes = (uint32_t)pb.size();
+            if (!pb.empty()) GM_TRY(bx_upload(pb, &R.d_poison_boxes));
+        }
         if (d->ipc) {
             GM_HIP(hipMalloc(&R.flags, bx_flag_words(S) * 8));
             GM_HIP(hipMemset(R.flags, 0, bx_flag_words(S) * 8));
@@ -899,10 +929,12 @@ static int bx_prepare(Ctx *c, DistBox *d, uint64_t root, int G, bool loopback) {
                 return GM_E_NOMEM;
             }
             R.owned = true;
-            // a virtual rank's table starts as 0xFF (LOSS in 0, the largest code): a read of a
-            // box the rank neither computed nor received would change its results
-            if (loopback) GM_HIP(hipMemset(R.table, 0xFF, 1ull << 32));
         }
+        // every rank's table starts as 0xFF (LOSS in 0, the largest code): a read of a box the
+        // rank neither computed nor received changes its results instead of reading leftover
+        // bytes (a fresh allocation or an adopted buffer); once per prepare, before the IPC
+        // rendezvous lets a peer store into it
+        if (R.table) GM_HIP(hipMemset(R.table, 0xFF, 1ull << 32));
         if (R.table) {
             for (uint32_t b : P.boxes) owner[b] = (uint8_t)tabs.size();
             tabs.push_back(R.table);
@@ -1036,7 +1068,8 @@ static int bx_exec(Ctx *c, DistBox *d, BxRank &R, size_t i, bool solo, bool op_e
                 for (size_t k = i; k < R.ops.size() && R.ops[k].kind == BOP_RECV && R.ops[k].arg == j; k++)
                     f[R.ops[k].axis] = R.flags + (size_t)R.ops[k].axis * d->S.nbatch + j;
                 hipLaunchKernelGGL(bx_flags_wait_kernel, dim3(1), dim3(64), 0, st, f[0], f[1], f[2],
-                                   (const uint64_t *)d->d_seq, 0, BX_IPC_WAIT_TICKS, R.d_err);
+                                   (const uint64_t *)d->d_seq, 0, BX_IPC_WAIT_TICKS, R.d_err,
+                                   (uint64_t)(c->poison >= 2 ? 2 : 0));
             }
         } else {
             for (uint64_t p = 0; p < n; p += 1ull << 30)
@@ -1135,7 +1168,10 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
                 }
             if (any)
                 hipLaunchKernelGGL(bx_flags_wait_kernel, dim3(1), dim3(64), 0, R.S, f[0], f[1], f[2],
-                                   (const uint64_t *)d->d_seq, -1, BX_IPC_WAIT_TICKS, R.d_err);
+                                   (const uint64_t *)d->d_seq, -1, BX_IPC_WAIT_TICKS, R.d_err, (uint64_t)0);
+            if (c->poison >= 2 && R.rank == 0)   // test hook: rank 0 (it only sends) late from solve 2 on
+                hipLaunchKernelGGL(bx_hold_from_kernel, dim3(1), dim3(64), 0, R.S, (const uint64_t *)d->d_seq,
+                                   (uint64_t)2, (uint64_t)(50 * 100000));
         }
     }
     if (d->flow) {
@@ -1167,6 +1203,11 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
     } else {
         GM_TRY(bx_enqueue(c, d, c->dist_solo, op_events));
     }
+    if (c->poison & 1)   // test hook: the halo boxes just read go back to 0xFF before the senders may store the next solve's
+        for (auto &R : d->ranks)
+            if (R.n_poison_boxes)
+                hipLaunchKernelGGL(bx_poison_kernel, dim3(R.n_poison_boxes), dim3(256), 0, R.S, R.table,
+                                   (const uint32_t *)R.d_poison_boxes);
     if (d->ipc)   // this solve's halos are read: the senders may write the next solve's (one launch)
         for (auto &R : d->ranks) {
             uint64_t *f[3] = {nullptr, nullptr, nullptr};
@@ -1256,7 +1297,7 @@ int dist_box_solve(Ctx *c, uint64_t root) {
     DistBox *d = c->dist_box;
     const uint32_t rh = box_index_of_key((uint32_t)root) >> 12;
     if (!d || d->S.G != G || d->loopback != loopback || d->S.root_hi != rh || d->want_batch != c->dist_batch ||
-        d->want_sym != c->dist_symmetry || d->want_split != c->box_split ||
+        d->want_sym != c->dist_symmetry || d->want_split != c->box_split || d->want_poison != c->poison ||
         (!loopback && c->adopted_dense && d->ranks[0].table != c->adopted_dense) ||
         (!loopback && d->ranks[0].rank != c->rank) || d->ipc != ipc || d->flow != ((loopback || ipc) && c->box_flow == 1)) {
         dist_box_free(c);
@@ -1515,7 +1556,7 @@ void dist_box_free(Ctx *c) {
             if (q) (void)hipFree(q);
     if (d->d_root_words) (void)hipFree(d->d_root_words);
     for (auto &R : d->ranks)
-        for (void *q : {(void *)R.d_groups, (void *)R.boxflag, (void *)R.d_recv_boxes})
+        for (void *q : {(void *)R.d_groups, (void *)R.boxflag, (void *)R.d_recv_boxes, (void *)R.d_poison_boxes})
             if (q) (void)hipFree(q);
     for (void *q : {(void *)d->d_desc, (void *)d->d_flow_err})
         if (q) (void)hipFree(q);

@@ -20,11 +20,168 @@
 //                    order (RESOLVE); the parent folds them with atomicMax and
 //                    turns the best score into its own (gm_common.hpp).
 //
-// Exchanges use RCCL point-to-point (one process per GPU) or, with
-// GM_OPT_VIRTUAL_RANKS, device copies between G virtual ranks in one context.
+// Exchanges use one of three transports:
+//   RCCL (GM_OPT_SPARSE_TRANSPORT 0, one process per GPU): counts all-gathered, keys and
+//     replies as one ncclGroup of send/recv per peer, totals all-reduced;
+//   IPC (GM_OPT_SPARSE_TRANSPORT 1, one process per rank on one node, ranks may share a GPU):
+//     each rank publishes HIP IPC handles of its two send buffers (keys, replies) in a POSIX
+//     shared-memory segment; after a host barrier each receiver PULLS its segments out of the
+//     senders' buffers (hipMemcpyAsync from the mapping), and a second barrier frees the send
+//     buffers for reuse.  Counts, totals and the root record are all-gathered through the same
+//     segment (SpIpc below);
+//   loopback (GM_OPT_VIRTUAL_RANKS): device copies between G virtual ranks in one context.
+// The three share the layout (layout_for): rank r's send segment for p starts at
+// lay(r).send_off[p], p's receive segment from r at lay(p).recv_off[r].
 #include "sparse_tables.hpp"
 
+#include <cstring>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 namespace gm {
+
+// ------------------------------------------------------------------ IPC transport
+// One segment per solve, /gmsp-<unique id>-<solve number> (identical on every rank: solves are
+// collective).  Slot r is written only by rank r.  A barrier is a monotone epoch: rank r
+// stores its epoch in slot r, then waits until every slot holds at least it.  The all-gather
+// payload is double-buffered by epoch parity: a rank writes buffer k & 1 before barrier k and
+// reads it after; it writes that buffer again only after barrier k + 1, which no rank passes
+// before every rank has finished reading it.
+constexpr int SP_IPC_WORDS = 512;
+constexpr double SP_IPC_WAIT_MS = 120e3;
+struct SpIpcSlot {
+    hipIpcMemHandle_t h[2];          // 0 = key send buffer (sendk), 1 = reply send buffer (reply_out)
+    uint64_t off[2], gen[2];         // the buffer's offset in its allocation; bumped per new buffer
+    uint64_t arrive;                 // barrier epoch reached
+    uint64_t failed;                 // the rank left the solve with an error
+    uint64_t val[2][SP_IPC_WORDS];   // all-gather payload, by epoch parity
+};
+
+struct SpIpc {
+    SpIpcSlot *slot = nullptr;
+    size_t bytes = 0;
+    int G = 0, me = 0;
+    uint64_t epoch = 0;
+    char name[96] = {};
+    void *pub[2] = {};               // what this rank published
+    uint64_t gen[2] = {};
+    std::vector<uint64_t> pgen[2];   // per peer: the generation mapped
+    std::vector<void *> pbase[2];    // per peer: the mapping (hipIpcCloseMemHandle on change / close)
+};
+
+static int sp_ipc_barrier(SpIpc &X) {
+    X.epoch++;
+    __atomic_store_n(&X.slot[X.me].arrive, X.epoch, __ATOMIC_RELEASE);
+    const double t0 = now_ms();
+    for (int r = 0; r < X.G; r++)
+        for (unsigned spin = 0; __atomic_load_n(&X.slot[r].arrive, __ATOMIC_ACQUIRE) < X.epoch; spin++) {
+            for (int q = 0; q < X.G; q++)
+                if (__atomic_load_n(&X.slot[q].failed, __ATOMIC_ACQUIRE)) {
+                    set_error("sparse IPC transport: rank %d failed (segment %s)", q, X.name);
+                    return GM_E_COMM;
+                }
+            if (now_ms() - t0 > SP_IPC_WAIT_MS) {
+                set_error("sparse IPC transport: rank %d did not reach barrier %llu within %.0f s (segment %s)", r,
+                          (unsigned long long)X.epoch, SP_IPC_WAIT_MS / 1e3, X.name);
+                return GM_E_COMM;
+            }
+            if (spin > 64) usleep(spin > 4096 ? 200 : 10);
+        }
+    return GM_OK;
+}
+
+// all[r * n + i] = rank r's mine[i]
+static int sp_ipc_allgather(SpIpc &X, const uint64_t *mine, size_t n, uint64_t *all) {
+    for (size_t o = 0; o < n || (!n && !o); o += SP_IPC_WORDS) {
+        const size_t k = std::min<size_t>(SP_IPC_WORDS, n - std::min(n, o));
+        const int buf = (int)((X.epoch + 1) & 1);
+        std::memcpy(X.slot[X.me].val[buf], mine + o, k * 8);
+        GM_TRY(sp_ipc_barrier(X));
+        for (int r = 0; r < X.G; r++) std::memcpy(all + (size_t)r * n + o, X.slot[r].val[buf], k * 8);
+        if (!n) break;
+    }
+    return GM_OK;
+}
+
+static int sp_ipc_open(Ctx *c, SpIpc &X, int G) {
+    uint64_t k0, k1;
+    std::memcpy(&k0, c->uid, 8);
+    std::memcpy(&k1, c->uid + 8, 8);
+    snprintf(X.name, sizeof X.name, "/gmsp-%016llx%016llx-%d", (unsigned long long)k0, (unsigned long long)k1,
+             c->sparse_solves++);
+    X.G = G;
+    X.me = c->rank;
+    X.bytes = sizeof(SpIpcSlot) * (size_t)G;
+    const int fd = shm_open(X.name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) { set_error("shm_open(%s) failed", X.name); return GM_E_COMM; }
+    if (ftruncate(fd, (off_t)X.bytes) != 0) {
+        close(fd);
+        set_error("ftruncate of %s failed", X.name);
+        return GM_E_COMM;
+    }
+    void *m = mmap(nullptr, X.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) { set_error("mmap of %s failed", X.name); return GM_E_COMM; }
+    X.slot = (SpIpcSlot *)m;
+    for (int k = 0; k < 2; k++) {
+        X.pgen[k].assign(G, 0);
+        X.pbase[k].assign(G, nullptr);
+    }
+    // every rank has the segment open once this barrier passes: its name can go
+    const int rc = sp_ipc_barrier(X);
+    if (rc == GM_OK && X.me == 0) shm_unlink(X.name);
+    return rc;
+}
+
+static void sp_ipc_fail(SpIpc &X) {
+    if (X.slot) __atomic_store_n(&X.slot[X.me].failed, 1, __ATOMIC_RELEASE);
+}
+
+static void sp_ipc_close(SpIpc &X) {
+    for (int k = 0; k < 2; k++)
+        for (void *p : X.pbase[k])
+            if (p) (void)hipIpcCloseMemHandle(p);
+    if (X.slot) munmap(X.slot, X.bytes);
+    X.slot = nullptr;
+}
+
+// publish this rank's send buffer of kind k (0 keys, 1 replies); the next barrier orders it
+static int sp_ipc_publish(SpIpc &X, int k, void *p) {
+    if (p == X.pub[k]) return GM_OK;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess ||
+        hipIpcGetMemHandle(&X.slot[X.me].h[k], (void *)base) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error("hipIpcGetMemHandle of rank %d's send buffer failed", X.me);
+        return GM_E_COMM;
+    }
+    X.slot[X.me].off[k] = (uint64_t)((char *)p - (char *)base);
+    X.slot[X.me].gen[k] = ++X.gen[k];
+    X.pub[k] = p;
+    return GM_OK;
+}
+
+// rank r's send buffer of kind k, mapped into this process (after the barrier that follows its publish)
+static int sp_ipc_peer(SpIpc &X, int r, int k, char **out) {
+    const uint64_t g = X.slot[r].gen[k];
+    if (!g) { set_error("rank %d published no send buffer", r); return GM_E_COMM; }
+    if (X.pgen[k][r] != g) {
+        if (X.pbase[k][r]) (void)hipIpcCloseMemHandle(X.pbase[k][r]);
+        X.pbase[k][r] = nullptr;
+        void *b = nullptr;
+        if (hipIpcOpenMemHandle(&b, X.slot[r].h[k], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error("hipIpcOpenMemHandle of rank %d's send buffer failed", r);
+            return GM_E_COMM;
+        }
+        X.pbase[k][r] = b;
+        X.pgen[k][r] = g;
+    }
+    *out = (char *)X.pbase[k][r] + X.slot[r].off[k];
+    return GM_OK;
+}
 
 struct SpRank {
     int rank = 0;
@@ -44,6 +201,8 @@ struct SpRank {
 struct DistSparse {
     int G = 1, S = 1;
     bool loopback = false;
+    bool ipc = false;                        // GM_OPT_SPARSE_TRANSPORT 1
+    SpIpc X;
     int64_t t_root = 0;
     std::vector<SpRank> ranks;
     std::vector<uint64_t> gcount;            // global positions per tier
@@ -173,6 +332,18 @@ __global__ void root_lookup_kernel(ResRef t, uint64_t key, uint32_t *out) {
 }
 
 // ------------------------------------------------------------------ host helpers
+// element-wise sum (or max) over ranks of a host vector, through the IPC segment
+static int sp_ipc_reduce(SpIpc &X, std::vector<uint64_t> &v, bool max) {
+    std::vector<uint64_t> all((size_t)X.G * v.size());
+    GM_TRY(sp_ipc_allgather(X, v.data(), v.size(), all.data()));
+    for (size_t i = 0; i < v.size(); i++) {
+        uint64_t a = 0;
+        for (int r = 0; r < X.G; r++) a = max ? std::max(a, all[(size_t)r * v.size() + i]) : a + all[(size_t)r * v.size() + i];
+        v[i] = a;
+    }
+    return GM_OK;
+}
+
 static int grow64(Ctx *c, uint64_t **p, uint64_t *cap, uint64_t need) {
     if (need <= *cap && *p) return GM_OK;
     dev_free(c, *p);
@@ -231,6 +402,12 @@ static int gather_counts(Ctx *c, DistSparse *d, std::vector<uint64_t> &mat) {
         GM_HIP(hipStreamSynchronize(c->stream));
         return GM_OK;
     }
+    if (d->ipc) {
+        std::vector<uint64_t> row(nb);
+        GM_HIP(hipMemcpyAsync(row.data(), d->ranks[0].d_hist, nb * 8, hipMemcpyDeviceToHost, c->stream));
+        GM_HIP(hipStreamSynchronize(c->stream));
+        return sp_ipc_allgather(d->X, row.data(), nb, mat.data());
+    }
     GM_NCCL(ncclAllGather(d->ranks[0].d_hist, d->d_mat, nb, ncclUint64, c->comm, c->stream));
     GM_HIP(hipMemcpyAsync(mat.data(), d->d_mat, mat.size() * 8, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
@@ -281,7 +458,45 @@ static Layout layout_for(DistSparse *d, const std::vector<uint64_t> &mat, int r)
 }
 
 // move every rank's segmented send buffer to the owners (or, reverse = true, the replies back)
-static int exchange(Ctx *c, DistSparse *d, std::vector<Layout> &lay, bool reply) {
+// IPC: publish this rank's send buffer, barrier, pull every segment addressed to this rank out
+// of the senders' buffers, barrier (the senders may then overwrite them)
+static int exchange_ipc(Ctx *c, DistSparse *d, const Layout &me, const std::vector<uint64_t> &mat, bool reply) {
+    SpRank &R = d->ranks[0];
+    SpIpc &X = d->X;
+    const int k = reply ? 1 : 0;
+    const size_t elem = reply ? 2 : 8;
+    char *mine = reply ? (char *)R.reply_out : (char *)R.sendk;
+    char *dst = reply ? (char *)R.reply_in : (char *)R.recvk;
+    GM_HIP(hipStreamSynchronize(c->stream));   // the send buffer is complete
+    GM_TRY(sp_ipc_publish(X, k, mine));
+    GM_TRY(sp_ipc_barrier(X));
+    for (int p = 0; p < d->G; p++) {
+        const Layout lp = layout_for(d, mat, p);
+        // keys: p's segment for me -> my receive segment from p; replies: p's answers to my
+        // requests (p's receive segment from me) -> my send-order slots for p
+        const uint64_t n = reply ? me.send_off[p + 1] - me.send_off[p] : me.recv_off[p + 1] - me.recv_off[p];
+        if (!n) continue;
+        const uint64_t src_off = reply ? lp.recv_off[X.me] : lp.send_off[X.me];
+        const uint64_t dst_off = reply ? me.send_off[p] : me.recv_off[p];
+        char *src = mine;
+        if (p != X.me) GM_TRY(sp_ipc_peer(X, p, k, &src));
+        GM_HIP(hipMemcpyAsync(dst + dst_off * elem, src + src_off * elem, n * elem, hipMemcpyDeviceToDevice,
+                              c->stream));
+    }
+    for (int p = 0; p < d->G; p++)   // what this rank sent: its segments other ranks pulled
+        if (p != X.me)
+            d->sent_bytes += (reply ? me.recv_off[p + 1] - me.recv_off[p] : me.send_off[p + 1] - me.send_off[p]) * elem;
+    GM_HIP(hipStreamSynchronize(c->stream));
+    return sp_ipc_barrier(X);
+}
+
+static int exchange(Ctx *c, DistSparse *d, std::vector<Layout> &lay, const std::vector<uint64_t> &mat, bool reply) {
+    if (c->poison)   // test hook: a segment that never lands reads as 0xFF, not as an earlier tier's data
+        for (size_t i = 0; i < d->ranks.size(); i++) {
+            SpRank &R = d->ranks[i];
+            const uint64_t n = reply ? lay[i].nsend : lay[i].nrecv;
+            if (n) GM_HIP(hipMemsetAsync(reply ? (void *)R.reply_in : (void *)R.recvk, 0xFF, n * (reply ? 2 : 8), c->stream));
+        }
     if (d->loopback) {
         for (size_t i = 0; i < d->ranks.size(); i++)
             for (size_t j = 0; j < d->ranks.size(); j++) {
@@ -302,6 +517,7 @@ static int exchange(Ctx *c, DistSparse *d, std::vector<Layout> &lay, bool reply)
         return GM_OK;
     }
     SpRank &R = d->ranks[0];
+    if (d->ipc) return exchange_ipc(c, d, lay[0], mat, reply);
     return reply ? sendrecv(c, d, R.reply_out, lay[0].recv_off.data(), R.reply_in, lay[0].send_off.data(), 2)
                  : sendrecv(c, d, R.sendk, lay[0].send_off.data(), R.recvk, lay[0].recv_off.data(), 8);
 }
@@ -350,15 +566,17 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     dist_sparse_free(c);
     DistSparse *d = c->dist_sp = new DistSparse();
     d->loopback = c->virtual_ranks > 1;
+    d->ipc = !d->loopback && c->sparse_transport == 1;
     d->G = d->loopback ? c->virtual_ranks : c->world;
     d->S = D::MAX_SKIP;
     d->t_root = desc.tier(root);
     const int G = d->G, S = d->S, nb = G * S;
-    if (!d->loopback && !c->comm) {
+    if (!d->loopback && !d->ipc && !c->comm) {
         set_error("the sharded sparse engine needs a communicator (gm_set_comm) or virtual ranks");
         return GM_E_ARG;
     }
     if (nb > MAXBINS) { set_error("too many ranks for the sharded sparse engine"); return GM_E_ARG; }
+    if (d->ipc) GM_TRY(sp_ipc_open(c, d->X, G));
     d->ranks.resize(d->loopback ? G : 1);
     for (size_t i = 0; i < d->ranks.size(); i++) {
         SpRank &R = d->ranks[i];
@@ -414,7 +632,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
             GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
             run_bucket<D, true, false>(c, d, desc, R, t, nullptr);
         }
-        GM_TRY(exchange(c, d, lay, false));
+        GM_TRY(exchange(c, d, lay, mat, false));
         // owners insert into their tier tables, sized for load <= 0.7 of the predicted
         // distinct keys; a misprediction re-runs the (idempotent) inserts once
         uint64_t offered = 0, before = 0;
@@ -462,7 +680,9 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
                 local[u] += hc[u];
             }
         }
-        if (!d->loopback) {
+        if (d->ipc) {
+            GM_TRY(sp_ipc_reduce(d->X, local, false));
+        } else if (!d->loopback) {
             if (need > d->tot_cap) {   // the tier count grows past the G*G*S count matrix
                 if (d->d_tot) dev_free(c, d->d_tot);
                 d->tot_cap = std::max<size_t>(64, 2 * need);
@@ -511,7 +731,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
             GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
             run_bucket<D, true, true>(c, d, desc, R, t, R.best);
         }
-        GM_TRY(exchange(c, d, lay, false));                       // LOOK_UP: keys to owners
+        GM_TRY(exchange(c, d, lay, mat, false));                  // LOOK_UP: keys to owners
         for (size_t i = 0; i < d->ranks.size(); i++) {            // owners look up the scores
             SpRank &R = d->ranks[i];
             for (int q = 0; q < G; q++)
@@ -523,7 +743,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
                                        R.reply_out + lay[i].recv_seg[q * S + s], R.d_err);
                 }
         }
-        GM_TRY(exchange(c, d, lay, true));                        // RESOLVE: scores back
+        GM_TRY(exchange(c, d, lay, mat, true));                   // RESOLVE: scores back
         for (size_t i = 0; i < d->ranks.size(); i++) {
             SpRank &R = d->ranks[i];
             SpTier &T = R.tiers[t];
@@ -544,16 +764,27 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
         if ((int)owner_rank(root, G) == R.rank && !R.tiers.empty())
             hipLaunchKernelGGL(root_lookup_kernel, dim3(1), dim3(64), 0, c->stream, res_ref_of(R.tiers[0]), root,
                                d->d_root);
-    if (!d->loopback) GM_NCCL(ncclAllReduce(d->d_root, d->d_root, 1, ncclUint32, ncclMax, c->comm, c->stream));
+    if (!d->loopback && !d->ipc) GM_NCCL(ncclAllReduce(d->d_root, d->d_root, 1, ncclUint32, ncclMax, c->comm, c->stream));
     uint32_t rs = 0;
     GM_HIP(hipMemcpyAsync(&rs, d->d_root, 4, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
+    if (d->ipc) {
+        std::vector<uint64_t> v{rs};
+        GM_TRY(sp_ipc_reduce(d->X, v, true));
+        rs = (uint32_t)v[0];
+    }
     c->root_record = record_of_score((uint16_t)rs);
     // positions per tier: the stored representatives' orbits (games.hpp), summed over ranks
-    std::vector<uint64_t> gall(d->gcount.size(), 0);
+    // (the last word: the stored representatives, summed over ranks too)
+    std::vector<uint64_t> gall(d->gcount.size() + 1, 0);
     for (auto &R : d->ranks)
-        for (size_t t = 0; t < gall.size() && t < R.tiers.size(); t++) gall[t] += R.tiers[t].count_all;
-    if (!d->loopback && !gall.empty()) {
+        for (size_t t = 0; t < d->gcount.size() && t < R.tiers.size(); t++) {
+            gall[t] += R.tiers[t].count_all;
+            gall.back() += R.tiers[t].count;
+        }
+    if (d->ipc) {
+        GM_TRY(sp_ipc_reduce(d->X, gall, false));
+    } else if (!d->loopback && !gall.empty()) {
         if (gall.size() > d->tot_cap) {
             if (d->d_tot) dev_free(c, d->d_tot);
             d->tot_cap = std::max<size_t>(64, 2 * gall.size());
@@ -564,6 +795,8 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
         GM_HIP(hipMemcpyAsync(gall.data(), d->d_tot, gall.size() * 8, hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
     }
+    const uint64_t stored = gall.back();
+    gall.pop_back();
     uint64_t n = 0, tb = 0;
     for (auto v : gall) n += v;
     for (auto &R : d->ranks)
@@ -571,6 +804,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     c->n_positions = n;
     c->tier_counts = gall;
     c->stats.n_positions = n;
+    c->stats.n_stored = stored;
     c->stats.n_tiers = (int32_t)d->gcount.size();
     c->stats.world = G;
     c->stats.forward_ms = t1 - t0;
@@ -596,15 +830,11 @@ static int with_game(Ctx *c, F &&f) {
 }
 
 int dist_sparse_solve(Ctx *c, uint64_t root) {
-    switch (c->game) {
-    case GM_GAME_FOUR_TO_ONE: return solve_sharded(c, c->f2o, root);
-    case GM_GAME_TTT: return solve_sharded(c, c->ttt, root);
-    case GM_GAME_TOOT: return solve_sharded(c, c->toot, root);
-    case GM_GAME_OTHELLO: return solve_sharded(c, c->oth, root);
-    case GM_GAME_SUBTRACT: return solve_sharded(c, c->sub, root);
-    }
-    set_error("unknown game");
-    return GM_E_GAME;
+    int rc = with_game(c, [&](const auto &desc) { return solve_sharded(c, desc, root); });
+    // IPC: a rank that leaves with an error marks the segment, so its peers' next barrier fails
+    // at once instead of waiting out the limit
+    if (rc != GM_OK && c->dist_sp) sp_ipc_fail(c->dist_sp->X);
+    return rc;
 }
 
 int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
@@ -726,6 +956,7 @@ void dist_sparse_free(Ctx *c) {
     if (d->d_tot) dev_free(c, d->d_tot);
     dev_free(c, d->d_root);
     (void)hipStreamSynchronize(c->stream);
+    sp_ipc_close(d->X);
     delete d;
     c->dist_sp = nullptr;
 }

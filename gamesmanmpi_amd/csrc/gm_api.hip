@@ -276,6 +276,14 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         if (v < 0 || v > 1) { set_error("GM_OPT_BOX_TRANSPORT must be 0 (RCCL) or 1 (IPC peer copies)"); return GM_E_ARG; }
         c->box_transport = (int)v;
         return GM_OK;
+    case GM_OPT_SPARSE_TRANSPORT:
+        if (v < 0 || v > 1) { set_error("GM_OPT_SPARSE_TRANSPORT must be 0 (RCCL) or 1 (IPC pulls)"); return GM_E_ARG; }
+        c->sparse_transport = (int)v;
+        return GM_OK;
+    case GM_OPT_POISON:
+        if (v < 0 || v > 2) { set_error("GM_OPT_POISON must be 0, 1 or 2"); return GM_E_ARG; }
+        c->poison = (int)v;
+        return GM_OK;
     case GM_OPT_BOX_SPLIT:
         if (v < 0 || v > 1) { set_error("box split must be 0 (halves) or 1 (comparisons)"); return GM_E_ARG; }
         c->box_split = (int)v;
@@ -359,8 +367,13 @@ int gm_comm_unique_id(void *uid, int bytes) {
 int gm_set_comm(gm_ctx *h, int rank, int world, const void *uid, int bytes) {
     if (!h || world < 1 || rank < 0 || rank >= world) { set_error("bad rank/world"); return GM_E_ARG; }
     Ctx *c = &h->c;
+    // the sharded engines' transports (per-axis communicators split from c->comm, IPC
+    // mappings) belong to the previous communicator: torn down first (dist_box_free
+    // synchronises the device and destroys the split communicators), then the parent
+    if (c->dist_box) dist_box_free(c);
+    if (c->dist_sub) dist_sub_free(c);
+    if (c->dist_sp) dist_sparse_free(c);
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
-    if (c->dist_box) dist_box_free(c);   // its transport belongs to the previous communicator
     c->rank = rank;
     c->world = world;
     c->have_uid = false;
@@ -403,16 +416,22 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     // heap counts and GM_OPT_SUB_INTERLEAVE != 20 keep the block engine's sharded path
     const bool box = !force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT &&
                      c->sub.heaps == 8 && c->sub_interleave == 20;
-    if (sharded && c->virtual_ranks <= 1 && (c->world > 1 || force_dist_sparse) && !(box && c->box_transport == 1)) {
+    // transports that need no communicator: the split box engine's IPC stores and the sparse
+    // engine's IPC pulls (both also run with the ranks sharing one GPU, where RCCL refuses)
+    const bool dense_sharded = !force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT;
+    const bool no_comm = box ? c->box_transport == 1 : (!dense_sharded && c->sparse_transport == 1);
+    if (sharded && c->virtual_ranks <= 1 && (c->world > 1 || force_dist_sparse) && no_comm && !c->have_uid) {
+        set_error("the IPC transport needs gm_set_comm with a unique id (it names the rendezvous)");
+        return GM_E_COMM;
+    }
+    if (sharded && c->virtual_ranks <= 1 && (c->world > 1 || force_dist_sparse) && !no_comm) {
         if (!c->have_uid) {
             set_error("a %d-rank solve of this game needs an RCCL communicator (gm_set_comm with a unique id)", c->world);
             return GM_E_COMM;
         }
         GM_TRY(ensure_comm(c));
     }
-    if (sharded && !box) eng = (!force_dist_sparse && eng == GM_ENGINE_DENSE && c->game == GM_GAME_SUBTRACT)
-                                   ? GM_ENGINE_DIST_DENSE
-                                   : GM_ENGINE_DIST_SPARSE;
+    if (sharded && !box) eng = dense_sharded ? GM_ENGINE_DIST_DENSE : GM_ENGINE_DIST_SPARSE;
     int rc;
     switch (eng) {
     case GM_ENGINE_DENSE:
@@ -423,6 +442,7 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     default: rc = sparse_solve(c, root);
     }
     if (rc != GM_OK) return rc;
+    if (!c->stats.n_stored) c->stats.n_stored = c->stats.n_positions;   // engines without a symmetry reduction
     c->engine = eng;
     c->stats.engine = (box && sharded) ? GM_ENGINE_DIST_DENSE : eng;
     c->stats.world = sharded ? (c->world > 1 ? c->world : c->virtual_ranks) : 1;

@@ -89,6 +89,9 @@ struct Ctx {
     unsigned char uid[128] = {};
     int box_transport = 0;       // split box engine across processes: 0 RCCL, 1 peer copies over IPC (GM_OPT_BOX_TRANSPORT)
     int box_prepares = 0;        // split box contexts built so far (names the IPC rendezvous of each)
+    int sparse_transport = 0;    // hash-sharded sparse engine across processes: 0 RCCL, 1 IPC pulls (GM_OPT_SPARSE_TRANSPORT)
+    int sparse_solves = 0;       // sharded sparse solves run with the IPC transport (names each one's segment)
+    int poison = 0;              // test hook (GM_OPT_POISON): received data pre-filled with 0xFF; 2 = early flag
     int virtual_ranks = 1;   // >1: run that many ranks inside this context (loopback transport)
     hipStream_t comm_stream = nullptr;
     int dist_batch = 4;      // sharded dense path: tiers per halo exchange

@@ -662,9 +662,10 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
         GM_TRY(sparse_query(c, rk, rr, 1));
         c->root_record = rr[0];
     }
-    uint64_t n = 0, tb = 0;
+    uint64_t n = 0, tb = 0, stored = 0;
     c->tier_counts.clear();
     for (auto &T : sp->tiers) {
+        stored += T.count;
         n += T.count_all;
         c->tier_counts.push_back(T.count_all);
         tb += T.cap * sizeof(RSlot) + T.ni * 13;
@@ -672,6 +673,7 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
     if (getenv("GM_SPARSE_PROBE_STATS")) GM_TRY(probe_stats(c, sp));
     c->n_positions = n;
     c->stats.n_positions = n;
+    c->stats.n_stored = stored;
     c->stats.n_tiers = (int32_t)sp->tiers.size();
     c->stats.forward_ms = t1 - t0;
     c->stats.backward_ms = t2 - t1;

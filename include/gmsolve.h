@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 1
+#define GM_ABI_VERSION 2   /* 2: gm_box_plan opts/axis, gm_rank_stats recv_bytes, gm_stats_t.flow_fallbacks,
+                               GM_OPT_SPARSE_TRANSPORT, GM_OPT_POISON */
 
 /* Game descriptors.  Params per game:
  *   GM_GAME_FOUR_TO_ONE  none                  (reference test_games/four_to_one.py)
@@ -127,7 +128,7 @@ enum {
     GM_OPT_BOX_SPLIT = 16,  /* box engine at N > 1 (gm_box_plan): 0 (default) = split heaps in halves
                                (rank bit a = [box coordinate >= half]); 1 = tier-balanced comparisons
                                (rank bit = [c_x < c_y], ties by a rule that keeps every axis one-way) */
-    GM_OPT_BOX_TRANSPORT = 17  /* box engine at N > 1, one process per rank: how a halo message
+    GM_OPT_BOX_TRANSPORT = 17, /* box engine at N > 1, one process per rank: how a halo message
                                travels.  0 (default) = ncclSend / ncclRecv on per-axis communicators;
                                1 = the sender's tier kernel stores its halo boxes straight into the
                                receiver's table, mapped through HIP IPC (hipIpcGetMemHandle, exchanged
@@ -136,6 +137,27 @@ enum {
                                poll (30 s limit, then GM_E_COMM).  1
                                also runs when the ranks share one GPU, where RCCL refuses; all the
                                ranks of one node.  Set on every rank before the first solve. */
+    GM_OPT_SPARSE_TRANSPORT = 18, /* hash-sharded sparse engine (GM_ENGINE_DIST_SPARSE; Toot, Othello, ...) at
+                               N > 1, one process per rank: how the per-tier LOOK_UP keys and RESOLVE
+                               scores travel (reference src/new_process.py:156-160, :179-187).  0 (default)
+                               = ncclSend / ncclRecv groups, counts all-gathered and totals all-reduced
+                               over RCCL; 1 = IPC: every rank publishes its send buffers' HIP IPC handles
+                               in a POSIX shared-memory segment named by the unique id, each receiver
+                               pulls its segments from the senders' buffers (hipMemcpyAsync from the
+                               mapping), and counts, totals and the root record are all-gathered through
+                               the same segment, ordered by host barriers (120 s limit, then GM_E_COMM;
+                               a rank that fails marks the segment and its peers fail at once).  1 runs
+                               when the ranks share one GPU (RCCL refuses that); all the ranks of one
+                               node.  Set on every rank before the solve. */
+    GM_OPT_POISON = 19      /* test hook, multi-process sharded solves: 1 = fill what a rank receives
+                               with 0xFF before it arrives -- the split box engine's table (IPC / RCCL
+                               transports) before every solve, the sparse engine's receive buffers
+                               before every exchange -- so a halo or reply that never lands, or lands
+                               late, changes the results instead of reading a previous solve's bytes.
+                               0 (default) = off.  2 (box engine, IPC, test only) = additionally set
+                               the first batch's arrival flag one solve early on every sending rank,
+                               so the receiver may read its halo before it is written: solve 2 must
+                               then differ from the oracle (tests/test_gpu_multiproc.py) */
 };
 
 /* Buffer roles for gm_adopt_buffer. */
@@ -162,6 +184,10 @@ typedef struct {
     int32_t engine;         /* GM_ENGINE_DENSE or GM_ENGINE_SPARSE */
     uint64_t n_edges;       /* sparse path: parent->child edges expanded (this rank) */
     int32_t flow_fallbacks; /* box engine: dataflow solves of this context redone with tier launches */
+    uint64_t n_stored;      /* positions the solve expanded and resolved (all ranks): with a symmetry
+                               reduction (GM_OPT_SYMMETRY) one representative per orbit, so <= n_positions,
+                               which counts every position the representatives stand for; = n_positions
+                               for the other engines */
 } gm_stats_t;
 
 /* Library version (GM_ABI_VERSION). */

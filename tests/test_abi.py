@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     assert declared <= exported
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.gm_version() == 1
+    assert lib.gm_version() == 2
 
 
 def test_library_is_gfx950_code():
@@ -210,3 +210,29 @@ def test_header_documents_query_per_engine():
     doc = text[:text.index("int gm_query(")].rsplit("/*", 1)[1]
     for phrase in ("0xFFFF", "multi-process", "box engine", "sparse", "virtual ranks"):
         assert phrase in doc, phrase
+
+
+def test_abi_layout_pinned(tmp_path):
+    """GM_ABI_VERSION 2 pins the struct and the signatures a ctypes caller relies
+    on.  gcc compiles the header and prints sizeof / offsetof of gm_stats_t; they equal the
+    ctypes mirror's.  gm_box_plan carries its opts and axis parameters, gm_rank_stats its
+    recv_bytes array."""
+    import ctypes
+    fields = [n for n, _ in _lib.Stats._fields_]
+    src = tmp_path / "pin.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gmsolve.h"\nint main(void){\n'
+                   '  printf("%zu\\n", sizeof(gm_stats_t));\n'
+                   + "".join('  printf("%%zu\\n", offsetof(gm_stats_t, %s));\n' % f for f in fields)
+                   + '  printf("%d\\n", GM_ABI_VERSION);\n  return 0;\n}\n')
+    exe = tmp_path / "pin"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(_lib.Stats)
+    assert vals[1:-1] == [getattr(_lib.Stats, f).offset for f in fields]
+    assert vals[-1] == _lib.ABI_VERSION == _lib.lib().gm_version()
+    text = open(os.path.join(REPO, "include", "gmsolve.h")).read()
+    assert re.search(r"int gm_box_plan\(uint64_t root_key, int world, int rank, const int32_t \*opts, int what, "
+                     r"int axis, uint32_t \*out,\s+uint64_t cap, uint64_t \*n\);", text)
+    assert re.search(r"int gm_rank_stats\(gm_ctx \*ctx, double \*kernel_ms, uint64_t \*boxes, uint64_t \*recv_bytes,",
+                     text)
+    assert len(_lib.lib().gm_box_plan.argtypes) == 9

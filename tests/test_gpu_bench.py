@@ -60,3 +60,21 @@ def test_bench_rehearsal_two_processes_one_gpu():
     assert d["n_gpus"] == 2 and d["parity"]["ok"] and d["halo_transport_fallback"] is None
     assert d["rehearsal"] and d["sharding"]["work_vs_one_gpu"] == 1.0
     assert d["parity"]["per_rank_vs_oracle"]["wrong_ranks"] == []
+
+
+def test_bench_rehearsal_failed_probe_exits_cleanly():
+    """a rehearsal whose IPC probe fails (forced by the GM_BENCH_PROBE_FAIL
+    hook) has nothing to fall back to, so bench.py ends at once with status 4 and one JSON
+    error line -- no autotune or timed solves on the broken transport, no traceback cascade."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29533", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--rehearse-one-gpu", "--dist-batch", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=280, cwd=REPO,
+                       env=dict(os.environ, GM_BENCH_PROBE_FAIL="1"))
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] is None and "probe failed" in d["error"]
+    assert 'bench.py", line' not in r.stderr, r.stderr[-3000:]   # no traceback through bench.py (torchrun
+    # itself reports the failed child with its own traceback)

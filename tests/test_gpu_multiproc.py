@@ -158,12 +158,13 @@ def test_box_ipc_ranks_vs_oracle(oracle, world, root, batch, sym):
     runs on a one-GPU box, the ranks sharing the GPU (RCCL refuses that).  Three solves in a
     row (the flags' sequence numbers and the back-pressure on reused buffers): the summed
     digests equal the C oracle's every time, every rank reports the root record, and every
-    sampled key is answered by exactly one rank (gm_query)."""
+    sampled key is answered by exactly one rank (gm_query).  GM_OPT_POISON 1: every received
+    box goes back to 0xFF after it is read, so solves 2 and 3 read nothing solve 1 left."""
     from gamesmanmpi_amd import _lib
     ok, orec, want = _oracle_box(oracle, root)
     sample = ok[:: max(1, len(ok) // 3000)]
     res = _run(world, SUB, (8,), {"box_transport": 1, "root": root, "dist_batch": batch, "dist_symmetry": sym,
-                                  "solves": 3, "query_keys": sample.tolist()}, shared=True)
+                                  "solves": 3, "poison": 1, "query_keys": sample.tolist()}, shared=True)
     for i in range(3):
         assert (sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1), sum(r["digests"][i][1] for r in res)) == want
     rec = orec[np.searchsorted(ok, root)]
@@ -179,7 +180,7 @@ def test_box_ipc_ranks_2_32_matches_oracle_digest():
     """Config 5 at full size over 4 processes with the IPC transport (sharing one GPU on a
     one-GPU box): the summed digests equal the committed oracle digest, twice."""
     ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["subtract_8"]
-    res = _run(4, SUB, (8,), {"box_transport": 1, "dist_batch": 1, "solves": 2}, shared=True)
+    res = _run(4, SUB, (8,), {"box_transport": 1, "dist_batch": 1, "solves": 2, "poison": 1}, shared=True)
     for i in range(2):
         assert (sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1),
                 sum(r["digests"][i][1] for r in res)) == (ref["digest"], 1 << 32)
@@ -195,6 +196,63 @@ def test_box_ipc_dataflow_ranks_vs_oracle(oracle, world):
     of the resident workgroups.  Three solves: the summed digests equal the oracle's."""
     root = 0x33557777
     ok, orec, want = _oracle_box(oracle, root)
-    res = _run(world, SUB, (8,), {"box_transport": 1, "box_flow": 1, "root": root, "solves": 3}, shared=True)
+    res = _run(world, SUB, (8,), {"box_transport": 1, "box_flow": 1, "root": root, "solves": 3, "poison": 1},
+               shared=True)
     for i in range(3):
         assert (sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1), sum(r["digests"][i][1] for r in res)) == want
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("name,game,params", [("othello_4x4", OTH, (4, 4)), ("toot_4x4", TOOT, (4, 4))])
+def test_sparse_ipc_ranks_vs_oracle_digest(world, name, game, params):
+    """the hash-sharded sparse engine (csrc/dist_sparse.hip, north_star's
+    partition for configs 3/4) across PROCESSES, one rank each, with the IPC transport
+    (GM_OPT_SPARSE_TRANSPORT 1): every tier's LOOK_UP keys and RESOLVE scores are pulled out of
+    the owners' send buffers through HIP IPC mappings, counts / totals / the root record
+    all-gathered through the shared-memory segment.  Runs on a one-GPU box, the ranks sharing
+    the GPU.  Receive buffers are poisoned with 0xFF before every exchange (GM_OPT_POISON 1), and
+    two solves run back to back: the summed digests, the per-tier counts and the root record
+    equal the committed oracle's both times (reference src/new_process.py:156-160, :179-187)."""
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))[name]
+    res = _run(world, game, params, {"sparse_transport": 1, "poison": 1, "solves": 2}, shared=True)
+    for i in range(2):
+        assert (sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1),
+                sum(r["digests"][i][1] for r in res)) == (ref["digest"], ref["positions"])
+    assert all(r["n"] == ref["positions"] and r["rec"] == ref["root_record"] for r in res)
+    per = ref.get("per_ply") or ref.get("per_tier")
+    assert all(r["tiers"] == per for r in res)
+    assert all(r["exchanged"] > 0 for r in res)
+
+
+def test_sparse_ipc_ranks_query_othello_golden():
+    """Othello 4x4 over 3 processes (IPC transport): every key of the reference plugin's golden
+    table is answered by exactly one rank (its hash owner), with the golden record."""
+    from gamesmanmpi_amd import _lib
+    g = np.load(os.path.join(GOLDEN, "othello_4x4.npz"))
+    res = _run(3, OTH, (4, 4), {"sparse_transport": 1, "query_keys": g["keys"].tolist()}, shared=True)
+    q = np.array([r["query"] for r in res])
+    answered = q != _lib.REC_UNSOLVED
+    assert (answered.sum(axis=0) == 1).all()
+    assert np.array_equal(np.where(answered, q, 0).sum(axis=0), g["records"])
+
+
+@pytest.mark.parametrize("poison,caught", [(2, True), (3, False)])
+def test_box_ipc_early_read_caught_by_poison(oracle, poison, caught):
+    """a fault injected into the IPC transport must fail solve 2, not only
+    solve 1.  Test hook GM_OPT_POISON 2 / 3: from solve 2 on, rank 1 reads its halo boxes
+    without waiting for their arrival flags (as if the flags were set early) while rank 0, the
+    sender, is held 50 ms at the start of its solve.  With the received boxes poisoned (2), the
+    early reads see 0xFF and solve 2's summed digest differs from the oracle's; solve 1 is
+    exact.  Without poisoning (3) the same fault is invisible -- the early reads find solve 1's
+    identical codes -- which is why the tests and the bench's probe poison."""
+    root = 0x33557777
+    ok, orec, want = _oracle_box(oracle, root)
+    res = _run(2, SUB, (8,), {"box_transport": 1, "root": root, "dist_batch": 1, "solves": 3, "poison": poison},
+               shared=True)
+    got = [(sum(r["digests"][i][0] for r in res) & ((1 << 64) - 1), sum(r["digests"][i][1] for r in res))
+           for i in range(3)]
+    assert got[0] == want
+    if caught:
+        assert got[1] != want and got[2] != want
+    else:
+        assert got[1] == want and got[2] == want
