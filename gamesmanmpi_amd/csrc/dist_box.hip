@@ -1203,7 +1203,7 @@ static int bx_run(Ctx *c, DistBox *d, bool op_events) {
     } else {
         GM_TRY(bx_enqueue(c, d, c->dist_solo, op_events));
     }
-    if (c->poison & 1)   // test hook: the halo boxes just read go back to 0xFF before the senders may store the next solve's
+    if (c->poison == 1 || c->poison == 2)   // test hook: the halo boxes just read go back to 0xFF before the senders may store the next solve's
         for (auto &R : d->ranks)
             if (R.n_poison_boxes)
                 hipLaunchKernelGGL(bx_poison_kernel, dim3(R.n_poison_boxes), dim3(256), 0, R.S, R.table,

@@ -281,7 +281,7 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
         c->sparse_transport = (int)v;
         return GM_OK;
     case GM_OPT_POISON:
-        if (v < 0 || v > 2) { set_error("GM_OPT_POISON must be 0, 1 or 2"); return GM_E_ARG; }
+        if (v < 0 || v > 3) { set_error("GM_OPT_POISON must be 0..3"); return GM_E_ARG; }
         c->poison = (int)v;
         return GM_OK;
     case GM_OPT_BOX_SPLIT:

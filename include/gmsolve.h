@@ -154,10 +154,12 @@ enum {
                                transports) before every solve, the sparse engine's receive buffers
                                before every exchange -- so a halo or reply that never lands, or lands
                                late, changes the results instead of reading a previous solve's bytes.
-                               0 (default) = off.  2 (box engine, IPC, test only) = additionally set
-                               the first batch's arrival flag one solve early on every sending rank,
-                               so the receiver may read its halo before it is written: solve 2 must
-                               then differ from the oracle (tests/test_gpu_multiproc.py) */
+                               0 (default) = off.  Fault hook (box engine, IPC transport, tests only):
+                               2 = 1 plus, from the second solve on, every receiver reads its halo boxes
+                               without waiting for their arrival flags (as if they were set early) while
+                               rank 0 is held 50 ms -- solve 2 then differs from the oracle; 3 = the
+                               same fault without the poisoning, which no digest can see (solve 2 reads
+                               solve 1's identical bytes; tests/test_gpu_multiproc.py) */
 };
 
 /* Buffer roles for gm_adopt_buffer. */
