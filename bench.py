@@ -354,7 +354,14 @@ def sparse_config(name, game, params, rank, world, dist, torch):
     n, rec, ts = timed_solves(ctx, root, rank, world, dist, torch)
     med = sorted(ts)[len(ts) // 2]
     st = ctx.stats()
+    # positions counted vs computed: with GM_OPT_SYMMETRY on (the default)
+    # the engine expands and resolves one representative per symmetry orbit and counts every
+    # position of the orbit; both rates are reported
     out = {"positions": n, "root_record": rec, "solve_ms": med * 1e3, "positions_per_s": n / med,
+           "positions_computed": st["n_stored"], "positions_computed_per_s": st["n_stored"] / med,
+           "positions_note": "positions = every position reached (each symmetry orbit counted whole); "
+                             "positions_computed = the orbit representatives the engine expanded and resolved "
+                             "(GM_OPT_SYMMETRY 1, the default)",
            "statistic": "median of %d solves after %d warm-up (max over ranks)" % (SIDE_REPEATS, SIDE_WARMUP),
            "solve_ms_all": [round(t * 1e3, 3) for t in ts],
            "ranks": world, "exchanged_bytes_rank%d" % rank: st["exchanged_bytes"]}
@@ -371,6 +378,19 @@ def sparse_config(name, game, params, rank, world, dist, torch):
         out["algo_bytes_per_position"] = st["algo_bytes"] / n
         if world == 1:
             out["roofline"] = toot_roofline(st["algo_bytes"], med)
+        # the same solve with the symmetry reduction off: every position computed
+        ctx.set_option(_lib.OPT_SYMMETRY, 0)
+        fn, frec, fts = timed_solves(ctx, root, rank, world, dist, torch, warmup=1, repeats=3)
+        fmed = sorted(fts)[1]
+        fst = ctx.stats()
+        fd, fm = summed_digest(ctx, world, dist, torch)
+        out["symmetry_off"] = {"solve_ms": fmed * 1e3, "positions": fn, "positions_computed": fst["n_stored"],
+                               "positions_per_s": fn / fmed, "edges": fst["n_edges"],
+                               "statistic": "median of 3 after 1 warm-up (max over ranks)",
+                               "digest": "%#018x" % fd,
+                               "digest_matches_oracle": (ref is not None and (fd, fm) == (ref["digest"], ref["positions"])
+                                                         and frec == ref["root_record"])}
+        ctx.set_option(_lib.OPT_SYMMETRY, 1)
         if world == 1:   # the CPU leg's bounded sample, solved here too: the same workload on both
             sub = toot_sample_root(params)
             sn, srec, sts = timed_solves(ctx, sub, rank, world, dist, torch, warmup=1, repeats=3)

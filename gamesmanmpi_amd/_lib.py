@@ -47,7 +47,8 @@ SYMBOLS = ("gm_version", "gm_last_error", "gm_device_count", "gm_open", "gm_set_
            "gm_set_option", "gm_pack_initial", "gm_expand_host", "gm_comm_unique_id",
            "gm_set_comm", "gm_solve", "gm_solve_graph", "gm_export", "gm_query", "gm_digest", "gm_stats",
            "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_dist_plan", "gm_box_plan",
-           "gm_rank_stats", "gm_rank_op_ms", "gm_close")
+           "gm_rank_stats", "gm_rank_op_ms", "gm_close", "gm_key_words", "gm_pack_initial_key",
+           "gm_expand_host_key", "gm_solve_key", "gm_export_key", "gm_query_key")
 
 
 class GMError(RuntimeError):
@@ -124,6 +125,12 @@ def lib():
         "gm_rank_stats": (ctypes.c_int, [vp, vp, vp, vp, ctypes.c_int, P(ctypes.c_int)]),
         "gm_rank_op_ms": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_int, P(ctypes.c_int)]),
         "gm_close": (None, [vp]),
+        "gm_key_words": (ctypes.c_int, [vp]),
+        "gm_pack_initial_key": (ctypes.c_int, [vp, vp]),
+        "gm_expand_host_key": (ctypes.c_int, [vp, vp, vp, ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int), P(i64)]),
+        "gm_solve_key": (ctypes.c_int, [vp, vp, P(u64), P(ctypes.c_uint16)]),
+        "gm_export_key": (ctypes.c_int, [vp, vp, vp, u64, P(u64)]),
+        "gm_query_key": (ctypes.c_int, [vp, vp, vp, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -168,3 +175,13 @@ def box_plan(world, rank, what, root=0xFFFFFFFF, axis=0, batch=4, symmetry=1, sp
     out = np.zeros(max(1, n.value), dtype=np.uint32)
     check(L.gm_box_plan(root, world, rank, opts, what, axis, out.ctypes.data, len(out), ctypes.byref(n)))
     return out[:n.value]
+
+
+def int_to_words(key, nwords):
+    """A key (Python int) as `nwords` u64 words, least significant first (include/gmsolve.h)."""
+    return [(int(key) >> (64 * i)) & ((1 << 64) - 1) for i in range(nwords)]
+
+
+def words_to_int(words):
+    """u64 key words (least significant first) -> one Python int."""
+    return sum(int(w) << (64 * i) for i, w in enumerate(words))

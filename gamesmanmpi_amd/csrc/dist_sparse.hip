@@ -183,28 +183,31 @@ static int sp_ipc_peer(SpIpc &X, int r, int k, char **out) {
     return GM_OK;
 }
 
-struct SpRank {
+template <class K>
+struct SpRankT {
     int rank = 0;
-    std::vector<SpTier> tiers;
+    std::vector<SpTierT<K>> tiers;
     unsigned long long *d_cnt = nullptr;     // per-tier frontier counts
     uint32_t *d_err = nullptr;
     unsigned long long *d_hist = nullptr;    // G*S bins
     unsigned long long *d_cursor = nullptr;  // G*S bins
     unsigned long long *d_seg = nullptr;     // G*S bins
     unsigned long long *d_scr = nullptr;     // [0,8) edges by step, [9] interior count, [10] seen, [12] cursor
-    uint64_t *sendk = nullptr, *recvk = nullptr;
+    K *sendk = nullptr, *recvk = nullptr;
     uint64_t send_cap = 0, recv_cap = 0, best_cap = 0;
     uint32_t *sendp = nullptr, *best = nullptr;
     uint16_t *reply_out = nullptr, *reply_in = nullptr;
 };
 
+// the key-independent part of a sharded solve (c->dist_sp); DistSparseK<K> adds the ranks
 struct DistSparse {
+    virtual ~DistSparse() = default;
     int G = 1, S = 1;
     bool loopback = false;
     bool ipc = false;                        // GM_OPT_SPARSE_TRANSPORT 1
+    bool wide = false;                       // 128-bit keys (DistSparseK<K128>)
     SpIpc X;
     int64_t t_root = 0;
-    std::vector<SpRank> ranks;
     std::vector<uint64_t> gcount;            // global positions per tier
     size_t cnt_cap = 0;
     unsigned long long *d_mat = nullptr;     // all-gathered G*G*S counts (RCCL mode)
@@ -213,6 +216,10 @@ struct DistSparse {
     uint32_t *d_root = nullptr;
     uint64_t sent_bytes = 0, edges = 0;
     DedupEstimate est;
+};
+template <class K>
+struct DistSparseK : DistSparse {
+    std::vector<SpRankT<K>> ranks;
 };
 
 // ------------------------------------------------------------------ kernels
@@ -226,13 +233,14 @@ constexpr int MAXBINS = 64 * 3;
 // scatter marks parents with a LOSS-in-0 child (iwon); the backward pass sends
 // nothing for them (their value is final: WIN in 1).
 template <class D, bool SCATTER, bool BACK>
-__global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n, int G,
+__global__ __launch_bounds__(256) void bucket_kernel(D d, const key_t<D> *__restrict__ ikeys, uint64_t n, int G,
                                                      unsigned long long *hist,
                                                      const unsigned long long *__restrict__ seg,
-                                                     unsigned long long *cursor, uint64_t *out_keys,
+                                                     unsigned long long *cursor, key_t<D> *out_keys,
                                                      uint32_t *out_parent, uint32_t *best, uint8_t *iwon,
                                                      uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
+    using K = key_t<D>;
     __shared__ unsigned int lh[MAXBINS], lh2[MAXBINS];
     __shared__ unsigned long long lbase[MAXBINS];
     const int nb = G * S;
@@ -242,14 +250,15 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__rest
         const uint64_t i = base + threadIdx.x;
         const bool won_before = BACK && i < n && iwon[i];
         const bool live = i < n && !won_before;
-        const uint64_t k = live ? ikeys[i] : 0;
+        K k{};
+        if (live) k = ikeys[i];
         const int64_t tk = live ? d.tier(k) : 0;
         // one pass over the children; `emit(c, bin)` is called for the ones that leave this thread
         bool won = false;
         auto walk = [&](auto emit) -> uint32_t {
             uint32_t local = 0;
             if (!live) return local;
-            d.visit(k, [&](uint64_t c) {
+            d.visit(k, [&](const K &c) {
                 if (SCATTER && !BACK && !won) won = d.primitive(c) == LOSS;
                 if (BACK) {
                     const int p = d.primitive(c);
@@ -265,7 +274,7 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__rest
             });
             return local;
         };
-        walk([&](uint64_t, int bin) { atomicAdd(&lh[bin], 1u); });
+        walk([&](const K &, int bin) { atomicAdd(&lh[bin], 1u); });
         __syncthreads();
         if (!SCATTER) {
             for (int b = threadIdx.x; b < nb; b += blockDim.x)
@@ -274,7 +283,7 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__rest
             for (int b = threadIdx.x; b < nb; b += blockDim.x)
                 lbase[b] = lh[b] ? seg[b] + atomicAdd(&cursor[b], (unsigned long long)lh[b]) : 0ull;
             __syncthreads();
-            const uint32_t local = walk([&](uint64_t c, int bin) {
+            const uint32_t local = walk([&](const K &c, int bin) {
                 const unsigned long long at = lbase[bin] + atomicAdd(&lh2[bin], 1u);
                 out_keys[at] = c;
                 if (BACK) out_parent[at] = (uint32_t)i;
@@ -287,7 +296,8 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const uint64_t *__rest
     }
 }
 
-__global__ void insert_recv_kernel(const uint64_t *__restrict__ in, uint64_t n, FrontRef t, uint32_t *err) {
+template <class K>
+__global__ void insert_recv_kernel(const K *__restrict__ in, uint64_t n, typename KT<K>::Front t, uint32_t *err) {
     uint64_t fresh = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
@@ -297,7 +307,8 @@ __global__ void insert_recv_kernel(const uint64_t *__restrict__ in, uint64_t n, 
     wave_add(t.count, fresh);
 }
 
-__global__ void lookup_kernel(const uint64_t *__restrict__ in, uint64_t n, ResRef t, uint16_t *out, uint32_t *err) {
+template <class K>
+__global__ void lookup_kernel(const K *__restrict__ in, uint64_t n, typename KT<K>::Res t, uint16_t *out, uint32_t *err) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const int s = res_find(t, in[i]);
@@ -313,8 +324,9 @@ __global__ void fold_kernel(const uint16_t *__restrict__ reply, const uint32_t *
         atomicMax(&best[parent[i]], (uint32_t)reply[i]);
 }
 
+template <class R>
 __global__ void finalize_kernel(const uint32_t *__restrict__ islot, const uint32_t *__restrict__ best, uint64_t n,
-                                ResRef self, uint32_t *err) {
+                                R self, uint32_t *err) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t b = best[i];
@@ -324,7 +336,8 @@ __global__ void finalize_kernel(const uint32_t *__restrict__ islot, const uint32
     }
 }
 
-__global__ void root_lookup_kernel(ResRef t, uint64_t key, uint32_t *out) {
+template <class K>
+__global__ void root_lookup_kernel(typename KT<K>::Res t, K key, uint32_t *out) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         const int s = res_find(t, key);
         *out = s < 0 ? 0u : (uint32_t)s;
@@ -344,24 +357,26 @@ static int sp_ipc_reduce(SpIpc &X, std::vector<uint64_t> &v, bool max) {
     return GM_OK;
 }
 
-static int grow64(Ctx *c, uint64_t **p, uint64_t *cap, uint64_t need) {
+template <class K>
+static int grow_keys(Ctx *c, K **p, uint64_t *cap, uint64_t need) {
     if (need <= *cap && *p) return GM_OK;
     dev_free(c, *p);
     const uint64_t nc = std::max<uint64_t>(need + need / 4, 1 << 16);
-    GM_TRY(dev_alloc(c, (void **)p, nc * 8));
+    GM_TRY(dev_alloc(c, (void **)p, nc * sizeof(K)));
     *cap = nc;
     return GM_OK;
 }
 
 template <class T>
-static int grow_to(Ctx *c, T **p, uint64_t n) {   // paired with a grow64'd buffer of n entries
+static int grow_to(Ctx *c, T **p, uint64_t n) {   // paired with a grow_keys'd buffer of n entries
     dev_free(c, *p);
     return dev_alloc(c, (void **)p, std::max<uint64_t>(n, 1) * sizeof(T));
 }
 
-static FrontRef fref(SpRank &R, size_t t) {
-    SpTier &T = R.tiers[t];
-    return FrontRef{T.slots, T.cap, R.d_cnt + t};
+template <class K>
+static typename KT<K>::Front fref(SpRankT<K> &R, size_t t) {
+    SpTierT<K> &T = R.tiers[t];
+    return typename KT<K>::Front{T.slots, T.cap, R.d_cnt + t};
 }
 
 // Cross-rank exchange of G-segmented arrays (RCCL mode; loopback copies are done by the caller).
@@ -385,15 +400,16 @@ static int sendrecv(Ctx *c, DistSparse *d, const void *send, const uint64_t *sen
 }
 
 template <class D, bool SCATTER, bool BACK>
-static void run_bucket(Ctx *c, DistSparse *d, const D &desc, SpRank &R, size_t t, uint32_t *best) {
-    SpTier &T = R.tiers[t];
+static void run_bucket(Ctx *c, DistSparse *d, const D &desc, SpRankT<key_t<D>> &R, size_t t, uint32_t *best) {
+    SpTierT<key_t<D>> &T = R.tiers[t];
     if (!T.ni) return;
     hipLaunchKernelGGL((bucket_kernel<D, SCATTER, BACK>), dim3(grid_for(T.ni)), dim3(256), 0, c->stream, desc, T.ikeys,
                        T.ni, d->G, R.d_hist, R.d_seg, R.d_cursor, R.sendk, R.sendp, best, T.iwon, R.d_err);
 }
 
 // counts[r][dest*S+dt] for all ranks -> host matrix (G x G*S)
-static int gather_counts(Ctx *c, DistSparse *d, std::vector<uint64_t> &mat) {
+template <class K>
+static int gather_counts(Ctx *c, DistSparseK<K> *d, std::vector<uint64_t> &mat) {
     const int nb = d->G * d->S;
     mat.assign((size_t)d->G * nb, 0);
     if (d->loopback) {
@@ -414,7 +430,8 @@ static int gather_counts(Ctx *c, DistSparse *d, std::vector<uint64_t> &mat) {
     return GM_OK;
 }
 
-static int check_err(Ctx *c, DistSparse *d) {
+template <class K>
+static int check_err(Ctx *c, DistSparseK<K> *d) {
     for (auto &R : d->ranks) {
         uint32_t e;
         GM_HIP(hipMemcpyAsync(&e, R.d_err, 4, hipMemcpyDeviceToHost, c->stream));
@@ -460,11 +477,12 @@ static Layout layout_for(DistSparse *d, const std::vector<uint64_t> &mat, int r)
 // move every rank's segmented send buffer to the owners (or, reverse = true, the replies back)
 // IPC: publish this rank's send buffer, barrier, pull every segment addressed to this rank out
 // of the senders' buffers, barrier (the senders may then overwrite them)
-static int exchange_ipc(Ctx *c, DistSparse *d, const Layout &me, const std::vector<uint64_t> &mat, bool reply) {
-    SpRank &R = d->ranks[0];
+template <class K>
+static int exchange_ipc(Ctx *c, DistSparseK<K> *d, const Layout &me, const std::vector<uint64_t> &mat, bool reply) {
+    SpRankT<K> &R = d->ranks[0];
     SpIpc &X = d->X;
     const int k = reply ? 1 : 0;
-    const size_t elem = reply ? 2 : 8;
+    const size_t elem = reply ? 2 : sizeof(K);
     char *mine = reply ? (char *)R.reply_out : (char *)R.sendk;
     char *dst = reply ? (char *)R.reply_in : (char *)R.recvk;
     GM_HIP(hipStreamSynchronize(c->stream));   // the send buffer is complete
@@ -490,12 +508,14 @@ static int exchange_ipc(Ctx *c, DistSparse *d, const Layout &me, const std::vect
     return sp_ipc_barrier(X);
 }
 
-static int exchange(Ctx *c, DistSparse *d, std::vector<Layout> &lay, const std::vector<uint64_t> &mat, bool reply) {
+template <class K>
+static int exchange(Ctx *c, DistSparseK<K> *d, std::vector<Layout> &lay, const std::vector<uint64_t> &mat, bool reply) {
+    constexpr uint64_t KB = sizeof(K);
     if (c->poison)   // test hook: a segment that never lands reads as 0xFF, not as an earlier tier's data
         for (size_t i = 0; i < d->ranks.size(); i++) {
-            SpRank &R = d->ranks[i];
+            SpRankT<K> &R = d->ranks[i];
             const uint64_t n = reply ? lay[i].nsend : lay[i].nrecv;
-            if (n) GM_HIP(hipMemsetAsync(reply ? (void *)R.reply_in : (void *)R.recvk, 0xFF, n * (reply ? 2 : 8), c->stream));
+            if (n) GM_HIP(hipMemsetAsync(reply ? (void *)R.reply_in : (void *)R.recvk, 0xFF, n * (reply ? 2 : KB), c->stream));
         }
     if (d->loopback) {
         for (size_t i = 0; i < d->ranks.size(); i++)
@@ -503,9 +523,9 @@ static int exchange(Ctx *c, DistSparse *d, std::vector<Layout> &lay, const std::
                 if (!reply) {   // keys: source j's segment for dest i -> i's recv segment from j
                     const uint64_t n = lay[i].recv_off[j + 1] - lay[i].recv_off[j];
                     if (n) GM_HIP(hipMemcpyAsync(d->ranks[i].recvk + lay[i].recv_off[j],
-                                                 d->ranks[j].sendk + lay[j].send_off[i], n * 8,
+                                                 d->ranks[j].sendk + lay[j].send_off[i], n * KB,
                                                  hipMemcpyDeviceToDevice, c->stream));
-                    if (i != j) d->sent_bytes += n * 8;
+                    if (i != j) d->sent_bytes += n * KB;
                 } else {        // replies: owner j's answers to requester i
                     const uint64_t n = lay[i].send_off[j + 1] - lay[i].send_off[j];
                     if (n) GM_HIP(hipMemcpyAsync(d->ranks[i].reply_in + lay[i].send_off[j],
@@ -516,13 +536,14 @@ static int exchange(Ctx *c, DistSparse *d, std::vector<Layout> &lay, const std::
             }
         return GM_OK;
     }
-    SpRank &R = d->ranks[0];
+    SpRankT<K> &R = d->ranks[0];
     if (d->ipc) return exchange_ipc(c, d, lay[0], mat, reply);
     return reply ? sendrecv(c, d, R.reply_out, lay[0].recv_off.data(), R.reply_in, lay[0].send_off.data(), 2)
-                 : sendrecv(c, d, R.sendk, lay[0].send_off.data(), R.recvk, lay[0].recv_off.data(), 8);
+                 : sendrecv(c, d, R.sendk, lay[0].send_off.data(), R.recvk, lay[0].recv_off.data(), KB);
 }
 
-static int ensure_cnt(Ctx *c, DistSparse *d, size_t ntiers) {
+template <class K>
+static int ensure_cnt(Ctx *c, DistSparseK<K> *d, size_t ntiers) {
     if (ntiers <= d->cnt_cap) return GM_OK;
     const size_t nc = std::max<size_t>(64, ntiers * 2);
     for (auto &R : d->ranks) {
@@ -541,9 +562,9 @@ static int ensure_cnt(Ctx *c, DistSparse *d, size_t ntiers) {
 
 // classify tier t of every rank (scores in place + interior list)
 template <class D>
-static int classify_tier(Ctx *c, DistSparse *d, const D &desc, size_t t) {
+static int classify_tier(Ctx *c, DistSparseK<key_t<D>> *d, const D &desc, size_t t) {
     for (auto &R : d->ranks) {
-        SpTier &T = R.tiers[t];
+        SpTierT<key_t<D>> &T = R.tiers[t];
         const uint64_t n = T.fcount;
         if (!n) continue;
         GM_TRY(classify_tier_table(c, desc, T, R.d_scr, R.d_err));
@@ -562,12 +583,16 @@ static int classify_tier(Ctx *c, DistSparse *d, const D &desc, size_t t) {
 }
 
 template <class D>
-static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
+static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
+    using K = key_t<D>;
     dist_sparse_free(c);
-    DistSparse *d = c->dist_sp = new DistSparse();
-    d->loopback = c->virtual_ranks > 1;
+    DistSparseK<K> *d = new DistSparseK<K>();
+    c->dist_sp = d;
+    d->wide = sizeof(K) > 8;
+    // one context, one GPU and no communicator (a 128-bit-key game's only engine): loopback, G = 1
+    d->loopback = c->virtual_ranks > 1 || (c->world <= 1 && !c->have_uid);
     d->ipc = !d->loopback && c->sparse_transport == 1;
-    d->G = d->loopback ? c->virtual_ranks : c->world;
+    d->G = d->loopback ? std::max(1, c->virtual_ranks) : c->world;
     d->S = D::MAX_SKIP;
     d->t_root = desc.tier(root);
     const int G = d->G, S = d->S, nb = G * S;
@@ -579,7 +604,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     if (d->ipc) GM_TRY(sp_ipc_open(c, d->X, G));
     d->ranks.resize(d->loopback ? G : 1);
     for (size_t i = 0; i < d->ranks.size(); i++) {
-        SpRank &R = d->ranks[i];
+        SpRankT<K> &R = d->ranks[i];
         R.rank = d->loopback ? (int)i : c->rank;
         GM_TRY(dev_alloc(c, (void **)&R.d_err, 4));
         GM_HIP(hipMemsetAsync(R.d_err, 0, 4, c->stream));
@@ -597,7 +622,10 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
         if ((int)owner_rank(root, G) == R.rank) {
             GM_TRY(tier_alloc(c, &R.tiers[0].slots, 1024));
             R.tiers[0].cap = 1024;
-            hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, fref(R, 0), root, R.d_err);
+            if constexpr (sizeof(K) > 8)
+                hipLaunchKernelGGL(front_insert_one_wkernel, dim3(1), dim3(64), 0, c->stream, fref(R, 0), root, R.d_err);
+            else
+                hipLaunchKernelGGL(front_insert_one_kernel, dim3(1), dim3(64), 0, c->stream, fref(R, 0), root, R.d_err);
             R.tiers[0].fcount = 1;
         }
     d->gcount.assign(1, 1);
@@ -623,11 +651,11 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
         GM_TRY(check_err(c, d));
         std::vector<Layout> lay(d->ranks.size());
         for (size_t i = 0; i < d->ranks.size(); i++) {
-            SpRank &R = d->ranks[i];
+            SpRankT<K> &R = d->ranks[i];
             lay[i] = layout_for(d, mat, R.rank);
             d->edges += lay[i].nsend;
-            GM_TRY(grow64(c, &R.sendk, &R.send_cap, lay[i].nsend));
-            GM_TRY(grow64(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
+            GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
+            GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
             GM_HIP(hipMemcpyAsync(R.d_seg, lay[i].seg.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
             GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
             run_bucket<D, true, false>(c, d, desc, R, t, nullptr);
@@ -637,7 +665,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
         // distinct keys; a misprediction re-runs the (idempotent) inserts once
         uint64_t offered = 0, before = 0;
         for (size_t i = 0; i < d->ranks.size(); i++) {
-            SpRank &R = d->ranks[i];
+            SpRankT<K> &R = d->ranks[i];
             std::vector<uint64_t> in(S, 0);
             for (int s = 0; s < S; s++) {
                 for (int q = 0; q < G; q++) in[s] += mat[(size_t)q * nb + R.rank * S + s];
@@ -648,13 +676,13 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
                 for (int s = 0; s < S; s++) {
                     if (!in[s]) continue;
                     const size_t u = t + 1 + s;
-                    SpTier &U = R.tiers[u];
+                    SpTierT<K> &U = R.tiers[u];
                     const uint64_t needc = table_cap_for(U.fcount + (attempt ? in[s] : d->est.distinct(in[s])));
                     if (U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
                     for (int q = 0; q < G; q++) {
                         const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
                         if (n)
-                            hipLaunchKernelGGL(insert_recv_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream,
+                            hipLaunchKernelGGL(insert_recv_kernel<K>, dim3(grid_for(n)), dim3(256), 0, c->stream,
                                                R.recvk + lay[i].recv_seg[q * S + s], n, fref(R, u), R.d_err);
                     }
                 }
@@ -712,15 +740,15 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
         GM_TRY(gather_counts(c, d, mat));
         std::vector<Layout> lay(d->ranks.size());
         for (size_t i = 0; i < d->ranks.size(); i++) {
-            SpRank &R = d->ranks[i];
+            SpRankT<K> &R = d->ranks[i];
             lay[i] = layout_for(d, mat, R.rank);
             const uint64_t pc = R.send_cap, rc = R.recv_cap;
-            GM_TRY(grow64(c, &R.sendk, &R.send_cap, lay[i].nsend));
+            GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
             if (R.send_cap != pc || !R.sendp) {
                 GM_TRY(grow_to(c, &R.sendp, R.send_cap));
                 GM_TRY(grow_to(c, &R.reply_in, R.send_cap));
             }
-            GM_TRY(grow64(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
+            GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
             if (R.recv_cap != rc || !R.reply_out) GM_TRY(grow_to(c, &R.reply_out, R.recv_cap));
             const uint64_t ni = R.tiers[t].ni;
             if (ni > R.best_cap || !R.best) {
@@ -733,25 +761,25 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
         }
         GM_TRY(exchange(c, d, lay, mat, false));                  // LOOK_UP: keys to owners
         for (size_t i = 0; i < d->ranks.size(); i++) {            // owners look up the scores
-            SpRank &R = d->ranks[i];
+            SpRankT<K> &R = d->ranks[i];
             for (int q = 0; q < G; q++)
                 for (int s = 0; s < S; s++) {
                     const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
                     if (!n) continue;
-                    hipLaunchKernelGGL(lookup_kernel, dim3(grid_for(n)), dim3(256), 0, c->stream,
+                    hipLaunchKernelGGL(lookup_kernel<K>, dim3(grid_for(n)), dim3(256), 0, c->stream,
                                        R.recvk + lay[i].recv_seg[q * S + s], n, res_ref_of(R.tiers[t + 1 + s]),
                                        R.reply_out + lay[i].recv_seg[q * S + s], R.d_err);
                 }
         }
         GM_TRY(exchange(c, d, lay, mat, true));                   // RESOLVE: scores back
         for (size_t i = 0; i < d->ranks.size(); i++) {
-            SpRank &R = d->ranks[i];
-            SpTier &T = R.tiers[t];
+            SpRankT<K> &R = d->ranks[i];
+            SpTierT<K> &T = R.tiers[t];
             if (lay[i].nsend)
                 hipLaunchKernelGGL(fold_kernel, dim3(grid_for(lay[i].nsend)), dim3(256), 0, c->stream, R.reply_in,
                                    R.sendp, lay[i].nsend, R.best);
             if (T.ni)
-                hipLaunchKernelGGL(finalize_kernel, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, T.islot, R.best,
+                hipLaunchKernelGGL(finalize_kernel<typename KT<K>::Res>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, T.islot, R.best,
                                    T.ni, res_ref_of(T), R.d_err);
         }
         GM_TRY(check_err(c, d));
@@ -762,7 +790,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     GM_HIP(hipMemsetAsync(d->d_root, 0, 4, c->stream));
     for (auto &R : d->ranks)
         if ((int)owner_rank(root, G) == R.rank && !R.tiers.empty())
-            hipLaunchKernelGGL(root_lookup_kernel, dim3(1), dim3(64), 0, c->stream, res_ref_of(R.tiers[0]), root,
+            hipLaunchKernelGGL(root_lookup_kernel<K>, dim3(1), dim3(64), 0, c->stream, res_ref_of(R.tiers[0]), root,
                                d->d_root);
     if (!d->loopback && !d->ipc) GM_NCCL(ncclAllReduce(d->d_root, d->d_root, 1, ncclUint32, ncclMax, c->comm, c->stream));
     uint32_t rs = 0;
@@ -800,7 +828,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     uint64_t n = 0, tb = 0;
     for (auto v : gall) n += v;
     for (auto &R : d->ranks)
-        for (auto &T : R.tiers) tb += T.cap * sizeof(RSlot) + T.ni * 13;
+        for (auto &T : R.tiers) tb += T.cap * sizeof(typename KT<K>::Slot) + T.ni * (sizeof(K) + 5);
     c->n_positions = n;
     c->tier_counts = gall;
     c->stats.n_positions = n;
@@ -816,6 +844,7 @@ static int solve_sharded(Ctx *c, const D &desc, uint64_t root) {
     return GM_OK;
 }
 
+// the context's descriptor: the 64-bit-key games (with_game) or Othello 8x8 (K128 keys)
 template <class F>
 static int with_game(Ctx *c, F &&f) {
     switch (c->game) {
@@ -828,41 +857,55 @@ static int with_game(Ctx *c, F &&f) {
     set_error("unknown game");
     return GM_E_GAME;
 }
+template <class F>
+static int with_any_game(Ctx *c, F &&f) {
+    if (c->wide) return f(c->oth8);
+    return with_game(c, f);
+}
 
-int dist_sparse_solve(Ctx *c, uint64_t root) {
-    int rc = with_game(c, [&](const auto &desc) { return solve_sharded(c, desc, root); });
+static int finish_solve(Ctx *c, int rc) {
     // IPC: a rank that leaves with an error marks the segment, so its peers' next barrier fails
     // at once instead of waiting out the limit
     if (rc != GM_OK && c->dist_sp) sp_ipc_fail(c->dist_sp->X);
     return rc;
 }
 
-int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
-    DistSparse *d = c->dist_sp;
+int dist_sparse_solve(Ctx *c, uint64_t root) {
+    if (c->wide) { set_error("this game's keys are 128-bit: gm_solve_key"); return GM_E_ARG; }
+    return finish_solve(c, with_game(c, [&](const auto &desc) { return solve_sharded(c, desc, root); }));
+}
+
+int dist_sparse_solve_wide(Ctx *c, const K128 &root) {
+    if (!c->wide) { set_error("not a 128-bit-key game"); return GM_E_ARG; }
+    return finish_solve(c, solve_sharded(c, c->oth8, root));
+}
+
+// every rank's positions (each representative's orbit expanded), sorted by key
+template <class D>
+static int export_ranks(Ctx *c, const D &desc, key_t<D> *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
+    using K = key_t<D>;
+    auto *d = static_cast<DistSparseK<K> *>(c->dist_sp);
     uint64_t total = 0;
     for (auto &R : d->ranks)
         for (auto &T : R.tiers) total += T.count_all;
     *n = total;
     if (!keys) return GM_OK;
     if (cap < total) { set_error("export buffer too small"); return GM_E_CAP; }
-    uint64_t *dk;
+    K *dk;
     uint16_t *dr;
     unsigned long long *cur;
-    GM_HIP(hipMalloc(&dk, std::max<uint64_t>(1, total) * 8));
+    GM_HIP(hipMalloc(&dk, std::max<uint64_t>(1, total) * sizeof(K)));
     GM_HIP(hipMalloc(&dr, std::max<uint64_t>(1, total) * 2));
     GM_HIP(hipMalloc(&cur, 8));
     GM_HIP(hipMemsetAsync(cur, 0, 8, c->stream));
-    GM_TRY(with_game(c, [&](const auto &desc) {
-        for (auto &R : d->ranks)
-            for (auto &T : R.tiers)
-                if (T.count)
-                    hipLaunchKernelGGL(res_gather_kernel<std::decay_t<decltype(desc)>>, dim3(grid_for(T.cap)),
-                                       dim3(256), 0, c->stream, desc, T.slots, T.cap, dk, dr, cur);
-        return GM_OK;
-    }));
-    std::vector<uint64_t> hk(total);
+    for (auto &R : d->ranks)
+        for (auto &T : R.tiers)
+            if (T.count)
+                hipLaunchKernelGGL(res_gather_kernel<D>, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, desc, T.slots,
+                                   T.cap, dk, dr, cur);
+    std::vector<K> hk(total);
     std::vector<uint16_t> hr(total);
-    GM_HIP(hipMemcpyAsync(hk.data(), dk, total * 8, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipMemcpyAsync(hk.data(), dk, total * sizeof(K), hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipMemcpyAsync(hr.data(), dr, total * 2, hipMemcpyDeviceToHost, c->stream));
     GM_HIP(hipStreamSynchronize(c->stream));
     (void)hipFree(dk);
@@ -875,20 +918,31 @@ int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uin
     return GM_OK;
 }
 
+int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
+    if (c->wide) { set_error("this game's keys are 128-bit: gm_export_key"); return GM_E_ARG; }
+    return with_game(c, [&](const auto &desc) { return export_ranks(c, desc, keys, recs, cap, n); });
+}
+
+int dist_sparse_export_wide(Ctx *c, K128 *keys, uint16_t *recs, uint64_t cap, uint64_t *n) {
+    if (!c->wide) { set_error("not a 128-bit-key game"); return GM_E_ARG; }
+    return export_ranks(c, c->oth8, keys, recs, cap, n);
+}
+
 int dist_sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
-    DistSparse *d = c->dist_sp;
     unsigned long long *acc;
     GM_HIP(hipMalloc(&acc, 8));
     GM_HIP(hipMemsetAsync(acc, 0, 8, c->stream));
     uint64_t total = 0;
-    for (auto &R : d->ranks)
-        for (auto &T : R.tiers) total += T.count_all;
-    GM_TRY(with_game(c, [&](const auto &desc) {
+    GM_TRY(with_any_game(c, [&](const auto &desc) {
+        using D = std::decay_t<decltype(desc)>;
+        auto *d = static_cast<DistSparseK<key_t<D>> *>(c->dist_sp);
         for (auto &R : d->ranks)
-            for (auto &T : R.tiers)
+            for (auto &T : R.tiers) {
+                total += T.count_all;
                 if (T.count)
-                    hipLaunchKernelGGL(res_digest_kernel<std::decay_t<decltype(desc)>>, dim3(grid_for(T.cap)),
-                                       dim3(256), 0, c->stream, desc, T.slots, T.cap, acc);
+                    hipLaunchKernelGGL(res_digest_kernel<D>, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, desc,
+                                       T.slots, T.cap, acc);
+            }
         return GM_OK;
     }));
     unsigned long long h;
@@ -901,21 +955,23 @@ int dist_sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
 }
 
 template <class D>
-static int query_ranks(Ctx *c, const D &desc, const uint64_t *keys, uint16_t *recs, uint64_t n) {
-    DistSparse *d = c->dist_sp;
-    uint64_t *dk;
+static int query_ranks(Ctx *c, const D &desc, const key_t<D> *keys, uint16_t *recs, uint64_t n) {
+    using K = key_t<D>;
+    using Res = typename KT<K>::Res;
+    auto *d = static_cast<DistSparseK<K> *>(c->dist_sp);
+    K *dk;
     uint16_t *dr;
-    GM_HIP(hipMalloc(&dk, n * 8));
+    GM_HIP(hipMalloc(&dk, n * sizeof(K)));
     GM_HIP(hipMalloc(&dr, n * 2));
-    GM_HIP(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
+    GM_HIP(hipMemcpyAsync(dk, keys, n * sizeof(K), hipMemcpyHostToDevice, c->stream));
     std::vector<uint16_t> part(n);
     for (uint64_t i = 0; i < n; i++) recs[i] = REC_UNSOLVED;
     for (auto &R : d->ranks) {
-        std::vector<ResRef> h(R.tiers.size());
+        std::vector<Res> h(R.tiers.size());
         for (size_t t = 0; t < h.size(); t++) h[t] = res_ref_of(R.tiers[t]);
-        ResRef *tabs;
-        GM_HIP(hipMalloc(&tabs, std::max<size_t>(1, h.size()) * sizeof(ResRef)));
-        if (!h.empty()) GM_HIP(hipMemcpyAsync(tabs, h.data(), h.size() * sizeof(ResRef), hipMemcpyHostToDevice, c->stream));
+        Res *tabs;
+        GM_HIP(hipMalloc(&tabs, std::max<size_t>(1, h.size()) * sizeof(Res)));
+        if (!h.empty()) GM_HIP(hipMemcpyAsync(tabs, h.data(), h.size() * sizeof(Res), hipMemcpyHostToDevice, c->stream));
         hipLaunchKernelGGL(query_kernel<D>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, desc,
                            d->t_root, tabs, (int)h.size(), dk, dr, n);
         GM_HIP(hipMemcpyAsync(part.data(), dr, n * 2, hipMemcpyDeviceToHost, c->stream));
@@ -931,20 +987,18 @@ static int query_ranks(Ctx *c, const D &desc, const uint64_t *keys, uint16_t *re
 
 int dist_sparse_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n) {
     if (!n) return GM_OK;
-    switch (c->game) {
-    case GM_GAME_FOUR_TO_ONE: return query_ranks(c, c->f2o, keys, recs, n);
-    case GM_GAME_TTT: return query_ranks(c, c->ttt, keys, recs, n);
-    case GM_GAME_TOOT: return query_ranks(c, c->toot, keys, recs, n);
-    case GM_GAME_OTHELLO: return query_ranks(c, c->oth, keys, recs, n);
-    case GM_GAME_SUBTRACT: return query_ranks(c, c->sub, keys, recs, n);
-    }
-    set_error("unknown game");
-    return GM_E_GAME;
+    if (c->wide) { set_error("this game's keys are 128-bit: gm_query_key"); return GM_E_ARG; }
+    return with_game(c, [&](const auto &desc) { return query_ranks(c, desc, keys, recs, n); });
 }
 
-void dist_sparse_free(Ctx *c) {
-    DistSparse *d = c->dist_sp;
-    if (!d) return;
+int dist_sparse_query_wide(Ctx *c, const K128 *keys, uint16_t *recs, uint64_t n) {
+    if (!n) return GM_OK;
+    if (!c->wide) { set_error("not a 128-bit-key game"); return GM_E_ARG; }
+    return query_ranks(c, c->oth8, keys, recs, n);
+}
+
+template <class K>
+static void free_ranks(Ctx *c, DistSparseK<K> *d) {
     for (auto &R : d->ranks) {
         for (auto &T : R.tiers) free_tier(c, T);
         for (void *p : {(void *)R.d_cnt, (void *)R.d_err, (void *)R.d_hist, (void *)R.d_cursor, (void *)R.d_seg,
@@ -952,6 +1006,13 @@ void dist_sparse_free(Ctx *c) {
                         (void *)R.best, (void *)R.reply_out, (void *)R.reply_in})
             dev_free(c, p);
     }
+}
+
+void dist_sparse_free(Ctx *c) {
+    DistSparse *d = c->dist_sp;
+    if (!d) return;
+    if (d->wide) free_ranks(c, static_cast<DistSparseK<K128> *>(d));
+    else free_ranks(c, static_cast<DistSparseK<uint64_t> *>(d));
     dev_free(c, d->d_mat);
     if (d->d_tot) dev_free(c, d->d_tot);
     dev_free(c, d->d_root);

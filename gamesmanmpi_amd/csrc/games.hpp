@@ -49,6 +49,18 @@ struct part_visit_t<D, std::void_t<decltype(D::PART_VISIT)>> {
     static constexpr bool value = D::PART_VISIT;
 };
 
+// The key type of a descriptor: D::Key when it declares one (DescOthello8: K128), else u64.
+template <class D, class = void>
+struct key_of {
+    using type = uint64_t;
+};
+template <class D>
+struct key_of<D, std::void_t<typename D::Key>> {
+    using type = typename D::Key;
+};
+template <class D>
+using key_t = typename key_of<D>::type;
+
 struct NoSym {
     GM_HD uint64_t canon(uint64_t k) const { return k; }
     template <class F>
@@ -455,6 +467,126 @@ GM_HD DescOthello unreduced(const DescOthello &d) {
     r.sym = 0;
     return r;
 }
+
+// ---------------------------------------------------------------- Othello 8x8 (128-bit keys)
+// The reference plugin at its default board, reference test_games/othello_bit_new.py:8 (8x8):
+// its position string is 2A + 16 = 144 bits (white plane, black plane, turn byte, pass byte,
+// :36-55), so the key is a K128 (gm_common.hpp) and the tables are 32-byte slots
+// (sparse_tables.hpp).  Planes are read big-endian from the string, so string bit j = 8y + x
+// is plane bit 63 - j: the board rotated by 180 degrees, which the rules do not see.
+//   lo = the white plane
+//   hi = the occupied plane (white | black) with its four centre bits -- squares that are
+//        occupied in every position (the start's four discs are never removed) -- reused:
+//        bit 27 = white to move (turn byte 2), bits 28 / 35 = pass count bits 0 / 1, bit 36 =
+//        the insert's publish bit (set in every key; never all-ones: pass 3 does not occur)
+// The ABI key (include/gmsolve.h, gm_key_words = 3) is the position string as one integer, in
+// little-endian u64 words (to_words / from_words).  Rules as DescOthello (pass keeps the mover,
+// :122-124; the game ends on a full board or a second pass, :82-84).  No symmetry reduction.
+struct DescOthello8 {
+    using Key = K128;
+    static constexpr int MAX_SKIP = 3;
+    static constexpr int MAXC = 64;
+    static constexpr uint64_t CENTRE = (1ull << 27) | (1ull << 28) | (1ull << 35) | (1ull << 36);
+    static constexpr uint64_t TURN_W = 1ull << 27, PASS0 = 1ull << 28, PASS1 = 1ull << 35, PUB = K128_PUB;
+    GM_HD K128 canon(const K128 &k) const { return k; }
+    template <class F>
+    GM_HD void orbit(const K128 &k, F &&f) const { f(k); }
+    GM_HD static uint64_t occ(const K128 &k) { return k.hi | CENTRE; }
+    GM_HD static int turn(const K128 &k) { return (k.hi & TURN_W) ? 2 : 1; }
+    GM_HD static int pass(const K128 &k) { return (int)((k.hi >> 28) & 1u) | (int)(((k.hi >> 35) & 1u) << 1); }
+    GM_HD static K128 pack(uint64_t w, uint64_t b, int turn, int pass) {
+        K128 k;
+        k.lo = w;
+        k.hi = ((w | b) & ~CENTRE) | (turn == 2 ? TURN_W : 0) | ((pass & 1) ? PASS0 : 0) | ((pass & 2) ? PASS1 : 0) | PUB;
+        return k;
+    }
+    GM_HD int primitive(const K128 &k) const {
+        const uint64_t o = occ(k), w = k.lo, b = o & ~w;
+        if (o != ~0ull && pass(k) < 2) return UNDECIDED;          // :75-84
+        const int nb = popc64(b), nw = popc64(w);
+        if (nb == nw) return TIE;
+        return ((nb > nw) != (turn(k) == 1)) ? LOSS : WIN;         // :59-73
+    }
+    // discs of `opp` flipped by `me` playing plane square p (flip_helper, :100-118)
+    GM_HD static uint64_t flips(uint64_t me, uint64_t opp, int p) {
+        uint64_t all = 0;
+        const int x = p & 7, y = p >> 3;
+        for (int dx = -1; dx <= 1; dx++)
+            for (int dy = -1; dy <= 1; dy++) {
+                if (!dx && !dy) continue;
+                uint64_t run = 0;
+                int cx = x + dx, cy = y + dy;
+                while (cx >= 0 && cy >= 0 && cx < 8 && cy < 8) {
+                    const uint64_t bit = 1ull << (8 * cy + cx);
+                    if (opp & bit) {
+                        run |= bit;
+                    } else {
+                        if (me & bit) all |= run;
+                        break;
+                    }
+                    cx += dx;
+                    cy += dy;
+                }
+            }
+        return all;
+    }
+    template <class F>
+    GM_HD void visit(const K128 &k, F &&fn) const {
+        const uint64_t o = occ(k), w = k.lo, b = o & ~w;
+        const int t = turn(k);
+        const bool black = t == 1;
+        const uint64_t me = black ? b : w, opp = black ? w : b;
+        int n = 0;
+        for (uint64_t e = ~o; e; e &= e - 1) {
+            const int p = __builtin_ctzll(e);
+            if (!(opp & adjacent(p))) continue;   // no line can start: not legit (:134-146)
+            const uint64_t f = flips(me, opp, p);
+            if (!f) continue;
+            const uint64_t nme = me | (1ull << p) | f, nopp = opp & ~f;
+            n++;
+            if (!fn(pack(black ? nopp : nme, black ? nme : nopp, 3 - t, 0))) return;   // incr_turn, reset_pass
+        }
+        if (!n) fn(pack(w, b, t, pass(k) + 1));                     // [None]: incr_pass only (:122-124)
+    }
+    GM_HD static uint64_t adjacent(int p) {
+        const uint64_t bit = 1ull << p;
+        const uint64_t notA = 0xFEFEFEFEFEFEFEFEull, notH = 0x7F7F7F7F7F7F7F7Full;
+        const uint64_t e = (bit << 1) & notA, wv = (bit >> 1) & notH;
+        const uint64_t row = bit | e | wv;
+        return (row | (row << 8) | (row >> 8)) & ~bit;
+    }
+    GM_HD int children(const K128 &k, K128 *out) const {
+        int n = 0;
+        visit(k, [&](const K128 &c) {
+            out[n++] = c;
+            return true;
+        });
+        return n;
+    }
+    GM_HD int64_t tier(const K128 &k) const { return 3 * popc64(occ(k)) + pass(k); }
+    GM_HD bool valid(const K128 &k) const {
+        if (!(k.hi & PUB) || k.hi == EMPTY_HI) return false;
+        if (k.lo & ~occ(k)) return false;
+        return pass(k) <= 2;
+    }
+    // ABI words (the 144-bit string integer I = W << 80 | B << 16 | turn << 8 | pass)
+    static void to_words(const K128 &k, uint64_t *wd) {
+        const uint64_t w = k.lo, b = occ(k) & ~w;
+        wd[0] = (b << 16) | ((uint64_t)turn(k) << 8) | (uint64_t)pass(k);
+        wd[1] = (b >> 48) | (w << 16);
+        wd[2] = w >> 48;
+    }
+    // false when the words are no position of this descriptor (a centre square empty, the
+    // planes overlapping, turn / pass out of range, bits above 144)
+    static bool from_words(const uint64_t *wd, K128 *k) {
+        if (wd[2] >> 16) return false;
+        const uint64_t w = (wd[1] >> 16) | (wd[2] << 48), b = (wd[0] >> 16) | (wd[1] << 48);
+        const int t = (int)((wd[0] >> 8) & 0xFF), ps = (int)(wd[0] & 0xFF);
+        if ((w & b) || ((w | b) & CENTRE) != CENTRE || (t != 1 && t != 2) || ps > 2) return false;
+        *k = pack(w, b, t, ps);
+        return true;
+    }
+};
 
 // ---------------------------------------------------------------- Subtract
 // The build's synthetic game: `heaps` heaps of 4 bits; a move

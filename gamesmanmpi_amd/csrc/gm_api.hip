@@ -142,6 +142,8 @@ using namespace gm;
 
 extern "C" {
 
+static int need_solved(gm_ctx *h);
+
 int gm_version(void) { return GM_ABI_VERSION; }
 
 const char *gm_last_error(void) { return g_err; }
@@ -167,7 +169,9 @@ int gm_open(int game, const int32_t *params, int nparams, int device, gm_ctx **o
         ok = DescToot::make(nparams > 0 ? params[0] : 6, nparams > 1 ? params[1] : 4, &c->toot);
         break;
     case GM_GAME_OTHELLO:
-        ok = DescOthello::make(nparams > 0 ? params[0] : 4, nparams > 1 ? params[1] : 4, &c->oth);
+        // 8x8 (the reference plugin's default board, othello_bit_new.py:8): 128-bit keys
+        c->wide = nparams > 1 && params[0] == 8 && params[1] == 8;
+        ok = c->wide || DescOthello::make(nparams > 0 ? params[0] : 4, nparams > 1 ? params[1] : 4, &c->oth);
         break;
     case GM_GAME_SUBTRACT:
         c->sub.heaps = nparams > 0 ? params[0] : 8;
@@ -304,6 +308,7 @@ int gm_set_option(gm_ctx *h, int opt, int64_t v) {
 int gm_pack_initial(gm_ctx *h, uint64_t *key) {
     if (!h || !key) return GM_E_ARG;
     Ctx *c = &h->c;
+    if (c->wide) { set_error("this game's keys have %d words: gm_pack_initial_key", gm_key_words(h)); return GM_E_ARG; }
     switch (c->game) {
     case GM_GAME_FOUR_TO_ONE: *key = 4; return GM_OK;   // four_to_one.py:8-10
     case GM_GAME_TTT: *key = 0; return GM_OK;           // empty board
@@ -325,6 +330,7 @@ int gm_pack_initial(gm_ctx *h, uint64_t *key) {
 int gm_expand_host(gm_ctx *h, uint64_t key, uint64_t *children, int cap, int *n, int *prim, int64_t *tier) {
     if (!h || !n || !prim || !tier) return GM_E_ARG;
     Ctx *c = &h->c;
+    if (c->wide) { set_error("this game's keys have %d words: gm_expand_host_key", gm_key_words(h)); return GM_E_ARG; }
     uint64_t kids[32];
     int p = UNDECIDED, k = 0;
     int64_t t = 0;
@@ -390,6 +396,7 @@ int gm_set_comm(gm_ctx *h, int rank, int world, const void *uid, int bytes) {
 int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_record) {
     if (!h) return GM_E_ARG;
     Ctx *c = &h->c;
+    if (c->wide) { set_error("this game's keys have %d words: gm_solve_key", gm_key_words(h)); return GM_E_ARG; }
     if (c->game == GM_GAME_GRAPH) { set_error("a GM_GAME_GRAPH context is solved with gm_solve_graph"); return GM_E_GAME; }
     if (c->device < 0) { set_error("no HIP device is visible: the solver needs an MI355X (gfx950)"); return GM_E_HIP; }
     if (!key_valid(c, root)) { set_error("root key 0x%llx is not a valid position", (unsigned long long)root); return GM_E_KEY; }
@@ -449,6 +456,125 @@ int gm_solve(gm_ctx *h, uint64_t root, uint64_t *n_positions, uint16_t *root_rec
     c->solved = true;
     if (n_positions) *n_positions = c->n_positions;
     if (root_record) *root_record = c->root_record;
+    return GM_OK;
+}
+
+// ---------------------------------------------------------------- multi-word keys
+static constexpr int WIDE_WORDS = 3;   // Othello 8x8: the 144-bit position string (games.hpp DescOthello8)
+
+int gm_key_words(gm_ctx *h) {
+    if (!h) return GM_E_ARG;
+    return h->c.wide ? WIDE_WORDS : 1;
+}
+
+int gm_pack_initial_key(gm_ctx *h, uint64_t *words) {
+    if (!h || !words) return GM_E_ARG;
+    if (!h->c.wide) return gm_pack_initial(h, words);
+    // othello_bit_new.py:36-55: white (3,3) (4,4), black (3,4) (4,3), turn 2, no pass
+    auto bit = [](int x, int y) { return 1ull << (63 - (8 * y + x)); };
+    const uint64_t w = bit(3, 3) | bit(4, 4), b = bit(3, 4) | bit(4, 3);
+    DescOthello8::to_words(DescOthello8::pack(w, b, 2, 0), words);
+    return GM_OK;
+}
+
+int gm_expand_host_key(gm_ctx *h, const uint64_t *words, uint64_t *children, int cap, int *n, int *prim,
+                       int64_t *tier) {
+    if (!h || !words || !n || !prim || !tier) return GM_E_ARG;
+    Ctx *c = &h->c;
+    if (!c->wide) return gm_expand_host(h, words[0], children, cap, n, prim, tier);
+    K128 k;
+    if (!DescOthello8::from_words(words, &k)) { set_error("key is not a valid position"); return GM_E_KEY; }
+    K128 kids[64];
+    const DescOthello8 &d = c->oth8;
+    *prim = d.primitive(k);
+    *tier = d.tier(k);
+    *n = *prim == UNDECIDED ? d.children(k, kids) : 0;
+    if (*n > cap) { set_error("children buffer holds %d, need %d", cap, *n); return GM_E_CAP; }
+    if (children)
+        for (int i = 0; i < *n; i++) DescOthello8::to_words(kids[i], children + (size_t)WIDE_WORDS * i);
+    return GM_OK;
+}
+
+int gm_solve_key(gm_ctx *h, const uint64_t *words, uint64_t *n_positions, uint16_t *root_record) {
+    if (!h || !words) return GM_E_ARG;
+    Ctx *c = &h->c;
+    if (!c->wide) return gm_solve(h, words[0], n_positions, root_record);
+    if (c->device < 0) { set_error("no HIP device is visible: the solver needs an MI355X (gfx950)"); return GM_E_HIP; }
+    K128 root;
+    if (!DescOthello8::from_words(words, &root)) {
+        set_error("root key is not a valid position (an 8x8 Othello position keeps its four centre squares)");
+        return GM_E_KEY;
+    }
+    GM_HIP(hipSetDevice(c->device));
+    c->solved = false;
+    c->stats = gm_stats_t{};
+    if (c->world > 1 && c->virtual_ranks > 1) {
+        set_error("virtual ranks and a multi-process communicator are exclusive");
+        return GM_E_ARG;
+    }
+    // the hash-sharded sparse engine is this game's engine: one GPU (G = 1), virtual ranks, or
+    // one process per rank over RCCL / the IPC transport
+    if (c->virtual_ranks <= 1 && (c->world > 1 || c->have_uid)) {
+        if (!c->have_uid) { set_error("a %d-rank solve needs gm_set_comm with a unique id", c->world); return GM_E_COMM; }
+        if (c->sparse_transport != 1) GM_TRY(ensure_comm(c));
+    }
+    GM_TRY(dist_sparse_solve_wide(c, root));
+    if (!c->stats.n_stored) c->stats.n_stored = c->stats.n_positions;
+    c->engine = GM_ENGINE_DIST_SPARSE;
+    c->stats.engine = GM_ENGINE_DIST_SPARSE;
+    c->stats.world = c->world > 1 ? c->world : std::max(1, c->virtual_ranks);
+    c->solved = true;
+    if (n_positions) *n_positions = c->n_positions;
+    if (root_record) *root_record = c->root_record;
+    return GM_OK;
+}
+
+int gm_export_key(gm_ctx *h, uint64_t *words, uint16_t *recs, uint64_t cap, uint64_t *n) {
+    GM_TRY(need_solved(h));
+    if (!n || (words && !recs)) return GM_E_ARG;
+    Ctx *c = &h->c;
+    if (!c->wide) return gm_export(h, words, recs, cap, n);
+    GM_HIP(hipSetDevice(c->device));
+    GM_TRY(dist_sparse_export_wide(c, nullptr, nullptr, 0, n));
+    if (!words) return GM_OK;
+    if (cap < *n) { set_error("export buffer too small"); return GM_E_CAP; }
+    std::vector<K128> k(*n);
+    std::vector<uint16_t> r(*n);
+    GM_TRY(dist_sparse_export_wide(c, k.data(), r.data(), *n, n));
+    std::vector<uint64_t> w((size_t)WIDE_WORDS * *n);
+    for (uint64_t i = 0; i < *n; i++) DescOthello8::to_words(k[i], &w[(size_t)WIDE_WORDS * i]);
+    // sorted by the key's integer value (most significant word first)
+    std::vector<uint64_t> idx(*n);
+    for (uint64_t i = 0; i < *n; i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) {
+        for (int j = WIDE_WORDS - 1; j >= 0; j--) {
+            const uint64_t x = w[(size_t)WIDE_WORDS * a + j], y = w[(size_t)WIDE_WORDS * b + j];
+            if (x != y) return x < y;
+        }
+        return false;
+    });
+    for (uint64_t i = 0; i < *n; i++) {
+        for (int j = 0; j < WIDE_WORDS; j++) words[(size_t)WIDE_WORDS * i + j] = w[(size_t)WIDE_WORDS * idx[i] + j];
+        recs[i] = r[idx[i]];
+    }
+    return GM_OK;
+}
+
+int gm_query_key(gm_ctx *h, const uint64_t *words, uint16_t *recs, uint64_t n) {
+    GM_TRY(need_solved(h));
+    if (n && (!words || !recs)) return GM_E_ARG;
+    Ctx *c = &h->c;
+    if (!c->wide) return gm_query(h, words, recs, n);
+    GM_HIP(hipSetDevice(c->device));
+    std::vector<K128> k(n);
+    std::vector<uint8_t> ok(n);
+    for (uint64_t i = 0; i < n; i++) {
+        ok[i] = DescOthello8::from_words(words + (size_t)WIDE_WORDS * i, &k[i]);
+        if (!ok[i]) k[i] = K128{0, 0};   // no valid key: answers 0xFFFF below
+    }
+    GM_TRY(dist_sparse_query_wide(c, k.data(), recs, n));
+    for (uint64_t i = 0; i < n; i++)
+        if (!ok[i]) recs[i] = REC_UNSOLVED;
     return GM_OK;
 }
 

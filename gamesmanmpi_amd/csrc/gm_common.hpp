@@ -105,6 +105,25 @@ GM_HD uint64_t digest_term(uint64_t key, uint16_t rec) {
     return mix64(key * 0x9E3779B97F4A7C15ull + rec);
 }
 
+// 128-bit keys (boards whose position string exceeds 64 bits: Othello 8x8, games.hpp
+// DescOthello8).  hi is the word a table insert claims with atomicCAS (sparse_tables.hpp): it
+// never holds EMPTY_HI in a real key, and its bit PUB is set once the slot's lo word is
+// written (1 in every complete key).
+struct K128 {
+    uint64_t lo, hi;
+};
+constexpr uint64_t EMPTY_HI = ~0ull;
+constexpr uint64_t K128_PUB = 1ull << 36;   // hi's publish bit (every K128 descriptor keeps it set in its keys)
+GM_HD bool operator==(const K128 &a, const K128 &b) { return a.lo == b.lo && a.hi == b.hi; }
+GM_HD bool operator!=(const K128 &a, const K128 &b) { return !(a == b); }
+GM_HD bool operator<(const K128 &a, const K128 &b) { return a.hi != b.hi ? a.hi < b.hi : a.lo < b.lo; }
+GM_HD uint64_t mix_key(uint64_t k) { return mix64(k); }
+GM_HD uint64_t mix_key(const K128 &k) { return mix64(k.lo ^ mix64(k.hi ^ 0x2545F4914F6CDD1Dull)); }
+GM_HD bool key_empty(uint64_t k) { return k == EMPTY_KEY; }
+GM_HD bool key_empty(const K128 &k) { return k.hi == EMPTY_HI; }
+// the digest of a 128-bit key folds it to one word first (include/gmsolve.h gm_digest)
+GM_HD uint64_t digest_term(const K128 &k, uint16_t rec) { return digest_term(mix_key(k), rec); }
+
 GM_HD int popc64(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return __popcll(x);

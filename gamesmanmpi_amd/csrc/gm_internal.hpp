@@ -70,6 +70,8 @@ struct Ctx {
     DescToot toot;
     DescOthello oth;
     DescSub sub;
+    DescOthello8 oth8;       // GM_GAME_OTHELLO at 8x8: 128-bit keys (wide)
+    bool wide = false;       // keys of more than 64 bits: gm_*_key entry points, the sharded sparse engine
 
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
@@ -203,6 +205,9 @@ int dist_sub_plan(int heaps, int world, int rank, const int32_t *opts, int what,
                   uint64_t off_cap, uint64_t *n_off, uint32_t *data, uint64_t data_cap, uint64_t *n_data);
 
 int dist_sparse_solve(Ctx *c, uint64_t root);
+int dist_sparse_solve_wide(Ctx *c, const K128 &root);
+int dist_sparse_export_wide(Ctx *c, K128 *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
+int dist_sparse_query_wide(Ctx *c, const K128 *keys, uint16_t *recs, uint64_t n);
 int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
 int dist_sparse_query(Ctx *c, const uint64_t *keys, uint16_t *recs, uint64_t n);
 int dist_sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n);

@@ -38,5 +38,6 @@ inline uint64_t pow2_at_least(uint64_t n) {
 // independent of the slot index (low bits).  Mirrors GameState.get_hash
 // (src/game_state.py:23-31): any function of the key works, only balance matters.
 GM_HD uint32_t owner_rank(uint64_t key, uint32_t G) { return (uint32_t)((mix64(key) >> 32) % G); }
+GM_HD uint32_t owner_rank(const K128 &key, uint32_t G) { return (uint32_t)((mix_key(key) >> 32) % G); }
 
 }  // namespace gm

@@ -46,6 +46,45 @@ inline GM_HD uint32_t eff_loc(uint32_t loc, uint64_t cap) {
     return (loc >> 8) && cap >= (2ull << (loc >> 8)) ? loc : 0u;
 }
 
+// 128-bit keys (gm_common.hpp K128): 32-byte slots.  An insert claims a slot by atomicCAS of
+// hi from EMPTY_HI to the key's hi without its publish bit, stores lo, then publishes hi with
+// a release store; a probe that meets a claimed but unpublished slot with its own hi re-reads
+// that slot (the claiming lane publishes in the same iteration of the probe loop, so lanes of
+// one wave never wait on each other across iterations).  Lookups run after the tier is
+// complete and read (hi, lo) with one 16-byte load.
+struct alignas(32) WSlot {
+    uint64_t hi, lo;
+    uint64_t score;   // u16 preference score in the low bits
+    uint64_t pad;
+};
+struct WFrontRef {
+    WSlot *s;
+    uint64_t cap;
+    unsigned long long *count;
+    uint32_t loc = 0;
+};
+struct WResRef {
+    WSlot *s;
+    uint64_t cap;
+    uint32_t loc = 0;
+};
+
+// the table types of a key type
+template <class K>
+struct KT;
+template <>
+struct KT<uint64_t> {
+    using Slot = RSlot;
+    using Front = FrontRef;
+    using Res = ResRef;
+};
+template <>
+struct KT<K128> {
+    using Slot = WSlot;
+    using Front = WFrontRef;
+    using Res = WResRef;
+};
+
 constexpr uint64_t MAX_PROBE = 2048;   // an insert probing further marks the table full
 constexpr double TABLE_LOAD = 0.7;     // planned load of a tier table
 template <int S>
@@ -57,23 +96,25 @@ struct Ress {
     ResRef t[S];
 };
 
-struct SpTier {
-    RSlot *slots = nullptr;
+template <class K>
+struct SpTierT {
+    typename KT<K>::Slot *slots = nullptr;
     uint64_t cap = 0;
     uint64_t fcount = 0;         // keys inserted so far (host mirror of the device counter)
     uint64_t count = 0;          // positions of the tier once classified (stored representatives)
     uint64_t count_all = 0;      // positions they stand for (orbits expanded, games.hpp NoSym)
-    uint64_t *ikeys = nullptr;   // interior (undecided) positions and their slots
+    K *ikeys = nullptr;          // interior (undecided) positions and their slots
     uint32_t *islot = nullptr;
     uint8_t *iwon = nullptr;     // per interior position: 1 = has a LOSS-in-0 child (set by expand)
     uint64_t ni = 0;
     // single-GPU engine, large tiers: the interior list sorted by the key's top bits
     // (sparse.hip, batch kernels); expand, retro and iwon then follow this order
-    uint64_t *skeys = nullptr;
+    K *skeys = nullptr;
     uint32_t *sslot = nullptr;
     int64_t tier = 0;            // the descriptor tier of the positions (root tier + index)
     uint32_t loc = 0;            // home function (FrontRef::loc) requested for this tier's table
 };
+using SpTier = SpTierT<uint64_t>;
 
 namespace {
 
@@ -120,9 +161,79 @@ __device__ __forceinline__ int res_find(const ResRef &t, uint64_t key) {
     return -1;
 }
 
-__global__ void slot_fill_kernel(RSlot *s, uint64_t n) {
+__device__ __forceinline__ uint64_t home_slot(const K128 &key, uint64_t cap, uint32_t) {
+    const uint64_t m = mix_key(key);
+    return __umul64hi((m << 32) | (m >> 32), cap);
+}
+
+__device__ __forceinline__ bool front_insert(const WFrontRef &t, const K128 &key, uint32_t *err) {
+    const uint64_t claim = key.hi & ~K128_PUB;
+    uint64_t h = home_slot(key, t.cap, t.loc);
+    const uint64_t lim = t.cap < MAX_PROBE ? t.cap : MAX_PROBE;
+    uint32_t spins = 0;
+    for (uint64_t probe = 0; probe < lim;) {
+        uint64_t cur = __hip_atomic_load(&t.s[h].hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == EMPTY_HI) {
+            const unsigned long long prev =
+                atomicCAS((unsigned long long *)&t.s[h].hi, (unsigned long long)EMPTY_HI, (unsigned long long)claim);
+            if (prev == EMPTY_HI) {
+                __hip_atomic_store(&t.s[h].lo, key.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&t.s[h].hi, key.hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                return true;
+            }
+            cur = __hip_atomic_load(&t.s[h].hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if ((cur | K128_PUB) == key.hi) {
+            if (!(cur & K128_PUB)) {   // claimed with this hi, lo not published yet: read the slot again
+                if (++spins > (1u << 24)) {
+                    atomicOr(err, DEV_ERR_TABLE_FULL);
+                    return false;
+                }
+                continue;
+            }
+            if (__hip_atomic_load(&t.s[h].lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key.lo) return false;
+        }
+        h = h + 1 == t.cap ? 0 : h + 1;
+        probe++;
+    }
+    atomicOr(err, DEV_ERR_TABLE_FULL);
+    return false;
+}
+
+__device__ __forceinline__ int res_find(const WResRef &t, const K128 &key) {
+    if (!t.s) return -1;
+    uint64_t h = home_slot(key, t.cap, t.loc);
+    for (uint64_t probe = 0; probe < t.cap; probe++) {
+        const u64x2 v = *(const u64x2 *)&t.s[h];
+        if (v[0] == key.hi && v[1] == key.lo) return (int)(t.s[h].score & 0xFFFFu);
+        if (v[0] == EMPTY_HI) return -1;
+        h = h + 1 == t.cap ? 0 : h + 1;
+    }
+    return -1;
+}
+
+// slot access shared by the two slot types
+__device__ __forceinline__ void slot_clear_key(uint64_t &k) { k = EMPTY_KEY; }
+__device__ __forceinline__ void slot_clear_key(K128 &k) { k = K128{0, EMPTY_HI}; }
+__device__ __forceinline__ uint64_t slot_key(const RSlot &s) { return s.key; }
+__device__ __forceinline__ K128 slot_key(const WSlot &s) {
+    const u64x2 v = *(const u64x2 *)&s;
+    return K128{v[1], v[0]};
+}
+__device__ __forceinline__ uint64_t slot_score(const RSlot &s) { return s.score; }
+__device__ __forceinline__ uint64_t slot_score(const WSlot &s) { return s.score; }
+__device__ __forceinline__ void slot_set(RSlot &s, uint64_t k, uint64_t score) { *(u64x2 *)&s = u64x2{k, score}; }
+__device__ __forceinline__ void slot_set(WSlot &s, const K128 &, uint64_t score) { s.score = score; }
+__device__ __forceinline__ void slot_clear(RSlot &s) { *(u64x2 *)&s = u64x2{EMPTY_KEY, 0}; }
+__device__ __forceinline__ void slot_clear(WSlot &s) {
+    *(u64x2 *)&s = u64x2{EMPTY_HI, 0};
+    *((u64x2 *)&s + 1) = u64x2{0, 0};
+}
+
+template <class Slot>
+__global__ void slot_fill_kernel(Slot *s, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        *(u64x2 *)&s[i] = u64x2{EMPTY_KEY, 0};
+        slot_clear(s[i]);
 }
 
 // every table of a replay in one launch: blockIdx.y = table, x strides inside it
@@ -132,11 +243,13 @@ __global__ void slot_fill_many_kernel(const ResRef *__restrict__ t) {
         *(u64x2 *)&r.s[i] = u64x2{EMPTY_KEY, 0};
 }
 
-__global__ void front_rehash_kernel(const RSlot *__restrict__ old, uint64_t ocap, FrontRef dst, uint32_t *err) {
+template <class K>
+__global__ void front_rehash_kernel(const typename KT<K>::Slot *__restrict__ old, uint64_t ocap,
+                                    typename KT<K>::Front dst, uint32_t *err) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ocap;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = old[i].key;
-        if (k != EMPTY_KEY) front_insert(dst, k, err);
+        const K k = slot_key(old[i]);
+        if (!key_empty(k)) front_insert(dst, k, err);
     }
 }
 
@@ -149,6 +262,9 @@ __global__ void res_lookup_one_kernel(ResRef t, uint64_t key, unsigned long long
 }
 
 __global__ void front_insert_one_kernel(FrontRef t, uint64_t key, uint32_t *err) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && front_insert(t, key, err)) atomicAdd(t.count, 1ull);
+}
+__global__ void front_insert_one_wkernel(WFrontRef t, K128 key, uint32_t *err) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && front_insert(t, key, err)) atomicAdd(t.count, 1ull);
 }
 
@@ -165,8 +281,8 @@ __global__ void front_insert_one_kernel(FrontRef t, uint64_t key, uint32_t *err)
 constexpr int CROWS = 16;
 constexpr uint64_t CLASSIFY_ROWS_MIN = 1ull << 22;
 template <class D, int ROWS, bool COUNT = true>
-__global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ slots, uint64_t cap,
-                                                       uint64_t *__restrict__ ikeys, uint32_t *__restrict__ islot,
+__global__ __launch_bounds__(256) void classify_kernel(D d, typename KT<key_t<D>>::Slot *__restrict__ slots, uint64_t cap,
+                                                       key_t<D> *__restrict__ ikeys, uint32_t *__restrict__ islot,
                                                        unsigned long long *icount, unsigned long long *edges,
                                                        unsigned long long *seen, uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
@@ -179,28 +295,31 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ 
     for (int s = 0; s < S; s++) cnt[s] = 0;
     uint64_t nseen = 0, nall = 0;
     for (uint64_t chunk = blockIdx.x * (256ull * ROWS); chunk < cap; chunk += (uint64_t)gridDim.x * 256ull * ROWS) {
-        uint64_t k[ROWS], m[ROWS];
+        using K = key_t<D>;
+        K k[ROWS];
+        uint64_t m[ROWS];
 #pragma unroll
         for (int r = 0; r < ROWS; r++) {
             const uint64_t i = chunk + 256ull * r + threadIdx.x;
-            k[r] = i < cap ? slots[i].key : EMPTY_KEY;
+            if (i < cap) k[r] = slot_key(slots[i]);
+            else slot_clear_key(k[r]);
         }
 #pragma unroll
         for (int r = 0; r < ROWS; r++) {
             bool interior = false;
-            if (k[r] != EMPTY_KEY) {
+            if (!key_empty(k[r])) {
                 nseen++;
-                if (COUNT) d.orbit(k[r], [&](uint64_t) { nall++; });   // a replay knows its orbit counts
+                if (COUNT) d.orbit(k[r], [&](const K &) { nall++; });   // a replay knows its orbit counts
                 const uint64_t i = chunk + 256ull * r + threadIdx.x;
                 const int p = d.primitive(k[r]);
                 if (p == DRAW) atomicOr(err, DEV_ERR_DRAW);
                 interior = p == UNDECIDED;
                 if (!interior) {
-                    *(u64x2 *)&slots[i] = u64x2{k[r], (uint64_t)score_of_primitive(p)};
+                    slot_set(slots[i], k[r], (uint64_t)score_of_primitive(p));
                 } else if (COUNT) {   // a replay knows its sizes: no edge counts
                     const int64_t tk = d.tier(k[r]);
                     int nk = 0;
-                    unreduced(d).visit(k[r], [&](uint64_t c) {   // tiers only: no canonical children
+                    unreduced(d).visit(k[r], [&](const K &c) {   // tiers only: no canonical children
                         const int64_t dt = d.tier(c) - tk;
                         nk++;
                         if (dt < 1 || dt > S) atomicOr(err, DEV_ERR_TIER);
@@ -241,11 +360,11 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, RSlot *__restrict__ 
 }
 
 template <class D>
-__global__ void query_kernel(D d, int64_t t_root, const ResRef *tabs, int ntabs, const uint64_t *__restrict__ keys,
-                             uint16_t *__restrict__ out, uint64_t n) {
+__global__ void query_kernel(D d, int64_t t_root, const typename KT<key_t<D>>::Res *tabs, int ntabs,
+                             const key_t<D> *__restrict__ keys, uint16_t *__restrict__ out, uint64_t n) {
     uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint64_t k = keys[i];
+    const key_t<D> k = keys[i];
     int64_t t = d.valid(k) ? d.tier(k) - t_root : -1;
     uint16_t r = REC_UNSOLVED;
     if (t >= 0 && t < ntabs) {
@@ -257,28 +376,31 @@ __global__ void query_kernel(D d, int64_t t_root, const ResRef *tabs, int ntabs,
 
 // digest and export expand every stored representative's orbit (games.hpp)
 template <class D>
-__global__ void res_digest_kernel(D d, const RSlot *__restrict__ s, uint64_t cap, unsigned long long *acc) {
+__global__ void res_digest_kernel(D d, const typename KT<key_t<D>>::Slot *__restrict__ s, uint64_t cap,
+                                  unsigned long long *acc) {
+    using K = key_t<D>;
     uint64_t sum = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const u64x2 v = *(const u64x2 *)&s[i];
-        if (v[0] != EMPTY_KEY) {
-            const uint16_t rec = record_of_score((uint16_t)v[1]);
-            d.orbit(v[0], [&](uint64_t k) { sum += digest_term(k, rec); });
+        const K key = slot_key(s[i]);
+        if (!key_empty(key)) {
+            const uint16_t rec = record_of_score((uint16_t)slot_score(s[i]));
+            d.orbit(key, [&](const K &k) { sum += digest_term(k, rec); });
         }
     }
     wave_add(acc, sum);
 }
 
 template <class D>
-__global__ void res_gather_kernel(D d, const RSlot *__restrict__ s, uint64_t cap, uint64_t *okeys, uint16_t *orec,
-                                  unsigned long long *cursor) {
+__global__ void res_gather_kernel(D d, const typename KT<key_t<D>>::Slot *__restrict__ s, uint64_t cap,
+                                  key_t<D> *okeys, uint16_t *orec, unsigned long long *cursor) {
+    using K = key_t<D>;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
          i += (uint64_t)gridDim.x * blockDim.x) {
-        const u64x2 v = *(const u64x2 *)&s[i];
-        if (v[0] == EMPTY_KEY) continue;
-        const uint16_t rec = record_of_score((uint16_t)v[1]);
-        d.orbit(v[0], [&](uint64_t k) {
+        const K key = slot_key(s[i]);
+        if (key_empty(key)) continue;
+        const uint16_t rec = record_of_score((uint16_t)slot_score(s[i]));
+        d.orbit(key, [&](const K &k) {
             const unsigned long long at = atomicAdd(cursor, 1ull);
             okeys[at] = k;
             orec[at] = rec;
@@ -288,19 +410,21 @@ __global__ void res_gather_kernel(D d, const RSlot *__restrict__ s, uint64_t cap
 
 }  // namespace
 
-inline int tier_alloc(Ctx *c, RSlot **slots, uint64_t cap) {
-    GM_TRY(dev_alloc(c, (void **)slots, cap * sizeof(RSlot)));
-    hipLaunchKernelGGL(slot_fill_kernel, dim3(grid_for(cap)), dim3(256), 0, c->stream, *slots, cap);
+template <class Slot>
+inline int tier_alloc(Ctx *c, Slot **slots, uint64_t cap) {
+    GM_TRY(dev_alloc(c, (void **)slots, cap * sizeof(Slot)));
+    hipLaunchKernelGGL(slot_fill_kernel<Slot>, dim3(grid_for(cap)), dim3(256), 0, c->stream, *slots, cap);
     return GM_OK;
 }
 
 // grow a tier table to `cap` slots, re-inserting the keys it holds
-inline int tier_grow(Ctx *c, SpTier &T, uint64_t cap, uint32_t *d_err) {
-    RSlot *ns;
+template <class K>
+inline int tier_grow(Ctx *c, SpTierT<K> &T, uint64_t cap, uint32_t *d_err) {
+    typename KT<K>::Slot *ns;
     GM_TRY(tier_alloc(c, &ns, cap));
     if (T.cap) {
-        FrontRef dst{ns, cap, nullptr, eff_loc(T.loc, cap)};
-        hipLaunchKernelGGL(front_rehash_kernel, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap, dst,
+        typename KT<K>::Front dst{ns, cap, nullptr, eff_loc(T.loc, cap)};
+        hipLaunchKernelGGL(front_rehash_kernel<K>, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, T.slots, T.cap, dst,
                            d_err);
         dev_free(c, T.slots);
     }
@@ -309,7 +433,10 @@ inline int tier_grow(Ctx *c, SpTier &T, uint64_t cap, uint32_t *d_err) {
     return GM_OK;
 }
 
-inline ResRef res_ref_of(const SpTier &T) { return ResRef{T.slots, T.cap, eff_loc(T.loc, T.cap)}; }
+template <class K>
+inline typename KT<K>::Res res_ref_of(const SpTierT<K> &T) {
+    return typename KT<K>::Res{T.slots, T.cap, eff_loc(T.loc, T.cap)};
+}
 
 // capacity for `n` keys at the planned load (multiple of 1024)
 inline uint64_t table_cap_for(uint64_t n) {
@@ -344,8 +471,8 @@ struct DedupEstimate {
 // (scr[0, S) edges by step, scr[9] interior count, scr[10] positions seen)
 // scr: [0, S) edges per tier step, [9] interior count, [10] positions, [11] positions with orbits
 template <class D, bool COUNT = true>
-inline void launch_classify(hipStream_t st, const D &d, RSlot *slots, uint64_t cap, uint64_t *ikeys, uint32_t *islot,
-                            unsigned long long *scr, uint32_t *err) {
+inline void launch_classify(hipStream_t st, const D &d, typename KT<key_t<D>>::Slot *slots, uint64_t cap,
+                            key_t<D> *ikeys, uint32_t *islot, unsigned long long *scr, uint32_t *err) {
     // a replay's classify (no edge or orbit counts) does less per row: 32 rows
     // per thread there (Toot 6x4 replay: 8.8 vs 9.5 ms; rows 8 / 4: 12.6 / 19.6 ms -- each
     // chunk's barriers and reservation atomic are paid fewer times)
@@ -359,9 +486,9 @@ inline void launch_classify(hipStream_t st, const D &d, RSlot *slots, uint64_t c
 }
 
 template <class D>
-inline int classify_tier_table(Ctx *c, const D &d, SpTier &T, unsigned long long *scr, uint32_t *d_err) {
+inline int classify_tier_table(Ctx *c, const D &d, SpTierT<key_t<D>> &T, unsigned long long *scr, uint32_t *d_err) {
     const uint64_t n = T.fcount;
-    GM_TRY(dev_alloc(c, (void **)&T.ikeys, std::max<uint64_t>(n, 1) * 8));
+    GM_TRY(dev_alloc(c, (void **)&T.ikeys, std::max<uint64_t>(n, 1) * sizeof(key_t<D>)));
     GM_TRY(dev_alloc(c, (void **)&T.islot, std::max<uint64_t>(n, 1) * 4));
     GM_TRY(dev_alloc(c, (void **)&T.iwon, std::max<uint64_t>(n, 1)));
     GM_HIP(hipMemsetAsync(scr, 0, 16 * sizeof(unsigned long long), c->stream));
@@ -370,10 +497,11 @@ inline int classify_tier_table(Ctx *c, const D &d, SpTier &T, unsigned long long
     return GM_OK;
 }
 
-inline void free_tier(Ctx *c, SpTier &T) {
+template <class K>
+inline void free_tier(Ctx *c, SpTierT<K> &T) {
     for (void *p : {(void *)T.slots, (void *)T.ikeys, (void *)T.islot, (void *)T.iwon, (void *)T.skeys, (void *)T.sslot})
         dev_free(c, p);
-    T = SpTier{};
+    T = SpTierT<K>{};
 }
 
 }  // namespace gm

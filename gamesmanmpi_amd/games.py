@@ -128,7 +128,8 @@ class TootCodec(Codec):
 
 
 class OthelloCodec(Codec):
-    """Latin-1 packed Othello positions (reference othello_bit_new.py); key = all bits."""
+    """Latin-1 packed Othello positions (reference othello_bit_new.py); key = all bits (8x8:
+    144 bits, a Python int the context passes as 3 u64 words, include/gmsolve.h gm_key_words)."""
     game_id = _lib.GAME_OTHELLO
     name = "othello"
 
@@ -195,16 +196,27 @@ class HostDescriptor:
         h = _lib.ctypes.c_void_p()
         _lib.check(L.gm_open(codec.game_id, params, len(codec.params), -1, _lib.ctypes.byref(h)))
         self.h = h
-        self._kids = (_lib.ctypes.c_uint64 * 64)()
+        self.words = L.gm_key_words(h)   # 3 for Othello 8x8 (keys past 64 bits)
+        self._kids = (_lib.ctypes.c_uint64 * (64 * self.words))()
+        self._key = (_lib.ctypes.c_uint64 * self.words)()
 
     def expand(self, key):
         L = _lib.lib()
         n, p, t = _lib.ctypes.c_int(), _lib.ctypes.c_int(), _lib.ctypes.c_int64()
+        if self.words > 1:
+            self._key[:] = _lib.int_to_words(key, self.words)
+            _lib.check(L.gm_expand_host_key(self.h, self._key, self._kids, 64, _lib.ctypes.byref(n),
+                                            _lib.ctypes.byref(p), _lib.ctypes.byref(t)))
+            w = self.words
+            return p.value, [_lib.words_to_int(self._kids[w * i:w * i + w]) for i in range(n.value)], t.value
         _lib.check(L.gm_expand_host(self.h, key, self._kids, 64, _lib.ctypes.byref(n),
                                     _lib.ctypes.byref(p), _lib.ctypes.byref(t)))
         return p.value, list(self._kids[:n.value]), t.value
 
     def initial(self):
+        if self.words > 1:
+            _lib.check(_lib.lib().gm_pack_initial_key(self.h, self._key))
+            return _lib.words_to_int(self._key)
         k = _lib.ctypes.c_uint64()
         _lib.check(_lib.lib().gm_pack_initial(self.h, _lib.ctypes.byref(k)))
         return k.value

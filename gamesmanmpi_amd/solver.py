@@ -40,6 +40,9 @@ class Context:
         self.h = h
         self.game_id = game_id
         self.params = tuple(params)
+        # u64 words per key: 1, or 3 for boards past 64 bits (Othello 8x8); keys are then Python
+        # ints on the host and (n, words) uint64 arrays in bulk (gm_*_key)
+        self.words = self.L.gm_key_words(h)
 
     def set_option(self, opt, value):
         _lib.check(self.L.gm_set_option(self.h, opt, int(value)))
@@ -52,6 +55,10 @@ class Context:
         _lib.check(self.L.gm_set_comm(self.h, rank, world, buf, 128 if buf is not None else 0))
 
     def initial(self):
+        if self.words > 1:
+            w = (ctypes.c_uint64 * self.words)()
+            _lib.check(self.L.gm_pack_initial_key(self.h, w))
+            return _lib.words_to_int(w)
         k = ctypes.c_uint64()
         _lib.check(self.L.gm_pack_initial(self.h, ctypes.byref(k)))
         return k.value
@@ -59,8 +66,21 @@ class Context:
     def solve(self, root):
         n = ctypes.c_uint64()
         r = ctypes.c_uint16()
-        _lib.check(self.L.gm_solve(self.h, root, ctypes.byref(n), ctypes.byref(r)))
+        if self.words > 1:
+            w = (ctypes.c_uint64 * self.words)(*_lib.int_to_words(root, self.words))
+            _lib.check(self.L.gm_solve_key(self.h, w, ctypes.byref(n), ctypes.byref(r)))
+        else:
+            _lib.check(self.L.gm_solve(self.h, root, ctypes.byref(n), ctypes.byref(r)))
         return n.value, r.value
+
+    def key_array(self, keys):
+        """Keys (Python ints, or an (n, words) uint64 array) -> the array gm_query_key takes."""
+        if self.words == 1:
+            return np.ascontiguousarray(keys, dtype=np.uint64)
+        a = np.asarray(keys) if not isinstance(keys, list) else None
+        if a is not None and a.dtype == np.uint64 and a.ndim == 2:
+            return np.ascontiguousarray(a)
+        return np.array([_lib.int_to_words(k, self.words) for k in keys], dtype=np.uint64).reshape(-1, self.words)
 
     def solve_graph(self, prim, off, kids):
         """gm_solve_graph over an explicit graph (gamesmanmpi_amd/graph.py)."""
@@ -74,7 +94,14 @@ class Context:
         return len(prim), r.value
 
     def export(self):
+        """Sorted keys and records (multi-word keys: an (n, words) uint64 array)."""
         n = ctypes.c_uint64()
+        if self.words > 1:
+            _lib.check(self.L.gm_export_key(self.h, None, None, 0, ctypes.byref(n)))
+            keys = np.empty((n.value, self.words), dtype=np.uint64)
+            recs = np.empty(n.value, dtype=np.uint16)
+            _lib.check(self.L.gm_export_key(self.h, keys.ctypes.data, recs.ctypes.data, n.value, ctypes.byref(n)))
+            return keys[:n.value], recs[:n.value]
         _lib.check(self.L.gm_export(self.h, None, None, 0, ctypes.byref(n)))
         keys = np.empty(n.value, dtype=np.uint64)
         recs = np.empty(n.value, dtype=np.uint16)
@@ -82,9 +109,12 @@ class Context:
         return keys[:n.value], recs[:n.value]
 
     def query(self, keys):
-        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        keys = self.key_array(keys)
         out = np.empty(len(keys), dtype=np.uint16)
-        _lib.check(self.L.gm_query(self.h, keys.ctypes.data, out.ctypes.data, len(keys)))
+        if self.words > 1:
+            _lib.check(self.L.gm_query_key(self.h, keys.ctypes.data, out.ctypes.data, len(keys)))
+        else:
+            _lib.check(self.L.gm_query(self.h, keys.ctypes.data, out.ctypes.data, len(keys)))
         return out
 
     def digest(self):

@@ -36,7 +36,8 @@ extern "C" {
  *   GM_GAME_FOUR_TO_ONE  none                  (reference test_games/four_to_one.py)
  *   GM_GAME_TTT          none                  (test_games/mttt.py, tic_tac_toe_np.py)
  *   GM_GAME_TOOT         {length, height}      (test_games/toot_and_otto_bitstring.py), 2*L*H+16 <= 64
- *   GM_GAME_OTHELLO      {length, height}      (test_games/othello_bit_new.py), square, 2*L*H+16 <= 64
+ *   GM_GAME_OTHELLO      {length, height}      (test_games/othello_bit_new.py), square, 2*L*H+16 <= 64,
+ *                                              or {8, 8} with 3-word keys (gm_key_words)
  *   GM_GAME_SUBTRACT     {heaps}               (the build's synthetic game, 1..8 heaps of 4 bits)
  *   GM_GAME_GRAPH        none                  (any plugin: an explicit graph from gm_solve_graph)
  */
@@ -245,6 +246,23 @@ int gm_set_comm(gm_ctx *ctx, int rank, int world, const void *uid, int bytes);
  * Replaces Process.run/lookup/distribute/check_for_updates/send_back/resolve
  * (src/new_process.py:37-265) and the root line of :42-53. */
 int gm_solve(gm_ctx *ctx, uint64_t root_key, uint64_t *n_positions, uint16_t *root_record);
+
+/* Keys of more than 64 bits.  A board whose position string exceeds 64 bits -- GM_GAME_OTHELLO
+ * with params {8, 8}, the reference plugin's default (test_games/othello_bit_new.py:8: 2A + 16 =
+ * 144 bits) -- has keys of gm_key_words() u64 words: the position string read as one big-endian
+ * integer, stored least significant word first (the one-word games' keys are that integer too).
+ * Such a context is solved by the hash-sharded sparse engine with 128-bit device keys (one GPU,
+ * virtual ranks, or one process per rank) and uses the *_key calls below; the one-word calls
+ * return GM_E_ARG for it.  For one-word games the *_key calls equal their one-word forms.
+ * gm_digest folds each key to one word first (mix64(lo ^ mix64(hi ^ c)) of the device key), so
+ * digests compare across ranks and world sizes, not with one-word games. */
+int gm_key_words(gm_ctx *ctx);
+int gm_pack_initial_key(gm_ctx *ctx, uint64_t *key_words);
+int gm_expand_host_key(gm_ctx *ctx, const uint64_t *key_words, uint64_t *children_words, int cap,
+                       int *n_children, int *primitive, int64_t *tier);
+int gm_solve_key(gm_ctx *ctx, const uint64_t *root_words, uint64_t *n_positions, uint16_t *root_record);
+int gm_export_key(gm_ctx *ctx, uint64_t *key_words, uint16_t *records, uint64_t cap, uint64_t *n);
+int gm_query_key(gm_ctx *ctx, const uint64_t *key_words, uint16_t *records, uint64_t n);
 
 /* Strong-solve an explicit position graph (context opened with GM_GAME_GRAPH):
  * for plugins no device descriptor reproduces, the host enumerates positions

@@ -156,9 +156,43 @@ def test_fingerprints_cover_this_repos_plugins():
         fp.fingerprint(load_plugin("test_games/othello_bit_new.py"))
 
 
-def test_othello_8x8_has_no_descriptor():
+def test_othello_8x8_binds_the_wide_descriptor():
+    """the reference plugin at its default 8x8 board (othello_bit_new.py:8,
+    144-bit positions) binds to the 128-bit-key descriptor (games.hpp DescOthello8): 3 key words,
+    the initial key is the plugin's initial position string as an integer, and the host twin
+    agrees with the plugin (primitive value and child set) on EVERY one of the 56,552 positions
+    below the seed-5 endgame root (tests/plugins/othello8_endgame.py)."""
     mod = load_plugin("test_games/othello_bit_new.py")     # reference default 8x8
-    assert games.identify(mod) is None
+    c = games.identify(mod)
+    assert c is not None and c.name == "othello" and c.params == (8, 8)
+    hd = games.HostDescriptor(c)
+    assert hd.words == 3 and hd.initial() == c.key(mod.initial_position())
+    hd.close()
+    end = load_plugin("tests/plugins/othello8_endgame.py")
+    ce = games.identify(end)
+    assert ce is not None and ce.params == (8, 8)
+    assert games.verify_exhaustive(end, ce, end.initial_position(), 100_000)
+
+
+def test_othello_8x8_key_words_round_trip():
+    """gm_expand_host_key rejects a key that is no 8x8 position (a centre square empty, planes
+    overlapping, turn 3), and the one-word calls refuse a 3-word context."""
+    from gamesmanmpi_amd import Context, GMError
+    ctx = Context(OTH, (8, 8))
+    assert ctx.words == 3
+    k = ctx.initial()
+    hd = games.HostDescriptor(games.OthelloCodec(8, 8))
+    prim, kids, tier = hd.expand(k)
+    assert prim == 4 and len(kids) == 4 and tier == 3 * 4
+    for bad in (k & ~(1 << (80 + 63 - 27)) & ~(1 << (16 + 63 - 27)),   # centre square (3, 3) emptied
+                k | (1 << (16 + 63 - 27)),                                  # (3, 3) white and black
+                (k & ~(0xFF << 8)) | (3 << 8)):                             # turn byte 3
+        with pytest.raises(GMError, match="valid"):
+            hd.expand(bad)
+    with pytest.raises(GMError, match="3 words"):
+        _lib.check(ctx.L.gm_pack_initial(ctx.h, ctypes.byref(ctypes.c_uint64())))
+    hd.close()
+    ctx.close()
 
 
 REF = "/root/reference"

@@ -53,6 +53,7 @@ def _rank_main(rank, world, phase, game, params, opts):
     ctx.set_comm(rank, world, uid[0])
     root = opts.pop("root", None)
     qkeys = opts.pop("query_keys", None)
+    want_export = opts.pop("export", False)
     solves = opts.pop("solves", 1)
     for k, v in opts.items():
         ctx.set_option(getattr(_lib, "OPT_" + k.upper()), v)
@@ -67,6 +68,9 @@ def _rank_main(rank, world, phase, game, params, opts):
            "tiers": [int(x) for x in ctx.tier_counts()], "exchanged": ctx.stats()["exchanged_bytes"]}
     if qkeys is not None:
         res["query"] = [int(x) for x in ctx.query(np.array(qkeys, dtype=np.uint64))]
+    if want_export:
+        k, r = ctx.export()
+        res["export"] = (k.tolist(), r.tolist())
     ctx.close()
     return res
 
@@ -256,3 +260,26 @@ def test_box_ipc_early_read_caught_by_poison(oracle, poison, caught):
         assert got[1] != want and got[2] != want
     else:
         assert got[1] == want and got[2] == want
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_othello8_ipc_ranks_vs_reference_golden(world):
+    """Othello 8x8 (128-bit keys) from the 10-empty endgame root across PROCESSES with the IPC
+    transport, the ranks sharing the GPU: the ranks' exports partition the solved set, and
+    every record equals the reference plugin's golden table."""
+    import hashlib
+    from conftest import golden
+    from gamesmanmpi_amd import _lib, games
+    codec = games.OthelloCodec(8, 8)
+    root = codec.key(bytes.fromhex("303800204018057a4646bfdebfe6fa800200").decode("latin-1"))
+    res = _run(world, OTH, (8, 8), {"sparse_transport": 1, "poison": 1, "root": root, "export": True}, shared=True)
+    got = {}
+    for r in res:
+        for w, rec in zip(*r["export"]):
+            pos = codec.pos(_lib.words_to_int(w))
+            h = int.from_bytes(hashlib.blake2b(pos.encode("ISO-8859-1"), digest_size=8).digest(), "big")
+            assert h not in got
+            got[h] = rec
+    keys, recs = golden("othello_8x8_endgame")
+    assert got == dict(zip(keys.tolist(), recs.tolist()))
+    assert all(r["n"] == 56552 for r in res)

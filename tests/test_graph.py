@@ -82,15 +82,16 @@ def test_graph_engine_matches_canonical_oracle_on_new_plugins(rel):
 @pytest.mark.gpu
 def test_graph_engine_othello_8x8_endgame_matches_golden():
     """Othello on the reference's default 8x8 board from an endgame root (10 empty squares,
-    56,552 positions; 144-bit positions no device descriptor holds): the solver takes the
-    explicit-graph path on its own (host walk with the plugin's functions, GPU resolve), and
-    every record equals the golden table of the REFERENCE's plugin from the same root."""
+    56,552 positions) through the explicit-graph path (host walk with the plugin's functions,
+    GPU resolve; graph=True -- the plugin also binds the 128-bit-key descriptor,
+    tests/test_gpu_othello8.py): every record equals the golden table of the REFERENCE's
+    plugin from the same root."""
     import hashlib
     import json
     from conftest import GOLDEN
     from gamesmanmpi_amd import Solver
     mod = load_plugin("tests/plugins/othello8_endgame.py")
-    s = Solver(mod, device=0)
+    s = Solver(mod, device=0, graph=True)
     n, rec = s.solve()
     keys, recs = golden("othello_8x8_endgame")
     assert s.ctx.stats()["engine"] == 5 and n == len(keys)
@@ -198,12 +199,11 @@ def test_small_plugins_start_no_worker(monkeypatch):
 
 
 def test_enumeration_fails_fast_with_a_projection():
-    """Othello at its 8x8 default has no device descriptor: the walk stops with the level
-    sizes and the projected next level once the projection passes the limit."""
+    """Othello at its 8x8 default from the start, walked on the host: the walk stops with the
+    level sizes and the projected next level once the projection passes the limit."""
     import time
     from gamesmanmpi_amd.graph import TooLarge
     mod = load_plugin("test_games/othello_bit_new.py")
-    assert games.identify(mod) is None
     t = time.perf_counter()
     with pytest.raises(TooLarge, match="projected"):
         enumerate_graph(mod, mod.initial_position(), limit=20_000, workers=1)
