@@ -160,7 +160,7 @@ def _mesh(me, nw, tag, key, timeout_s=120.0):
     import socket
     import struct
     from multiprocessing import AuthenticationError
-    from multiprocessing.connection import Client, Connection, answer_challenge, deliver_challenge
+    from multiprocessing.connection import Connection, answer_challenge, deliver_challenge
     name = "\0" + tag + "-%d"
     srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
     srv.bind(name % me)
@@ -178,15 +178,31 @@ def _mesh(me, nw, tag, key, timeout_s=120.0):
 
     try:
         for p in range(me):
+            # connecting side: a raw socket with a connect timeout, then the
+            # challenge exchange under SO_RCVTIMEO, so a lower-numbered peer that accepted but
+            # never answers ends the mesh with TimeoutError too
             while True:
+                so = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
                 try:
-                    c = Client(name % p, family="AF_UNIX", authkey=key)
+                    so.settimeout(max(0.05, deadline - time.time()))
+                    so.connect(name % p)
                     break
-                except (FileNotFoundError, ConnectionRefusedError):
+                except (FileNotFoundError, ConnectionRefusedError, socket.timeout):
+                    so.close()
                     if time.time() > deadline:
-                        raise
+                        raise TimeoutError("walk worker %d: peer %d did not accept within %.0f s" % (me, p, timeout_s))
                     time.sleep(0.002)
-            c.send_bytes(b"%d" % me)
+            so.settimeout(None)
+            c = Connection(so.detach())
+            try:
+                rcvtimeo(c, max(1.0, min(HANDSHAKE_S, deadline - time.time())))
+                answer_challenge(c, key)
+                deliver_challenge(c, key)
+                c.send_bytes(b"%d" % me)
+                rcvtimeo(c, 0)
+            except (EOFError, OSError) as e:
+                c.close()
+                raise TimeoutError("walk worker %d: handshake with peer %d failed or timed out (%s)" % (me, p, e))
             peers[p] = c
         left = nw - 1 - me
         while left:

@@ -393,3 +393,26 @@ def test_walk_mesh_survives_a_silent_connection_and_times_out():
         s2.close()
     finally:
         walk_worker.HANDSHAKE_S = old
+
+
+def test_walk_mesh_connecting_side_times_out_on_a_silent_acceptor():
+    """the CONNECTING side is bounded too -- a lower-numbered 'peer' that accepts
+    the connection and never sends the HMAC challenge ends worker 1's mesh with TimeoutError
+    within the handshake limit instead of blocking in the challenge exchange."""
+    import os
+    import socket
+    from gamesmanmpi_amd import walk_worker
+    old = walk_worker.HANDSHAKE_S
+    walk_worker.HANDSHAKE_S = 1.0
+    tag = "gmtest-acc-%d-%s" % (os.getpid(), os.urandom(3).hex())
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    srv.bind("\0" + tag + "-0")
+    srv.listen(4)
+    try:
+        t = time.time()
+        with pytest.raises(TimeoutError):
+            walk_worker._mesh(1, 2, tag, os.urandom(32), timeout_s=20)
+        assert time.time() - t < 10
+    finally:
+        walk_worker.HANDSHAKE_S = old
+        srv.close()
