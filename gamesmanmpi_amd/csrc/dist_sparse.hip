@@ -508,9 +508,19 @@ static int exchange_ipc(Ctx *c, DistSparseK<K> *d, const Layout &me, const std::
     return sp_ipc_barrier(X);
 }
 
+// One rank in one context (a 128-bit-key game on one GPU): its send order IS its receive
+// order (one destination, one source), so the receive side reads the send buffers in place
+// and the exchange copies nothing.
+static bool self_only(const DistSparse *d) { return d->loopback && d->G == 1; }
+template <class K>
+static K *recv_keys(const DistSparse *d, SpRankT<K> &R) { return self_only(d) ? R.sendk : R.recvk; }
+template <class K>
+static uint16_t *recv_replies(const DistSparse *d, SpRankT<K> &R) { return self_only(d) ? R.reply_out : R.reply_in; }
+
 template <class K>
 static int exchange(Ctx *c, DistSparseK<K> *d, std::vector<Layout> &lay, const std::vector<uint64_t> &mat, bool reply) {
     constexpr uint64_t KB = sizeof(K);
+    if (self_only(d)) return GM_OK;
     if (c->poison)   // test hook: a segment that never lands reads as 0xFF, not as an earlier tier's data
         for (size_t i = 0; i < d->ranks.size(); i++) {
             SpRankT<K> &R = d->ranks[i];
@@ -655,7 +665,7 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
             lay[i] = layout_for(d, mat, R.rank);
             d->edges += lay[i].nsend;
             GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
-            GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
+            if (!self_only(d)) GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
             GM_HIP(hipMemcpyAsync(R.d_seg, lay[i].seg.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
             GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
             run_bucket<D, true, false>(c, d, desc, R, t, nullptr);
@@ -683,7 +693,7 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                         const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
                         if (n)
                             hipLaunchKernelGGL(insert_recv_kernel<K>, dim3(grid_for(n)), dim3(256), 0, c->stream,
-                                               R.recvk + lay[i].recv_seg[q * S + s], n, fref(R, u), R.d_err);
+                                               recv_keys(d, R) + lay[i].recv_seg[q * S + s], n, fref(R, u), R.d_err);
                     }
                 }
                 uint32_t e;
@@ -746,10 +756,14 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
             GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
             if (R.send_cap != pc || !R.sendp) {
                 GM_TRY(grow_to(c, &R.sendp, R.send_cap));
-                GM_TRY(grow_to(c, &R.reply_in, R.send_cap));
+                if (!self_only(d)) GM_TRY(grow_to(c, &R.reply_in, R.send_cap));
             }
-            GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
-            if (R.recv_cap != rc || !R.reply_out) GM_TRY(grow_to(c, &R.reply_out, R.recv_cap));
+            if (!self_only(d)) GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
+            if (self_only(d)) {   // the replies are written and folded in send order
+                if (R.send_cap != pc || !R.reply_out) GM_TRY(grow_to(c, &R.reply_out, R.send_cap));
+            } else if (R.recv_cap != rc || !R.reply_out) {
+                GM_TRY(grow_to(c, &R.reply_out, R.recv_cap));
+            }
             const uint64_t ni = R.tiers[t].ni;
             if (ni > R.best_cap || !R.best) {
                 R.best_cap = std::max<uint64_t>(ni + ni / 4, 1 << 16);
@@ -767,7 +781,7 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                     const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
                     if (!n) continue;
                     hipLaunchKernelGGL(lookup_kernel<K>, dim3(grid_for(n)), dim3(256), 0, c->stream,
-                                       R.recvk + lay[i].recv_seg[q * S + s], n, res_ref_of(R.tiers[t + 1 + s]),
+                                       recv_keys(d, R) + lay[i].recv_seg[q * S + s], n, res_ref_of(R.tiers[t + 1 + s]),
                                        R.reply_out + lay[i].recv_seg[q * S + s], R.d_err);
                 }
         }
@@ -776,7 +790,7 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
             SpRankT<K> &R = d->ranks[i];
             SpTierT<K> &T = R.tiers[t];
             if (lay[i].nsend)
-                hipLaunchKernelGGL(fold_kernel, dim3(grid_for(lay[i].nsend)), dim3(256), 0, c->stream, R.reply_in,
+                hipLaunchKernelGGL(fold_kernel, dim3(grid_for(lay[i].nsend)), dim3(256), 0, c->stream, recv_replies(d, R),
                                    R.sendp, lay[i].nsend, R.best);
             if (T.ni)
                 hipLaunchKernelGGL(finalize_kernel<typename KT<K>::Res>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, T.islot, R.best,

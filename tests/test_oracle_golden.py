@@ -127,10 +127,12 @@ def test_python_canonical_on_our_othello_8x8_endgame():
     """§8f.3 at the reference's own 8x8 board: our plugin (test_games/othello_bit_new.py at its
     default 8x8) from the endgame root of tests/plugins/othello8_endgame.py gives, under the
     canonical oracle, exactly the golden table made from the REFERENCE's plugin (positions
-    keyed by an 8-byte blake2b of their 144-bit string); no device descriptor claims it."""
+    keyed by an 8-byte blake2b of their 144-bit string).  It binds the 128-bit-key descriptor,
+    whose device tables tests/test_gpu_othello8.py checks against the same golden table."""
     from gamesmanmpi_amd import games
     mod = load_plugin("tests/plugins/othello8_endgame.py")
-    assert games.identify(mod) is None
+    c = games.identify(mod)
+    assert c is not None and c.params == (8, 8)
     table, positions = canonical.solve(mod)
     keys, recs = golden("othello_8x8_endgame")
     got = sorted((_blake8(positions[k]), (v << 14) | r) for k, (v, r) in table.items())
