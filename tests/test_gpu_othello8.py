@@ -82,16 +82,22 @@ def test_othello8_virtual_ranks_digest_equals_one_gpu(monkeypatch):
     assert digests[0] == digests[1] == digests[2] and digests[0][1] == 56552
 
 
-def test_othello8_endgame_12_device_vs_graph_path(monkeypatch):
-    """12 empties (1.2 M positions): the device descriptor's table equals the explicit-graph
-    path's record for record (position strings of the plugin)."""
-    from gamesmanmpi_amd import Solver
-    mod = _endgame(monkeypatch, ROOT12)
-    s = Solver(mod, device=0)
+def test_othello8_endgame_12_device_vs_graph_path():
+    """12 empties (1.2 M positions): the plugin at its default 8x8 with the root passed as a
+    custom position (solver_launcher.py --custom) binds the descriptor by its code fingerprint,
+    and the device table equals the explicit-graph path's record for record (position strings
+    of the plugin).  (tests/plugins/othello8_endgame.py changes initial_position, so it has no
+    known fingerprint and binds only through the exhaustive replay, capped at 10^6 positions.)"""
+    from gamesmanmpi_amd import Solver, _lib
+    mod = load_plugin("test_games/othello_bit_new.py")
+    root = bytes.fromhex(ROOT12).decode("latin-1")
+    s = Solver(mod, root=root, device=0)
+    assert s.ctx.words == 3
     n, rec = s.solve()
+    assert s.ctx.stats()["engine"] == _lib.ENGINE_DIST_SPARSE
     dev = _table_by_pos(s)
     s.close()
-    g = Solver(mod, device=0, graph=True)
+    g = Solver(mod, root=root, device=0, graph=True)
     gn, grec = g.solve()
     idx, r = g.table()
     ref = {g.codec.pos(i): int(x) for i, x in zip(idx.tolist(), r.tolist())}
