@@ -405,6 +405,46 @@ def sparse_config(name, game, params, rank, world, dist, torch):
     return out
 
 
+# Othello at the reference's default 8x8 board (othello_bit_new.py:8) on the device, 128-bit keys
+# (DESIGN.md §4.4): positions of the seed-5 playout from the standard start with E empty squares
+# (tools/othello8_scale.py playout_roots; E = 10 is tests/plugins/othello8_endgame.py's root,
+# pinned by the reference plugin's golden table in tests/test_gpu_othello8.py)
+OTHELLO8_ROOTS = {10: "303800204018057a4646bfdebfe6fa800200", 14: "30300c2c503841784646b1d2afc6be000200",
+                  16: "3030242050384178460699daafc6be000200", 18: "30302420583e4160460699daa7c0bc100200"}
+OTHELLO8_EMPTIES = int(os.environ.get("GM_BENCH_OTHELLO8_EMPTIES", 16))
+
+
+def othello8_config(rank, world, dist, torch):
+    """§8f.3 on the device: one seed-5 endgame of OTHELLO8_EMPTIES empty squares, one GPU
+    (rank 0 at N = 1 only).  Parity: the same root on 8 virtual ranks gives the same digest,
+    position count and root record (the 10-empty root is pinned to the reference plugin's
+    golden table by tests/test_gpu_othello8.py).  Time: median of 3 solves after 1 warm-up."""
+    from gamesmanmpi_amd import Context, _lib, games
+    e = OTHELLO8_EMPTIES
+    codec = games.OthelloCodec(8, 8)
+    key = codec.key(bytes.fromhex(OTHELLO8_ROOTS[e]).decode("latin-1"))
+    ctx = Context(_lib.GAME_OTHELLO, (8, 8), device=int(os.environ.get("LOCAL_RANK", 0)))
+    n, rec, ts = timed_solves(ctx, key, rank, 1, dist, torch, warmup=1, repeats=3)
+    med = sorted(ts)[1]
+    st = ctx.stats()
+    d1 = ctx.digest()
+    ctx.close()
+    v = Context(_lib.GAME_OTHELLO, (8, 8), device=int(os.environ.get("LOCAL_RANK", 0)))
+    v.set_option(_lib.OPT_VIRTUAL_RANKS, 8)
+    vn, vrec = v.solve(key)
+    d8 = v.digest()
+    v.close()
+    return {"workload": "Othello 8x8 (the reference plugin's default board), seed-5 playout position with %d "
+                        "empty squares, 128-bit keys, sparse engine on one GPU" % e,
+            "root_hex": OTHELLO8_ROOTS[e], "positions": n, "root_record": rec, "solve_ms": med * 1e3,
+            "solve_ms_all": [round(t * 1e3, 3) for t in ts], "positions_per_s": n / med,
+            "statistic": "median of 3 solves after 1 warm-up", "edges": st["n_edges"], "tiers": st["n_tiers"],
+            "table_gb": st["table_bytes"] / 1e9, "digest": "%#018x" % d1[0],
+            "ok": (vn, vrec, d8) == (n, rec, d1),
+            "parity": "the same root on 8 virtual ranks (hash-sharded, loopback exchange): digest, positions and "
+                      "root record equal"}
+
+
 RANDOM_LOAD_PEAK = 47e9   # random 16-B loads/s from an 8 GiB table (tools/randbench.hip, profiles/r01_randbench.txt)
 RANDOM_CAS_PEAK = 17e9    # random 8-B CAS/s from an 8 GiB table (same)
 TOOT_PROFILE = os.path.join(REPO, "profiles", "traffic_toot6x4.json")
@@ -494,6 +534,11 @@ def other_configs(rank, world, dist, torch, budget_s=240.0, emit=None):
             if cb is not None:
                 res[name]["cpu_baseline"] = cb
                 res[name]["speedup_vs_cpu_baseline"] = res[name]["positions_per_s"] / cb["value"]
+    if world == 1 and rank == 0 and not os.environ.get("GM_BENCH_NO_OTHELLO8"):
+        try:
+            res["othello_8x8_endgame"] = othello8_config(rank, world, dist, torch)
+        except Exception as e:  # reported in the line
+            res["othello_8x8_endgame"] = {"error": "%s: %s" % (type(e).__name__, e)}
     timer.cancel()
     return res
 
