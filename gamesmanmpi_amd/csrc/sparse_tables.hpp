@@ -47,9 +47,9 @@ inline GM_HD uint32_t eff_loc(uint32_t loc, uint64_t cap) {
 }
 
 // 128-bit keys (gm_common.hpp K128): 32-byte slots.  An insert claims a slot by atomicCAS of
-// hi from EMPTY_HI to the key's hi without its publish bit, stores lo, then publishes hi with
-// a release store; a probe that meets a claimed but unpublished slot with its own hi re-reads
-// that slot (the claiming lane publishes in the same iteration of the probe loop, so lanes of
+// hi from EMPTY_HI to the key's hi without its publish bit, stores lo, then publishes hi
+// (coherent stores, ordered by a wait: front_insert below); a probe that meets a claimed but
+// unpublished slot with its own hi re-reads that slot (the claiming lane publishes in the same iteration of the probe loop, so lanes of
 // one wave never wait on each other across iterations).  Lookups run after the tier is
 // complete and read (hi, lo) with one 16-byte load.
 struct alignas(32) WSlot {
@@ -167,21 +167,31 @@ __device__ __forceinline__ uint64_t home_slot(const K128 &key, uint64_t cap, uin
 }
 
 __device__ __forceinline__ bool front_insert(const WFrontRef &t, const K128 &key, uint32_t *err) {
+    // No acquire / release here: on this chip an agent-scope acquire invalidates the XCD's L2
+    // (buffer_inv sc1) and a release writes it back (buffer_wbl2 sc1) -- per probe, that made
+    // the 8x8 forward pass ~10x slower.  Instead lo is stored with a coherent (sc1) atomic
+    // store that the wave waits for before it publishes hi with another; a reader that sees
+    // the published hi reads lo with a coherent load.  The first read of a slot is a plain
+    // load: a stale view can only show the slot emptier than it is (EMPTY for claimed, claimed
+    // for published -- the CAS, or a coherent re-read, settles it), never another key.
     const uint64_t claim = key.hi & ~K128_PUB;
     uint64_t h = home_slot(key, t.cap, t.loc);
     const uint64_t lim = t.cap < MAX_PROBE ? t.cap : MAX_PROBE;
     uint32_t spins = 0;
+    bool coherent = false;   // this slot was seen claimed but unpublished: re-read it coherently
     for (uint64_t probe = 0; probe < lim;) {
-        uint64_t cur = __hip_atomic_load(&t.s[h].hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t cur = coherent ? __hip_atomic_load(&t.s[h].hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : t.s[h].hi;
         if (cur == EMPTY_HI) {
             const unsigned long long prev =
                 atomicCAS((unsigned long long *)&t.s[h].hi, (unsigned long long)EMPTY_HI, (unsigned long long)claim);
             if (prev == EMPTY_HI) {
                 __hip_atomic_store(&t.s[h].lo, key.lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&t.s[h].hi, key.hi, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // lo has reached the coherent level
+                __hip_atomic_store(&t.s[h].hi, key.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return true;
             }
-            cur = __hip_atomic_load(&t.s[h].hi, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            cur = prev;
         }
         if ((cur | K128_PUB) == key.hi) {
             if (!(cur & K128_PUB)) {   // claimed with this hi, lo not published yet: read the slot again
@@ -189,10 +199,12 @@ __device__ __forceinline__ bool front_insert(const WFrontRef &t, const K128 &key
                     atomicOr(err, DEV_ERR_TABLE_FULL);
                     return false;
                 }
+                coherent = true;
                 continue;
             }
             if (__hip_atomic_load(&t.s[h].lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key.lo) return false;
         }
+        coherent = false;
         h = h + 1 == t.cap ? 0 : h + 1;
         probe++;
     }
