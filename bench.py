@@ -251,6 +251,12 @@ def box_sharding(world, args, root, st, rstats, per_rank, autotune, torch, dist)
                            "(GM_OPT_BOX_TRANSPORT 1)"
                            if args.box_transport == "ipc" else "RCCL send / recv, one communicator per axis")
                           if world > 1 else "loopback (direct stores between the virtual ranks' tables, event per batch)",
+        "halo_transport_verified_before_this_run": ("IPC: across 2-4 processes sharing ONE GPU, with poisoned halos "
+                                                    "and an injected early-read fault (tests/test_gpu_multiproc.py); "
+                                                    "RCCL: the op lists over gloo on the CPU only; neither between "
+                                                    "two GPUs (no multi-GPU box in the build pipeline) -- this run's "
+                                                    "probe and per-rank oracle digests are the check"
+                                                    if world > 1 else None),
         "halo_bytes_sent_per_step_by_rank": sent,
         "halo_bytes_received_per_step_by_rank": recvd,
         "per_rank_gpu_ms_and_enqueue_ms_per_step": per_rank,
