@@ -93,14 +93,15 @@ static int sp_ipc_barrier(SpIpc &X) {
 
 // all[r * n + i] = rank r's mine[i]
 static int sp_ipc_allgather(SpIpc &X, const uint64_t *mine, size_t n, uint64_t *all) {
-    for (size_t o = 0; o < n || (!n && !o); o += SP_IPC_WORDS) {
-        const size_t k = std::min<size_t>(SP_IPC_WORDS, n - std::min(n, o));
+    size_t o = 0;
+    do {   // chunks of SP_IPC_WORDS, one barrier each (at least one, so every rank calls alike)
+        const size_t k = std::min<size_t>(SP_IPC_WORDS, n - o);
         const int buf = (int)((X.epoch + 1) & 1);
         std::memcpy(X.slot[X.me].val[buf], mine + o, k * 8);
         GM_TRY(sp_ipc_barrier(X));
         for (int r = 0; r < X.G; r++) std::memcpy(all + (size_t)r * n + o, X.slot[r].val[buf], k * 8);
-        if (!n) break;
-    }
+        o += k;
+    } while (o < n);
     return GM_OK;
 }
 

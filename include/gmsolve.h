@@ -236,7 +236,9 @@ int gm_expand_host(gm_ctx *ctx, uint64_t key, uint64_t *children, int cap,
  * first sharded solve), not by this call, so ranks whose transport needs none -- the split box
  * engine with GM_OPT_BOX_TRANSPORT 1, possibly several ranks on one GPU -- never make it.
  * uid NULL sets rank and world only, with no communicator; every sharded engine then refuses to
- * solve (GM_E_COMM). */
+ * solve (GM_E_COMM).  gm_solve checks the root key and the options before it makes the
+ * communicator, so a call that every rank makes with the same arguments fails on every rank
+ * before the first collective; a sharded solve's first call must be made by all ranks. */
 int gm_comm_unique_id(void *uid, int bytes);
 int gm_set_comm(gm_ctx *ctx, int rank, int world, const void *uid, int bytes);
 
