@@ -48,7 +48,7 @@ SYMBOLS = ("gm_version", "gm_last_error", "gm_device_count", "gm_open", "gm_set_
            "gm_set_comm", "gm_solve", "gm_solve_graph", "gm_export", "gm_query", "gm_digest", "gm_stats",
            "gm_tier_counts", "gm_adopt_buffer", "gm_dense_table", "gm_dist_plan", "gm_box_plan",
            "gm_rank_stats", "gm_rank_op_ms", "gm_close", "gm_key_words", "gm_pack_initial_key",
-           "gm_expand_host_key", "gm_solve_key", "gm_export_key", "gm_query_key")
+           "gm_expand_host_key", "gm_solve_key", "gm_export_key", "gm_query_key", "gm_sparse_layout")
 
 
 class GMError(RuntimeError):
@@ -131,6 +131,7 @@ def lib():
         "gm_solve_key": (ctypes.c_int, [vp, vp, P(u64), P(ctypes.c_uint16)]),
         "gm_export_key": (ctypes.c_int, [vp, vp, vp, u64, P(u64)]),
         "gm_query_key": (ctypes.c_int, [vp, vp, vp, u64]),
+        "gm_sparse_layout": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -185,3 +186,17 @@ def int_to_words(key, nwords):
 def words_to_int(words):
     """u64 key words (least significant first) -> one Python int."""
     return sum(int(w) << (64 * i) for i, w in enumerate(words))
+
+
+def sparse_layout(world, steps, counts, rank):
+    """gm_sparse_layout (host only): (seg, send_off, recv_off, recv_seg) of rank `rank` for the
+    world x (world * steps) count matrix of one exchange of the hash-sharded sparse engine."""
+    import numpy as np
+    m = np.ascontiguousarray(counts, dtype=np.uint64).reshape(world, world * steps)
+    seg = np.zeros(world * steps, dtype=np.uint64)
+    so = np.zeros(world + 1, dtype=np.uint64)
+    ro = np.zeros(world + 1, dtype=np.uint64)
+    rs = np.zeros(world * steps, dtype=np.uint64)
+    check(lib().gm_sparse_layout(world, steps, m.ctypes.data, rank, seg.ctypes.data, so.ctypes.data, ro.ctypes.data,
+                                 rs.ctypes.data))
+    return seg, so, ro, rs

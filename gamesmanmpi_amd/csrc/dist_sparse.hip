@@ -451,8 +451,8 @@ struct Layout {
     uint64_t nsend = 0, nrecv = 0;
 };
 
-static Layout layout_for(DistSparse *d, const std::vector<uint64_t> &mat, int r) {
-    const int G = d->G, S = d->S, nb = G * S;
+static Layout layout_for(int G, int S, const uint64_t *mat, int r) {
+    const int nb = G * S;
     Layout L;
     L.seg.resize(nb);
     L.send_off.assign(G + 1, 0);
@@ -473,6 +473,26 @@ static Layout layout_for(DistSparse *d, const std::vector<uint64_t> &mat, int r)
     L.recv_off[G] = acc;
     L.nrecv = acc;
     return L;
+}
+
+static Layout layout_for(DistSparse *d, const std::vector<uint64_t> &mat, int r) {
+    return layout_for(d->G, d->S, mat.data(), r);
+}
+
+// Host only (gm_sparse_layout): the layout every transport uses, for the CPU tests that replay
+// the RCCL op list over gloo
+int dist_sparse_layout(int G, int S, const uint64_t *mat, int r, uint64_t *seg, uint64_t *send_off,
+                       uint64_t *recv_off, uint64_t *recv_seg) {
+    if (G < 1 || S < 1 || G * S > MAXBINS || r < 0 || r >= G || !mat) {
+        set_error("bad sparse layout arguments");
+        return GM_E_ARG;
+    }
+    const Layout L = layout_for(G, S, mat, r);
+    if (seg) std::copy(L.seg.begin(), L.seg.end(), seg);
+    if (send_off) std::copy(L.send_off.begin(), L.send_off.end(), send_off);
+    if (recv_off) std::copy(L.recv_off.begin(), L.recv_off.end(), recv_off);
+    if (recv_seg) std::copy(L.recv_seg.begin(), L.recv_seg.end(), recv_seg);
+    return GM_OK;
 }
 
 // move every rank's segmented send buffer to the owners (or, reverse = true, the replies back)

@@ -691,6 +691,11 @@ int gm_box_plan(uint64_t root, int world, int rank, const int32_t *opts, int wha
     return dist_box_plan(root, world, rank, opts, what, axis, out, cap, n);
 }
 
+int gm_sparse_layout(int world, int steps, const uint64_t *counts, int rank, uint64_t *seg, uint64_t *send_off,
+                     uint64_t *recv_off, uint64_t *recv_seg) {
+    return dist_sparse_layout(world, steps, counts, rank, seg, send_off, recv_off, recv_seg);
+}
+
 int gm_rank_stats(gm_ctx *h, double *kernel_ms, uint64_t *boxes, uint64_t *recv_bytes, int cap, int *n) {
     GM_TRY(need_solved(h));
     if (!n) return GM_E_ARG;

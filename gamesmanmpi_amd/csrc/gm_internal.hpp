@@ -206,6 +206,8 @@ int dist_sub_plan(int heaps, int world, int rank, const int32_t *opts, int what,
 
 int dist_sparse_solve(Ctx *c, uint64_t root);
 int dist_sparse_solve_wide(Ctx *c, const K128 &root);
+int dist_sparse_layout(int G, int S, const uint64_t *mat, int r, uint64_t *seg, uint64_t *send_off,
+                       uint64_t *recv_off, uint64_t *recv_seg);
 int dist_sparse_export_wide(Ctx *c, K128 *keys, uint16_t *recs, uint64_t cap, uint64_t *n);
 int dist_sparse_query_wide(Ctx *c, const K128 *keys, uint16_t *recs, uint64_t n);
 int dist_sparse_export(Ctx *c, uint64_t *keys, uint16_t *recs, uint64_t cap, uint64_t *n);

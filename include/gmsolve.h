@@ -394,6 +394,19 @@ enum { GM_BOXPLAN_SHAPE = 0, GM_BOXPLAN_BOXES = 1, GM_BOXPLAN_FILLS = 2, GM_BOXP
 int gm_box_plan(uint64_t root_key, int world, int rank, const int32_t *opts, int what, int axis, uint32_t *out,
                 uint64_t cap, uint64_t *n);
 
+/* Host only (no HIP or RCCL call): the layout of one exchange of the hash-sharded sparse engine
+ * (csrc/dist_sparse.hip), the same for its RCCL, IPC and loopback transports.  counts is the
+ * world x (world * steps) matrix of one exchange: row q = source rank, column p * steps + s =
+ * children of q's parents owned by rank p that lie s + 1 tiers deeper.  For rank `rank`:
+ *   seg[p * steps + s]       where that bin starts in rank's send buffer (destination-major)
+ *   send_off[p], p <= world  rank's send segment for destination p (all steps)
+ *   recv_off[q], q <= world  rank's receive segment from source q (all steps)
+ *   recv_seg[q * steps + s]  where source q's keys of step s start in rank's receive buffer
+ * LOOK_UP keys go send_off -> recv_off; RESOLVE scores come back recv_off -> send_off
+ * (reference src/new_process.py:156-160, :179-187).  Any array may be NULL. */
+int gm_sparse_layout(int world, int steps, const uint64_t *counts, int rank, uint64_t *seg, uint64_t *send_off,
+                     uint64_t *recv_off, uint64_t *recv_seg);
+
 /* Per rank this context ran in its last solve on the split box engine (all virtual ranks, or its
  * own rank of a multi-process solve): with GM_OPT_TIMING the GPU time from the start of the rank's
  * first tier launch to the end of its last, the boxes it computed, and the halo bytes it receives
