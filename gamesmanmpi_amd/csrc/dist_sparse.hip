@@ -67,7 +67,10 @@ struct SpIpc {
     void *pub[2] = {};               // what this rank published
     uint64_t gen[2] = {};
     std::vector<uint64_t> pgen[2];   // per peer: the generation mapped
-    std::vector<void *> pbase[2];    // per peer: the mapping (hipIpcCloseMemHandle on change / close)
+    std::vector<void *> pbase[2];    // per peer: the mapping of that generation's allocation
+    // per peer, every allocation mapped in this solve (a peer's buffer can come back from its
+    // allocation cache as another kind: one mapping per allocation, closed at the end)
+    std::vector<std::vector<std::pair<hipIpcMemHandle_t, void *>>> maps;
 };
 
 static int sp_ipc_barrier(SpIpc &X) {
@@ -129,6 +132,7 @@ static int sp_ipc_open(Ctx *c, SpIpc &X, int G) {
         X.pgen[k].assign(G, 0);
         X.pbase[k].assign(G, nullptr);
     }
+    X.maps.assign(G, {});
     // every rank has the segment open once this barrier passes: its name can go
     const int rc = sp_ipc_barrier(X);
     if (rc == GM_OK && X.me == 0) shm_unlink(X.name);
@@ -140,9 +144,9 @@ static void sp_ipc_fail(SpIpc &X) {
 }
 
 static void sp_ipc_close(SpIpc &X) {
-    for (int k = 0; k < 2; k++)
-        for (void *p : X.pbase[k])
-            if (p) (void)hipIpcCloseMemHandle(p);
+    for (auto &m : X.maps)
+        for (auto &e : m) (void)hipIpcCloseMemHandle(e.second);
+    X.maps.clear();
     if (X.slot) munmap(X.slot, X.bytes);
     X.slot = nullptr;
 }
@@ -169,13 +173,17 @@ static int sp_ipc_peer(SpIpc &X, int r, int k, char **out) {
     const uint64_t g = X.slot[r].gen[k];
     if (!g) { set_error("rank %d published no send buffer", r); return GM_E_COMM; }
     if (X.pgen[k][r] != g) {
-        if (X.pbase[k][r]) (void)hipIpcCloseMemHandle(X.pbase[k][r]);
-        X.pbase[k][r] = nullptr;
+        const hipIpcMemHandle_t &h = X.slot[r].h[k];
         void *b = nullptr;
-        if (hipIpcOpenMemHandle(&b, X.slot[r].h[k], hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
-            (void)hipGetLastError();
-            set_error("hipIpcOpenMemHandle of rank %d's send buffer failed", r);
-            return GM_E_COMM;
+        for (auto &e : X.maps[r])
+            if (!std::memcmp(&e.first, &h, sizeof h)) b = e.second;
+        if (!b) {
+            if (hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void)hipGetLastError();
+                set_error("hipIpcOpenMemHandle of rank %d's send buffer failed", r);
+                return GM_E_COMM;
+            }
+            X.maps[r].emplace_back(h, b);
         }
         X.pbase[k][r] = b;
         X.pgen[k][r] = g;

@@ -228,6 +228,18 @@ def test_sparse_ipc_ranks_vs_oracle_digest(world, name, game, params):
     assert all(r["exchanged"] > 0 for r in res)
 
 
+def test_sparse_ipc_ranks_toot_5x4_vs_oracle_digest():
+    """Toot 5x4 (70,184,763 positions) over 3 processes with the IPC transport: larger tiers,
+    so the send buffers grow and come back from the allocation cache between exchanges (each
+    peer allocation is mapped once per solve); summed digests, per-ply counts and the root
+    record equal the committed oracle's."""
+    ref = json.load(open(os.path.join(GOLDEN, "oracle_digests.json")))["toot_5x4"]
+    res = _run(3, TOOT, (5, 4), {"sparse_transport": 1}, shared=True)
+    assert _summed(res) == (ref["digest"], ref["positions"])
+    assert all(r["n"] == ref["positions"] and r["rec"] == ref["root_record"] for r in res)
+    assert all(r["tiers"] == ref["per_ply"] for r in res)
+
+
 def test_sparse_ipc_ranks_query_othello_golden():
     """Othello 4x4 over 3 processes (IPC transport): every key of the reference plugin's golden
     table is answered by exactly one rank (its hash owner), with the golden record."""
