@@ -104,3 +104,43 @@ def test_othello8_endgame_12_device_vs_graph_path():
     g.close()
     assert n == gn == len(dev) == len(ref) and rec == grec
     assert dev == ref
+
+
+def _empties(p):
+    b = p.encode("latin-1")
+    return 64 - bin(int.from_bytes(b[0:8], "big") | int.from_bytes(b[8:16], "big")).count("1")
+
+
+def test_othello8_edge_roots_vs_canonical():
+    """Edge roots on the device path, each table equal to the canonical oracle over the plugin
+    (oracle/canonical.py): a full board (primitive: one position), a board with one empty
+    square, and a position of at most 10 empties whose mover must pass (the pass keeps the
+    mover, othello_bit_new.py:122-124; a second pass ends the game, :82)."""
+    import random
+    from gamesmanmpi_amd import Solver
+    import canonical
+    mod = load_plugin("test_games/othello_bit_new.py")
+    rng = random.Random(11)
+    found = {}
+    for _ in range(400):
+        p = mod.initial_position()
+        while mod.primitive(p) == 4:
+            ms = mod.gen_moves(p)
+            if ms == [None] and _empties(p) <= 10:
+                found.setdefault("pass", p)
+            if _empties(p) == 1:
+                found.setdefault("one_empty", p)
+            p = mod.do_move(p, ms[rng.randrange(len(ms))])
+        if _empties(p) == 0:
+            found.setdefault("full", p)
+        if len(found) == 3:
+            break
+    assert set(found) == {"pass", "one_empty", "full"}, found.keys()
+    for name, root in found.items():
+        s = Solver(mod, root=root, device=0)
+        n, rec = s.solve()
+        dev = _table_by_pos(s)
+        s.close()
+        table, positions = canonical.solve(mod, root)
+        ref = {positions[k]: (v << 14) | r for k, (v, r) in table.items()}
+        assert n == len(ref) and dev == ref, name
