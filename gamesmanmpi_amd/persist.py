@@ -9,7 +9,8 @@ src/cache_dict.py:19-42, opened at src/new_process.py:76-77):
 where a position lives on rank ``md5(str(pos)) % world_size``
 (GameState.get_hash, src/game_state.py:23-31) and int keys are stringified
 (src/cache_dict.py:62-66).  ``write_reference_tables`` writes a solved table
-(``gm_export``: sorted u64 keys + u16 records) in that layout, so tooling that
+(``gm_export``: sorted u64 keys + u16 records; ``gm_export_key``'s (n, words) arrays for
+keys past 64 bits) in that layout, so tooling that
 reads the reference's ``-sd`` directory reads ours; ``read_reference_tables``
 reads it back (tests, and resuming from a reference run's tables).
 """
@@ -46,12 +47,14 @@ def write_reference_tables(statsdir, codec, keys, records, world_size=1):
     """
     keys = np.asarray(keys, dtype=np.uint64)
     records = np.asarray(records, dtype=np.uint16)
+    # keys past 64 bits (Othello 8x8) come as (n, words) u64 arrays: one Python int each
+    key_list = [_lib.words_to_int(w) for w in keys.tolist()] if keys.ndim == 2 else keys.tolist()
     shelves = []
     for r in range(world_size):
         shelves.append((shelve.open(_path(statsdir, r, "resolved")), shelve.open(_path(statsdir, r, "remote"))))
     counts = [0] * world_size
     try:
-        for k, rec in zip(keys.tolist(), records.tolist()):
+        for k, rec in zip(key_list, records.tolist()):
             if rec == _lib.REC_UNSOLVED:
                 continue
             for pos in (codec.members(k) if hasattr(codec, "members") else (codec.pos(k),)):

@@ -211,3 +211,29 @@ def test_solve_local_messages(capsys):
     solve_local.main([os.path.join(REPO, "test_games/othello_bit_new.py"), "--dims", "4x4"])
     assert capsys.readouterr().out.splitlines() == [
         "Winning position", "Tie", "TIE in 9 moves", "Losing position"]
+
+
+@pytest.mark.gpu
+def test_launcher_othello_8x8_endgame_on_the_device(tmp_path):
+    """`solver_launcher.py tests/plugins/othello8_endgame.py -sd DIR`: the 8x8 plugin binds the
+    128-bit-key descriptor, the launcher prints the canonical root line, and -sd writes the
+    (n, 3)-word key table and the reference's shelves, every record equal to the reference
+    plugin's golden table (keys = blake2b-8 of the position string)."""
+    import hashlib
+    import json
+    import numpy as np
+    from gamesmanmpi_amd.persist import read_reference_tables
+    args = solver_launcher.build_parser().parse_args(_abs(["tests/plugins/othello8_endgame.py"])
+                                                     + ["-sd", str(tmp_path), "--sd-format", "both"])
+    out = io.StringIO()
+    solver_launcher.run(args, out=out)
+    roots = json.load(open(os.path.join(GOLDEN, "roots.json")))
+    assert out.getvalue() == roots["othello_8x8_endgame"]["canonical"] + "\n"
+    d = np.load(tmp_path / "stats" / "0" / "table.npz")
+    assert d["keys"].shape == (56552, 3)
+    back = read_reference_tables(str(tmp_path))
+    g = np.load(os.path.join(GOLDEN, "othello_8x8_endgame.npz"))
+    want = dict(zip(g["keys"].tolist(), g["records"].tolist()))
+    got = {int.from_bytes(hashlib.blake2b(p.encode("ISO-8859-1"), digest_size=8).digest(), "big"): (v << 14) | r
+           for p, (v, r) in back.items()}
+    assert got == want

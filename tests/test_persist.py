@@ -41,3 +41,19 @@ def test_reference_keys_are_the_plugin_positions(tmp_path):
     keys, recs = golden("four_to_one_four")
     write_reference_tables(str(tmp_path / "f2o"), games.FourToOneCodec(), keys, recs)
     assert read_reference_tables(str(tmp_path / "f2o"))["4"] == (0, 3)   # WIN in 3
+
+
+def test_wide_keys_round_trip(tmp_path):
+    """Keys past 64 bits (Othello 8x8: (n, 3) u64 word arrays from gm_export_key) are written
+    as the plugin's position strings, like any other key."""
+    from gamesmanmpi_amd import _lib, games
+    from gamesmanmpi_amd.persist import read_reference_tables, write_reference_tables
+    codec = games.OthelloCodec(8, 8)
+    pos = [bytes.fromhex(h).decode("latin-1") for h in ("303800204018057a4646bfdebfe6fa800200",
+                                                        "30380028503841784646bfd6afc6be000200")]
+    keys = np.array([_lib.int_to_words(codec.key(p), 3) for p in pos], dtype=np.uint64)
+    recs = np.array([(1 << 14) | 11, 13], dtype=np.uint16)
+    counts = write_reference_tables(str(tmp_path), codec, keys, recs, 2)
+    assert sum(counts) == 2
+    back = read_reference_tables(str(tmp_path), 2)
+    assert back == {pos[0]: (1, 11), pos[1]: (0, 13)}
