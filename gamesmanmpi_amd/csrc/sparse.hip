@@ -234,6 +234,97 @@ __global__ __launch_bounds__(256) void retro_split_kernel(D d, const uint64_t *_
     }
 }
 
+// GM_SPARSE_CSR=1 (round 6; games whose moves go one tier deeper): expand
+// also records, per interior position in the order it walks them, the slots its undecided
+// children occupy in the next tier's table (a CSR: coff / ccnt / cslot) and the best score of
+// its primitive children (pbest); retro then reads those slots and makes one direct load per
+// child, with no move generation, probe chain or key compare.  A lane stages its slots in LDS
+// (a dynamically indexed register array would go to scratch), and a wave reserves one
+// contiguous run for its 64 positions with one atomic.
+template <class D>
+__global__ __launch_bounds__(256) void expand_csr_kernel(D d, const uint64_t *__restrict__ ikeys, uint64_t n,
+                                                         FrontRef next, uint8_t *__restrict__ iwon,
+                                                         uint32_t *__restrict__ coff, uint8_t *__restrict__ ccnt,
+                                                         uint16_t *__restrict__ pbest, uint32_t *__restrict__ cslot,
+                                                         unsigned long long *cursor, uint32_t *err) {
+    constexpr int C = D::MAXC;
+    __shared__ uint32_t stage[256 * C];
+    uint32_t *my = stage + threadIdx.x * C;
+    const int lane = threadIdx.x & 63;
+    uint64_t fresh = 0;
+    // every lane of a wave runs every iteration (the wave's prefix sum below)
+    for (uint64_t base = blockIdx.x * (uint64_t)blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const bool live = i < n && !(*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL);
+        uint32_t m = 0, pb = 0;
+        bool won = false;
+        if (live)
+            d.visit(ikeys[i], [&](uint64_t c) {
+                uint32_t sl;
+                if (front_insert_slot(next, c, err, &sl)) fresh++;
+                const int p = d.primitive(c);
+                if (p != UNDECIDED) {
+                    pb = max(pb, (uint32_t)score_of_primitive(p));
+                    won = won || p == LOSS;
+                } else if (m < (uint32_t)C) {
+                    my[m++] = sl;
+                }
+                return true;
+            });
+        uint32_t incl = m;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        const uint32_t total = __shfl(incl, 63);
+        uint32_t wb = 0;
+        if (lane == 63 && total) wb = (uint32_t)atomicAdd(cursor, (unsigned long long)total);
+        wb = __shfl(wb, 63);
+        if (live) {
+            const uint32_t at = wb + incl - m;
+            iwon[i] = won ? 1 : 0;
+            coff[i] = at;
+            ccnt[i] = (uint8_t)m;
+            pbest[i] = (uint16_t)pb;
+            for (uint32_t j = 0; j < m; j++) cslot[at + j] = my[j];
+        }
+    }
+    wave_add(next.count, fresh);
+}
+
+template <class D>
+__global__ __launch_bounds__(256) void retro_csr_kernel(const uint32_t *__restrict__ islot,
+                                                        const uint8_t *__restrict__ iwon,
+                                                        const uint32_t *__restrict__ coff,
+                                                        const uint8_t *__restrict__ ccnt,
+                                                        const uint16_t *__restrict__ pbest,
+                                                        const uint32_t *__restrict__ cslot, uint64_t n, ResRef self,
+                                                        ResRef next, uint32_t *err) {
+    constexpr int C = D::MAXC;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t best = 0xFFFFu;
+        if (!iwon[i]) {   // (a LOSS-in-0 child: nothing beats it)
+            best = pbest[i];
+            const uint32_t o = coff[i], m = ccnt[i];
+            uint32_t sl[C];
+#pragma unroll
+            for (int j = 0; j < C; j++) sl[j] = (uint32_t)j < m ? cslot[o + j] : ~0u;
+#pragma unroll
+            for (int j = 0; j < C; j++)   // independent loads: every child's in flight at once
+                if (sl[j] != ~0u) best = max(best, (uint32_t)(next.s[sl[j]].score & 0xFFFFu));
+        }
+        if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
+        self.s[islot[i]].score = parent_score(best);
+    }
+}
+
+static bool csr_enabled() {
+    static const bool on = getenv("GM_SPARSE_CSR") && atoi(getenv("GM_SPARSE_CSR")) == 1;
+    return on;
+}
+
 // Large tiers (round 4): the interior list sorted by the key's top BATCH_SORT_BITS bits
 // (hipcub radix sort of (key, slot) pairs, a few ms per solve).  Positions that agree on
 // the top cells of the T and O planes then sit together and share many children (69 % of
@@ -268,7 +359,17 @@ static int sort_bits() {   // GM_SPARSE_SORT_BITS (development): key bits the li
 // expand / retro of one tier: the split kernels below SPLIT_MAX interior positions, else
 // the plain kernels over the sorted interior list (or the unsorted one, GM_SPARSE_BATCH 0)
 template <class D>
-static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fronts<D::MAX_SKIP> &nx, uint32_t *err) {
+static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fronts<D::MAX_SKIP> &nx, uint32_t *err,
+                          unsigned long long *csr_cursor = nullptr) {
+    if constexpr (D::MAX_SKIP == 1) {
+        if (T.cslot && csr_cursor && T.ni >= split_max()) {
+            (void)hipMemsetAsync(csr_cursor, 0, 8, st);
+            hipLaunchKernelGGL(expand_csr_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d,
+                               T.skeys ? T.skeys : T.ikeys, T.ni, nx.t[0], T.iwon, T.coff, T.ccnt, T.pbest, T.cslot,
+                               csr_cursor, err);
+            return;
+        }
+    }
     if (T.ni < split_max())
         hipLaunchKernelGGL(expand_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys, T.ni,
                            nx, T.iwon, err);
@@ -280,6 +381,14 @@ static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fro
 template <class D>
 static void launch_retro(hipStream_t st, const D &d, const SpTier &T, const ResRef &self,
                          const Ress<D::MAX_SKIP> &nx, uint32_t *err) {
+    if constexpr (D::MAX_SKIP == 1) {
+        if (T.cslot && T.ni >= split_max()) {
+            hipLaunchKernelGGL(retro_csr_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st,
+                               T.skeys ? T.sslot : T.islot, T.iwon, T.coff, T.ccnt, T.pbest, T.cslot, T.ni, self,
+                               nx.t[0], err);
+            return;
+        }
+    }
     if (T.ni < split_max())
         hipLaunchKernelGGL(retro_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys,
                            T.islot, T.iwon, T.ni, self, nx, err);
@@ -444,7 +553,7 @@ static int replay_with(Ctx *c, const D &d, uint64_t root) {
             if (Tt.skeys && batch_sort(c, sp, Tt, false) != GM_OK) return abort_capture(c, GM_E_HIP);
             Fronts<S> nx;   // a tier past the last one received nothing: no table (cap 0)
             for (int s = 0; s < S; s++) nx.t[s] = fref(t + 1 + s);
-            launch_expand(c->stream, d, Tt, nx, err);
+            launch_expand(c->stream, d, Tt, nx, err, sp->d_scratch + 40);
         }
         for (size_t tt = T; tt-- > 0;) {
             SpTier &Tt = sp->tiers[tt];
@@ -604,11 +713,22 @@ static int solve_with(Ctx *c, const D &d, uint64_t root) {
             const uint64_t need = table_cap_for(sp->tiers[u].fcount + est.distinct(sc[s]));
             if (sc[s] && sp->tiers[u].cap < need) GM_TRY(tier_grow(c, sp, u, need));
         }
+        // GM_SPARSE_CSR: the expand records its children's slots for retro (one-step games,
+        // the plain kernels; slots and offsets in 32 bits)
+        if (S == 1 && csr_enabled() && sp->tiers[t].ni >= split_max() && sp->tiers[t + 1].cap < (1ull << 32) &&
+            sc[0] < (1ull << 32)) {
+            SpTier &Tt = sp->tiers[t];
+            const uint64_t ni = Tt.ni;
+            GM_TRY(dev_alloc(c, (void **)&Tt.coff, ni * 4));
+            GM_TRY(dev_alloc(c, (void **)&Tt.ccnt, ni));
+            GM_TRY(dev_alloc(c, (void **)&Tt.pbest, ni * 2));
+            GM_TRY(dev_alloc(c, (void **)&Tt.cslot, std::max<uint64_t>(sc[0], 1) * 4));
+        }
         // 3. expand the interior positions
         for (int attempt = 0;; attempt++) {
             Fronts<S> nx;
             for (int s = 0; s < S; s++) nx.t[s] = front_ref(sp, t + 1 + s);
-            launch_expand(c->stream, d, sp->tiers[t], nx, sp->d_err);
+            launch_expand(c->stream, d, sp->tiers[t], nx, sp->d_err, sp->d_scratch + 40);
             GM_HIP(hipGetLastError());
             uint32_t e;
             GM_HIP(hipMemcpyAsync(&e, sp->d_err, 4, hipMemcpyDeviceToHost, c->stream));

@@ -113,6 +113,12 @@ struct SpTierT {
     uint32_t *sslot = nullptr;
     int64_t tier = 0;            // the descriptor tier of the positions (root tier + index)
     uint32_t loc = 0;            // home function (FrontRef::loc) requested for this tier's table
+    // GM_SPARSE_CSR (sparse.hip, one-step games on the plain kernels): per interior position
+    // in the order expand / retro walk it, its undecided children's slots in the next tier's
+    // table (cslot[coff .. coff + ccnt)) and the best score of its primitive children
+    uint32_t *coff = nullptr, *cslot = nullptr;
+    uint8_t *ccnt = nullptr;
+    uint16_t *pbest = nullptr;
 };
 using SpTier = SpTierT<uint64_t>;
 
@@ -145,6 +151,25 @@ __device__ __forceinline__ bool front_insert(const FrontRef &t, uint64_t key, ui
         h = h + 1 == t.cap ? 0 : h + 1;
     }
     atomicOr(err, DEV_ERR_TABLE_FULL);
+    return false;
+}
+
+// as front_insert, and the key's slot (new or found) in *slot (~0u when the table is full)
+__device__ __forceinline__ bool front_insert_slot(const FrontRef &t, uint64_t key, uint32_t *err, uint32_t *slot) {
+    uint64_t h = home_slot(key, t.cap, t.loc);
+    const uint64_t lim = t.cap < MAX_PROBE ? t.cap : MAX_PROBE;
+    for (uint64_t probe = 0; probe < lim; probe++) {
+        const uint64_t cur = t.s[h].key;
+        if (cur == key) { *slot = (uint32_t)h; return false; }
+        if (cur == EMPTY_KEY) {
+            const unsigned long long prev = atomicCAS((unsigned long long *)&t.s[h].key,
+                                                      (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+            if (prev == EMPTY_KEY || prev == key) { *slot = (uint32_t)h; return prev == EMPTY_KEY; }
+        }
+        h = h + 1 == t.cap ? 0 : h + 1;
+    }
+    atomicOr(err, DEV_ERR_TABLE_FULL);
+    *slot = ~0u;
     return false;
 }
 
@@ -511,7 +536,8 @@ inline int classify_tier_table(Ctx *c, const D &d, SpTierT<key_t<D>> &T, unsigne
 
 template <class K>
 inline void free_tier(Ctx *c, SpTierT<K> &T) {
-    for (void *p : {(void *)T.slots, (void *)T.ikeys, (void *)T.islot, (void *)T.iwon, (void *)T.skeys, (void *)T.sslot})
+    for (void *p : {(void *)T.slots, (void *)T.ikeys, (void *)T.islot, (void *)T.iwon, (void *)T.skeys, (void *)T.sslot,
+                    (void *)T.coff, (void *)T.cslot, (void *)T.ccnt, (void *)T.pbest})
         dev_free(c, p);
     T = SpTierT<K>{};
 }

@@ -287,6 +287,21 @@ def test_sparse_sorted_lists_everywhere_vs_golden(split_max, mode):
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("split_max", ["1", "4096"])
+def test_sparse_csr_retro_vs_golden(split_max):
+    """GM_SPARSE_CSR=1 (csrc/sparse.hip expand_csr_kernel / retro_csr_kernel: expand records its
+    undecided children's table slots, retro reads them instead of regenerating and probing)
+    on every tier of these games that takes the plain kernels: the reference plugins' golden
+    tables and the Toot 4x4 oracle digest, synced solve and replay (fresh process)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GM_SPARSE_CSR="1", GM_SPARSE_SPLIT_MAX=split_max)
+    r = subprocess.run([sys.executable, "-c", _SPARSE_BATCH_EVERYWHERE, repo], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("home_w", ["16", "20"])
 def test_sparse_locality_home_vs_golden(home_w):
     """GM_SPARSE_HOME_W (development knob, DESIGN.md §4.2: measured and not kept): the tier
