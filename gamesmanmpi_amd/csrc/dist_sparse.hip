@@ -353,6 +353,89 @@ __global__ void root_lookup_kernel(typename KT<K>::Res t, K key, uint32_t *out) 
     }
 }
 
+// One rank in one context (self_only below: a 128-bit-key game on one GPU) exchanges nothing,
+// so the bucket / insert / lookup / fold kernels above collapse into two: the lane that
+// generates a child inserts it into its tier's table (forward) or looks it up there (backward),
+// as the single-GPU engine's expand / retro do (sparse.hip).  One move generation per pass
+// instead of the bucket kernels' three, and no key, parent or reply lists.
+template <class K, int S>
+struct FrontsK {
+    typename KT<K>::Front t[S];
+};
+template <class K, int S>
+struct RessK {
+    typename KT<K>::Res t[S];
+};
+
+template <class D>
+__global__ __launch_bounds__(256) void self_expand_kernel(D d, const key_t<D> *__restrict__ ikeys, uint64_t n,
+                                                          FrontsK<key_t<D>, D::MAX_SKIP> next,
+                                                          uint8_t *__restrict__ iwon, uint32_t *err) {
+    constexpr int S = D::MAX_SKIP;
+    using K = key_t<D>;
+    uint64_t fresh[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) fresh[s] = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL) break;   // re-run into larger tables
+        const K k = ikeys[i];
+        const int64_t tk = d.tier(k);
+        bool won = false;
+        d.visit(k, [&](const K &c) {
+            const int64_t dt = d.tier(c) - tk;
+            if (dt < 1 || dt > S) atomicOr(err, DEV_ERR_TIER);
+#pragma unroll
+            for (int s = 0; s < S; s++)
+                if (dt == s + 1 && front_insert(next.t[s], c, err)) fresh[s]++;
+            if (!won) won = d.primitive(c) == LOSS;
+            return true;
+        });
+        iwon[i] = won ? 1 : 0;
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
+}
+
+template <class D>
+__global__ __launch_bounds__(256) void self_retro_kernel(D d, const key_t<D> *__restrict__ ikeys,
+                                                         const uint32_t *__restrict__ islot,
+                                                         const uint8_t *__restrict__ iwon, uint64_t n,
+                                                         typename KT<key_t<D>>::Res self,
+                                                         RessK<key_t<D>, D::MAX_SKIP> next, uint32_t *err) {
+    constexpr int S = D::MAX_SKIP;
+    using K = key_t<D>;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t best = 0xFFFFu;   // a LOSS-in-0 child (iwon): nothing beats it, no lookup needed
+        if (!iwon[i]) {
+            best = 0;
+            const K k = ikeys[i];
+            const int64_t tk = d.tier(k);
+            d.visit(k, [&](const K &c) {
+                const int p = d.primitive(c);
+                uint32_t sc;
+                if (p != UNDECIDED) {
+                    sc = score_of_primitive(p);
+                } else {
+                    const int64_t dt = d.tier(c) - tk;
+                    int f = -1;
+#pragma unroll
+                    for (int s = 0; s < S; s++)
+                        if (dt == s + 1) f = res_find(next.t[s], c);
+                    if (f < 0) { atomicOr(err, DEV_ERR_MISSING_CHILD); f = 0; }
+                    sc = (uint32_t)f;
+                }
+                best = max(best, sc);
+                return best != 0xFFFFu;
+            });
+        }
+        if (!best) atomicOr(err, DEV_ERR_MISSING_CHILD);
+        if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
+        self.s[islot[i]].score = parent_score(best);
+    }
+}
+
 // ------------------------------------------------------------------ host helpers
 // element-wise sum (or max) over ranks of a host vector, through the IPC segment
 static int sp_ipc_reduce(SpIpc &X, std::vector<uint64_t> &v, bool max) {
@@ -541,6 +624,11 @@ static int exchange_ipc(Ctx *c, DistSparseK<K> *d, const Layout &me, const std::
 // order (one destination, one source), so the receive side reads the send buffers in place
 // and the exchange copies nothing.
 static bool self_only(const DistSparse *d) { return d->loopback && d->G == 1; }
+// ... and then the fused kernels run (GM_SPARSE_SELF_FUSED=0, development: the bucket path)
+static bool self_fused(const DistSparse *d) {
+    static const bool on = !getenv("GM_SPARSE_SELF_FUSED") || atoi(getenv("GM_SPARSE_SELF_FUSED")) != 0;
+    return on && self_only(d);
+}
 template <class K>
 static K *recv_keys(const DistSparse *d, SpRankT<K> &R) { return self_only(d) ? R.sendk : R.recvk; }
 template <class K>
@@ -621,6 +709,46 @@ static int classify_tier(Ctx *c, DistSparseK<key_t<D>> *d, const D &desc, size_t
     return GM_OK;
 }
 
+// forward step of tier t on one rank in one context (self_fused): classify's edge counts per
+// tier step size the next tiers' tables; the expand inserts the children itself
+template <class D>
+static int self_expand(Ctx *c, DistSparseK<key_t<D>> *d, const D &desc, size_t t, uint64_t &offered,
+                       uint64_t &before) {
+    using K = key_t<D>;
+    constexpr int S = D::MAX_SKIP;
+    SpRankT<K> &R = d->ranks[0];
+    SpTierT<K> &T = R.tiers[t];
+    unsigned long long sc[S];
+    GM_HIP(hipMemcpyAsync(sc, R.d_scr, sizeof sc, hipMemcpyDeviceToHost, c->stream));
+    GM_HIP(hipStreamSynchronize(c->stream));
+    for (int s = 0; s < S; s++) {
+        offered += sc[s];
+        before += R.tiers[t + 1 + s].fcount;
+        d->edges += sc[s];
+    }
+    if (!T.ni) return GM_OK;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        FrontsK<K, S> nx;
+        for (int s = 0; s < S; s++) {
+            SpTierT<K> &U = R.tiers[t + 1 + s];
+            const uint64_t need = table_cap_for(U.fcount + (attempt ? sc[s] : d->est.distinct(sc[s])));
+            if (sc[s] && U.cap < need) GM_TRY(tier_grow(c, U, need, R.d_err));
+            nx.t[s] = fref(R, t + 1 + s);
+        }
+        hipLaunchKernelGGL(self_expand_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, desc, T.ikeys, T.ni,
+                           nx, T.iwon, R.d_err);
+        GM_HIP(hipGetLastError());
+        uint32_t e;
+        GM_HIP(hipMemcpyAsync(&e, R.d_err, 4, hipMemcpyDeviceToHost, c->stream));
+        GM_HIP(hipStreamSynchronize(c->stream));
+        if (e != DEV_ERR_TABLE_FULL || attempt) break;
+        if (trace_on()) fprintf(stderr, "[gm] tier %zu: tables full at ratio %.3f, re-running\n", t, d->est.ratio);
+        GM_HIP(hipMemsetAsync(R.d_err, 0, 4, c->stream));
+        d->est.missed();
+    }
+    return GM_OK;
+}
+
 template <class D>
 static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
     using K = key_t<D>;
@@ -681,59 +809,63 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
             if (R.tiers.size() < need) R.tiers.resize(need);
         GM_TRY(classify_tier(c, d, desc, t));
         GM_TRY(check_err(c, d));
-        // children -> owners
-        for (auto &R : d->ranks) {
-            GM_HIP(hipMemsetAsync(R.d_hist, 0, nb * 8, c->stream));
-            run_bucket<D, false, false>(c, d, desc, R, t, nullptr);
-        }
-        GM_TRY(gather_counts(c, d, mat));
-        GM_TRY(check_err(c, d));
-        std::vector<Layout> lay(d->ranks.size());
-        for (size_t i = 0; i < d->ranks.size(); i++) {
-            SpRankT<K> &R = d->ranks[i];
-            lay[i] = layout_for(d, mat, R.rank);
-            d->edges += lay[i].nsend;
-            GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
-            if (!self_only(d)) GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
-            GM_HIP(hipMemcpyAsync(R.d_seg, lay[i].seg.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
-            GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
-            run_bucket<D, true, false>(c, d, desc, R, t, nullptr);
-        }
-        GM_TRY(exchange(c, d, lay, mat, false));
-        // owners insert into their tier tables, sized for load <= 0.7 of the predicted
-        // distinct keys; a misprediction re-runs the (idempotent) inserts once
         uint64_t offered = 0, before = 0;
-        for (size_t i = 0; i < d->ranks.size(); i++) {
-            SpRankT<K> &R = d->ranks[i];
-            std::vector<uint64_t> in(S, 0);
-            for (int s = 0; s < S; s++) {
-                for (int q = 0; q < G; q++) in[s] += mat[(size_t)q * nb + R.rank * S + s];
-                offered += in[s];
-                before += R.tiers[t + 1 + s].fcount;
+        if (self_fused(d)) {
+            GM_TRY(self_expand(c, d, desc, t, offered, before));
+        } else {
+            // children -> owners
+            for (auto &R : d->ranks) {
+                GM_HIP(hipMemsetAsync(R.d_hist, 0, nb * 8, c->stream));
+                run_bucket<D, false, false>(c, d, desc, R, t, nullptr);
             }
-            for (int attempt = 0; attempt < 2; attempt++) {
+            GM_TRY(gather_counts(c, d, mat));
+            GM_TRY(check_err(c, d));
+            std::vector<Layout> lay(d->ranks.size());
+            for (size_t i = 0; i < d->ranks.size(); i++) {
+                SpRankT<K> &R = d->ranks[i];
+                lay[i] = layout_for(d, mat, R.rank);
+                d->edges += lay[i].nsend;
+                GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
+                if (!self_only(d)) GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
+                GM_HIP(hipMemcpyAsync(R.d_seg, lay[i].seg.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
+                GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
+                run_bucket<D, true, false>(c, d, desc, R, t, nullptr);
+            }
+            GM_TRY(exchange(c, d, lay, mat, false));
+            // owners insert into their tier tables, sized for load <= 0.7 of the predicted
+            // distinct keys; a misprediction re-runs the (idempotent) inserts once
+            for (size_t i = 0; i < d->ranks.size(); i++) {
+                SpRankT<K> &R = d->ranks[i];
+                std::vector<uint64_t> in(S, 0);
                 for (int s = 0; s < S; s++) {
-                    if (!in[s]) continue;
-                    const size_t u = t + 1 + s;
-                    SpTierT<K> &U = R.tiers[u];
-                    const uint64_t needc = table_cap_for(U.fcount + (attempt ? in[s] : d->est.distinct(in[s])));
-                    if (U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
-                    for (int q = 0; q < G; q++) {
-                        const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
-                        if (n)
-                            hipLaunchKernelGGL(insert_recv_kernel<K>, dim3(grid_for(n)), dim3(256), 0, c->stream,
-                                               recv_keys(d, R) + lay[i].recv_seg[q * S + s], n, fref(R, u), R.d_err);
-                    }
+                    for (int q = 0; q < G; q++) in[s] += mat[(size_t)q * nb + R.rank * S + s];
+                    offered += in[s];
+                    before += R.tiers[t + 1 + s].fcount;
                 }
-                uint32_t e;
-                GM_HIP(hipMemcpyAsync(&e, R.d_err, 4, hipMemcpyDeviceToHost, c->stream));
-                GM_HIP(hipStreamSynchronize(c->stream));
-                if (e != DEV_ERR_TABLE_FULL || attempt) break;
-                if (trace_on())
-                    fprintf(stderr, "[gm] rank %d tier %zu: tables full at ratio %.3f, re-running\n", R.rank, t,
-                            d->est.ratio);
-                GM_HIP(hipMemsetAsync(R.d_err, 0, 4, c->stream));
-                d->est.missed();
+                for (int attempt = 0; attempt < 2; attempt++) {
+                    for (int s = 0; s < S; s++) {
+                        if (!in[s]) continue;
+                        const size_t u = t + 1 + s;
+                        SpTierT<K> &U = R.tiers[u];
+                        const uint64_t needc = table_cap_for(U.fcount + (attempt ? in[s] : d->est.distinct(in[s])));
+                        if (U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
+                        for (int q = 0; q < G; q++) {
+                            const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
+                            if (n)
+                                hipLaunchKernelGGL(insert_recv_kernel<K>, dim3(grid_for(n)), dim3(256), 0, c->stream,
+                                                   recv_keys(d, R) + lay[i].recv_seg[q * S + s], n, fref(R, u), R.d_err);
+                        }
+                    }
+                    uint32_t e;
+                    GM_HIP(hipMemcpyAsync(&e, R.d_err, 4, hipMemcpyDeviceToHost, c->stream));
+                    GM_HIP(hipStreamSynchronize(c->stream));
+                    if (e != DEV_ERR_TABLE_FULL || attempt) break;
+                    if (trace_on())
+                        fprintf(stderr, "[gm] rank %d tier %zu: tables full at ratio %.3f, re-running\n", R.rank, t,
+                                d->est.ratio);
+                    GM_HIP(hipMemsetAsync(R.d_err, 0, 4, c->stream));
+                    d->est.missed();
+                }
             }
         }
         GM_TRY(check_err(c, d));
@@ -772,6 +904,23 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
     // ---------------- backward
     for (size_t t = d->gcount.size(); t-- > 0;) {
         if (!d->gcount[t]) continue;
+        if (self_fused(d)) {
+            SpRankT<K> &R = d->ranks[0];
+            SpTierT<K> &T = R.tiers[t];
+            if (T.ni) {
+                constexpr int SS = D::MAX_SKIP;
+                RessK<K, SS> nx;
+                for (int s = 0; s < SS; s++) {
+                    const size_t u = t + 1 + s;
+                    nx.t[s] = u < R.tiers.size() ? res_ref_of(R.tiers[u]) : typename KT<K>::Res{nullptr, 0};
+                }
+                hipLaunchKernelGGL(self_retro_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, desc, T.ikeys,
+                                   T.islot, T.iwon, T.ni, res_ref_of(T), nx, R.d_err);
+                GM_HIP(hipGetLastError());
+            }
+            GM_TRY(check_err(c, d));
+            continue;
+        }
         for (auto &R : d->ranks) {
             GM_HIP(hipMemsetAsync(R.d_hist, 0, nb * 8, c->stream));
             run_bucket<D, false, true>(c, d, desc, R, t, nullptr);

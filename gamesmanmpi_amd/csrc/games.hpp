@@ -49,6 +49,17 @@ struct part_visit_t<D, std::void_t<decltype(D::PART_VISIT)>> {
     static constexpr bool value = D::PART_VISIT;
 };
 
+// descriptors with a count_children(k, &dt) (classify's edge counts by tier step without
+// making the children: every child of k lands dt tiers deeper)
+template <class D, class = void>
+struct step_count_t {
+    static constexpr bool value = false;
+};
+template <class D>
+struct step_count_t<D, std::void_t<decltype(D::STEP_COUNT)>> {
+    static constexpr bool value = D::STEP_COUNT;
+};
+
 // The key type of a descriptor: D::Key when it declares one (DescOthello8: K128), else u64.
 template <class D, class = void>
 struct key_of {
@@ -507,28 +518,56 @@ struct DescOthello8 {
         if (nb == nw) return TIE;
         return ((nb > nw) != (turn(k) == 1)) ? LOSS : WIN;         // :59-73
     }
-    // discs of `opp` flipped by `me` playing plane square p (flip_helper, :100-118)
-    GM_HD static uint64_t flips(uint64_t me, uint64_t opp, int p) {
-        uint64_t all = 0;
-        const int x = p & 7, y = p >> 3;
-        for (int dx = -1; dx <= 1; dx++)
-            for (int dy = -1; dy <= 1; dy++) {
-                if (!dx && !dy) continue;
-                uint64_t run = 0;
-                int cx = x + dx, cy = y + dy;
-                while (cx >= 0 && cy >= 0 && cx < 8 && cy < 8) {
-                    const uint64_t bit = 1ull << (8 * cy + cx);
-                    if (opp & bit) {
-                        run |= bit;
-                    } else {
-                        if (me & bit) all |= run;
-                        break;
-                    }
-                    cx += dx;
-                    cy += dy;
-                }
-            }
-        return all;
+    // Bitboard move generation (round 6; round 5 walked the squares, a loop per direction --
+    // gm_expand_host_key's tests pin the children to the plugin's either way).  step<DIR> moves every
+    // disc of a plane one square in direction DIR (E W S N SE SW NE NW on bit 8y + x), clearing
+    // the column a shift wraps into; run<DIR>(from, opp) is the opp discs in an unbroken line
+    // from the squares next to `from` (at most 6 on an 8-wide board).  Every lane runs the same
+    // instructions, where the square walk's loops diverged with each lane's position.
+    template <int DIR>
+    GM_HD static uint64_t step(uint64_t b) {
+        constexpr uint64_t notA = 0xFEFEFEFEFEFEFEFEull, notH = 0x7F7F7F7F7F7F7F7Full;
+        if constexpr (DIR == 0) return (b << 1) & notA;
+        else if constexpr (DIR == 1) return (b >> 1) & notH;
+        else if constexpr (DIR == 2) return b << 8;
+        else if constexpr (DIR == 3) return b >> 8;
+        else if constexpr (DIR == 4) return (b << 9) & notA;
+        else if constexpr (DIR == 5) return (b << 7) & notH;
+        else if constexpr (DIR == 6) return (b >> 7) & notA;
+        else return (b >> 9) & notH;
+    }
+    template <int DIR>
+    GM_HD static uint64_t run(uint64_t from, uint64_t opp) {
+        uint64_t t = step<DIR>(from) & opp;
+#pragma unroll
+        for (int i = 0; i < 5; i++) t |= step<DIR>(t) & opp;
+        return t;
+    }
+    // the squares `me` can play: empty, at the end of a run of opp discs that starts next to a me disc
+    template <int DIR = 0>
+    GM_HD static uint64_t legal(uint64_t me, uint64_t opp) {
+        const uint64_t m = step<DIR>(run<DIR>(me, opp)) & ~(me | opp);
+        if constexpr (DIR < 7) return m | legal<DIR + 1>(me, opp);
+        else return m;
+    }
+    // the opp discs `me` flips by playing the square `bit` (flip_helper, :100-118): each
+    // direction's run, when a me disc ends it
+    template <int DIR = 0>
+    GM_HD static uint64_t flips_at(uint64_t me, uint64_t opp, uint64_t bit) {
+        const uint64_t t = run<DIR>(bit, opp);
+        const uint64_t f = (step<DIR>(t) & me) ? t : 0ull;
+        if constexpr (DIR < 7) return f | flips_at<DIR + 1>(me, opp, bit);
+        else return f;
+    }
+    // classify's edge counts without making the children: every move lands 3 - pass tiers
+    // deeper (one more disc, the pass count reset), the pass child 1 (sparse_tables.hpp)
+    static constexpr bool STEP_COUNT = true;
+    GM_HD int count_children(const K128 &k, int *dt) const {
+        const uint64_t o = occ(k), w = k.lo, b = o & ~w;
+        const bool black = turn(k) == 1;
+        const int n = popc64(legal(black ? b : w, black ? w : b));
+        *dt = n ? 3 - pass(k) : 1;
+        return n ? n : 1;
     }
     template <class F>
     GM_HD void visit(const K128 &k, F &&fn) const {
@@ -536,24 +575,17 @@ struct DescOthello8 {
         const int t = turn(k);
         const bool black = t == 1;
         const uint64_t me = black ? b : w, opp = black ? w : b;
-        int n = 0;
-        for (uint64_t e = ~o; e; e &= e - 1) {
-            const int p = __builtin_ctzll(e);
-            if (!(opp & adjacent(p))) continue;   // no line can start: not legit (:134-146)
-            const uint64_t f = flips(me, opp, p);
-            if (!f) continue;
-            const uint64_t nme = me | (1ull << p) | f, nopp = opp & ~f;
-            n++;
+        uint64_t mv = legal(me, opp);   // legit moves (:134-146), in square order
+        if (!mv) {
+            fn(pack(w, b, t, pass(k) + 1));                         // [None]: incr_pass only (:122-124)
+            return;
+        }
+        for (; mv; mv &= mv - 1) {
+            const uint64_t bit = mv & (~mv + 1);
+            const uint64_t f = flips_at(me, opp, bit);
+            const uint64_t nme = me | bit | f, nopp = opp & ~f;
             if (!fn(pack(black ? nopp : nme, black ? nme : nopp, 3 - t, 0))) return;   // incr_turn, reset_pass
         }
-        if (!n) fn(pack(w, b, t, pass(k) + 1));                     // [None]: incr_pass only (:122-124)
-    }
-    GM_HD static uint64_t adjacent(int p) {
-        const uint64_t bit = 1ull << p;
-        const uint64_t notA = 0xFEFEFEFEFEFEFEFEull, notH = 0x7F7F7F7F7F7F7F7Full;
-        const uint64_t e = (bit << 1) & notA, wv = (bit >> 1) & notH;
-        const uint64_t row = bit | e | wv;
-        return (row | (row << 8) | (row >> 8)) & ~bit;
     }
     GM_HD int children(const K128 &k, K128 *out) const {
         int n = 0;

@@ -354,17 +354,25 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, typename KT<key_t<D>
                 if (!interior) {
                     slot_set(slots[i], k[r], (uint64_t)score_of_primitive(p));
                 } else if (COUNT) {   // a replay knows its sizes: no edge counts
-                    const int64_t tk = d.tier(k[r]);
-                    int nk = 0;
-                    unreduced(d).visit(k[r], [&](const K &c) {   // tiers only: no canonical children
-                        const int64_t dt = d.tier(c) - tk;
-                        nk++;
+                    if constexpr (step_count_t<D>::value) {
+                        int dt = 0;
+                        const int nk = d.count_children(k[r], &dt);
                         if (dt < 1 || dt > S) atomicOr(err, DEV_ERR_TIER);
 #pragma unroll
-                        for (int s = 0; s < S; s++) cnt[s] += dt == s + 1;
-                        return true;
-                    });
-                    if (!nk) atomicOr(err, DEV_ERR_NOMOVES);
+                        for (int s = 0; s < S; s++) cnt[s] += dt == s + 1 ? (uint64_t)nk : 0ull;
+                    } else {
+                        const int64_t tk = d.tier(k[r]);
+                        int nk = 0;
+                        unreduced(d).visit(k[r], [&](const K &c) {   // tiers only: no canonical children
+                            const int64_t dt = d.tier(c) - tk;
+                            nk++;
+                            if (dt < 1 || dt > S) atomicOr(err, DEV_ERR_TIER);
+#pragma unroll
+                            for (int s = 0; s < S; s++) cnt[s] += dt == s + 1;
+                            return true;
+                        });
+                        if (!nk) atomicOr(err, DEV_ERR_NOMOVES);
+                    }
                 }
             }
             m[r] = __ballot(interior);

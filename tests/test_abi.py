@@ -174,6 +174,33 @@ def test_othello_8x8_binds_the_wide_descriptor():
     assert games.verify_exhaustive(end, ce, end.initial_position(), 100_000)
 
 
+def test_othello_8x8_bitboard_moves_vs_plugin_on_random_games():
+    """The bitboard move generator of the 8x8 descriptor (games.hpp DescOthello8::legal /
+    flips_at, the code the device kernels run) against the plugin over WHOLE games: seeded
+    random playouts from the 8x8 start, every position's primitive value and child set (the
+    endgame test above only sees near-full boards)."""
+    import random
+    mod = load_plugin("test_games/othello_bit_new.py")
+    c = games.identify(mod)
+    hd = games.HostDescriptor(c)
+    rng = random.Random(11)
+    n = passes = 0
+    for _ in range(150):
+        p = mod.initial_position()
+        while True:
+            prim, kids, _ = hd.expand(c.key(p))
+            assert prim == mod.primitive(p)
+            if prim != 4:
+                break
+            ch = [mod.do_move(p, m) for m in mod.gen_moves(p)]
+            assert sorted(kids) == sorted(c.key(x) for x in ch)
+            n += 1
+            passes += len(ch) == 1 and mod.gen_moves(p) == [None]
+            p = ch[rng.randrange(len(ch))]
+    hd.close()
+    assert n > 8000 and passes > 0
+
+
 def test_othello_8x8_key_words_round_trip():
     """gm_expand_host_key rejects a key that is no 8x8 position (a centre square empty, planes
     overlapping, turn 3), and the one-word calls refuse a 3-word context."""
