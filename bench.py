@@ -446,6 +446,8 @@ def othello8_config(rank, world, dist, torch):
             "solve_ms_all": [round(t * 1e3, 3) for t in ts], "positions_per_s": n / med,
             "statistic": "median of 3 solves after 1 warm-up", "edges": st["n_edges"], "tiers": st["n_tiers"],
             "table_gb": st["table_bytes"] / 1e9, "digest": "%#018x" % d1[0],
+            "roofline": (sparse_roofline(None, med, OTHELLO8_PROFILE, ("self_expand_kernel", "self_retro_kernel"),
+                                         "kernel_sum_ms_per_replay") if e == 16 else None),
             "ok": (vn, vrec, d8) == (n, rec, d1),
             "parity": "the same root on 8 virtual ranks (hash-sharded, loopback exchange): digest, positions and "
                       "root record equal"}
@@ -465,33 +467,46 @@ def toot_roofline(algo_bytes, solve_s):
     kernel trace of replayed solves + one-solve PMC passes, tools/sparse_replay_profile.py)
     against the measured random-access peaks; and it sets the counted HBM-side bytes of a
     solve beside the SURVEY §8d algorithmic bytes (10 + 18 d per position)."""
+    return sparse_roofline(algo_bytes, solve_s, TOOT_PROFILE, ("expand_kernel", "retro_kernel"),
+                           "kernel_sum_ms_per_replay")
+
+
+def sparse_roofline(algo_bytes, solve_s, path, names, sum_key):
     try:
-        prof = json.load(open(TOOT_PROFILE))
+        prof = json.load(open(path))
     except (OSError, ValueError):
         return None
     ks = prof["kernels"]
     per = {}
-    for k in ("expand_kernel", "retro_kernel"):
+    for k in names:
         x = ks[k]
         sec = x["ms"] / 1e3
         per[k] = {"ms": x["ms"], "ea_read_req": x["ea_read_req"], "ea_write_req": x["ea_write_req"],
                   "read_req_per_s": x["ea_read_req"] / sec, "write_req_per_s": x["ea_write_req"] / sec,
-                  "frac_of_random_load_peak": x["ea_read_req"] / sec / RANDOM_LOAD_PEAK, "l2_hit": x["l2_hit"]}
+                  "frac_of_random_load_peak": x["ea_read_req"] / sec / RANDOM_LOAD_PEAK,
+                  "requests_per_s": (x["ea_read_req"] + x["ea_write_req"]) / sec,
+                  "l2_hit": x["l2_hit"]}
     rd = sum(per[k]["ea_read_req"] for k in per)
+    wr = sum(per[k]["ea_write_req"] for k in per)
     sec = sum(per[k]["ms"] for k in per) / 1e3
     counted = sum(x["fetch_bytes"] + x["write_bytes"] for x in ks.values())
     return {"bound": "random access", "unit": "requests/s",
             "achieved": rd / sec, "peak": RANDOM_LOAD_PEAK, "frac": rd / sec / RANDOM_LOAD_PEAK,
-            "achieved_note": "memory-side read requests of expand + retro per second of their kernel time",
+            "frac_all_requests": (rd + wr) / sec / RANDOM_LOAD_PEAK,
+            "achieved_note": "memory-side read requests of the two kernels per second of their kernel time "
+                             "(requests_per_s per kernel adds the write requests: CAS and stores)",
             "peak_cas_per_s": RANDOM_CAS_PEAK,
             "peak_source": "tools/randbench.hip (profiles/r01_randbench.txt): random 16-B loads 47 G/s, "
                            "random 8-B CAS 17 G/s, 8 GiB table",
             "kernels": per,
-            "algo_bytes_per_solve": algo_bytes, "algo_gbs": algo_bytes / solve_s / 1e9,
-            "algo_frac_of_hbm_peak": algo_bytes / solve_s / 1e9 / HBM_PEAK_GBS,
-            "counted_bytes_per_solve": counted, "counted_over_algo_bytes": counted / algo_bytes,
-            "profile": "profiles/traffic_toot6x4.json",
-            "profile_kernel_sum_ms": min(prof["kernel_sum_ms_per_replay"])}
+            "algo_bytes_per_solve": algo_bytes, "algo_gbs": algo_bytes / solve_s / 1e9 if algo_bytes else None,
+            "algo_frac_of_hbm_peak": algo_bytes / solve_s / 1e9 / HBM_PEAK_GBS if algo_bytes else None,
+            "counted_bytes_per_solve": counted, "counted_over_algo_bytes": counted / algo_bytes if algo_bytes else None,
+            "profile": os.path.relpath(path, REPO),
+            "profile_kernel_sum_ms": min(prof[sum_key])}
+
+
+OTHELLO8_PROFILE = os.path.join(REPO, "profiles", "traffic_othello8_16.json")
 
 
 SPARSE_CPU_SAMPLE = {"othello_4x4": (4, (4, 4)),    # the whole config-4 workload

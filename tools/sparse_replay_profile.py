@@ -2,6 +2,8 @@
 """Per-replay kernel times and counters of a sparse-engine profile (development aid).
 
     python tools/sparse_replay_profile.py gpurun_out/r05g sp [--json profiles/traffic_toot6x4.json]
+    python tools/sparse_replay_profile.py gpurun_out/r06p o8 --window front_insert_one_wkernel --skip 1 \
+        --json profiles/traffic_othello8_15.json     # Othello 8x8: synced solves, each starting at its root insert
 
 <dir>/<tag>_kt: rocprofv3 --kernel-trace of `tools/solve_timed.py toot 6 4 N` (1 synced solve,
 then N - 1 replays).  A replay starts with slot_fill_many_kernel (the one-launch refill of every
@@ -39,13 +41,15 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("tag")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--window", default="slot_fill_many_kernel", help="the kernel that starts each solve's window")
+    ap.add_argument("--skip", type=int, default=0, help="windows to leave out first (warm-up solves)")
     a = ap.parse_args()
     rows = []
     for f in glob.glob("%s/%s_kt/**/*kernel_trace.csv" % (a.dir, a.tag), recursive=True):
         for r in csv.DictReader(open(f)):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     rows.sort()
-    starts = [s for s, _, k in rows if k == "slot_fill_many_kernel"]
+    starts = [s for s, _, k in rows if k == a.window]
     if not starts:
         raise SystemExit("no replay in the trace")
     wins = []
@@ -53,6 +57,7 @@ def main():
         e = starts[i + 1] if i + 1 < len(starts) else float("inf")
         ks = [(s, t, k) for s, t, k in rows if b <= s < e and k != "res_digest_kernel"]
         wins.append(ks)
+    wins = wins[a.skip:]
     per = defaultdict(float)
     sums, spans = [], []
     for ks in wins:
