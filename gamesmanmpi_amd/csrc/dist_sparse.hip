@@ -13,12 +13,13 @@
 //                    counts are all-gathered; keys move with one ncclGroup of
 //                    send/recv per peer; owners insert them into their tier
 //                    tables (deduplicating on insert).
-// backward, tier t:  each rank regenerates its interior positions' children;
-//                    a primitive child is scored locally from primitive() (a
-//                    LOSS-in-0 child ends the search), the others go to their
-//                    owners (LOOK_UP), who answer with the u16 scores in the same
-//                    order (RESOLVE); the parent folds them with atomicMax and
-//                    turns the best score into its own (gm_common.hpp).
+// backward, tier t:  the owners look up again the keys they received in the
+//                    forward exchange of tier t (kept per tier, as each sender
+//                    keeps the parent index of every key it sent) and answer with
+//                    the u16 scores in the same order (RESOLVE); the parent folds
+//                    them with atomicMax and turns the best score into its own
+//                    (gm_common.hpp).  So the backward pass makes no move and
+//                    sends no key: the LOOK_UP of a child happened once, forward.
 //
 // Exchanges use one of three transports:
 //   RCCL (GM_OPT_SPARSE_TRANSPORT 0, one process per GPU): counts all-gathered, keys and
@@ -192,6 +193,15 @@ static int sp_ipc_peer(SpIpc &X, int r, int k, char **out) {
     return GM_OK;
 }
 
+// Layout of one exchange: mat is G x (G*S), row = source rank, column = dest*S + dt.
+struct Layout {
+    std::vector<uint64_t> seg;        // send segment bases per bin (dest-major), size G*S
+    std::vector<uint64_t> send_off;   // per dest, size G+1
+    std::vector<uint64_t> recv_off;   // per source, size G+1 (all dts of that source)
+    std::vector<uint64_t> recv_seg;   // per (source, dt) base in the recv buffer, size G*S
+    uint64_t nsend = 0, nrecv = 0;
+};
+
 template <class K>
 struct SpRankT {
     int rank = 0;
@@ -202,10 +212,16 @@ struct SpRankT {
     unsigned long long *d_cursor = nullptr;  // G*S bins
     unsigned long long *d_seg = nullptr;     // G*S bins
     unsigned long long *d_scr = nullptr;     // [0,8) edges by step, [9] interior count, [10] seen, [12] cursor
-    K *sendk = nullptr, *recvk = nullptr;
-    uint64_t send_cap = 0, recv_cap = 0, best_cap = 0;
+    uint64_t *d_rb = nullptr;                // G*S + 1 receive-segment bounds (insert_bins / lookup_bins)
+    K *sendk = nullptr, *recvk = nullptr;    // recvk / sendp: the current tier's (t_recvk / t_sendp)
+    uint64_t send_cap = 0, best_cap = 0, rout_cap = 0, rin_cap = 0;
     uint32_t *sendp = nullptr, *best = nullptr;
     uint16_t *reply_out = nullptr, *reply_in = nullptr;
+    // per tier, from the forward exchange to the backward one: the keys this rank received as
+    // their owner (one rank in one context: the keys it sent itself) and, per key it sent, its
+    // parent's interior index
+    std::vector<K *> t_recvk;
+    std::vector<uint32_t *> t_sendp;
 };
 
 // the key-independent part of a sharded solve (c->dist_sp); DistSparseK<K> adds the ranks
@@ -229,101 +245,66 @@ struct DistSparse {
 template <class K>
 struct DistSparseK : DistSparse {
     std::vector<SpRankT<K>> ranks;
+    std::vector<std::vector<Layout>> t_lay;      // per tier: every local rank's exchange layout
+    std::vector<std::vector<uint64_t>> t_mat;    // per tier: the all-gathered count matrix
 };
 
 // ------------------------------------------------------------------ kernels
 constexpr int MAXBINS = 64 * 3;
 
 // Children of the interior positions of a tier, bucketed by bin = owner * S + (step - 1).
-// COUNT: LDS histogram, one global atomic per bin per workgroup.  SCATTER: the
-// workgroup reserves a range per bin and a second visit writes the keys (and, in
-// the backward pass, the parent's interior index).  BACK: primitive children are
-// folded locally (never sent) and the local best initialises best[i].  The forward
-// scatter marks parents with a LOSS-in-0 child (iwon); the backward pass sends
-// nothing for them (their value is final: WIN in 1).
-template <class D, bool SCATTER, bool BACK>
+// COUNT: an LDS histogram over all of the workgroup's chunks, added to hist once at the end
+// (atomics on one line serialise: block_add).  SCATTER: per chunk the workgroup reserves a
+// range per bin, and a second visit writes the keys and each key's parent (its interior
+// index, kept for the backward fold).
+template <class D, bool SCATTER>
 __global__ __launch_bounds__(256) void bucket_kernel(D d, const key_t<D> *__restrict__ ikeys, uint64_t n, int G,
                                                      unsigned long long *hist,
                                                      const unsigned long long *__restrict__ seg,
                                                      unsigned long long *cursor, key_t<D> *out_keys,
-                                                     uint32_t *out_parent, uint32_t *best, uint8_t *iwon,
-                                                     uint32_t *err) {
+                                                     uint32_t *out_parent, uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
     using K = key_t<D>;
     __shared__ unsigned int lh[MAXBINS], lh2[MAXBINS];
     __shared__ unsigned long long lbase[MAXBINS];
     const int nb = G * S;
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) lh[b] = lh2[b] = 0;
     for (uint64_t base = blockIdx.x * 256ull; base < n; base += (uint64_t)gridDim.x * 256ull) {
-        for (int b = threadIdx.x; b < nb; b += blockDim.x) lh[b] = lh2[b] = 0;
+        if (SCATTER)
+            for (int b = threadIdx.x; b < nb; b += blockDim.x) lh[b] = lh2[b] = 0;
         __syncthreads();
         const uint64_t i = base + threadIdx.x;
-        const bool won_before = BACK && i < n && iwon[i];
-        const bool live = i < n && !won_before;
+        const bool live = i < n;
         K k{};
         if (live) k = ikeys[i];
         const int64_t tk = live ? d.tier(k) : 0;
-        // one pass over the children; `emit(c, bin)` is called for the ones that leave this thread
-        bool won = false;
-        auto walk = [&](auto emit) -> uint32_t {
-            uint32_t local = 0;
-            if (!live) return local;
+        // one pass over the children, `emit(c, bin)` for each
+        auto walk = [&](auto emit) {
+            if (!live) return;
             d.visit(k, [&](const K &c) {
-                if (SCATTER && !BACK && !won) won = d.primitive(c) == LOSS;
-                if (BACK) {
-                    const int p = d.primitive(c);
-                    if (p != UNDECIDED) {
-                        local = max(local, (uint32_t)score_of_primitive(p));
-                        return local != 0xFFFFu;
-                    }
-                }
                 int64_t dt = d.tier(c) - tk;
                 if (dt < 1 || dt > S) { atomicOr(err, DEV_ERR_TIER); dt = 1; }
                 emit(c, (int)(owner_rank(c, (uint32_t)G) * S + (dt - 1)));
                 return true;
             });
-            return local;
         };
         walk([&](const K &, int bin) { atomicAdd(&lh[bin], 1u); });
         __syncthreads();
-        if (!SCATTER) {
-            for (int b = threadIdx.x; b < nb; b += blockDim.x)
-                if (lh[b]) atomicAdd(&hist[b], (unsigned long long)lh[b]);
-        } else {
+        if (SCATTER) {
             for (int b = threadIdx.x; b < nb; b += blockDim.x)
                 lbase[b] = lh[b] ? seg[b] + atomicAdd(&cursor[b], (unsigned long long)lh[b]) : 0ull;
             __syncthreads();
-            const uint32_t local = walk([&](const K &c, int bin) {
+            walk([&](const K &c, int bin) {
                 const unsigned long long at = lbase[bin] + atomicAdd(&lh2[bin], 1u);
                 out_keys[at] = c;
-                if (BACK) out_parent[at] = (uint32_t)i;
+                out_parent[at] = (uint32_t)i;
             });
-            if (BACK && live) best[i] = local;
-            if (BACK && won_before) best[i] = 0xFFFFu;
-            if (!BACK && live) iwon[i] = won ? 1 : 0;
         }
         __syncthreads();
     }
-}
-
-template <class K>
-__global__ void insert_recv_kernel(const K *__restrict__ in, uint64_t n, typename KT<K>::Front t, uint32_t *err) {
-    uint64_t fresh = 0;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        if (*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL) break;   // re-run into a larger table
-        if (front_insert(t, in[i], err)) fresh++;
-    }
-    wave_add(t.count, fresh);
-}
-
-template <class K>
-__global__ void lookup_kernel(const K *__restrict__ in, uint64_t n, typename KT<K>::Res t, uint16_t *out, uint32_t *err) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const int s = res_find(t, in[i]);
-        if (s < 0) atomicOr(err, DEV_ERR_MISSING_CHILD);
-        out[i] = s < 0 ? 0 : (uint16_t)s;
-    }
+    if (!SCATTER)
+        for (int b = threadIdx.x; b < nb; b += blockDim.x)
+            if (lh[b]) atomicAdd(&hist[b], (unsigned long long)lh[b]);
 }
 
 __global__ void fold_kernel(const uint16_t *__restrict__ reply, const uint32_t *__restrict__ parent, uint64_t n,
@@ -394,7 +375,7 @@ __global__ __launch_bounds__(256) void self_expand_kernel(D d, const key_t<D> *_
         iwon[i] = won ? 1 : 0;
     }
 #pragma unroll
-    for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
+    for (int s = 0; s < S; s++) block_add(next.t[s].count, fresh[s]);
 }
 
 template <class D>
@@ -433,6 +414,72 @@ __global__ __launch_bounds__(256) void self_retro_kernel(D d, const key_t<D> *__
         if (!best) atomicOr(err, DEV_ERR_MISSING_CHILD);
         if (score_overflows(best)) atomicOr(err, DEV_ERR_OVERFLOW);
         self.s[islot[i]].score = parent_score(best);
+    }
+}
+
+// A rank's whole receive buffer of a tier in ONE launch: segment (q, s) -- source q, tier step
+// s + 1 -- starts at bounds[q S + s] (the exchange layout's recv_seg; bounds[G S] = the total),
+// and each key finds its step by a binary search over the G S + 1 bounds.  One launch per rank
+// and tier instead of one per segment: the launch tails and the counter atomics are paid once.
+template <int S>
+__device__ __forceinline__ int bin_step(const uint64_t *__restrict__ bounds, int nbins, uint64_t j) {
+    if constexpr (S == 1) {
+        return 0;
+    } else {
+        int lo = 0, hi = nbins;   // bounds[lo] <= j < bounds[hi]
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (bounds[mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        return lo % S;
+    }
+}
+
+template <class K, int S>
+__global__ __launch_bounds__(256) void insert_bins_kernel(const K *__restrict__ in, uint64_t n,
+                                                          const uint64_t *__restrict__ bounds, int nbins,
+                                                          FrontsK<K, S> t, uint32_t *err) {
+    uint64_t fresh[S];
+#pragma unroll
+    for (int s = 0; s < S; s++) fresh[s] = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (*(volatile uint32_t *)err & DEV_ERR_TABLE_FULL) break;   // re-run into larger tables
+        const int st = bin_step<S>(bounds, nbins, i);
+        const K k = in[i];
+#pragma unroll
+        for (int s = 0; s < S; s++)
+            if (s == st && front_insert(t.t[s], k, err)) fresh[s]++;
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) block_add(t.t[s].count, fresh[s]);
+}
+
+// (a primitive key is answered from primitive(), as classify scored it, with no table access)
+template <class D>
+__global__ __launch_bounds__(256) void lookup_bins_kernel(D d, const key_t<D> *__restrict__ in, uint64_t n,
+                                                          const uint64_t *__restrict__ bounds, int nbins,
+                                                          RessK<key_t<D>, D::MAX_SKIP> t, uint16_t *out,
+                                                          uint32_t *err) {
+    constexpr int S = D::MAX_SKIP;
+    using K = key_t<D>;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const K k = in[i];
+        const int p = d.primitive(k);
+        int f;
+        if (p != UNDECIDED) {
+            f = score_of_primitive(p);
+        } else {
+            const int st = bin_step<S>(bounds, nbins, i);
+            f = -1;
+#pragma unroll
+            for (int s = 0; s < S; s++)
+                if (s == st) f = res_find(t.t[s], k);
+            if (f < 0) atomicOr(err, DEV_ERR_MISSING_CHILD);
+        }
+        out[i] = f < 0 ? 0 : (uint16_t)f;
     }
 }
 
@@ -491,12 +538,12 @@ static int sendrecv(Ctx *c, DistSparse *d, const void *send, const uint64_t *sen
     return GM_OK;
 }
 
-template <class D, bool SCATTER, bool BACK>
-static void run_bucket(Ctx *c, DistSparse *d, const D &desc, SpRankT<key_t<D>> &R, size_t t, uint32_t *best) {
+template <class D, bool SCATTER>
+static void run_bucket(Ctx *c, DistSparse *d, const D &desc, SpRankT<key_t<D>> &R, size_t t) {
     SpTierT<key_t<D>> &T = R.tiers[t];
     if (!T.ni) return;
-    hipLaunchKernelGGL((bucket_kernel<D, SCATTER, BACK>), dim3(grid_for(T.ni)), dim3(256), 0, c->stream, desc, T.ikeys,
-                       T.ni, d->G, R.d_hist, R.d_seg, R.d_cursor, R.sendk, R.sendp, best, T.iwon, R.d_err);
+    hipLaunchKernelGGL((bucket_kernel<D, SCATTER>), dim3(grid_counted(T.ni)), dim3(256), 0, c->stream, desc, T.ikeys,
+                       T.ni, d->G, R.d_hist, R.d_seg, R.d_cursor, R.sendk, R.sendp, R.d_err);
 }
 
 // counts[r][dest*S+dt] for all ranks -> host matrix (G x G*S)
@@ -533,14 +580,6 @@ static int check_err(Ctx *c, DistSparseK<K> *d) {
     return GM_OK;
 }
 
-// Layout of one exchange: mat is G x (G*S), row = source rank, column = dest*S + dt.
-struct Layout {
-    std::vector<uint64_t> seg;        // send segment bases per bin (dest-major), size G*S
-    std::vector<uint64_t> send_off;   // per dest, size G+1
-    std::vector<uint64_t> recv_off;   // per source, size G+1 (all dts of that source)
-    std::vector<uint64_t> recv_seg;   // per (source, dt) base in the recv buffer, size G*S
-    uint64_t nsend = 0, nrecv = 0;
-};
 
 static Layout layout_for(int G, int S, const uint64_t *mat, int r) {
     const int nb = G * S;
@@ -635,7 +674,8 @@ template <class K>
 static uint16_t *recv_replies(const DistSparse *d, SpRankT<K> &R) { return self_only(d) ? R.reply_out : R.reply_in; }
 
 template <class K>
-static int exchange(Ctx *c, DistSparseK<K> *d, std::vector<Layout> &lay, const std::vector<uint64_t> &mat, bool reply) {
+static int exchange(Ctx *c, DistSparseK<K> *d, const std::vector<Layout> &lay, const std::vector<uint64_t> &mat,
+                    bool reply) {
     constexpr uint64_t KB = sizeof(K);
     if (self_only(d)) return GM_OK;
     if (c->poison)   // test hook: a segment that never lands reads as 0xFF, not as an earlier tier's data
@@ -694,7 +734,7 @@ static int classify_tier(Ctx *c, DistSparseK<key_t<D>> *d, const D &desc, size_t
         SpTierT<key_t<D>> &T = R.tiers[t];
         const uint64_t n = T.fcount;
         if (!n) continue;
-        GM_TRY(classify_tier_table(c, desc, T, R.d_scr, R.d_err));
+        GM_TRY(classify_tier_table(c, desc, T, R.d_scr, R.d_err, self_fused(d)));
         unsigned long long sc[12];
         GM_HIP(hipMemcpyAsync(sc, R.d_scr, sizeof sc, hipMemcpyDeviceToHost, c->stream));
         GM_HIP(hipStreamSynchronize(c->stream));
@@ -779,6 +819,7 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
         GM_TRY(dev_alloc(c, (void **)&R.d_cursor, nb * 8));
         GM_TRY(dev_alloc(c, (void **)&R.d_seg, nb * 8));
         GM_TRY(dev_alloc(c, (void **)&R.d_scr, 16 * 8));
+        GM_TRY(dev_alloc(c, (void **)&R.d_rb, (nb + 1) * 8));
         R.tiers.resize(1);
     }
     GM_TRY(dev_alloc(c, (void **)&d->d_mat, (size_t)G * nb * 8));
@@ -816,20 +857,38 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
             // children -> owners
             for (auto &R : d->ranks) {
                 GM_HIP(hipMemsetAsync(R.d_hist, 0, nb * 8, c->stream));
-                run_bucket<D, false, false>(c, d, desc, R, t, nullptr);
+                run_bucket<D, false>(c, d, desc, R, t);
             }
             GM_TRY(gather_counts(c, d, mat));
             GM_TRY(check_err(c, d));
-            std::vector<Layout> lay(d->ranks.size());
+            if (d->t_lay.size() < need) {
+                d->t_lay.resize(need);
+                d->t_mat.resize(need);
+            }
+            std::vector<Layout> &lay = d->t_lay[t];
+            lay.assign(d->ranks.size(), Layout{});
+            d->t_mat[t] = mat;
             for (size_t i = 0; i < d->ranks.size(); i++) {
                 SpRankT<K> &R = d->ranks[i];
                 lay[i] = layout_for(d, mat, R.rank);
                 d->edges += lay[i].nsend;
-                GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
-                if (!self_only(d)) GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
+                if (R.t_recvk.size() < need) {
+                    R.t_recvk.resize(need, nullptr);
+                    R.t_sendp.resize(need, nullptr);
+                }
+                GM_TRY(dev_alloc(c, (void **)&R.t_sendp[t], std::max<uint64_t>(lay[i].nsend, 1) * 4));
+                R.sendp = R.t_sendp[t];
+                if (self_only(d)) {   // one rank, one context: what it sends is what it receives, kept
+                    GM_TRY(dev_alloc(c, (void **)&R.t_recvk[t], std::max<uint64_t>(lay[i].nsend, 1) * sizeof(K)));
+                    R.sendk = R.t_recvk[t];
+                } else {
+                    GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
+                    GM_TRY(dev_alloc(c, (void **)&R.t_recvk[t], std::max<uint64_t>(lay[i].nrecv, 1) * sizeof(K)));
+                    R.recvk = R.t_recvk[t];
+                }
                 GM_HIP(hipMemcpyAsync(R.d_seg, lay[i].seg.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
                 GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
-                run_bucket<D, true, false>(c, d, desc, R, t, nullptr);
+                run_bucket<D, true>(c, d, desc, R, t);
             }
             GM_TRY(exchange(c, d, lay, mat, false));
             // owners insert into their tier tables, sized for load <= 0.7 of the predicted
@@ -842,20 +901,23 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                     offered += in[s];
                     before += R.tiers[t + 1 + s].fcount;
                 }
+                std::vector<uint64_t> rb(lay[i].recv_seg);
+                rb.push_back(lay[i].nrecv);
+                GM_HIP(hipMemcpyAsync(R.d_rb, rb.data(), rb.size() * 8, hipMemcpyHostToDevice, c->stream));
                 for (int attempt = 0; attempt < 2; attempt++) {
+                    constexpr int SS = D::MAX_SKIP;
+                    FrontsK<K, SS> nx;
                     for (int s = 0; s < S; s++) {
-                        if (!in[s]) continue;
                         const size_t u = t + 1 + s;
                         SpTierT<K> &U = R.tiers[u];
                         const uint64_t needc = table_cap_for(U.fcount + (attempt ? in[s] : d->est.distinct(in[s])));
-                        if (U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
-                        for (int q = 0; q < G; q++) {
-                            const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
-                            if (n)
-                                hipLaunchKernelGGL(insert_recv_kernel<K>, dim3(grid_for(n)), dim3(256), 0, c->stream,
-                                                   recv_keys(d, R) + lay[i].recv_seg[q * S + s], n, fref(R, u), R.d_err);
-                        }
+                        if (in[s] && U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
+                        nx.t[s] = fref(R, u);
                     }
+                    if (lay[i].nrecv)
+                        hipLaunchKernelGGL((insert_bins_kernel<K, SS>), dim3(grid_for(lay[i].nrecv)), dim3(256), 0,
+                                           c->stream, recv_keys(d, R), lay[i].nrecv, R.d_rb, nb, nx, R.d_err);
+                    GM_HIP(hipGetLastError());
                     uint32_t e;
                     GM_HIP(hipMemcpyAsync(&e, R.d_err, 4, hipMemcpyDeviceToHost, c->stream));
                     GM_HIP(hipStreamSynchronize(c->stream));
@@ -866,6 +928,10 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                     GM_HIP(hipMemsetAsync(R.d_err, 0, 4, c->stream));
                     d->est.missed();
                 }
+                // the tier's buffers now belong to t_recvk / t_sendp
+                R.recvk = nullptr;
+                R.sendp = nullptr;
+                if (self_only(d)) R.sendk = nullptr;
             }
         }
         GM_TRY(check_err(c, d));
@@ -921,60 +987,60 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
             GM_TRY(check_err(c, d));
             continue;
         }
-        for (auto &R : d->ranks) {
-            GM_HIP(hipMemsetAsync(R.d_hist, 0, nb * 8, c->stream));
-            run_bucket<D, false, true>(c, d, desc, R, t, nullptr);
-        }
-        GM_TRY(gather_counts(c, d, mat));
-        std::vector<Layout> lay(d->ranks.size());
+        // RESOLVE: each owner looks up again the keys it received for tier t, the scores go back
+        // in the same layout, and each sender folds them into the parents it recorded
+        const std::vector<Layout> &lay = d->t_lay[t];
+        const std::vector<uint64_t> &tmat = d->t_mat[t];
+        std::vector<std::vector<uint64_t>> rbs(d->ranks.size());   // (alive until the stream syncs below)
         for (size_t i = 0; i < d->ranks.size(); i++) {
             SpRankT<K> &R = d->ranks[i];
-            lay[i] = layout_for(d, mat, R.rank);
-            const uint64_t pc = R.send_cap, rc = R.recv_cap;
-            GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
-            if (R.send_cap != pc || !R.sendp) {
-                GM_TRY(grow_to(c, &R.sendp, R.send_cap));
-                if (!self_only(d)) GM_TRY(grow_to(c, &R.reply_in, R.send_cap));
+            const uint64_t nrecv = self_only(d) ? lay[i].nsend : lay[i].nrecv;
+            if (nrecv > R.rout_cap || !R.reply_out) {
+                R.rout_cap = std::max<uint64_t>(nrecv + nrecv / 4, 1 << 16);
+                GM_TRY(grow_to(c, &R.reply_out, R.rout_cap));
             }
-            if (!self_only(d)) GM_TRY(grow_keys(c, &R.recvk, &R.recv_cap, lay[i].nrecv));
-            if (self_only(d)) {   // the replies are written and folded in send order
-                if (R.send_cap != pc || !R.reply_out) GM_TRY(grow_to(c, &R.reply_out, R.send_cap));
-            } else if (R.recv_cap != rc || !R.reply_out) {
-                GM_TRY(grow_to(c, &R.reply_out, R.recv_cap));
+            if (!self_only(d) && (lay[i].nsend > R.rin_cap || !R.reply_in)) {
+                R.rin_cap = std::max<uint64_t>(lay[i].nsend + lay[i].nsend / 4, 1 << 16);
+                GM_TRY(grow_to(c, &R.reply_in, R.rin_cap));
             }
             const uint64_t ni = R.tiers[t].ni;
             if (ni > R.best_cap || !R.best) {
                 R.best_cap = std::max<uint64_t>(ni + ni / 4, 1 << 16);
                 GM_TRY(grow_to(c, &R.best, R.best_cap));
             }
-            GM_HIP(hipMemcpyAsync(R.d_seg, lay[i].seg.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
-            GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
-            run_bucket<D, true, true>(c, d, desc, R, t, R.best);
+            if (ni) GM_HIP(hipMemsetAsync(R.best, 0, ni * 4, c->stream));
+            if (!nrecv) continue;
+            constexpr int SS = D::MAX_SKIP;
+            RessK<K, SS> nx;
+            for (int s = 0; s < S; s++) {
+                const size_t u = t + 1 + s;
+                nx.t[s] = u < R.tiers.size() ? res_ref_of(R.tiers[u]) : typename KT<K>::Res{nullptr, 0};
+            }
+            std::vector<uint64_t> &rb = rbs[i];
+            rb = lay[i].recv_seg;
+            rb.push_back(lay[i].nrecv);
+            GM_HIP(hipMemcpyAsync(R.d_rb, rb.data(), rb.size() * 8, hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(lookup_bins_kernel<D>, dim3(grid_for(nrecv)), dim3(256), 0, c->stream, desc,
+                               R.t_recvk[t], nrecv, R.d_rb, nb, nx, R.reply_out, R.d_err);
         }
-        GM_TRY(exchange(c, d, lay, mat, false));                  // LOOK_UP: keys to owners
-        for (size_t i = 0; i < d->ranks.size(); i++) {            // owners look up the scores
-            SpRankT<K> &R = d->ranks[i];
-            for (int q = 0; q < G; q++)
-                for (int s = 0; s < S; s++) {
-                    const uint64_t n = mat[(size_t)q * nb + R.rank * S + s];
-                    if (!n) continue;
-                    hipLaunchKernelGGL(lookup_kernel<K>, dim3(grid_for(n)), dim3(256), 0, c->stream,
-                                       recv_keys(d, R) + lay[i].recv_seg[q * S + s], n, res_ref_of(R.tiers[t + 1 + s]),
-                                       R.reply_out + lay[i].recv_seg[q * S + s], R.d_err);
-                }
-        }
-        GM_TRY(exchange(c, d, lay, mat, true));                   // RESOLVE: scores back
+        GM_TRY(exchange(c, d, lay, tmat, true));                  // RESOLVE: scores back
         for (size_t i = 0; i < d->ranks.size(); i++) {
             SpRankT<K> &R = d->ranks[i];
             SpTierT<K> &T = R.tiers[t];
             if (lay[i].nsend)
                 hipLaunchKernelGGL(fold_kernel, dim3(grid_for(lay[i].nsend)), dim3(256), 0, c->stream, recv_replies(d, R),
-                                   R.sendp, lay[i].nsend, R.best);
+                                   R.t_sendp[t], lay[i].nsend, R.best);
             if (T.ni)
                 hipLaunchKernelGGL(finalize_kernel<typename KT<K>::Res>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, T.islot, R.best,
                                    T.ni, res_ref_of(T), R.d_err);
         }
         GM_TRY(check_err(c, d));
+        for (auto &R : d->ranks) {   // tier t is resolved: its keys and parents can go
+            dev_free(c, R.t_recvk[t]);
+            dev_free(c, R.t_sendp[t]);
+            R.t_recvk[t] = nullptr;
+            R.t_sendp[t] = nullptr;
+        }
     }
     const double t2 = now_ms();
 
@@ -1132,7 +1198,7 @@ int dist_sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
             for (auto &T : R.tiers) {
                 total += T.count_all;
                 if (T.count)
-                    hipLaunchKernelGGL(res_digest_kernel<D>, dim3(grid_for(T.cap)), dim3(256), 0, c->stream, desc,
+                    hipLaunchKernelGGL(res_digest_kernel<D>, dim3(grid_counted(T.cap)), dim3(256), 0, c->stream, desc,
                                        T.slots, T.cap, acc);
             }
         return GM_OK;
@@ -1193,10 +1259,15 @@ template <class K>
 static void free_ranks(Ctx *c, DistSparseK<K> *d) {
     for (auto &R : d->ranks) {
         for (auto &T : R.tiers) free_tier(c, T);
-        for (void *p : {(void *)R.d_cnt, (void *)R.d_err, (void *)R.d_hist, (void *)R.d_cursor, (void *)R.d_seg,
-                        (void *)R.d_scr, (void *)R.sendk, (void *)R.recvk, (void *)R.sendp,
-                        (void *)R.best, (void *)R.reply_out, (void *)R.reply_in})
-            dev_free(c, p);
+        // every buffer once: after a failed solve recvk / sendp / sendk may still alias a tier's
+        std::vector<void *> ps = {(void *)R.d_cnt, (void *)R.d_err, (void *)R.d_hist, (void *)R.d_cursor,
+                                  (void *)R.d_seg, (void *)R.d_scr, (void *)R.d_rb, (void *)R.sendk, (void *)R.recvk,
+                                  (void *)R.sendp, (void *)R.best, (void *)R.reply_out, (void *)R.reply_in};
+        ps.insert(ps.end(), R.t_recvk.begin(), R.t_recvk.end());
+        ps.insert(ps.end(), R.t_sendp.begin(), R.t_sendp.end());
+        std::sort(ps.begin(), ps.end());
+        ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
+        for (void *p : ps) dev_free(c, p);
     }
 }
 

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void expand_kernel(D d, const uint64_t *__rest
         iwon[i] = won ? 1 : 0;
     }
 #pragma unroll
-    for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
+    for (int s = 0; s < S; s++) block_add(next.t[s].count, fresh[s]);
 }
 
 template <class D>
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void expand_split_kernel(D d, const uint64_t *
         if (sub == 0) iwon[i] = m ? 1 : 0;
     }
 #pragma unroll
-    for (int s = 0; s < S; s++) wave_add(next.t[s].count, fresh[s]);
+    for (int s = 0; s < S; s++) block_add(next.t[s].count, fresh[s]);
 }
 
 template <class D>
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void expand_csr_kernel(D d, const uint64_t *__
             for (uint32_t j = 0; j < m; j++) cslot[at + j] = my[j];
         }
     }
-    wave_add(next.count, fresh);
+    block_add(next.count, fresh);
 }
 
 template <class D>
@@ -371,7 +371,7 @@ static void launch_expand(hipStream_t st, const D &d, const SpTier &T, const Fro
         }
     }
     if (T.ni < split_max())
-        hipLaunchKernelGGL(expand_split_kernel<D>, dim3(grid_for(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys, T.ni,
+        hipLaunchKernelGGL(expand_split_kernel<D>, dim3(grid_counted(T.ni * SPLIT_G)), dim3(256), 0, st, d, T.ikeys, T.ni,
                            nx, T.iwon, err);
     else
         hipLaunchKernelGGL(expand_kernel<D>, dim3(grid_for(T.ni)), dim3(256), 0, st, d, T.skeys ? T.skeys : T.ikeys,
@@ -919,7 +919,7 @@ int sparse_digest(Ctx *c, uint64_t *digest, uint64_t *n) {
     GM_TRY(with_desc(c, [&](const auto &d) {
         for (auto &T : sp->tiers)
             if (T.count)
-                hipLaunchKernelGGL(res_digest_kernel<std::decay_t<decltype(d)>>, dim3(grid_for(T.cap)), dim3(256), 0,
+                hipLaunchKernelGGL(res_digest_kernel<std::decay_t<decltype(d)>>, dim3(grid_counted(T.cap)), dim3(256), 0,
                                    c->stream, d, T.slots, T.cap, sp->d_scratch + 12);
         return GM_OK;
     }));

@@ -317,7 +317,7 @@ __global__ void front_insert_one_wkernel(WFrontRef t, K128 key, uint32_t *err) {
 // turn (Othello 4x4: classify 0.1-0.4 ms per tier, most of the solve).
 constexpr int CROWS = 16;
 constexpr uint64_t CLASSIFY_ROWS_MIN = 1ull << 22;
-template <class D, int ROWS, bool COUNT = true>
+template <class D, int ROWS, bool COUNT = true, bool EDGES = COUNT>
 __global__ __launch_bounds__(256) void classify_kernel(D d, typename KT<key_t<D>>::Slot *__restrict__ slots, uint64_t cap,
                                                        key_t<D> *__restrict__ ikeys, uint32_t *__restrict__ islot,
                                                        unsigned long long *icount, unsigned long long *edges,
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, typename KT<key_t<D>
                 interior = p == UNDECIDED;
                 if (!interior) {
                     slot_set(slots[i], k[r], (uint64_t)score_of_primitive(p));
-                } else if (COUNT) {   // a replay knows its sizes: no edge counts
+                } else if (EDGES) {   // a replay knows its sizes, the sharded path counts bins: no edge counts
                     if constexpr (step_count_t<D>::value) {
                         int dt = 0;
                         const int nk = d.count_children(k[r], &dt);
@@ -399,9 +399,9 @@ __global__ __launch_bounds__(256) void classify_kernel(D d, typename KT<key_t<D>
         __syncthreads();
     }
 #pragma unroll
-    for (int s = 0; s < S; s++) wave_add(edges + s, cnt[s]);
-    wave_add(seen, nseen);
-    wave_add(seen + 1, nall);
+    for (int s = 0; s < S; s++) block_add(edges + s, cnt[s]);
+    block_add(seen, nseen);
+    block_add(seen + 1, nall);
 }
 
 template <class D>
@@ -433,7 +433,7 @@ __global__ void res_digest_kernel(D d, const typename KT<key_t<D>>::Slot *__rest
             d.orbit(key, [&](const K &k) { sum += digest_term(k, rec); });
         }
     }
-    wave_add(acc, sum);
+    block_add(acc, sum);
 }
 
 template <class D>
@@ -515,7 +515,7 @@ struct DedupEstimate {
 // classify a finished tier table: scores in place, interior list, edge counts
 // (scr[0, S) edges by step, scr[9] interior count, scr[10] positions seen)
 // scr: [0, S) edges per tier step, [9] interior count, [10] positions, [11] positions with orbits
-template <class D, bool COUNT = true>
+template <class D, bool COUNT = true, bool EDGES = COUNT>
 inline void launch_classify(hipStream_t st, const D &d, typename KT<key_t<D>>::Slot *slots, uint64_t cap,
                             key_t<D> *ikeys, uint32_t *islot, unsigned long long *scr, uint32_t *err) {
     // a replay's classify (no edge or orbit counts) does less per row: 32 rows
@@ -523,21 +523,26 @@ inline void launch_classify(hipStream_t st, const D &d, typename KT<key_t<D>>::S
     // chunk's barriers and reservation atomic are paid fewer times)
     constexpr int rows = COUNT ? CROWS : 32;
     if (cap >= CLASSIFY_ROWS_MIN)
-        hipLaunchKernelGGL((classify_kernel<D, rows, COUNT>), dim3(grid_for(cap / rows + 1)), dim3(256), 0, st, d,
-                           slots, cap, ikeys, islot, scr + 9, scr, scr + 10, err);
+        hipLaunchKernelGGL((classify_kernel<D, rows, COUNT, EDGES>), dim3(grid_counted(cap / rows + 1)), dim3(256), 0,
+                           st, d, slots, cap, ikeys, islot, scr + 9, scr, scr + 10, err);
     else
-        hipLaunchKernelGGL((classify_kernel<D, 1, COUNT>), dim3(grid_for(cap)), dim3(256), 0, st, d, slots, cap, ikeys,
-                           islot, scr + 9, scr, scr + 10, err);
+        hipLaunchKernelGGL((classify_kernel<D, 1, COUNT, EDGES>), dim3(grid_counted(cap)), dim3(256), 0, st, d, slots,
+                           cap, ikeys, islot, scr + 9, scr, scr + 10, err);
 }
 
+// edges = false (the sharded path, whose bucket pass counts the children per bin): no edge counts
 template <class D>
-inline int classify_tier_table(Ctx *c, const D &d, SpTierT<key_t<D>> &T, unsigned long long *scr, uint32_t *d_err) {
+inline int classify_tier_table(Ctx *c, const D &d, SpTierT<key_t<D>> &T, unsigned long long *scr, uint32_t *d_err,
+                               bool edges = true) {
     const uint64_t n = T.fcount;
     GM_TRY(dev_alloc(c, (void **)&T.ikeys, std::max<uint64_t>(n, 1) * sizeof(key_t<D>)));
     GM_TRY(dev_alloc(c, (void **)&T.islot, std::max<uint64_t>(n, 1) * 4));
     GM_TRY(dev_alloc(c, (void **)&T.iwon, std::max<uint64_t>(n, 1)));
     GM_HIP(hipMemsetAsync(scr, 0, 16 * sizeof(unsigned long long), c->stream));
-    launch_classify(c->stream, d, T.slots, T.cap, T.ikeys, T.islot, scr, d_err);
+    if (edges)
+        launch_classify(c->stream, d, T.slots, T.cap, T.ikeys, T.islot, scr, d_err);
+    else
+        launch_classify<D, true, false>(c->stream, d, T.slots, T.cap, T.ikeys, T.islot, scr, d_err);
     GM_HIP(hipGetLastError());
     return GM_OK;
 }

@@ -4,20 +4,22 @@ item 1's floor; csrc/dist_sparse.hip).
 On a one-GPU box the engine's RCCL transport cannot run with two processes (RCCL refuses two
 ranks on one device), so its cross-process exchange is replayed here with the library's own
 layout (gm_sparse_layout, the function every transport uses) and real data: the reference
-plugin's Othello 4x4 golden table.  Per tier, each rank
+plugin's Othello 4x4 golden table.
 
+Forward, per tier t (LOOK_UP, reference src/new_process.py:156-160), each rank
   1. generates its interior positions' children with the descriptor's host twin
-     (gm_expand_host), folds the primitive ones locally and bins the others by
-     (owner = (mix64(key) >> 32) % world, tier step) -- the engine's bucket_kernel;
+     (gm_expand_host) and bins them by (owner = (mix64(key) >> 32) % world, tier step) -- the
+     engine's bucket_kernel, which also records each key's parent;
   2. all-gathers the per-bin counts (ncclAllGather) and takes its layout;
   3. sends each owner its segment and receives its own, with the offsets the RCCL branch
      passes to ncclSend / ncclRecv (send_off -> recv_off; one isend / irecv per peer, as one
-     ncclGroup) -- LOOK_UP, reference src/new_process.py:156-160;
-  4. as the owner, checks every received key is its own and in the tier the bin says, and
-     answers with its score from the golden table (lookup_kernel);
-  5. sends the scores back (recv_off -> send_off) -- RESOLVE, :179-187 -- folds them per
-     parent (fold_kernel) and turns the best into the parent's record (finalize_kernel),
-     which must equal the golden record of the parent.
+     ncclGroup), and keeps -- as the owner -- the keys it received, checking each is its own
+     and in the tier its bin says (insert_bins_kernel inserts them).
+Backward, tiers deepest first (RESOLVE, :179-187): each owner answers the keys it kept for the
+tier with their scores from the golden table (lookup_bins_kernel), in the same layout, sends
+them back (recv_off -> send_off), and each sender folds them into the parents it recorded
+(fold_kernel) and turns the best into the parent's record (finalize_kernel), which must equal
+the golden record of the parent.  No key moves in the backward pass.
 """
 import os
 
@@ -49,10 +51,6 @@ def score_of_record(r):
     return 0x4000 | rem if v == WIN else (0x8000 | (0x3FFF - rem) if v == TIE else 0xC000 | (0x3FFF - rem))
 
 
-def score_of_primitive(v):
-    return 0x4000 if v == WIN else (0xFFFF if v == LOSS else 0xBFFF)
-
-
 def parent_score(b):
     low, cls = b & 0x3FFF, b >> 14
     return 0x8000 - low if cls == 3 else (b - 1 if cls == 2 else 0xFFFE - low)
@@ -76,18 +74,33 @@ def _rank_main(rank, world, phase):
     hd.close()
     mine = [k for k in table if owner(k, world) == rank]
     tiers = sorted({info[k][2] for k in table})
+
+    def exchange(src, soff, dst, doff):
+        reqs = []
+        for p in range(world):
+            a, b, x, y = int(soff[p]), int(soff[p + 1]), int(doff[p]), int(doff[p + 1])
+            if p == rank:
+                dst[x:y] = src[a:b]
+                continue
+            if b > a:
+                out = src[a:b].clone()
+                reqs.append((dist.isend(out, p), out, None, None))
+            if y > x:
+                buf = torch.zeros(y - x, dtype=src.dtype)
+                reqs.append((dist.irecv(buf, p), buf, x, y))
+        for work, buf, x, y in reqs:
+            work.wait()
+            if x is not None:
+                dst[x:y] = buf
+
+    kept = {}   # tier -> (parents, sendp, layout, keys received as the owner)
     checked = sent = 0
-    for t in tiers:
-        phase("tier %d" % t)
+    for t in tiers:                                  # forward: LOOK_UP
+        phase("forward tier %d" % t)
         parents = [k for k in mine if info[k][2] == t and info[k][0] == UNDECIDED]
-        best = [0] * len(parents)
         bins = [[] for _ in range(world * S)]
         for i, k in enumerate(parents):
             for c in info[k][1]:
-                p = info[c][0]
-                if p != UNDECIDED:                       # primitive children are folded locally
-                    best[i] = max(best[i], score_of_primitive(p))
-                    continue
                 dt = info[c][2] - t
                 assert 1 <= dt <= S
                 bins[owner(c, world) * S + dt - 1].append((c, i))
@@ -95,7 +108,8 @@ def _rank_main(rank, world, phase):
         allr = [torch.zeros_like(row) for _ in range(world)]
         dist.all_gather(allr, row)
         mat = torch.stack(allr).numpy().astype(np.uint64)
-        seg, send_off, recv_off, recv_seg = (a.astype(np.int64) for a in _lib.sparse_layout(world, S, mat, rank))
+        lay = [a.astype(np.int64) for a in _lib.sparse_layout(world, S, mat, rank)]
+        seg, send_off, recv_off, recv_seg = lay
         sendk = torch.zeros(int(send_off[-1]), dtype=torch.int64)
         sendp = np.zeros(int(send_off[-1]), dtype=np.int64)
         for b, lst in enumerate(bins):
@@ -103,42 +117,27 @@ def _rank_main(rank, world, phase):
                 sendk[seg[b] + j] = c
                 sendp[seg[b] + j] = i
         recvk = torch.zeros(int(recv_off[-1]), dtype=torch.int64)
-
-        def exchange(src, soff, dst, doff):
-            reqs = []
-            for p in range(world):
-                a, b, x, y = int(soff[p]), int(soff[p + 1]), int(doff[p]), int(doff[p + 1])
-                if p == rank:
-                    dst[x:y] = src[a:b]
-                    continue
-                if b > a:
-                    out = src[a:b].clone()
-                    reqs.append((dist.isend(out, p), out, None, None))
-                if y > x:
-                    buf = torch.zeros(y - x, dtype=src.dtype)
-                    reqs.append((dist.irecv(buf, p), buf, x, y))
-            for work, buf, x, y in reqs:
-                work.wait()
-                if x is not None:
-                    dst[x:y] = buf
-        exchange(sendk, send_off, recvk, recv_off)       # LOOK_UP
-        reply = torch.zeros(len(recvk), dtype=torch.int64)
+        exchange(sendk, send_off, recvk, recv_off)
         for q in range(world):
             for s in range(S):
                 a = int(recv_seg[q * S + s])
-                n = int(mat[q, rank * S + s])
-                for j in range(a, a + n):
+                for j in range(a, a + int(mat[q, rank * S + s])):
                     c = int(recvk[j])
                     assert owner(c, world) == rank and info[c][2] == t + 1 + s, "a key reached the wrong rank/tier"
-                    reply[j] = score_of_record(table[c])
-        reply_in = torch.zeros(len(sendk), dtype=torch.int64)
-        exchange(reply, recv_off, reply_in, send_off)    # RESOLVE
-        for j in range(len(sendk)):
+        kept[t] = (parents, sendp, (send_off, recv_off), recvk)
+        sent += int(send_off[-1]) - int(send_off[rank + 1] - send_off[rank])
+    for t in reversed(tiers):                        # backward: RESOLVE only
+        phase("backward tier %d" % t)
+        parents, sendp, (send_off, recv_off), recvk = kept.pop(t)
+        reply = torch.tensor([score_of_record(table[int(c)]) for c in recvk.tolist()], dtype=torch.int64)
+        reply_in = torch.zeros(int(send_off[-1]), dtype=torch.int64)
+        exchange(reply, recv_off, reply_in, send_off)
+        best = [0] * len(parents)
+        for j in range(len(reply_in)):
             best[sendp[j]] = max(best[sendp[j]], int(reply_in[j]))
         for i, k in enumerate(parents):
             assert record_of_score(parent_score(best[i])) == table[k], "parent %#x" % k
             checked += 1
-        sent += int(send_off[-1]) - int(send_off[rank + 1] - send_off[rank])
     dist.barrier()
     dist.destroy_process_group()
     return {"rank": rank, "checked": checked, "sent": sent}
