@@ -213,15 +213,17 @@ struct SpRankT {
     unsigned long long *d_seg = nullptr;     // G*S bins
     unsigned long long *d_scr = nullptr;     // [0,8) edges by step, [9] interior count, [10] seen, [12] cursor
     uint64_t *d_rb = nullptr;                // G*S + 1 receive-segment bounds (insert_bins / lookup_bins)
-    K *sendk = nullptr, *recvk = nullptr;    // recvk / sendp: the current tier's (t_recvk / t_sendp)
-    uint64_t send_cap = 0, best_cap = 0, rout_cap = 0, rin_cap = 0;
-    uint32_t *sendp = nullptr, *best = nullptr;
+    K *sendk = nullptr, *recvk = nullptr;    // recvk: the current tier's (kept[t].recvk)
+    uint64_t send_cap = 0, rout_cap = 0, rin_cap = 0;
     uint16_t *reply_out = nullptr, *reply_in = nullptr;
-    // per tier, from the forward exchange to the backward one: the keys this rank received as
-    // their owner (one rank in one context: the keys it sent itself) and, per key it sent, its
-    // parent's interior index
-    std::vector<K *> t_recvk;
-    std::vector<uint32_t *> t_sendp;
+    // per tier, from the forward exchange to the backward one
+    struct Kept {
+        K *recvk = nullptr;          // the keys this rank received as their owner (one rank, one context: sent)
+        uint8_t *lp = nullptr;       // per key sent: its parent's index within its chunk of 256 parents
+        uint64_t *cbase = nullptr;   // per (chunk, bin): where the chunk's keys for the bin start, send order
+        uint32_t *ccnt = nullptr;    // ... and how many there are
+    };
+    std::vector<Kept> kept;
 };
 
 // the key-independent part of a sharded solve (c->dist_sp); DistSparseK<K> adds the ranks
@@ -254,15 +256,16 @@ constexpr int MAXBINS = 64 * 3;
 
 // Children of the interior positions of a tier, bucketed by bin = owner * S + (step - 1).
 // COUNT: an LDS histogram over all of the workgroup's chunks, added to hist once at the end
-// (atomics on one line serialise: block_add).  SCATTER: per chunk the workgroup reserves a
-// range per bin, and a second visit writes the keys and each key's parent (its interior
-// index, kept for the backward fold).
+// (atomics on one line serialise: block_add).  SCATTER: per chunk of 256 parents the workgroup
+// reserves a range per bin, and a second visit writes the keys; kept for the backward fold are
+// each key's parent within its chunk (out_lp, one byte) and each (chunk, bin) range.
 template <class D, bool SCATTER>
 __global__ __launch_bounds__(256) void bucket_kernel(D d, const key_t<D> *__restrict__ ikeys, uint64_t n, int G,
                                                      unsigned long long *hist,
                                                      const unsigned long long *__restrict__ seg,
                                                      unsigned long long *cursor, key_t<D> *out_keys,
-                                                     uint32_t *out_parent, uint32_t *err) {
+                                                     uint8_t *out_lp, uint64_t *cbase, uint32_t *ccnt,
+                                                     uint32_t *err) {
     constexpr int S = D::MAX_SKIP;
     using K = key_t<D>;
     __shared__ unsigned int lh[MAXBINS], lh2[MAXBINS];
@@ -291,13 +294,17 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const key_t<D> *__rest
         walk([&](const K &, int bin) { atomicAdd(&lh[bin], 1u); });
         __syncthreads();
         if (SCATTER) {
-            for (int b = threadIdx.x; b < nb; b += blockDim.x)
+            const uint64_t k = base / 256;
+            for (int b = threadIdx.x; b < nb; b += blockDim.x) {
                 lbase[b] = lh[b] ? seg[b] + atomicAdd(&cursor[b], (unsigned long long)lh[b]) : 0ull;
+                cbase[k * nb + b] = lbase[b];
+                ccnt[k * nb + b] = lh[b];
+            }
             __syncthreads();
             walk([&](const K &c, int bin) {
                 const unsigned long long at = lbase[bin] + atomicAdd(&lh2[bin], 1u);
                 out_keys[at] = c;
-                out_parent[at] = (uint32_t)i;
+                out_lp[at] = (uint8_t)threadIdx.x;
             });
         }
         __syncthreads();
@@ -307,22 +314,36 @@ __global__ __launch_bounds__(256) void bucket_kernel(D d, const key_t<D> *__rest
             if (lh[b]) atomicAdd(&hist[b], (unsigned long long)lh[b]);
 }
 
-__global__ void fold_kernel(const uint16_t *__restrict__ reply, const uint32_t *__restrict__ parent, uint64_t n,
-                            uint32_t *best) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        atomicMax(&best[parent[i]], (uint32_t)reply[i]);
-}
-
+// Backward fold and finalize of a tier in one pass, one workgroup per chunk of 256 parents: the
+// scores that came back for the chunk's keys (contiguous per bin, in send order) meet in LDS,
+// and each parent's best child score becomes its own (gm_common.hpp parent_score).
 template <class R>
-__global__ void finalize_kernel(const uint32_t *__restrict__ islot, const uint32_t *__restrict__ best, uint64_t n,
-                                R self, uint32_t *err) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t b = best[i];
-        if (!b) atomicOr(err, DEV_ERR_MISSING_CHILD);
-        if (score_overflows(b)) atomicOr(err, DEV_ERR_OVERFLOW);
-        self.s[islot[i]].score = parent_score(b);
+__global__ __launch_bounds__(256) void fold_finalize_kernel(const uint16_t *__restrict__ reply,
+                                                            const uint8_t *__restrict__ lp,
+                                                            const uint64_t *__restrict__ cbase,
+                                                            const uint32_t *__restrict__ ccnt, int nb,
+                                                            const uint32_t *__restrict__ islot, uint64_t n, R self,
+                                                            uint32_t *err) {
+    __shared__ uint32_t best[256];
+    const uint64_t nchunks = (n + 255) / 256;
+    for (uint64_t k = blockIdx.x; k < nchunks; k += gridDim.x) {
+        best[threadIdx.x] = 0;
+        __syncthreads();
+        for (int b = 0; b < nb; b++) {
+            const uint64_t base = cbase[k * nb + b];
+            const uint32_t cnt = ccnt[k * nb + b];
+            for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x)
+                atomicMax(&best[lp[base + j]], (uint32_t)reply[base + j]);
+        }
+        __syncthreads();
+        const uint64_t i = k * 256 + threadIdx.x;
+        if (i < n) {
+            const uint32_t v = best[threadIdx.x];
+            if (!v) atomicOr(err, DEV_ERR_MISSING_CHILD);
+            if (score_overflows(v)) atomicOr(err, DEV_ERR_OVERFLOW);
+            self.s[islot[i]].score = parent_score(v);
+        }
+        __syncthreads();
     }
 }
 
@@ -542,8 +563,10 @@ template <class D, bool SCATTER>
 static void run_bucket(Ctx *c, DistSparse *d, const D &desc, SpRankT<key_t<D>> &R, size_t t) {
     SpTierT<key_t<D>> &T = R.tiers[t];
     if (!T.ni) return;
+    typename SpRankT<key_t<D>>::Kept none{};
+    const auto &kp = SCATTER ? R.kept[t] : none;
     hipLaunchKernelGGL((bucket_kernel<D, SCATTER>), dim3(grid_counted(T.ni)), dim3(256), 0, c->stream, desc, T.ikeys,
-                       T.ni, d->G, R.d_hist, R.d_seg, R.d_cursor, R.sendk, R.sendp, R.d_err);
+                       T.ni, d->G, R.d_hist, R.d_seg, R.d_cursor, R.sendk, kp.lp, kp.cbase, kp.ccnt, R.d_err);
 }
 
 // counts[r][dest*S+dt] for all ranks -> host matrix (G x G*S)
@@ -872,19 +895,19 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                 SpRankT<K> &R = d->ranks[i];
                 lay[i] = layout_for(d, mat, R.rank);
                 d->edges += lay[i].nsend;
-                if (R.t_recvk.size() < need) {
-                    R.t_recvk.resize(need, nullptr);
-                    R.t_sendp.resize(need, nullptr);
-                }
-                GM_TRY(dev_alloc(c, (void **)&R.t_sendp[t], std::max<uint64_t>(lay[i].nsend, 1) * 4));
-                R.sendp = R.t_sendp[t];
+                if (R.kept.size() < need) R.kept.resize(need);
+                auto &kp = R.kept[t];
+                const uint64_t nch = std::max<uint64_t>((R.tiers[t].ni + 255) / 256, 1);
+                GM_TRY(dev_alloc(c, (void **)&kp.lp, std::max<uint64_t>(lay[i].nsend, 1)));
+                GM_TRY(dev_alloc(c, (void **)&kp.cbase, nch * nb * 8));
+                GM_TRY(dev_alloc(c, (void **)&kp.ccnt, nch * nb * 4));
                 if (self_only(d)) {   // one rank, one context: what it sends is what it receives, kept
-                    GM_TRY(dev_alloc(c, (void **)&R.t_recvk[t], std::max<uint64_t>(lay[i].nsend, 1) * sizeof(K)));
-                    R.sendk = R.t_recvk[t];
+                    GM_TRY(dev_alloc(c, (void **)&kp.recvk, std::max<uint64_t>(lay[i].nsend, 1) * sizeof(K)));
+                    R.sendk = kp.recvk;
                 } else {
                     GM_TRY(grow_keys(c, &R.sendk, &R.send_cap, lay[i].nsend));
-                    GM_TRY(dev_alloc(c, (void **)&R.t_recvk[t], std::max<uint64_t>(lay[i].nrecv, 1) * sizeof(K)));
-                    R.recvk = R.t_recvk[t];
+                    GM_TRY(dev_alloc(c, (void **)&kp.recvk, std::max<uint64_t>(lay[i].nrecv, 1) * sizeof(K)));
+                    R.recvk = kp.recvk;
                 }
                 GM_HIP(hipMemcpyAsync(R.d_seg, lay[i].seg.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
                 GM_HIP(hipMemsetAsync(R.d_cursor, 0, nb * 8, c->stream));
@@ -928,9 +951,8 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                     GM_HIP(hipMemsetAsync(R.d_err, 0, 4, c->stream));
                     d->est.missed();
                 }
-                // the tier's buffers now belong to t_recvk / t_sendp
+                // the tier's buffers now belong to kept[t]
                 R.recvk = nullptr;
-                R.sendp = nullptr;
                 if (self_only(d)) R.sendk = nullptr;
             }
         }
@@ -1003,12 +1025,6 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                 R.rin_cap = std::max<uint64_t>(lay[i].nsend + lay[i].nsend / 4, 1 << 16);
                 GM_TRY(grow_to(c, &R.reply_in, R.rin_cap));
             }
-            const uint64_t ni = R.tiers[t].ni;
-            if (ni > R.best_cap || !R.best) {
-                R.best_cap = std::max<uint64_t>(ni + ni / 4, 1 << 16);
-                GM_TRY(grow_to(c, &R.best, R.best_cap));
-            }
-            if (ni) GM_HIP(hipMemsetAsync(R.best, 0, ni * 4, c->stream));
             if (!nrecv) continue;
             constexpr int SS = D::MAX_SKIP;
             RessK<K, SS> nx;
@@ -1021,25 +1037,23 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
             rb.push_back(lay[i].nrecv);
             GM_HIP(hipMemcpyAsync(R.d_rb, rb.data(), rb.size() * 8, hipMemcpyHostToDevice, c->stream));
             hipLaunchKernelGGL(lookup_bins_kernel<D>, dim3(grid_for(nrecv)), dim3(256), 0, c->stream, desc,
-                               R.t_recvk[t], nrecv, R.d_rb, nb, nx, R.reply_out, R.d_err);
+                               R.kept[t].recvk, nrecv, R.d_rb, nb, nx, R.reply_out, R.d_err);
         }
         GM_TRY(exchange(c, d, lay, tmat, true));                  // RESOLVE: scores back
         for (size_t i = 0; i < d->ranks.size(); i++) {
             SpRankT<K> &R = d->ranks[i];
             SpTierT<K> &T = R.tiers[t];
-            if (lay[i].nsend)
-                hipLaunchKernelGGL(fold_kernel, dim3(grid_for(lay[i].nsend)), dim3(256), 0, c->stream, recv_replies(d, R),
-                                   R.t_sendp[t], lay[i].nsend, R.best);
+            const auto &kp = R.kept[t];
             if (T.ni)
-                hipLaunchKernelGGL(finalize_kernel<typename KT<K>::Res>, dim3(grid_for(T.ni)), dim3(256), 0, c->stream, T.islot, R.best,
-                                   T.ni, res_ref_of(T), R.d_err);
+                hipLaunchKernelGGL(fold_finalize_kernel<typename KT<K>::Res>, dim3(grid_for(T.ni)), dim3(256), 0,
+                                   c->stream, recv_replies(d, R), kp.lp, kp.cbase, kp.ccnt, nb, T.islot, T.ni,
+                                   res_ref_of(T), R.d_err);
         }
         GM_TRY(check_err(c, d));
-        for (auto &R : d->ranks) {   // tier t is resolved: its keys and parents can go
-            dev_free(c, R.t_recvk[t]);
-            dev_free(c, R.t_sendp[t]);
-            R.t_recvk[t] = nullptr;
-            R.t_sendp[t] = nullptr;
+        for (auto &R : d->ranks) {   // tier t is resolved: what the forward kept for it can go
+            auto &kp = R.kept[t];
+            for (void *p : {(void *)kp.recvk, (void *)kp.lp, (void *)kp.cbase, (void *)kp.ccnt}) dev_free(c, p);
+            kp = typename SpRankT<K>::Kept{};
         }
     }
     const double t2 = now_ms();
@@ -1259,12 +1273,12 @@ template <class K>
 static void free_ranks(Ctx *c, DistSparseK<K> *d) {
     for (auto &R : d->ranks) {
         for (auto &T : R.tiers) free_tier(c, T);
-        // every buffer once: after a failed solve recvk / sendp / sendk may still alias a tier's
+        // every buffer once: after a failed solve recvk / sendk may still alias a tier's
         std::vector<void *> ps = {(void *)R.d_cnt, (void *)R.d_err, (void *)R.d_hist, (void *)R.d_cursor,
                                   (void *)R.d_seg, (void *)R.d_scr, (void *)R.d_rb, (void *)R.sendk, (void *)R.recvk,
-                                  (void *)R.sendp, (void *)R.best, (void *)R.reply_out, (void *)R.reply_in};
-        ps.insert(ps.end(), R.t_recvk.begin(), R.t_recvk.end());
-        ps.insert(ps.end(), R.t_sendp.begin(), R.t_sendp.end());
+                                  (void *)R.reply_out, (void *)R.reply_in};
+        for (auto &kp : R.kept)
+            for (void *p : {(void *)kp.recvk, (void *)kp.lp, (void *)kp.cbase, (void *)kp.ccnt}) ps.push_back(p);
         std::sort(ps.begin(), ps.end());
         ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
         for (void *p : ps) dev_free(c, p);
