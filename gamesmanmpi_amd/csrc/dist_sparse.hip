@@ -15,11 +15,12 @@
 //                    tables (deduplicating on insert).
 // backward, tier t:  the owners look up again the keys they received in the
 //                    forward exchange of tier t (kept per tier, as each sender
-//                    keeps the parent index of every key it sent) and answer with
-//                    the u16 scores in the same order (RESOLVE); the parent folds
-//                    them with atomicMax and turns the best score into its own
-//                    (gm_common.hpp).  So the backward pass makes no move and
-//                    sends no key: the LOOK_UP of a child happened once, forward.
+//                    keeps the parent of every key it sent) and answer with the
+//                    u16 scores in the same order (RESOLVE); per chunk of 256
+//                    parents the scores meet in LDS (max) and each best becomes
+//                    its parent's score (gm_common.hpp).  So the backward pass
+//                    makes no move and sends no key: the LOOK_UP of a child
+//                    happened once, forward.
 //
 // Exchanges use one of three transports:
 //   RCCL (GM_OPT_SPARSE_TRANSPORT 0, one process per GPU): counts all-gathered, keys and
