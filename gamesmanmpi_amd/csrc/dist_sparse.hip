@@ -36,6 +36,7 @@
 // lay(r).send_off[p], p's receive segment from r at lay(p).recv_off[r].
 #include "sparse_tables.hpp"
 
+#include <array>
 #include <cstring>
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -213,7 +214,6 @@ struct SpRankT {
     unsigned long long *d_cursor = nullptr;  // G*S bins
     unsigned long long *d_seg = nullptr;     // G*S bins
     unsigned long long *d_scr = nullptr;     // [0,8) edges by step, [9] interior count, [10] seen, [12] cursor
-    uint64_t *d_rb = nullptr;                // G*S + 1 receive-segment bounds (insert_bins / lookup_bins)
     K *sendk = nullptr, *recvk = nullptr;    // recvk: the current tier's (kept[t].recvk)
     uint64_t send_cap = 0, rout_cap = 0, rin_cap = 0;
     uint16_t *reply_out = nullptr, *reply_in = nullptr;
@@ -223,6 +223,7 @@ struct SpRankT {
         uint8_t *lp = nullptr;       // per key sent: its parent's index within its chunk of 256 parents
         uint64_t *cbase = nullptr;   // per (chunk, bin): where the chunk's keys for the bin start, send order
         uint32_t *ccnt = nullptr;    // ... and how many there are
+        uint64_t *rb = nullptr;      // the receive segments' bounds (insert_bins / lookup_bins)
     };
     std::vector<Kept> kept;
 };
@@ -570,38 +571,55 @@ static void run_bucket(Ctx *c, DistSparse *d, const D &desc, SpRankT<key_t<D>> &
                        T.ni, d->G, R.d_hist, R.d_seg, R.d_cursor, R.sendk, kp.lp, kp.cbase, kp.ccnt, R.d_err);
 }
 
+// every local rank's device error word: enqueue the reads (read_errs), then after the stream
+// synchronises turn the first set one into a status (errs_rc) -- one sync for all the ranks
+template <class K>
+static int read_errs(Ctx *c, DistSparseK<K> *d, std::vector<uint32_t> &errs) {
+    errs.assign(d->ranks.size(), 0);
+    for (size_t i = 0; i < d->ranks.size(); i++)
+        GM_HIP(hipMemcpyAsync(&errs[i], d->ranks[i].d_err, 4, hipMemcpyDeviceToHost, c->stream));
+    return GM_OK;
+}
+static int errs_rc(const std::vector<uint32_t> &errs) {
+    for (uint32_t e : errs)
+        if (e) return dev_error_to_gm(e);
+    return GM_OK;
+}
 // counts[r][dest*S+dt] for all ranks -> host matrix (G x G*S)
+// (the local ranks' device errors are read in the same synchronisation)
 template <class K>
 static int gather_counts(Ctx *c, DistSparseK<K> *d, std::vector<uint64_t> &mat) {
     const int nb = d->G * d->S;
     mat.assign((size_t)d->G * nb, 0);
+    std::vector<uint32_t> errs;
     if (d->loopback) {
         for (auto &R : d->ranks)
             GM_HIP(hipMemcpyAsync(&mat[(size_t)R.rank * nb], R.d_hist, nb * 8, hipMemcpyDeviceToHost, c->stream));
+        GM_TRY(read_errs(c, d, errs));
         GM_HIP(hipStreamSynchronize(c->stream));
-        return GM_OK;
+        return errs_rc(errs);
     }
     if (d->ipc) {
         std::vector<uint64_t> row(nb);
         GM_HIP(hipMemcpyAsync(row.data(), d->ranks[0].d_hist, nb * 8, hipMemcpyDeviceToHost, c->stream));
+        GM_TRY(read_errs(c, d, errs));
         GM_HIP(hipStreamSynchronize(c->stream));
+        GM_TRY(errs_rc(errs));
         return sp_ipc_allgather(d->X, row.data(), nb, mat.data());
     }
     GM_NCCL(ncclAllGather(d->ranks[0].d_hist, d->d_mat, nb, ncclUint64, c->comm, c->stream));
     GM_HIP(hipMemcpyAsync(mat.data(), d->d_mat, mat.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    GM_TRY(read_errs(c, d, errs));
     GM_HIP(hipStreamSynchronize(c->stream));
-    return GM_OK;
+    return errs_rc(errs);
 }
 
 template <class K>
 static int check_err(Ctx *c, DistSparseK<K> *d) {
-    for (auto &R : d->ranks) {
-        uint32_t e;
-        GM_HIP(hipMemcpyAsync(&e, R.d_err, 4, hipMemcpyDeviceToHost, c->stream));
-        GM_HIP(hipStreamSynchronize(c->stream));
-        if (e) return dev_error_to_gm(e);
-    }
-    return GM_OK;
+    std::vector<uint32_t> errs;
+    GM_TRY(read_errs(c, d, errs));
+    GM_HIP(hipStreamSynchronize(c->stream));
+    return errs_rc(errs);
 }
 
 
@@ -752,23 +770,32 @@ static int ensure_cnt(Ctx *c, DistSparseK<K> *d, size_t ntiers) {
 }
 
 // classify tier t of every rank (scores in place + interior list)
+// (every rank's classify enqueued, then one synchronisation reads the counters and the errors)
 template <class D>
 static int classify_tier(Ctx *c, DistSparseK<key_t<D>> *d, const D &desc, size_t t) {
-    for (auto &R : d->ranks) {
+    std::vector<std::array<unsigned long long, 12>> sc(d->ranks.size());
+    for (size_t i = 0; i < d->ranks.size(); i++) {
+        SpRankT<key_t<D>> &R = d->ranks[i];
+        if (!R.tiers[t].fcount) continue;
+        GM_TRY(classify_tier_table(c, desc, R.tiers[t], R.d_scr, R.d_err, self_fused(d)));
+        GM_HIP(hipMemcpyAsync(sc[i].data(), R.d_scr, sizeof sc[i], hipMemcpyDeviceToHost, c->stream));
+    }
+    std::vector<uint32_t> errs;
+    GM_TRY(read_errs(c, d, errs));
+    GM_HIP(hipStreamSynchronize(c->stream));
+    GM_TRY(errs_rc(errs));
+    for (size_t i = 0; i < d->ranks.size(); i++) {
+        SpRankT<key_t<D>> &R = d->ranks[i];
         SpTierT<key_t<D>> &T = R.tiers[t];
         const uint64_t n = T.fcount;
         if (!n) continue;
-        GM_TRY(classify_tier_table(c, desc, T, R.d_scr, R.d_err, self_fused(d)));
-        unsigned long long sc[12];
-        GM_HIP(hipMemcpyAsync(sc, R.d_scr, sizeof sc, hipMemcpyDeviceToHost, c->stream));
-        GM_HIP(hipStreamSynchronize(c->stream));
-        if (sc[10] != n) {
-            set_error("rank %d tier %zu: found %llu of %llu keys", R.rank, t, sc[10], (unsigned long long)n);
+        if (sc[i][10] != n) {
+            set_error("rank %d tier %zu: found %llu of %llu keys", R.rank, t, sc[i][10], (unsigned long long)n);
             return GM_E_STATE;
         }
         T.count = n;
-        T.count_all = sc[11];
-        T.ni = sc[9];
+        T.count_all = sc[i][11];
+        T.ni = sc[i][9];
     }
     return GM_OK;
 }
@@ -843,7 +870,6 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
         GM_TRY(dev_alloc(c, (void **)&R.d_cursor, nb * 8));
         GM_TRY(dev_alloc(c, (void **)&R.d_seg, nb * 8));
         GM_TRY(dev_alloc(c, (void **)&R.d_scr, 16 * 8));
-        GM_TRY(dev_alloc(c, (void **)&R.d_rb, (nb + 1) * 8));
         R.tiers.resize(1);
     }
     GM_TRY(dev_alloc(c, (void **)&d->d_mat, (size_t)G * nb * 8));
@@ -873,8 +899,9 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
         for (auto &R : d->ranks)
             if (R.tiers.size() < need) R.tiers.resize(need);
         GM_TRY(classify_tier(c, d, desc, t));
-        GM_TRY(check_err(c, d));
         uint64_t offered = 0, before = 0;
+        std::vector<std::vector<uint64_t>> hcs(d->ranks.size(), std::vector<uint64_t>(need, 0));
+        bool counted = false;   // hcs read already (the bucket path reads them with its errors)
         if (self_fused(d)) {
             GM_TRY(self_expand(c, d, desc, t, offered, before));
         } else {
@@ -884,7 +911,6 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                 run_bucket<D, false>(c, d, desc, R, t);
             }
             GM_TRY(gather_counts(c, d, mat));
-            GM_TRY(check_err(c, d));
             if (d->t_lay.size() < need) {
                 d->t_lay.resize(need);
                 d->t_mat.resize(need);
@@ -916,56 +942,87 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
             }
             GM_TRY(exchange(c, d, lay, mat, false));
             // owners insert into their tier tables, sized for load <= 0.7 of the predicted
-            // distinct keys; a misprediction re-runs the (idempotent) inserts once
-            for (size_t i = 0; i < d->ranks.size(); i++) {
+            // distinct keys; a misprediction re-runs the (idempotent) inserts once.  Every rank's
+            // inserts are enqueued, then one synchronisation reads the errors and the frontier
+            // counts of all of them.
+            const size_t NR = d->ranks.size();
+            std::vector<std::vector<uint64_t>> in(NR, std::vector<uint64_t>(S, 0)), rbs(NR);
+            for (size_t i = 0; i < NR; i++) {
                 SpRankT<K> &R = d->ranks[i];
-                std::vector<uint64_t> in(S, 0);
                 for (int s = 0; s < S; s++) {
-                    for (int q = 0; q < G; q++) in[s] += mat[(size_t)q * nb + R.rank * S + s];
-                    offered += in[s];
+                    for (int q = 0; q < G; q++) in[i][s] += mat[(size_t)q * nb + R.rank * S + s];
+                    offered += in[i][s];
                     before += R.tiers[t + 1 + s].fcount;
                 }
-                std::vector<uint64_t> rb(lay[i].recv_seg);
-                rb.push_back(lay[i].nrecv);
-                GM_HIP(hipMemcpyAsync(R.d_rb, rb.data(), rb.size() * 8, hipMemcpyHostToDevice, c->stream));
-                for (int attempt = 0; attempt < 2; attempt++) {
+                rbs[i] = lay[i].recv_seg;
+                rbs[i].push_back(lay[i].nrecv);
+                GM_TRY(dev_alloc(c, (void **)&R.kept[t].rb, (nb + 1) * 8));
+                GM_HIP(hipMemcpyAsync(R.kept[t].rb, rbs[i].data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
+            }
+            std::vector<char> todo(NR, 1);
+            for (int attempt = 0; attempt < 2; attempt++) {
+                for (size_t i = 0; i < NR; i++) {
+                    if (!todo[i]) continue;
+                    SpRankT<K> &R = d->ranks[i];
                     constexpr int SS = D::MAX_SKIP;
                     FrontsK<K, SS> nx;
                     for (int s = 0; s < S; s++) {
                         const size_t u = t + 1 + s;
                         SpTierT<K> &U = R.tiers[u];
-                        const uint64_t needc = table_cap_for(U.fcount + (attempt ? in[s] : d->est.distinct(in[s])));
-                        if (in[s] && U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
+                        const uint64_t nd = attempt ? in[i][s] : d->est.distinct(in[i][s]);
+                        const uint64_t needc = table_cap_for(U.fcount + nd);
+                        if (in[i][s] && U.cap < needc) GM_TRY(tier_grow(c, U, needc, R.d_err));
                         nx.t[s] = fref(R, u);
                     }
                     if (lay[i].nrecv)
                         hipLaunchKernelGGL((insert_bins_kernel<K, SS>), dim3(grid_for(lay[i].nrecv)), dim3(256), 0,
-                                           c->stream, recv_keys(d, R), lay[i].nrecv, R.d_rb, nb, nx, R.d_err);
+                                           c->stream, R.kept[t].recvk, lay[i].nrecv, R.kept[t].rb, nb, nx, R.d_err);
                     GM_HIP(hipGetLastError());
-                    uint32_t e;
-                    GM_HIP(hipMemcpyAsync(&e, R.d_err, 4, hipMemcpyDeviceToHost, c->stream));
-                    GM_HIP(hipStreamSynchronize(c->stream));
-                    if (e != DEV_ERR_TABLE_FULL || attempt) break;
-                    if (trace_on())
-                        fprintf(stderr, "[gm] rank %d tier %zu: tables full at ratio %.3f, re-running\n", R.rank, t,
-                                d->est.ratio);
-                    GM_HIP(hipMemsetAsync(R.d_err, 0, 4, c->stream));
-                    d->est.missed();
                 }
-                // the tier's buffers now belong to kept[t]
+                std::vector<uint32_t> errs;
+                GM_TRY(read_errs(c, d, errs));
+                for (size_t i = 0; i < NR; i++)
+                    GM_HIP(hipMemcpyAsync(hcs[i].data(), d->ranks[i].d_cnt, need * 8, hipMemcpyDeviceToHost,
+                                          c->stream));
+                GM_HIP(hipStreamSynchronize(c->stream));
+                bool again = false;
+                for (size_t i = 0; i < NR; i++) {
+                    if (!todo[i]) continue;
+                    todo[i] = 0;
+                    if (errs[i] == DEV_ERR_TABLE_FULL && !attempt) {
+                        if (trace_on())
+                            fprintf(stderr, "[gm] rank %d tier %zu: tables full at ratio %.3f, re-running\n",
+                                    d->ranks[i].rank, t, d->est.ratio);
+                        GM_HIP(hipMemsetAsync(d->ranks[i].d_err, 0, 4, c->stream));
+                        d->est.missed();
+                        todo[i] = 1;
+                        again = true;
+                    }
+                }
+                if (!again) {
+                    GM_TRY(errs_rc(errs));
+                    break;
+                }
+            }
+            for (auto &R : d->ranks) {   // the tier's buffers now belong to kept[t]
                 R.recvk = nullptr;
                 if (self_only(d)) R.sendk = nullptr;
             }
+            counted = true;
         }
-        GM_TRY(check_err(c, d));
-        // global tier counts (sum over ranks of each rank's frontier counts)
-        std::vector<uint64_t> local(need, 0), hc(need);
-        for (auto &R : d->ranks) {
-            GM_HIP(hipMemcpyAsync(hc.data(), R.d_cnt, need * 8, hipMemcpyDeviceToHost, c->stream));
+        if (!counted) {   // (the fused path)
+            GM_TRY(check_err(c, d));
+            for (size_t i = 0; i < d->ranks.size(); i++)
+                GM_HIP(hipMemcpyAsync(hcs[i].data(), d->ranks[i].d_cnt, need * 8, hipMemcpyDeviceToHost, c->stream));
             GM_HIP(hipStreamSynchronize(c->stream));
+        }
+        // global tier counts (sum over ranks of each rank's frontier counts)
+        std::vector<uint64_t> local(need, 0);
+        for (size_t i = 0; i < d->ranks.size(); i++) {
+            SpRankT<K> &R = d->ranks[i];
             for (size_t u = t + 1; u < need; u++) {
-                R.tiers[u].fcount = hc[u];
-                local[u] += hc[u];
+                R.tiers[u].fcount = hcs[i][u];
+                local[u] += hcs[i][u];
             }
         }
         if (d->ipc) {
@@ -1014,7 +1071,6 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
         // in the same layout, and each sender folds them into the parents it recorded
         const std::vector<Layout> &lay = d->t_lay[t];
         const std::vector<uint64_t> &tmat = d->t_mat[t];
-        std::vector<std::vector<uint64_t>> rbs(d->ranks.size());   // (alive until the stream syncs below)
         for (size_t i = 0; i < d->ranks.size(); i++) {
             SpRankT<K> &R = d->ranks[i];
             const uint64_t nrecv = self_only(d) ? lay[i].nsend : lay[i].nrecv;
@@ -1033,12 +1089,8 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                 const size_t u = t + 1 + s;
                 nx.t[s] = u < R.tiers.size() ? res_ref_of(R.tiers[u]) : typename KT<K>::Res{nullptr, 0};
             }
-            std::vector<uint64_t> &rb = rbs[i];
-            rb = lay[i].recv_seg;
-            rb.push_back(lay[i].nrecv);
-            GM_HIP(hipMemcpyAsync(R.d_rb, rb.data(), rb.size() * 8, hipMemcpyHostToDevice, c->stream));
             hipLaunchKernelGGL(lookup_bins_kernel<D>, dim3(grid_for(nrecv)), dim3(256), 0, c->stream, desc,
-                               R.kept[t].recvk, nrecv, R.d_rb, nb, nx, R.reply_out, R.d_err);
+                               R.kept[t].recvk, nrecv, R.kept[t].rb, nb, nx, R.reply_out, R.d_err);
         }
         GM_TRY(exchange(c, d, lay, tmat, true));                  // RESOLVE: scores back
         for (size_t i = 0; i < d->ranks.size(); i++) {
@@ -1050,13 +1102,16 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
                                    c->stream, recv_replies(d, R), kp.lp, kp.cbase, kp.ccnt, nb, T.islot, T.ni,
                                    res_ref_of(T), R.d_err);
         }
-        GM_TRY(check_err(c, d));
+        // (no synchronisation per tier: the device errors are sticky and read after the pass; the
+        // buffers below are stream-ordered, so the allocator may hand them out again at once)
         for (auto &R : d->ranks) {   // tier t is resolved: what the forward kept for it can go
             auto &kp = R.kept[t];
-            for (void *p : {(void *)kp.recvk, (void *)kp.lp, (void *)kp.cbase, (void *)kp.ccnt}) dev_free(c, p);
+            for (void *p : {(void *)kp.recvk, (void *)kp.lp, (void *)kp.cbase, (void *)kp.ccnt, (void *)kp.rb})
+                dev_free(c, p);
             kp = typename SpRankT<K>::Kept{};
         }
     }
+    GM_TRY(check_err(c, d));
     const double t2 = now_ms();
 
     // root record: the owner's score, max-reduced over ranks
@@ -1276,10 +1331,11 @@ static void free_ranks(Ctx *c, DistSparseK<K> *d) {
         for (auto &T : R.tiers) free_tier(c, T);
         // every buffer once: after a failed solve recvk / sendk may still alias a tier's
         std::vector<void *> ps = {(void *)R.d_cnt, (void *)R.d_err, (void *)R.d_hist, (void *)R.d_cursor,
-                                  (void *)R.d_seg, (void *)R.d_scr, (void *)R.d_rb, (void *)R.sendk, (void *)R.recvk,
+                                  (void *)R.d_seg, (void *)R.d_scr, (void *)R.sendk, (void *)R.recvk,
                                   (void *)R.reply_out, (void *)R.reply_in};
         for (auto &kp : R.kept)
-            for (void *p : {(void *)kp.recvk, (void *)kp.lp, (void *)kp.cbase, (void *)kp.ccnt}) ps.push_back(p);
+            for (void *p : {(void *)kp.recvk, (void *)kp.lp, (void *)kp.cbase, (void *)kp.ccnt, (void *)kp.rb})
+                ps.push_back(p);
         std::sort(ps.begin(), ps.end());
         ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
         for (void *p : ps) dev_free(c, p);
