@@ -299,6 +299,9 @@ TOOT_6X4_PER_PLY = [1, 12, 114, 748, 4266, 19692, 81140, 285708, 928196, 2665424
 
 
 SIDE_WARMUP, SIDE_REPEATS = 1, 5   # median of 5 runs after 1 warm-up
+# --rehearse-one-gpu: the side configs' ranks share device 0 and exchange over the sparse
+# engine's IPC transport (RCCL refuses two ranks on one GPU)
+SIDE_DEVICE, SIDE_SPARSE_IPC = None, False
 
 
 def toot_sample_root(params=(6, 4), plies=3):
@@ -347,7 +350,7 @@ def sparse_config(name, game, params, rank, world, dist, torch):
     over ranks against the C oracle's (tests/golden/oracle_digests.json).  Time =
     max over ranks, median of 5 after 1 warm-up."""
     from gamesmanmpi_amd import Context, _lib
-    ctx = Context(game, params, device=int(os.environ.get("LOCAL_RANK", 0)))
+    ctx = Context(game, params, device=SIDE_DEVICE if SIDE_DEVICE is not None else int(os.environ.get("LOCAL_RANK", 0)))
     if world > 1:
         uid = [None]
         if rank == 0:
@@ -356,6 +359,8 @@ def sparse_config(name, game, params, rank, world, dist, torch):
             uid[0] = buf.raw
         dist.broadcast_object_list(uid, src=0)
         ctx.set_comm(rank, world, uid[0])
+        if SIDE_SPARSE_IPC:
+            ctx.set_option(_lib.OPT_SPARSE_TRANSPORT, 1)
     root = ctx.initial()
     n, rec, ts = timed_solves(ctx, root, rank, world, dist, torch)
     med = sorted(ts)[len(ts) // 2]
@@ -370,7 +375,9 @@ def sparse_config(name, game, params, rank, world, dist, torch):
                              "(GM_OPT_SYMMETRY 1, the default)",
            "statistic": "median of %d solves after %d warm-up (max over ranks)" % (SIDE_REPEATS, SIDE_WARMUP),
            "solve_ms_all": [round(t * 1e3, 3) for t in ts],
-           "ranks": world, "exchanged_bytes_rank%d" % rank: st["exchanged_bytes"]}
+           "ranks": world, "exchanged_bytes_rank%d" % rank: st["exchanged_bytes"],
+           "transport": None if world == 1 else ("IPC, the ranks sharing one GPU (rehearsal)" if SIDE_SPARSE_IPC
+                                                 else "RCCL, one GPU per rank")}
     ref = committed_digest(name)
     d, m = summed_digest(ctx, world, dist, torch)
     out["digest"] = "%#018x" % d
@@ -592,6 +599,9 @@ def copy_bandwidth(torch, nbytes=1 << 31, reps=10):
 
 
 def main():
+    if os.environ.get("GM_BENCH_STACKS"):   # development: every rank's Python stacks on stderr after N s
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GM_BENCH_STACKS"]), repeat=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -622,6 +632,10 @@ def main():
                     help="N>1 rehearsal on a one-GPU box: every rank on device 0, bench.py's collectives over "
                          "gloo, the box engine's halos over the IPC transport (RCCL refuses two ranks on one "
                          "GPU), no side configs; the ranks share the GPU, so the time is not a multi-GPU result")
+    ap.add_argument("--rehearse-side", action="store_true",
+                    help="with --rehearse-one-gpu: also the side configs, hash-sharded over the sparse IPC transport "
+                         "(development: the 6x4 solve without the symmetry reduction stalls in hipIpcOpenMemHandle, "
+                         "DESIGN.md §5.2)")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     ap.add_argument("--watchdog", type=float, default=None,
@@ -633,11 +647,13 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
-    global COLL_DEV
+    global COLL_DEV, SIDE_DEVICE, SIDE_SPARSE_IPC
     if args.rehearse_one_gpu:
         if args.heaps != 8 or args.block_engine:
             ap.error("--rehearse-one-gpu runs the 8-heap box engine")
-        local, COLL_DEV, args.no_toot, args.box_transport = 0, "cpu", True, "ipc"
+        local, COLL_DEV, args.box_transport = 0, "cpu", "ipc"
+        args.no_toot = args.no_toot or not args.rehearse_side
+        SIDE_DEVICE, SIDE_SPARSE_IPC = 0, True
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))
 

@@ -74,6 +74,7 @@ struct SpIpc {
     // per peer, every allocation mapped in this solve (a peer's buffer can come back from its
     // allocation cache as another kind: one mapping per allocation, closed at the end)
     std::vector<std::vector<std::pair<hipIpcMemHandle_t, void *>>> maps;
+    uint64_t gsum[2] = {};           // the sum of every rank's published generation, when last mapped
 };
 
 static int sp_ipc_barrier(SpIpc &X) {
@@ -181,6 +182,8 @@ static int sp_ipc_peer(SpIpc &X, int r, int k, char **out) {
         for (auto &e : X.maps[r])
             if (!std::memcmp(&e.first, &h, sizeof h)) b = e.second;
         if (!b) {
+            if (trace_on()) fprintf(stderr, "[gm] ipc rank %d opens rank %d's buffer gen %llu\n", X.me, r,
+                                    (unsigned long long)g);
             if (hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
                 (void)hipGetLastError();
                 set_error("hipIpcOpenMemHandle of rank %d's send buffer failed", r);
@@ -678,9 +681,30 @@ static int exchange_ipc(Ctx *c, DistSparseK<K> *d, const Layout &me, const std::
     const size_t elem = reply ? 2 : sizeof(K);
     char *mine = reply ? (char *)R.reply_out : (char *)R.sendk;
     char *dst = reply ? (char *)R.reply_in : (char *)R.recvk;
+    if (trace_on()) fprintf(stderr, "[gm] ipc rank %d exchange %s: sync\n", X.me, reply ? "replies" : "keys");
     GM_HIP(hipStreamSynchronize(c->stream));   // the send buffer is complete
     GM_TRY(sp_ipc_publish(X, k, mine));
+    if (trace_on()) fprintf(stderr, "[gm] ipc rank %d published %p gen %llu; barrier\n", X.me, (void *)mine,
+                            (unsigned long long)X.gen[k]);
     GM_TRY(sp_ipc_barrier(X));
+    // A peer published a new buffer: map them one rank at a time.  Two processes opening each
+    // other's IPC handles at the same moment can block each other inside the runtime for good
+    // (Toot 6x4 over 2 processes: both ranks in hipIpcOpenMemHandle, profiles/r06/r06ae_*).  The
+    // sum of the published generations is the same on every rank after the barrier, so every rank
+    // takes the same G barriers.
+    uint64_t gs = 0;
+    for (int p = 0; p < d->G; p++) gs += X.slot[p].gen[k];
+    if (gs != X.gsum[k]) {
+        X.gsum[k] = gs;
+        for (int turn = 0; turn < d->G; turn++) {
+            if (turn == X.me)
+                for (int p = 0; p < d->G; p++) {
+                    char *unused;
+                    if (p != X.me) GM_TRY(sp_ipc_peer(X, p, k, &unused));
+                }
+            GM_TRY(sp_ipc_barrier(X));
+        }
+    }
     for (int p = 0; p < d->G; p++) {
         const Layout lp = layout_for(d, mat, p);
         // keys: p's segment for me -> my receive segment from p; replies: p's answers to my
@@ -691,6 +715,9 @@ static int exchange_ipc(Ctx *c, DistSparseK<K> *d, const Layout &me, const std::
         const uint64_t dst_off = reply ? me.send_off[p] : me.recv_off[p];
         char *src = mine;
         if (p != X.me) GM_TRY(sp_ipc_peer(X, p, k, &src));
+        if (trace_on())
+            fprintf(stderr, "[gm] ipc rank %d pulls %llu B from rank %d (%p + %llu)\n", X.me,
+                    (unsigned long long)(n * elem), p, (void *)src, (unsigned long long)(src_off * elem));
         GM_HIP(hipMemcpyAsync(dst + dst_off * elem, src + src_off * elem, n * elem, hipMemcpyDeviceToDevice,
                               c->stream));
     }
@@ -1043,6 +1070,9 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
         for (auto &R : d->ranks)
             for (int s = 0; s < S; s++) after += R.tiers[t + 1 + s].fcount;
         d->est.observe(after - before, offered);
+        if (trace_on())
+            fprintf(stderr, "[gm] sharded rank %d forward tier %zu: %llu positions (all ranks), at %.1f ms\n",
+                    d->ranks[0].rank, t, (unsigned long long)d->gcount[t], now_ms() - t0);
     }
     while (!d->gcount.empty() && !d->gcount.back()) d->gcount.pop_back();
     const double t1 = now_ms();
@@ -1050,6 +1080,8 @@ static int solve_sharded(Ctx *c, const D &desc, const key_t<D> &root) {
     // ---------------- backward
     for (size_t t = d->gcount.size(); t-- > 0;) {
         if (!d->gcount[t]) continue;
+        if (trace_on())
+            fprintf(stderr, "[gm] sharded rank %d backward tier %zu at %.1f ms\n", d->ranks[0].rank, t, now_ms() - t0);
         if (self_fused(d)) {
             SpRankT<K> &R = d->ranks[0];
             SpTierT<K> &T = R.tiers[t];
