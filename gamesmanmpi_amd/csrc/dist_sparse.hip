@@ -670,6 +670,27 @@ int dist_sparse_layout(int G, int S, const uint64_t *mat, int r, uint64_t *seg, 
     return GM_OK;
 }
 
+// A pull out of a peer's IPC-mapped buffer: hipMemcpyAsync takes the runtime's copy path for
+// such memory (tools/ipc_big_probe.hip: 26-54 GB/s for 1 GiB on one GPU); a kernel reading the
+// mapping directly streams like any device copy.  8-byte words (the key segments; the 2-byte
+// reply segments go through hipMemcpyAsync unless they happen to be aligned).
+__global__ __launch_bounds__(256) void ipc_pull_kernel(uint64_t *__restrict__ dst, const uint64_t *__restrict__ src,
+                                                       uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+static int ipc_pull(Ctx *c, char *dst, const char *src, uint64_t bytes) {
+    if (!bytes) return GM_OK;
+    if (((uintptr_t)dst | (uintptr_t)src | bytes) & 7u) {
+        GM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+        return GM_OK;
+    }
+    hipLaunchKernelGGL(ipc_pull_kernel, dim3(grid_for(bytes / 8)), dim3(256), 0, c->stream, (uint64_t *)dst,
+                       (const uint64_t *)src, bytes / 8);
+    GM_HIP(hipGetLastError());
+    return GM_OK;
+}
+
 // move every rank's segmented send buffer to the owners (or, reverse = true, the replies back)
 // IPC: publish this rank's send buffer, barrier, pull every segment addressed to this rank out
 // of the senders' buffers, barrier (the senders may then overwrite them)
@@ -718,8 +739,7 @@ static int exchange_ipc(Ctx *c, DistSparseK<K> *d, const Layout &me, const std::
         if (trace_on())
             fprintf(stderr, "[gm] ipc rank %d pulls %llu B from rank %d (%p + %llu)\n", X.me,
                     (unsigned long long)(n * elem), p, (void *)src, (unsigned long long)(src_off * elem));
-        GM_HIP(hipMemcpyAsync(dst + dst_off * elem, src + src_off * elem, n * elem, hipMemcpyDeviceToDevice,
-                              c->stream));
+        GM_TRY(ipc_pull(c, dst + dst_off * elem, src + src_off * elem, n * elem));
     }
     for (int p = 0; p < d->G; p++)   // what this rank sent: its segments other ranks pulled
         if (p != X.me)
