@@ -630,12 +630,9 @@ def main():
                          "halo messages over RCCL send / recv, launched eagerly (the library's default transport)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 rehearsal on a one-GPU box: every rank on device 0, bench.py's collectives over "
-                         "gloo, the box engine's halos over the IPC transport (RCCL refuses two ranks on one "
-                         "GPU), no side configs; the ranks share the GPU, so the time is not a multi-GPU result")
-    ap.add_argument("--rehearse-side", action="store_true",
-                    help="with --rehearse-one-gpu: also the side configs, hash-sharded over the sparse IPC transport "
-                         "(development: the 6x4 solve without the symmetry reduction stalls in hipIpcOpenMemHandle, "
-                         "DESIGN.md §5.2)")
+                         "gloo, the box engine's halos and the side configs' exchanges over the IPC transports "
+                         "(RCCL refuses two ranks on one GPU); the ranks share the GPU, so the times are not "
+                         "multi-GPU results")
     ap.add_argument("--virtual-ranks", type=int, default=1,
                     help="diagnostic: run the sharded algorithm with V loopback ranks on this one GPU")
     ap.add_argument("--watchdog", type=float, default=None,
@@ -652,7 +649,6 @@ def main():
         if args.heaps != 8 or args.block_engine:
             ap.error("--rehearse-one-gpu runs the 8-heap box engine")
         local, COLL_DEV, args.box_transport = 0, "cpu", "ipc"
-        args.no_toot = args.no_toot or not args.rehearse_side
         SIDE_DEVICE, SIDE_SPARSE_IPC = 0, True
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE %d" % (args.gpus, world))

@@ -26,11 +26,11 @@
 //   RCCL (GM_OPT_SPARSE_TRANSPORT 0, one process per GPU): counts all-gathered, keys and
 //     replies as one ncclGroup of send/recv per peer, totals all-reduced;
 //   IPC (GM_OPT_SPARSE_TRANSPORT 1, one process per rank on one node, ranks may share a GPU):
-//     each rank publishes HIP IPC handles of its two send buffers (keys, replies) in a POSIX
-//     shared-memory segment; after a host barrier each receiver PULLS its segments out of the
-//     senders' buffers (hipMemcpyAsync from the mapping), and a second barrier frees the send
-//     buffers for reuse.  Counts, totals and the root record are all-gathered through the same
-//     segment (SpIpc below);
+//     each rank publishes the HIP IPC handle of one fixed exchange window in a POSIX
+//     shared-memory segment; per round the senders copy the next part of their send buffers
+//     into their windows, a host barrier, each receiver PULLS its pieces out of the peers'
+//     windows (a copy kernel reading the mapping), a second barrier frees the windows.  Counts,
+//     totals and the root record are all-gathered through the same segment (SpIpc below);
 //   loopback (GM_OPT_VIRTUAL_RANKS): device copies between G virtual ranks in one context.
 // The three share the layout (layout_for): rank r's send segment for p starts at
 // lay(r).send_off[p], p's receive segment from r at lay(p).recv_off[r].
@@ -54,7 +54,7 @@ namespace gm {
 constexpr int SP_IPC_WORDS = 512;
 constexpr double SP_IPC_WAIT_MS = 120e3;
 struct SpIpcSlot {
-    hipIpcMemHandle_t h[2];          // 0 = key send buffer (sendk), 1 = reply send buffer (reply_out)
+    hipIpcMemHandle_t h[2];          // 0 = the rank's exchange window (exchange_ipc); 1 unused
     uint64_t off[2], gen[2];         // the buffer's offset in its allocation; bumped per new buffer
     uint64_t arrive;                 // barrier epoch reached
     uint64_t failed;                 // the rank left the solve with an error
@@ -74,7 +74,6 @@ struct SpIpc {
     // per peer, every allocation mapped in this solve (a peer's buffer can come back from its
     // allocation cache as another kind: one mapping per allocation, closed at the end)
     std::vector<std::vector<std::pair<hipIpcMemHandle_t, void *>>> maps;
-    uint64_t gsum[2] = {};           // the sum of every rank's published generation, when last mapped
 };
 
 static int sp_ipc_barrier(SpIpc &X) {
@@ -248,6 +247,7 @@ struct DistSparse {
     uint32_t *d_root = nullptr;
     uint64_t sent_bytes = 0, edges = 0;
     DedupEstimate est;
+    char *win = nullptr;                     // IPC: this rank's exchange window (SP_IPC_WIN bytes)
 };
 template <class K>
 struct DistSparseK : DistSparse {
@@ -670,82 +670,104 @@ int dist_sparse_layout(int G, int S, const uint64_t *mat, int r, uint64_t *seg, 
     return GM_OK;
 }
 
-// A pull out of a peer's IPC-mapped buffer: hipMemcpyAsync takes the runtime's copy path for
+// A pull out of a peer's IPC-mapped window: hipMemcpyAsync takes the runtime's copy path for
 // such memory (tools/ipc_big_probe.hip: 26-54 GB/s for 1 GiB on one GPU); a kernel reading the
-// mapping directly streams like any device copy.  8-byte words (the key segments; the 2-byte
-// reply segments go through hipMemcpyAsync unless they happen to be aligned).
-__global__ __launch_bounds__(256) void ipc_pull_kernel(uint64_t *__restrict__ dst, const uint64_t *__restrict__ src,
-                                                       uint64_t n) {
+// mapping directly streams like any device copy.  8-byte words (key segments) or 2-byte ones
+// (reply segments).
+template <class W>
+__global__ __launch_bounds__(256) void ipc_pull_kernel(W *__restrict__ dst, const W *__restrict__ src, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         dst[i] = src[i];
 }
 static int ipc_pull(Ctx *c, char *dst, const char *src, uint64_t bytes) {
     if (!bytes) return GM_OK;
-    if (((uintptr_t)dst | (uintptr_t)src | bytes) & 7u) {
+    const uintptr_t a = (uintptr_t)dst | (uintptr_t)src | bytes;
+    if (!(a & 7u))
+        hipLaunchKernelGGL(ipc_pull_kernel<uint64_t>, dim3(grid_for(bytes / 8)), dim3(256), 0, c->stream,
+                           (uint64_t *)dst, (const uint64_t *)src, bytes / 8);
+    else if (!(a & 1u))
+        hipLaunchKernelGGL(ipc_pull_kernel<uint16_t>, dim3(grid_for(bytes / 2)), dim3(256), 0, c->stream,
+                           (uint16_t *)dst, (const uint16_t *)src, bytes / 2);
+    else
         GM_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
-        return GM_OK;
-    }
-    hipLaunchKernelGGL(ipc_pull_kernel, dim3(grid_for(bytes / 8)), dim3(256), 0, c->stream, (uint64_t *)dst,
-                       (const uint64_t *)src, bytes / 8);
     GM_HIP(hipGetLastError());
     return GM_OK;
 }
 
-// move every rank's segmented send buffer to the owners (or, reverse = true, the replies back)
-// IPC: publish this rank's send buffer, barrier, pull every segment addressed to this rank out
-// of the senders' buffers, barrier (the senders may then overwrite them)
+// move every rank's segmented send buffer to the owners (or, reverse = true, the replies back).
+// IPC: through one fixed window per rank, exported and mapped once per solve (SP_IPC_WIN bytes).
+// Mapping each grown send buffer afresh stalled: Toot 6x4 without the symmetry reduction, the
+// import of a 2.6 GB send buffer never returned (profiles/r06/r06ae_*, r06ak_*).  An exchange
+// runs in rounds: the sender copies the next window-sized part of its send buffer into its
+// window, a barrier, every receiver pulls the pieces of its segments that lie in that part out
+// of the peers' windows, a barrier.  Every rank knows every rank's layout, so all take the same
+// number of rounds.
+constexpr uint64_t SP_IPC_WIN = 1ull << 30;
 template <class K>
 static int exchange_ipc(Ctx *c, DistSparseK<K> *d, const Layout &me, const std::vector<uint64_t> &mat, bool reply) {
     SpRankT<K> &R = d->ranks[0];
     SpIpc &X = d->X;
-    const int k = reply ? 1 : 0;
+    const int G = d->G;
     const size_t elem = reply ? 2 : sizeof(K);
     char *mine = reply ? (char *)R.reply_out : (char *)R.sendk;
     char *dst = reply ? (char *)R.reply_in : (char *)R.recvk;
-    if (trace_on()) fprintf(stderr, "[gm] ipc rank %d exchange %s: sync\n", X.me, reply ? "replies" : "keys");
-    GM_HIP(hipStreamSynchronize(c->stream));   // the send buffer is complete
-    GM_TRY(sp_ipc_publish(X, k, mine));
-    if (trace_on()) fprintf(stderr, "[gm] ipc rank %d published %p gen %llu; barrier\n", X.me, (void *)mine,
-                            (unsigned long long)X.gen[k]);
-    GM_TRY(sp_ipc_barrier(X));
-    // A peer published a new buffer: map them one rank at a time.  Two processes opening each
-    // other's IPC handles at the same moment can block each other inside the runtime for good
-    // (Toot 6x4 over 2 processes: both ranks in hipIpcOpenMemHandle, profiles/r06/r06ae_*).  The
-    // sum of the published generations is the same on every rank after the barrier, so every rank
-    // takes the same G barriers.
-    uint64_t gs = 0;
-    for (int p = 0; p < d->G; p++) gs += X.slot[p].gen[k];
-    if (gs != X.gsum[k]) {
-        X.gsum[k] = gs;
-        for (int turn = 0; turn < d->G; turn++) {
+    if (!d->win) {   // once per solve: publish the window, then map the peers' one rank at a time
+        // (two processes opening each other's IPC handles at once can block each other)
+        GM_TRY(dev_alloc(c, (void **)&d->win, SP_IPC_WIN));
+        GM_TRY(sp_ipc_publish(X, 0, d->win));
+        GM_TRY(sp_ipc_barrier(X));
+        for (int turn = 0; turn < G; turn++) {
             if (turn == X.me)
-                for (int p = 0; p < d->G; p++) {
+                for (int p = 0; p < G; p++) {
                     char *unused;
-                    if (p != X.me) GM_TRY(sp_ipc_peer(X, p, k, &unused));
+                    if (p != X.me) GM_TRY(sp_ipc_peer(X, p, 0, &unused));
                 }
             GM_TRY(sp_ipc_barrier(X));
         }
     }
-    for (int p = 0; p < d->G; p++) {
-        const Layout lp = layout_for(d, mat, p);
-        // keys: p's segment for me -> my receive segment from p; replies: p's answers to my
-        // requests (p's receive segment from me) -> my send-order slots for p
-        const uint64_t n = reply ? me.send_off[p + 1] - me.send_off[p] : me.recv_off[p + 1] - me.recv_off[p];
-        if (!n) continue;
-        const uint64_t src_off = reply ? lp.recv_off[X.me] : lp.send_off[X.me];
-        const uint64_t dst_off = reply ? me.send_off[p] : me.recv_off[p];
-        char *src = mine;
-        if (p != X.me) GM_TRY(sp_ipc_peer(X, p, k, &src));
-        if (trace_on())
-            fprintf(stderr, "[gm] ipc rank %d pulls %llu B from rank %d (%p + %llu)\n", X.me,
-                    (unsigned long long)(n * elem), p, (void *)src, (unsigned long long)(src_off * elem));
-        GM_TRY(ipc_pull(c, dst + dst_off * elem, src + src_off * elem, n * elem));
+    std::vector<Layout> L(G);
+    uint64_t rounds = 1;
+    for (int p = 0; p < G; p++) {
+        L[p] = layout_for(d, mat, p);
+        const uint64_t tb = (reply ? L[p].nrecv : L[p].nsend) * elem;   // p's send buffer, bytes
+        rounds = std::max<uint64_t>(rounds, (tb + SP_IPC_WIN - 1) / SP_IPC_WIN);
     }
-    for (int p = 0; p < d->G; p++)   // what this rank sent: its segments other ranks pulled
+    const uint64_t tme = (reply ? me.nrecv : me.nsend) * elem;
+    GM_HIP(hipStreamSynchronize(c->stream));   // the send buffer is complete
+    {   // this rank's own segment: a local copy
+        const uint64_t n = reply ? me.send_off[X.me + 1] - me.send_off[X.me] : me.recv_off[X.me + 1] - me.recv_off[X.me];
+        const uint64_t so = reply ? me.recv_off[X.me] : me.send_off[X.me];
+        const uint64_t dof = reply ? me.send_off[X.me] : me.recv_off[X.me];
+        GM_TRY(ipc_pull(c, dst + dof * elem, mine + so * elem, n * elem));
+    }
+    for (uint64_t j = 0; j < rounds; j++) {
+        const uint64_t lo = j * SP_IPC_WIN, hi = lo + SP_IPC_WIN;
+        if (lo < tme) GM_TRY(ipc_pull(c, d->win, mine + lo, std::min(hi, tme) - lo));
+        GM_HIP(hipStreamSynchronize(c->stream));
+        GM_TRY(sp_ipc_barrier(X));
+        for (int p = 0; p < G; p++) {
+            if (p == X.me) continue;
+            // p's bytes for this rank, in p's send order: keys its send segment, replies its
+            // answers to this rank's requests (p's receive segment from this rank)
+            const uint64_t a = (reply ? L[p].recv_off[X.me] : L[p].send_off[X.me]) * elem;
+            const uint64_t b = (reply ? L[p].recv_off[X.me + 1] : L[p].send_off[X.me + 1]) * elem;
+            const uint64_t s0 = std::max(a, lo), e0 = std::min(b, hi);
+            if (s0 >= e0) continue;
+            char *pw;
+            GM_TRY(sp_ipc_peer(X, p, 0, &pw));
+            const uint64_t dof = (reply ? me.send_off[p] : me.recv_off[p]) * elem + (s0 - a);
+            if (trace_on())
+                fprintf(stderr, "[gm] ipc rank %d round %llu pulls %llu B from rank %d\n", X.me,
+                        (unsigned long long)j, (unsigned long long)(e0 - s0), p);
+            GM_TRY(ipc_pull(c, dst + dof, pw + (s0 - lo), e0 - s0));
+        }
+        GM_HIP(hipStreamSynchronize(c->stream));
+        GM_TRY(sp_ipc_barrier(X));   // the windows may be refilled
+    }
+    for (int p = 0; p < G; p++)   // what this rank sent: its segments other ranks pulled
         if (p != X.me)
             d->sent_bytes += (reply ? me.recv_off[p + 1] - me.recv_off[p] : me.send_off[p + 1] - me.send_off[p]) * elem;
-    GM_HIP(hipStreamSynchronize(c->stream));
-    return sp_ipc_barrier(X);
+    return GM_OK;
 }
 
 // One rank in one context (a 128-bit-key game on one GPU): its send order IS its receive
@@ -1402,6 +1424,7 @@ void dist_sparse_free(Ctx *c) {
     dev_free(c, d->d_mat);
     if (d->d_tot) dev_free(c, d->d_tot);
     dev_free(c, d->d_root);
+    dev_free(c, d->win);   // (to the allocation cache: a peer may not have closed its mapping yet)
     (void)hipStreamSynchronize(c->stream);
     sp_ipc_close(d->X);
     delete d;

@@ -48,7 +48,8 @@ def test_bench_rehearsal_two_processes_one_gpu():
     """bench.py at N = 2 as the driver launches it (torch.distributed.run, one process per
     rank), both ranks on this one GPU (--rehearse-one-gpu: gloo for the bench's collectives,
     the IPC transport for the halos): the IPC probe passes (no fallback), every rank's owned
-    digest equals the oracle's, and the line says it is a rehearsal."""
+    digest equals the oracle's, the side configs shard over the sparse IPC transport, and the
+    line says it is a rehearsal."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29531", os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--rehearse-one-gpu", "--dist-batch", "1"]
@@ -60,6 +61,12 @@ def test_bench_rehearsal_two_processes_one_gpu():
     assert d["n_gpus"] == 2 and d["parity"]["ok"] and d["halo_transport_fallback"] is None
     assert d["rehearsal"] and d["sharding"]["work_vs_one_gpu"] == 1.0
     assert d["parity"]["per_rank_vs_oracle"]["wrong_ranks"] == []
+    # the side configs' hash-sharded solves at N = 2, over the sparse IPC transport (RCCL refuses
+    # two ranks on one GPU): summed digests, counts and root records equal the oracle's
+    oc = d["other_configs"]
+    for name in ("othello_4x4", "toot_6x4"):
+        assert oc[name]["ok"] and oc[name]["ranks"] == 2 and "IPC" in oc[name]["transport"], oc[name]
+    assert oc["toot_6x4"]["symmetry_off"]["digest_matches_oracle"]
 
 
 def test_bench_rehearsal_failed_probe_exits_cleanly():

@@ -13,6 +13,7 @@
 #include <string>
 #include <thread>
 #include <unistd.h>
+#include <vector>
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -79,6 +80,46 @@ int main(int argc, char **argv) {
     const size_t bytes = strtoull(argv[2], nullptr, 10);
     const std::string dir = argv[3];
     const int reps = argc > 4 ? atoi(argv[4]) : 1;
+    // role 2 / 3 (exporter / importer, a 5th argument "a,b,c" of sizes): a growing buffer, as a
+    // rank's send buffer in a solve -- a new allocation of each size exported in turn, the
+    // importer keeping every earlier mapping open
+    if (role >= 2) {
+        std::vector<size_t> sizes;
+        for (char *q = argv[5]; *q;) {
+            sizes.push_back(strtoull(q, &q, 10));
+            if (*q == ',') q++;
+        }
+        std::vector<void *> maps;
+        for (size_t i = 0; i < sizes.size(); i++) {
+            const std::string sfx = "." + std::to_string(i);
+            const std::string hf = dir + "/handle" + sfx + ".bin", done = dir + "/done" + sfx;
+            if (role == 2) {
+                void *q = nullptr;
+                if (hipMalloc(&q, sizes[i]) != hipSuccess) { fprintf(stderr, "hipMalloc failed\n"); return 1; }
+                (void)hipMemset(q, 0x5A, sizes[i]);
+                (void)hipDeviceSynchronize();
+                if (exporter(q, sizes[i], hf, done)) return 1;
+            } else {
+                if (!wait_file(hf, 60.0)) { fprintf(stderr, "no handle %zu\n", i); return 1; }
+                hipIpcMemHandle_t h;
+                FILE *f = fopen(hf.c_str(), "rb");
+                if (fread(&h, sizeof h, 1, f) != 1) { fclose(f); return 1; }
+                fclose(f);
+                printf("importer: opening %zu bytes (%zu mappings open)\n", sizes[i], maps.size());
+                fflush(stdout);
+                const double t0 = now_s();
+                void *src = nullptr;
+                if (hipIpcOpenMemHandle(&src, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return 1;
+                printf("importer: opened in %.3f s\n", now_s() - t0);
+                fflush(stdout);
+                maps.push_back(src);
+                FILE *d = fopen(done.c_str(), "w");
+                fclose(d);
+            }
+        }
+        for (void *m : maps) (void)hipIpcCloseMemHandle(m);
+        return 0;
+    }
     void *p = nullptr;
     if (role == 0) {
         if (hipMalloc(&p, bytes) != hipSuccess) { fprintf(stderr, "hipMalloc failed\n"); return 1; }
