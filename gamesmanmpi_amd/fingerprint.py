@@ -8,13 +8,20 @@ one that differs only in deep or rare positions.  Certainty comes from one of:
 * its code is one of the plugin files the descriptors were written from and tested
   against: the reference's ``test_games/{four_to_one,mttt,tic_tac_toe_np,
   toot_and_otto_bitstring,othello_bit_new}.py`` and this repo's ``test_games/*.py``.
-  The fingerprint is a SHA-256 over the bytecode of the four API functions and of
+  The fingerprint is a SHA-256 over the bytecode of the three rule functions
+  (``gen_moves``, ``do_move``, ``primitive``) and of
   everything they reach -- module functions they call (transitively), closures
   (the ``src.utils`` encode/decode decorators), default arguments, and the values of
   the module globals they read (``BLANK``, ``MAX_TAKE``, ...).  Board dimensions
   and heap counts (``length``, ``height``, ``area``, ``HEAPS``) are left out: they
   are the descriptor's parameters, read from the module by the codec;
 * or an exhaustive cross-check of every reachable position (games.identify).
+
+``initial_position`` does not enter it either: it only names the root, which the solver
+is handed explicitly and checks on its own (the codec must encode it, and the plugin and
+the descriptor must agree on positions sampled below it).  The launcher's ``--custom FILE
+--init_pos NAME`` replaces that function, as the reference's does (solver_launcher.py:106-111),
+and a plugin solved from another root keeps its binding.
 
 Docstrings and line numbers do not enter the hash; any change of code or of a
 constant does.  Bytecode is interpreter-specific, so the stored fingerprints carry
@@ -32,7 +39,7 @@ import types
 HERE = os.path.dirname(os.path.abspath(__file__))
 STORE = os.path.join(HERE, "plugin_fingerprints.json")
 PARAM_NAMES = frozenset({"length", "height", "area", "HEAPS"})
-API = ("initial_position", "gen_moves", "do_move", "primitive")
+RULES = ("gen_moves", "do_move", "primitive")
 _SIMPLE = (int, float, complex, str, bytes, bool, type(None))
 
 
@@ -127,7 +134,7 @@ def fingerprint(module):
     """SHA-256 hex digest of the plugin's game code (module docstring for the rules)."""
     h = _Hasher()
     h.put("python", "%d.%d" % sys.version_info[:2])
-    for name in API:
+    for name in RULES:
         f = getattr(module, name, None)
         h.put("api", name)
         if isinstance(f, (types.FunctionType, types.MethodType)):

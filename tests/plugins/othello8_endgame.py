@@ -3,9 +3,9 @@
 The plugin functions are test_games/othello_bit_new.py's (8x8, as the reference ships it,
 `othello_bit_new.py:8`); only the root differs: the position after a fixed random playout
 from the standard start (seed 5), 10 empty squares left, 56,552 positions below it.  An 8x8
-position is 2A + 16 = 144 bits, more than the device descriptors' 64-bit keys, so the solver
-binds no descriptor and takes the explicit-graph path: the positions are enumerated on the
-host with these functions and resolved on the GPU (gm_solve_graph).  The golden table
+position is 2A + 16 = 144 bits; the rules are the plugin's own code, so the solver binds the
+128-bit-key descriptor by their fingerprint (`graph=True` takes the
+explicit-graph path instead, tests/test_graph.py).  The golden table
 (tests/golden/othello_8x8_endgame.npz) is the canonical solution of the REFERENCE's plugin
 from the same root (tests/golden/make_golden.py --only othello8).
 """

@@ -156,6 +156,24 @@ def test_fingerprints_cover_this_repos_plugins():
         fp.fingerprint(load_plugin("test_games/othello_bit_new.py"))
 
 
+def test_launcher_custom_root_keeps_the_fingerprint_binding():
+    """`solver_launcher.py GAME --custom FILE --init_pos NAME` replaces the module's
+    initial_position (as the reference's launcher does, solver_launcher.py:106-111); the rules
+    are unchanged, so the 8x8 plugin still binds the 128-bit-key descriptor by its fingerprint
+    and not through the exhaustive replay, which is capped at 10^6 positions (a 16-empty root
+    has 1.48 G below it)."""
+    import solver_launcher
+    from gamesmanmpi_amd import fingerprint as fp
+    args = solver_launcher.build_parser().parse_args(
+        [os.path.join(REPO, "test_games/othello_bit_new.py"), "--custom",
+         os.path.join(REPO, "tools/othello8_roots.py"), "--init_pos", "endgame_16"])
+    game, root = solver_launcher.prepare_game(args)
+    assert game.initial_position.__name__ == "endgame_16" and len(root) == 18
+    assert fp.known().get(fp.fingerprint(game), {}).get("codec") == "othello"
+    c = games.identify(game, root, exhaustive_max=0)
+    assert c is not None and c.name == "othello" and c.params == (8, 8)
+
+
 def test_othello_8x8_binds_the_wide_descriptor():
     """the reference plugin at its default 8x8 board (othello_bit_new.py:8,
     144-bit positions) binds to the 128-bit-key descriptor (games.hpp DescOthello8): 3 key words,

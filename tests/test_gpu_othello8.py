@@ -86,8 +86,9 @@ def test_othello8_endgame_12_device_vs_graph_path():
     """12 empties (1.2 M positions): the plugin at its default 8x8 with the root passed as a
     custom position (solver_launcher.py --custom) binds the descriptor by its code fingerprint,
     and the device table equals the explicit-graph path's record for record (position strings
-    of the plugin).  (tests/plugins/othello8_endgame.py changes initial_position, so it has no
-    known fingerprint and binds only through the exhaustive replay, capped at 10^6 positions.)"""
+    of the plugin).  (The fingerprint covers the rule functions, not initial_position, so the
+    launcher's --custom root keeps the binding: tests/test_abi.py
+    ::test_launcher_custom_root_keeps_the_fingerprint_binding.)"""
     from gamesmanmpi_amd import Solver, _lib
     mod = load_plugin("test_games/othello_bit_new.py")
     root = bytes.fromhex(ROOT12).decode("latin-1")
