@@ -237,3 +237,33 @@ def test_launcher_othello_8x8_endgame_on_the_device(tmp_path):
     got = {int.from_bytes(hashlib.blake2b(p.encode("ISO-8859-1"), digest_size=8).digest(), "big"): (v << 14) | r
            for p, (v, r) in back.items()}
     assert got == want
+
+
+@pytest.mark.gpu
+def test_launcher_othello_8x8_custom_root_on_the_device(tmp_path, capsys):
+    """`solver_launcher.py test_games/othello_bit_new.py --custom tools/othello8_roots.py
+    --init_pos endgame_10`: the unmodified plugin with the root from a custom file (the
+    reference's launcher patches initial_position, solver_launcher.py:106-111) keeps the
+    device binding -- the hash-sharded sparse engine, not the graph path -- and every record
+    equals the reference plugin's golden table for that root."""
+    import hashlib
+    import json
+    import numpy as np
+    from gamesmanmpi_amd import _lib
+    args = solver_launcher.build_parser().parse_args(
+        _abs(["test_games/othello_bit_new.py", "--custom", "tools/othello8_roots.py"])
+        + ["--init_pos", "endgame_10", "--stats", "-sd", str(tmp_path), "--sd-format", "npz"])
+    out = io.StringIO()
+    solver_launcher.run(args, out=out)
+    roots = json.load(open(os.path.join(GOLDEN, "roots.json")))
+    assert out.getvalue() == roots["othello_8x8_endgame"]["canonical"] + "\n"
+    stats = json.loads(capsys.readouterr().err.strip().splitlines()[-1])
+    assert stats["engine"] == _lib.ENGINE_DIST_SPARSE
+    d = np.load(tmp_path / "stats" / "0" / "table.npz")
+    g = np.load(os.path.join(GOLDEN, "othello_8x8_endgame.npz"))
+    want = dict(zip(g["keys"].tolist(), g["records"].tolist()))
+    got = {}
+    for w, r in zip(d["keys"].tolist(), d["records"].tolist()):
+        pos = sum(int(x) << (64 * i) for i, x in enumerate(w)).to_bytes(18, "big")
+        got[int.from_bytes(hashlib.blake2b(pos, digest_size=8).digest(), "big")] = int(r)
+    assert got == want
